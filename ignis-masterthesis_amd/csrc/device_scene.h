@@ -1,0 +1,57 @@
+// Device-resident scene and stream layouts (shared by host upload code and kernels).
+// See DESIGN.md "HBM layout".  All arrays are 16-byte element aligned so every
+// record is fetched with global_load_dwordx4.
+#pragma once
+
+#include <stdint.h>
+
+#ifndef __HIPCC__
+struct float4_ { float x, y, z, w; };
+#endif
+
+namespace igxd {
+
+// Traversal encodings (see host/bvh_build.h)
+constexpr int32_t REF_MARKER = (int32_t)0x80000000; // return from a BLAS to the TLAS
+constexpr int32_t REF_EXIT = (int32_t)0x80000001;   // bottom of the traversal stack
+constexpr int LEAF_COUNT_BITS = 4;
+
+// Instance record (one per TLAS leaf slot): 64 B
+//   row0..row2: to_local 3x4 (row-major, xyz = linear row, w = translation)
+//   info: x = entity id, y = shape type (0 trimesh, 1 sphere), z = BLAS root node
+//         index (trimesh) or sphere index (sphere), w = visibility flags
+// The reference's EntityLeaf1 (traversal/bvh.art:52-61) carries the same data
+// plus the entity box, which here lives in the parent TLAS node.
+
+// Per-entity shading record: 3 rows of to_global, 3 rows of normal matrix,
+// info (shape, material, vtx_offset, idx_offset) -> 7 x 16 B.
+constexpr int ENT_STRIDE = 7;
+
+enum : int32_t { MAT_DIFFUSE = 0, MAT_DIELECTRIC = 1 };
+struct DevMaterial {   // 64 B
+    int32_t type, light, thin, pad;
+    float kd[4];
+    float ks[4];
+    float kt[4];        // w unused
+    // n1 = ext_ior in ks[3], n2 = int_ior in kt[3]
+};
+
+enum : int32_t { LIGHT_PLANE = 1, LIGHT_ENV = 2, LIGHT_POINT = 3, LIGHT_SPOT = 4 };
+struct DevLight {      // 128 B
+    int32_t type, infinite, delta, pad;
+    float radiance[4];
+    float origin[4];   // plane origin / point/spot position; w = plane width
+    float ex[4];       // plane x axis normalised; w = plane height
+    float ey[4];       // plane y axis normalised; w = inv_area
+    float normal[4];   // plane normal / spot direction; w = area
+    float spot[4];     // cos_cutoff, cos_falloff, blend range, 0
+    float pad2[4];
+};
+
+struct DevCamera {
+    float eye[3], dir[3], up[3], right[3];
+    float scale_x, scale_y;
+    float tmin, tmax;
+};
+
+} // namespace igxd

@@ -1,0 +1,1184 @@
+// MI355X (gfx950) wavefront path-tracing device: kernels + host driver + C-ABI.
+//
+// Hot path = the reference's per-iteration loop gpu_trace
+// (src/artic/driver/mapping_gpu.art:728-870) re-designed for CDNA4:
+//   * all paths of an iteration are resident in HBM (capacity = spi*W*H up to
+//     16M paths) instead of refilling a 1M-ray stream (mapping_gpu.art:1125);
+//   * one fused "extend" kernel per bounce does closest-hit traversal AND
+//     shading (the reference launches traverse, 3 sort kernels with a host scan,
+//     one hit-shade kernel per material, miss shade, then compaction with a D2H
+//     sync: mapping_gpu.art:45-68, 403-498, 114-205, 229-266, 685-714);
+//   * surviving paths and shadow rays are compacted on the fly with a 64-lane
+//     ballot and one atomic per wave (no sort, no host round trip);
+//   * shadow rays are traced by a separate any-hit kernel over the compacted
+//     shadow stream (gpu_traverse_secondary, mapping_gpu.art:70-112);
+//   * radiance is accumulated per path slot with plain read-modify-writes (each
+//     slot is owned by exactly one ray at a time), then a resolve kernel adds
+//     sum(L_s)/spi to the framebuffer -- deterministic, no float atomics
+//     (the reference splats with atomic adds, driver/accumulator.art:4-21).
+#include "igx.h"
+
+#include "device_math.h"
+#include "device_scene.h"
+#include "igx_kernels.h"
+#include "../host/bvh_build.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+using namespace igxd;
+
+namespace {
+
+constexpr int BLOCK = 256;
+constexpr int MAX_BOUNCES = 256;
+
+// ---------------------------------------------------------------------------
+// Streams (SoA of 16-byte records)
+// ---------------------------------------------------------------------------
+struct PathBuf {
+    float4* p0; // org.xyz, (slot | depth << 24) as int bits
+    float4* p1; // dir.xyz, rnd counter
+    float4* p2; // contrib.rgb, inv_pdf
+    float* p3;  // eta
+};
+struct ShadowBuf {
+    float4* s0; // org.xyz, slot
+    float4* s1; // dir.xyz, tmax
+    float4* s2; // colour.rgb, -
+};
+
+struct FrameArgs {
+    int width, height, spi, iter, frame, seed;
+    int tile_size, tile_offset, tile_stride, tiles_x;
+    int num_rays;
+    const float* rays;   // device copy of the ray list (ray-list mode)
+    int chunk_pixel0;    // first local pixel of this chunk
+    int chunk_pixels;    // local pixels in this chunk
+    float inv_spi;
+};
+
+// local pixel -> global (x, y); false if the slot lies outside the film
+__device__ __forceinline__ bool local_to_global(const FrameArgs& fa, int lp, int& x, int& y) {
+    if (fa.num_rays > 0) { x = lp; y = 0; return lp < fa.num_rays; }
+    if (fa.tile_size <= 0) { y = lp / fa.width; x = lp - y * fa.width; return true; }
+    int T = fa.tile_size;
+    int k = lp / (T * T);
+    int r = lp - k * T * T;
+    int ty = r / T, tx = r - ty * T;
+    int t = fa.tile_offset + k * fa.tile_stride;
+    int tyy = t / fa.tiles_x, txx = t - tyy * fa.tiles_x;
+    x = txx * T + tx;
+    y = tyy * T + ty;
+    return x < fa.width && y < fa.height;
+}
+
+__device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+
+// wave-level stream compaction: returns the output index for lanes with `take`
+__device__ __forceinline__ int wave_append(bool take, int* counter) {
+    uint64_t mask = __ballot(take);
+    int lane = lane_id();
+    int prefix = __popcll(mask & ((1ull << lane) - 1ull));
+    int total = __popcll(mask);
+    int base = 0;
+    if (lane == 0 && total > 0) base = atomicAdd(counter, total);
+    base = __shfl(base, 0);
+    return base + prefix;
+}
+
+template <typename T>
+__device__ __forceinline__ T uniform_load(const T* p) {
+    return __builtin_amdgcn_readfirstlane(*p);
+}
+
+// ---------------------------------------------------------------------------
+// generate: camera rays (gpu_generate_rays, mapping_gpu.art:618-667;
+// make_camera_emitter, driver/emitter.art:6-16; perspective camera,
+// camera/perspective.art:29-42; uniform pixel sampler, sampler/pixel_sampler.art:4-10)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(BLOCK) k_generate(FrameArgs fa, SceneView sv, PathBuf out, float4* L, int* cnt0) {
+    const int n = fa.chunk_pixels * fa.spi;
+    const int total_waves = gridDim.x * (BLOCK / 64);
+    const int wave = blockIdx.x * (BLOCK / 64) + threadIdx.x / 64;
+    for (int base = wave * 64; base < n; base += total_waves * 64) {
+        int i = base + lane_id();
+        bool alive = false;
+        f3 o = mk(0, 0, 0), d = mk(0, 0, 1);
+        uint32_t counter = 1;
+        if (i < n) {
+            L[i] = make_float4(0, 0, 0, 0);
+            int lp = fa.chunk_pixel0 + i / fa.spi;
+            int sample = i - (i / fa.spi) * fa.spi;
+            int x, y;
+            if (local_to_global(fa, lp, x, y)) {
+                alive = true;
+                Rng rnd{create_random_seed(sample, fa.iter, fa.frame, x, y, fa.seed), 1};
+                if (fa.num_rays > 0) {
+                    // make_list_emitter (driver/emitter.art:18-30): no random draws
+                    const float* r = fa.rays + 8 * x;
+                    o = mk(r[0], r[1], r[2]);
+                    d = mk(r[3], r[4], r[5]);
+                } else {
+                    float rx = rnd.next_f32();
+                    float ry = rnd.next_f32();
+                    float nx = 2 * ((float)x + rx) / (float)fa.width - 1;
+                    float ny = 1 - 2 * ((float)y + ry) / (float)fa.height;
+                    const DevCamera& c = sv.cam;
+                    f3 v = mk(c.scale_x * nx, c.scale_y * ny, 1);
+                    f3 w = mk(c.right[0] * v.x + c.up[0] * v.y + c.dir[0] * v.z,
+                              c.right[1] * v.x + c.up[1] * v.y + c.dir[1] * v.z,
+                              c.right[2] * v.x + c.up[2] * v.y + c.dir[2] * v.z);
+                    o = mk(c.eye[0], c.eye[1], c.eye[2]);
+                    d = normalize(w);
+                }
+                counter = rnd.counter;
+            }
+        }
+        int dst = wave_append(alive, cnt0);
+        if (alive) {
+            out.p0[dst] = make_float4(o.x, o.y, o.z, __int_as_float(i | (1 << 24)));
+            out.p1[dst] = make_float4(d.x, d.y, d.z, __uint_as_float(counter));
+            out.p2[dst] = make_float4(1, 1, 1, 0); // init_pt_raypayload (technique/pathtracer.art:33-38)
+            out.p3[dst] = 1.0f;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// extend: closest hit + shading for every live path of one bounce
+// (gpu_traverse_primary + gpu_hit_shade + gpu_miss_shade, restating
+// technique/pathtracer.art:52-200 on_hit / on_shadow / on_bounce / on_miss)
+// ---------------------------------------------------------------------------
+struct KernelCounters {
+    int* cnt_in;
+    int* cnt_out;
+    int* cnt_shadow;
+    unsigned long long* stats; // 8 counters (instrumentation)
+};
+
+__device__ __forceinline__ f3 handle_color(const SceneView& sv, f3 c) {
+    if (sv.clamp > 0) return mk(fminf(c.x, sv.clamp), fminf(c.y, sv.clamp), fminf(c.z, sv.clamp));
+    return c;
+}
+
+template <int STACK, bool STATS>
+__global__ void __launch_bounds__(BLOCK) k_extend(FrameArgs fa, SceneView sv, PathBuf in, PathBuf out, ShadowBuf sh,
+                                                  float4* L, KernelCounters kc) {
+    __shared__ int stack_mem[STACK * BLOCK];
+    int* stk = stack_mem + threadIdx.x;
+    const int n = uniform_load(kc.cnt_in);
+    const int total_waves = gridDim.x * (BLOCK / 64);
+    const int wave = blockIdx.x * (BLOCK / 64) + threadIdx.x / 64;
+    TraceStats st{0, 0, 0, 0};
+    for (int base = wave * 64; base < n; base += total_waves * 64) {
+        int i = base + lane_id();
+        bool alive = false, shadow = false;
+        f3 no = mk(0, 0, 0), nd = mk(0, 0, 0), ncontrib = mk(0, 0, 0);
+        float ninv_pdf = 0, neta = 1;
+        uint32_t ncounter = 0;
+        f3 so = mk(0, 0, 0), sdir = mk(0, 0, 0), scol = mk(0, 0, 0);
+        float stmax = 0;
+        int slot = 0, depth = 0;
+        if (i < n) {
+            float4 p0 = in.p0[i], p1 = in.p1[i], p2 = in.p2[i];
+            float eta = in.p3[i];
+            int sd = __float_as_int(p0.w);
+            slot = sd & 0xFFFFFF;
+            depth = sd >> 24;
+            f3 ro = f3of(p0), rd = f3of(p1);
+            uint32_t counter = __float_as_uint(p1.w);
+            f3 contrib = f3of(p2);
+            float inv_pdf = p2.w;
+            float tmin, tmax;
+            uint32_t rflags;
+            if (depth == 1) {
+                if (fa.num_rays > 0) {
+                    int lp = fa.chunk_pixel0 + slot / fa.spi;
+                    tmin = fa.rays[8 * lp + 6];
+                    tmax = fa.rays[8 * lp + 7];
+                    rflags = 0;
+                } else {
+                    tmin = sv.cam.tmin;
+                    tmax = sv.cam.tmax;
+                    rflags = RAY_CAMERA;
+                }
+            } else {
+                tmin = 0.001f; // offset (pathtracer.art:41)
+                tmax = FLT_MAX_;
+                rflags = RAY_BOUNCE;
+            }
+            int hit_ent, hit_prim;
+            float hu = 0, hv = 0;
+            trace_ray<false, STATS>(sv, ro, rd, tmin, tmax, rflags, stk, BLOCK, hit_ent, hit_prim, hu, hv, st);
+
+            f3 Lacc = mk(0, 0, 0);
+            bool has_l = false;
+            if (hit_ent < 0) {
+                // on_miss (pathtracer.art:136-163): every infinite, non-delta light
+                for (int li = 0; li < sv.num_infinite; ++li) {
+                    const DevLight& Lt = sv.lights[li];
+                    if (Lt.delta) continue;
+                    f3 emit = mk(Lt.radiance[0], Lt.radiance[1], Lt.radiance[2]);
+                    float pdf_s = 1 / (4 * PI_);
+                    float mis = sv.nee ? 1 / (1 + inv_pdf * (1.0f / (float)sv.num_lights) * pdf_s) : 1.0f;
+                    Lacc = add(Lacc, handle_color(sv, mulf(mul(contrib, emit), mis)));
+                    has_l = true;
+                }
+            } else {
+                int mat_id;
+                Surface s = surface_element(sv, hit_ent, hit_prim, tmax, hu, hv, ro, rd, mat_id);
+                const DevMaterial& m = sv.mats[mat_id];
+                // on_hit (pathtracer.art:114-134)
+                if (m.light >= 0 && s.entering) {
+                    float dt = -dot(rd, s.local.n);
+                    if (dt > FLT_EPS_) {
+                        const DevLight& Lt = sv.lights[m.light];
+                        f3 emit = mk(Lt.radiance[0], Lt.radiance[1], Lt.radiance[2]);
+                        float pdf_s = light_pdf_direct_solid(Lt, ro, dt, tmax * tmax);
+                        float mis = sv.nee ? 1 / (1 + inv_pdf * (1.0f / (float)sv.num_lights) * pdf_s) : 1.0f;
+                        Lacc = add(Lacc, handle_color(sv, mulf(mul(contrib, emit), mis)));
+                        has_l = true;
+                    }
+                }
+                int sample = slot - (slot / fa.spi) * fa.spi;
+                int px, py;
+                local_to_global(fa, fa.chunk_pixel0 + slot / fa.spi, px, py);
+                Rng rnd{create_random_seed(sample, fa.iter, fa.frame, px, py, fa.seed), counter};
+                f3 out_dir = neg(rd);
+                bool specular = m.type == MAT_DIELECTRIC;
+                // on_shadow (pathtracer.art:52-112)
+                if (sv.nee && !specular && sv.num_lights > 0 && depth + 1 <= sv.max_depth) {
+                    int lid = sv.num_lights <= 1 ? 0 : rnd.next_i32(0, sv.num_lights - 1);
+                    float sel_pdf = sv.num_lights == 0 ? 1.0f : 1.0f / (float)sv.num_lights;
+                    const DevLight& Lt = sv.lights[lid];
+                    DirectSample ls = light_sample_direct(sv, Lt, rnd, s);
+                    float pdf_l_s = pdf_as_solid(ls.pdf_value, ls.pdf_solid, ls.cos, ls.dist * ls.dist) * sel_pdf;
+                    if (pdf_l_s > FLT_EPS_ && ls.cos > FLT_EPS_) {
+                        f3 in_dir = ls.dir;
+                        f3 kd = mk(m.kd[0], m.kd[1], m.kd[2]);
+                        float mis;
+                        if (Lt.delta) {
+                            mis = 1.0f;
+                        } else {
+                            float c = dot(in_dir, s.local.n);
+                            float pdf_e_s = (c >= 0 ? c : 0) / PI_; // cosine_hemisphere_pdf(positive_cos)
+                            mis = 1 / (1 + pdf_e_s / pdf_l_s);
+                        }
+                        float factor = ls.pdf_value / pdf_l_s;
+                        f3 ev = mulf(kd, fabsf(dot(in_dir, s.local.n)) * INV_PI_); // Lambert eval
+                        scol = handle_color(sv, mulf(mul(ls.intensity, mul(contrib, ev)), mis * factor));
+                        so = s.point;
+                        if (Lt.infinite) {
+                            sdir = in_dir;
+                            stmax = FLT_MAX_;
+                        } else {
+                            sdir = sub(ls.pos, s.point);
+                            stmax = 1 - 0.001f;
+                        }
+                        shadow = true;
+                    }
+                }
+                // on_bounce (pathtracer.art:165-200)
+                if (depth + 1 <= sv.max_depth) {
+                    BsdfSample bs = sample_bsdf(m, s, rnd, out_dir);
+                    f3 c2 = mul(contrib, bs.color);
+                    float rr = 1.0f;
+                    if (depth + 1 > sv.min_depth) {
+                        f3 e = mulf(c2, eta * eta);
+                        rr = clampf(fmaxf(fmaxf(e.x, e.y), e.z), 0.05f, 0.95f); // russian_roulette_pbrt
+                    }
+                    if (!(rnd.next_f32() >= rr)) {
+                        alive = true;
+                        ninv_pdf = specular ? 0 : 1 / bs.pdf;
+                        ncontrib = mulf(c2, 1 / rr);
+                        neta = eta * bs.eta;
+                        no = s.point;
+                        nd = bs.in_dir;
+                        ncounter = rnd.counter;
+                    }
+                }
+            }
+            if (has_l) {
+                float4 l = L[slot];
+                L[slot] = make_float4(l.x + Lacc.x, l.y + Lacc.y, l.z + Lacc.z, 0);
+            }
+        }
+        int dst = wave_append(alive, kc.cnt_out);
+        if (alive) {
+            out.p0[dst] = make_float4(no.x, no.y, no.z, __int_as_float(slot | ((depth + 1) << 24)));
+            out.p1[dst] = make_float4(nd.x, nd.y, nd.z, __uint_as_float(ncounter));
+            out.p2[dst] = make_float4(ncontrib.x, ncontrib.y, ncontrib.z, ninv_pdf);
+            out.p3[dst] = neta;
+        }
+        int sdst = wave_append(shadow, kc.cnt_shadow);
+        if (shadow) {
+            sh.s0[sdst] = make_float4(so.x, so.y, so.z, __int_as_float(slot));
+            sh.s1[sdst] = make_float4(sdir.x, sdir.y, sdir.z, stmax);
+            sh.s2[sdst] = make_float4(scol.x, scol.y, scol.z, 0);
+        }
+    }
+    if (STATS) {
+        unsigned long long a = st.nodes, b = st.leaves, c = st.tris, e = st.blas;
+        for (int off = 32; off > 0; off >>= 1) {
+            a += __shfl_down(a, off);
+            b += __shfl_down(b, off);
+            c += __shfl_down(c, off);
+            e += __shfl_down(e, off);
+        }
+        if (lane_id() == 0) {
+            atomicAdd(&kc.stats[0], a);
+            atomicAdd(&kc.stats[1], b);
+            atomicAdd(&kc.stats[2], c);
+            atomicAdd(&kc.stats[3], e);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// shadow: any-hit traversal; on miss add the NEE contribution
+// (gpu_traverse_secondary, mapping_gpu.art:70-112; on_shadow_miss, pathtracer.art:202-209)
+// ---------------------------------------------------------------------------
+template <int STACK, bool STATS>
+__global__ void __launch_bounds__(BLOCK) k_shadow(SceneView sv, ShadowBuf sh, float4* L, const int* cnt,
+                                                  unsigned long long* stats) {
+    __shared__ int stack_mem[STACK * BLOCK];
+    int* stk = stack_mem + threadIdx.x;
+    const int n = uniform_load(cnt);
+    const int total_waves = gridDim.x * (BLOCK / 64);
+    const int wave = blockIdx.x * (BLOCK / 64) + threadIdx.x / 64;
+    TraceStats st{0, 0, 0, 0};
+    for (int base = wave * 64; base < n; base += total_waves * 64) {
+        int i = base + lane_id();
+        if (i < n) {
+            float4 s0 = sh.s0[i], s1 = sh.s1[i];
+            float tmax = s1.w;
+            int e, p;
+            float u, v;
+            bool occluded = trace_ray<true, STATS>(sv, f3of(s0), f3of(s1), 0.001f, tmax, RAY_SHADOW, stk, BLOCK, e, p, u, v, st);
+            if (!occluded) {
+                int slot = __float_as_int(s0.w);
+                float4 c = sh.s2[i];
+                float4 l = L[slot];
+                L[slot] = make_float4(l.x + c.x, l.y + c.y, l.z + c.z, 0);
+            }
+        }
+    }
+    if (STATS) {
+        unsigned long long a = st.nodes, b = st.leaves, c = st.tris, e = st.blas;
+        for (int off = 32; off > 0; off >>= 1) {
+            a += __shfl_down(a, off);
+            b += __shfl_down(b, off);
+            c += __shfl_down(c, off);
+            e += __shfl_down(e, off);
+        }
+        if (lane_id() == 0) {
+            atomicAdd(&stats[4], a);
+            atomicAdd(&stats[5], b);
+            atomicAdd(&stats[6], c);
+            atomicAdd(&stats[7], e);
+        }
+    }
+}
+
+// resolve: fb += sum_s L_s / spi (driver/accumulator.art:13-19, make_standard_accumulator)
+__global__ void __launch_bounds__(BLOCK) k_resolve(FrameArgs fa, const float4* L, float* fb, int fb_width) {
+    int p = blockIdx.x * BLOCK + threadIdx.x;
+    if (p >= fa.chunk_pixels) return;
+    int x, y;
+    if (!local_to_global(fa, fa.chunk_pixel0 + p, x, y)) return;
+    float r = 0, g = 0, b = 0;
+    for (int s = 0; s < fa.spi; ++s) {
+        float4 l = L[p * fa.spi + s];
+        r += l.x * fa.inv_spi;
+        g += l.y * fa.inv_spi;
+        b += l.z * fa.inv_spi;
+    }
+    size_t o = 3 * ((size_t)y * fb_width + x);
+    fb[o + 0] += r;
+    fb[o + 1] += g;
+    fb[o + 2] += b;
+}
+
+__global__ void k_pack_tiles(FrameArgs fa, const float* fb, float* dst, int num_tiles) {
+    int T = fa.tile_size;
+    long long total = (long long)num_tiles * T * T;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+        int x, y;
+        bool in = local_to_global(fa, (int)i, x, y);
+        for (int c = 0; c < 3; ++c) dst[3 * i + c] = in ? fb[3 * ((size_t)y * fa.width + x) + c] : 0.0f;
+    }
+}
+
+// hit-level test kernels (one ray per lane)
+template <int STACK>
+__global__ void __launch_bounds__(BLOCK) k_trace_hits(SceneView sv, const float* rays, int n, uint32_t flags, int* ent_prim,
+                                                      float* tuv, int any) {
+    __shared__ int stack_mem[STACK * BLOCK];
+    int* stk = stack_mem + threadIdx.x;
+    int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const float* r = rays + 8 * i;
+    float tmax = r[7];
+    int e, p;
+    float u = 0, v = 0;
+    TraceStats st{0, 0, 0, 0};
+    if (any) {
+        bool occ = trace_ray<true, false>(sv, mk(r[0], r[1], r[2]), mk(r[3], r[4], r[5]), r[6], tmax, flags, stk, BLOCK, e, p, u, v, st);
+        ent_prim[i] = occ ? 1 : 0;
+    } else {
+        trace_ray<false, false>(sv, mk(r[0], r[1], r[2]), mk(r[3], r[4], r[5]), r[6], tmax, flags, stk, BLOCK, e, p, u, v, st);
+        ent_prim[2 * i] = e;
+        ent_prim[2 * i + 1] = p;
+        tuv[3 * i] = e >= 0 ? tmax : r[7];
+        tuv[3 * i + 1] = u;
+        tuv[3 * i + 2] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------
+template <typename T>
+struct DevArray {
+    T* ptr = nullptr;
+    size_t count = 0;
+};
+
+} // namespace
+
+struct igx_device {
+    int hip_device = 0;
+    hipStream_t stream = nullptr;
+    std::string last_error;
+    int num_cus = 256;
+    // options
+    bool timing = false;
+    bool instrument = false;
+    int64_t capacity_opt = 0;
+    int leaf_size = 4;
+    // scene
+    bool has_scene = false;
+    std::vector<void*> scene_allocs;
+    SceneView sv{};
+    igxd::DevCamera cam_base{};
+    igx_camera cam_desc{};
+    int stack_depth = 32;
+    int scene_depth = 0;
+    // streams
+    size_t capacity = 0;
+    PathBuf pa{}, pb{};
+    ShadowBuf sh{};
+    float4* L = nullptr;
+    int* counters = nullptr;          // [2*MAX_BOUNCES+4]
+    unsigned long long* dstats = nullptr;
+    int* pinned_counts = nullptr;     // host pinned mirror of counters
+    float* ray_list = nullptr;
+    size_t ray_list_cap = 0;
+    // framebuffer
+    float* fb = nullptr;
+    size_t fb_count = 0;
+    int fb_w = 0, fb_h = 0;
+    uint64_t iteration_count = 0;
+    // stats
+    igx_stats stats{};
+    std::vector<hipEvent_t> ev_pool;
+};
+
+namespace {
+
+igx_status fail(igx_device* d, igx_status s, const std::string& msg) {
+    if (d) d->last_error = msg;
+    return s;
+}
+
+#define HIPCHK(expr)                                                                                  \
+    do {                                                                                              \
+        hipError_t e_ = (expr);                                                                       \
+        if (e_ != hipSuccess)                                                                         \
+            return fail(dev, e_ == hipErrorOutOfMemory ? IGX_ERR_OUT_OF_MEMORY : IGX_ERR_HIP,         \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));                           \
+    } while (0)
+
+template <typename T>
+igx_status upload(igx_device* dev, const std::vector<T>& v, const T** out) {
+    size_t bytes = std::max<size_t>(v.size() * sizeof(T), 16);
+    void* p = nullptr;
+    HIPCHK(hipMalloc(&p, bytes));
+    dev->scene_allocs.push_back(p);
+    if (!v.empty()) HIPCHK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    *out = reinterpret_cast<const T*>(p);
+    return IGX_OK;
+}
+
+void free_scene(igx_device* dev) {
+    for (void* p : dev->scene_allocs) (void)hipFree(p);
+    dev->scene_allocs.clear();
+    dev->has_scene = false;
+}
+
+void free_streams(igx_device* dev) {
+    void* ptrs[] = {dev->pa.p0, dev->pa.p1, dev->pa.p2, dev->pa.p3, dev->pb.p0, dev->pb.p1, dev->pb.p2, dev->pb.p3,
+                    dev->sh.s0, dev->sh.s1, dev->sh.s2, dev->L};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    dev->pa = PathBuf{};
+    dev->pb = PathBuf{};
+    dev->sh = ShadowBuf{};
+    dev->L = nullptr;
+    dev->capacity = 0;
+}
+
+igx_status ensure_streams(igx_device* dev, size_t cap) {
+    if (dev->capacity >= cap) return IGX_OK;
+    free_streams(dev);
+    auto alloc4 = [&](float4** p) -> igx_status { HIPCHK(hipMalloc((void**)p, cap * sizeof(float4))); return IGX_OK; };
+    igx_status s;
+    if ((s = alloc4(&dev->pa.p0)) || (s = alloc4(&dev->pa.p1)) || (s = alloc4(&dev->pa.p2))) return s;
+    HIPCHK(hipMalloc((void**)&dev->pa.p3, cap * sizeof(float)));
+    if ((s = alloc4(&dev->pb.p0)) || (s = alloc4(&dev->pb.p1)) || (s = alloc4(&dev->pb.p2))) return s;
+    HIPCHK(hipMalloc((void**)&dev->pb.p3, cap * sizeof(float)));
+    if ((s = alloc4(&dev->sh.s0)) || (s = alloc4(&dev->sh.s1)) || (s = alloc4(&dev->sh.s2)) || (s = alloc4(&dev->L))) return s;
+    dev->capacity = cap;
+    return IGX_OK;
+}
+
+int grid_for(igx_device* dev, long long items, int blocks_per_cu) {
+    long long need = (items + BLOCK - 1) / BLOCK;
+    long long cap = (long long)dev->num_cus * blocks_per_cu;
+    return (int)std::max<long long>(1, std::min(need, cap));
+}
+
+// Launch helpers dispatching on the traversal stack depth
+template <bool STATS>
+void launch_extend(igx_device* dev, int grid, const FrameArgs& fa, const PathBuf& in, const PathBuf& out, const KernelCounters& kc) {
+    if (dev->stack_depth <= 32)
+        hipLaunchKernelGGL((k_extend<32, STATS>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, out, dev->sh, dev->L, kc);
+    else
+        hipLaunchKernelGGL((k_extend<64, STATS>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, out, dev->sh, dev->L, kc);
+}
+template <bool STATS>
+void launch_shadow(igx_device* dev, int grid, const int* cnt) {
+    if (dev->stack_depth <= 32)
+        hipLaunchKernelGGL((k_shadow<32, STATS>), dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, dev->sh, dev->L, cnt, dev->dstats);
+    else
+        hipLaunchKernelGGL((k_shadow<64, STATS>), dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, dev->sh, dev->L, cnt, dev->dstats);
+}
+
+struct TimedLaunch {
+    hipEvent_t a, b;
+    int kind; // 0 extend, 1 shadow, 2 generate, 3 resolve
+};
+
+} // namespace
+
+// ===========================================================================
+// C-ABI
+// ===========================================================================
+extern "C" const char* igx_version(void) { return "igx 0.1 (gfx950 wavefront path tracer)"; }
+
+extern "C" igx_status igx_create(int hip_device, igx_device** out) {
+    if (!out) return IGX_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    igx_device* dev = new igx_device();
+    dev->hip_device = hip_device;
+    hipError_t e = hipSetDevice(hip_device);
+    if (e != hipSuccess) {
+        delete dev;
+        return IGX_ERR_HIP;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, hip_device) == hipSuccess) dev->num_cus = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete dev;
+        return IGX_ERR_HIP;
+    }
+    if (hipMalloc((void**)&dev->counters, (2 * MAX_BOUNCES + 4) * sizeof(int)) != hipSuccess ||
+        hipMalloc((void**)&dev->dstats, 8 * sizeof(unsigned long long)) != hipSuccess ||
+        hipHostMalloc((void**)&dev->pinned_counts, (2 * MAX_BOUNCES + 4) * sizeof(int), hipHostMallocDefault) != hipSuccess) {
+        delete dev;
+        return IGX_ERR_OUT_OF_MEMORY;
+    }
+    (void)hipMemset(dev->dstats, 0, 8 * sizeof(unsigned long long));
+    *out = dev;
+    return IGX_OK;
+}
+
+extern "C" igx_status igx_destroy(igx_device* dev) {
+    if (!dev) return IGX_ERR_INVALID_ARGUMENT;
+    (void)hipSetDevice(dev->hip_device);
+    if (dev->stream) (void)hipStreamSynchronize(dev->stream);
+    free_scene(dev);
+    free_streams(dev);
+    if (dev->fb) (void)hipFree(dev->fb);
+    if (dev->counters) (void)hipFree(dev->counters);
+    if (dev->dstats) (void)hipFree(dev->dstats);
+    if (dev->pinned_counts) (void)hipHostFree(dev->pinned_counts);
+    if (dev->ray_list) (void)hipFree(dev->ray_list);
+    for (auto& e : dev->ev_pool) (void)hipEventDestroy(e);
+    if (dev->stream) (void)hipStreamDestroy(dev->stream);
+    delete dev;
+    return IGX_OK;
+}
+
+extern "C" const char* igx_last_error(const igx_device* dev) { return dev ? dev->last_error.c_str() : "null device"; }
+
+extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t value) {
+    if (!dev || !key) return IGX_ERR_INVALID_ARGUMENT;
+    std::string k(key);
+    if (k == "timing") dev->timing = value != 0;
+    else if (k == "instrument") dev->instrument = value != 0;
+    else if (k == "capacity") dev->capacity_opt = value;
+    else if (k == "bvh_leaf_size") {
+        if (value < 1 || value > 16) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "bvh_leaf_size must be in [1, 16]");
+        dev->leaf_size = (int)value;
+    } else return fail(dev, IGX_ERR_INVALID_ARGUMENT, "unknown option '" + k + "'");
+    return IGX_OK;
+}
+
+extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* desc) {
+    if (!dev || !desc) return IGX_ERR_INVALID_ARGUMENT;
+    HIPCHK(hipSetDevice(dev->hip_device));
+    HIPCHK(hipStreamSynchronize(dev->stream));
+    free_scene(dev);
+
+    // ---- BLAS per trimesh shape, analytic spheres -------------------------
+    std::vector<igx::BvhNode> nodes;
+    std::vector<float4> tris, vtx, nrm, spheres;
+    std::vector<int4> idx;
+    struct ShapeDev { int type, root, vtx_off, idx_off_or_sphere; };
+    std::vector<ShapeDev> sdev(desc->num_shapes);
+    int blas_depth = 0;
+    for (uint32_t s = 0; s < desc->num_shapes; ++s) {
+        const igx_shape& sh = desc->shapes[s];
+        if (sh.type == IGX_SHAPE_SPHERE) {
+            sdev[s] = {1, -1, 0, (int)spheres.size()};
+            spheres.push_back(make_float4(sh.sphere[0], sh.sphere[1], sh.sphere[2], sh.sphere[3]));
+            continue;
+        }
+        if (sh.mesh < 0 || (uint32_t)sh.mesh >= desc->num_meshes)
+            return fail(dev, IGX_ERR_INVALID_ARGUMENT, "shape references an invalid mesh");
+        const igx_mesh& m = desc->meshes[sh.mesh];
+        igx::BvhBuildInput bi;
+        bi.bmin.resize(3 * m.num_faces);
+        bi.bmax.resize(3 * m.num_faces);
+        bi.centroid.resize(3 * m.num_faces);
+        for (uint32_t f = 0; f < m.num_faces; ++f) {
+            for (int a = 0; a < 3; ++a) {
+                float lo = 3.4e38f, hi = -3.4e38f;
+                for (int k = 0; k < 3; ++k) {
+                    uint32_t vi = m.indices[3 * f + k];
+                    if (vi >= m.num_vertices) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "mesh index out of range");
+                    float v = m.vertices[3 * vi + a];
+                    lo = std::min(lo, v);
+                    hi = std::max(hi, v);
+                }
+                bi.bmin[3 * f + a] = lo;
+                bi.bmax[3 * f + a] = hi;
+                bi.centroid[3 * f + a] = 0.5f * (lo + hi);
+            }
+        }
+        igx::BvhBuildResult br;
+        try {
+            br = igx::build_bvh2(bi, dev->leaf_size);
+        } catch (const std::exception& ex) {
+            return fail(dev, IGX_ERR_INVALID_ARGUMENT, ex.what());
+        }
+        blas_depth = std::max(blas_depth, br.depth);
+        int node_off = (int)nodes.size();
+        int tri_off = (int)(tris.size() / 3);
+        for (auto nd : br.nodes) {
+            for (int k = 0; k < 2; ++k) {
+                if (nd.ref[k] >= 0) nd.ref[k] += node_off;
+                else if (nd.b[k * 6] <= nd.b[k * 6 + 1]) { // leaf (empty children keep ref -1)
+                    int code = ~nd.ref[k];
+                    int first = (code >> igx::kLeafCountBits) + tri_off;
+                    int count = (code & ((1 << igx::kLeafCountBits) - 1)) + 1;
+                    if (first >= (1 << 26)) return fail(dev, IGX_ERR_UNSUPPORTED, "too many triangles for the leaf encoding");
+                    nd.ref[k] = igx::encode_leaf(first, count);
+                }
+            }
+            nodes.push_back(nd);
+        }
+        for (uint32_t slot = 0; slot < br.prim_order.size(); ++slot) {
+            uint32_t f = br.prim_order[slot];
+            const uint32_t* ix = m.indices + 3 * f;
+            const float* v0 = m.vertices + 3 * ix[0];
+            const float* v1 = m.vertices + 3 * ix[1];
+            const float* v2 = m.vertices + 3 * ix[2];
+            // Tri1 (shapes/trimesh.art:107-114; TriBVHAdapter.h:148-158): e1 = v0 - v1, e2 = v2 - v0
+            float4 q0 = make_float4(v0[0], v0[1], v0[2], 0);
+            int32_t pid = (int32_t)f;
+            std::memcpy(&q0.w, &pid, 4);
+            tris.push_back(q0);
+            tris.push_back(make_float4(v0[0] - v1[0], v0[1] - v1[1], v0[2] - v1[2], 0));
+            tris.push_back(make_float4(v2[0] - v0[0], v2[1] - v0[1], v2[2] - v0[2], 0));
+        }
+        sdev[s] = {0, node_off, (int)vtx.size(), (int)idx.size()};
+        for (uint32_t v = 0; v < m.num_vertices; ++v) {
+            vtx.push_back(make_float4(m.vertices[3 * v], m.vertices[3 * v + 1], m.vertices[3 * v + 2], 0));
+            nrm.push_back(make_float4(m.normals[3 * v], m.normals[3 * v + 1], m.normals[3 * v + 2], 0));
+        }
+        for (uint32_t f = 0; f < m.num_faces; ++f)
+            idx.push_back(make_int4((int)m.indices[3 * f], (int)m.indices[3 * f + 1], (int)m.indices[3 * f + 2], 0));
+    }
+
+    // ---- TLAS over entities (leaf size 1), instance records ---------------
+    std::vector<float4> inst, ent;
+    int tlas_root = -1;
+    int tlas_depth = 0;
+    if (desc->num_entities > 0) {
+        igx::BvhBuildInput bi;
+        for (uint32_t e = 0; e < desc->num_entities; ++e) {
+            const igx_entity& en = desc->entities[e];
+            if (en.shape < 0 || (uint32_t)en.shape >= desc->num_shapes)
+                return fail(dev, IGX_ERR_INVALID_ARGUMENT, "entity references an invalid shape");
+            if (en.material < 0 || (uint32_t)en.material >= desc->num_materials)
+                return fail(dev, IGX_ERR_INVALID_ARGUMENT, "entity references an invalid material");
+            for (int a = 0; a < 3; ++a) {
+                bi.bmin.push_back(en.bbox_min[a]);
+                bi.bmax.push_back(en.bbox_max[a]);
+                bi.centroid.push_back(0.5f * (en.bbox_min[a] + en.bbox_max[a]));
+            }
+        }
+        igx::BvhBuildResult br = igx::build_bvh2(bi, 1);
+        tlas_depth = br.depth;
+        int node_off = (int)nodes.size();
+        for (auto nd : br.nodes) {
+            for (int k = 0; k < 2; ++k)
+                if (nd.ref[k] >= 0) nd.ref[k] += node_off;
+            nodes.push_back(nd);
+        }
+        tlas_root = node_off;
+        for (uint32_t slot = 0; slot < br.prim_order.size(); ++slot) {
+            uint32_t e = br.prim_order[slot];
+            const igx_entity& en = desc->entities[e];
+            const ShapeDev& sd = sdev[en.shape];
+            for (int r = 0; r < 3; ++r)
+                inst.push_back(make_float4(en.to_local[r * 4 + 0], en.to_local[r * 4 + 1], en.to_local[r * 4 + 2], en.to_local[r * 4 + 3]));
+            int4 info = make_int4((int)e, sd.type, sd.type == 1 ? sd.idx_off_or_sphere : sd.root, (int)en.flags);
+            float4 fi;
+            std::memcpy(&fi, &info, 16);
+            inst.push_back(fi);
+        }
+        for (uint32_t e = 0; e < desc->num_entities; ++e) {
+            const igx_entity& en = desc->entities[e];
+            const ShapeDev& sd = sdev[en.shape];
+            for (int r = 0; r < 3; ++r)
+                ent.push_back(make_float4(en.to_global[r * 4 + 0], en.to_global[r * 4 + 1], en.to_global[r * 4 + 2], en.to_global[r * 4 + 3]));
+            for (int r = 0; r < 3; ++r) ent.push_back(make_float4(en.normal[r * 3 + 0], en.normal[r * 3 + 1], en.normal[r * 3 + 2], 0));
+            int4 info = make_int4(sd.type, en.material, sd.vtx_off, sd.idx_off_or_sphere);
+            float4 fi;
+            std::memcpy(&fi, &info, 16);
+            ent.push_back(fi);
+        }
+    }
+
+    // ---- materials and lights (infinite lights first) --------------------
+    std::vector<int> light_remap(desc->num_lights, -1);
+    std::vector<DevLight> lights;
+    for (int pass = 0; pass < 2; ++pass)
+        for (uint32_t l = 0; l < desc->num_lights; ++l) {
+            const igx_light& L = desc->lights[l];
+            bool infinite = L.type == IGX_LIGHT_ENV;
+            if ((pass == 0) != infinite) continue;
+            DevLight d{};
+            d.type = L.type;
+            d.infinite = infinite ? 1 : 0;
+            d.delta = (L.type == IGX_LIGHT_POINT || L.type == IGX_LIGHT_SPOT) ? 1 : 0;
+            for (int i = 0; i < 3; ++i) d.radiance[i] = L.radiance[i];
+            if (L.type == IGX_LIGHT_PLANE) {
+                // make_plane_area_emitter constants (light/area.art:107-115)
+                float xa[3] = {L.x_axis[0], L.x_axis[1], L.x_axis[2]};
+                float ya[3] = {L.y_axis[0], L.y_axis[1], L.y_axis[2]};
+                float width = std::sqrt(xa[0] * xa[0] + xa[1] * xa[1] + xa[2] * xa[2]);
+                float height = std::sqrt(ya[0] * ya[0] + ya[1] * ya[1] + ya[2] * ya[2]);
+                float iw = 1 / width, ih = 1 / height;
+                for (int i = 0; i < 3; ++i) {
+                    d.origin[i] = L.origin[i];
+                    d.ex[i] = xa[i] * iw;
+                    d.ey[i] = ya[i] * ih;
+                    d.normal[i] = L.normal[i];
+                }
+                d.origin[3] = width;
+                d.ex[3] = height;
+                d.ey[3] = 1 / L.area;
+                d.normal[3] = L.area;
+            } else if (L.type == IGX_LIGHT_POINT) {
+                for (int i = 0; i < 3; ++i) d.origin[i] = L.origin[i];
+            } else if (L.type == IGX_LIGHT_SPOT) {
+                for (int i = 0; i < 3; ++i) { d.origin[i] = L.origin[i]; d.normal[i] = L.normal[i]; }
+                float cc = std::cos(L.cutoff), cf = std::cos(L.falloff);
+                d.spot[0] = cc;
+                d.spot[1] = cf;
+                d.spot[2] = cf - cc;
+            } else if (L.type != IGX_LIGHT_ENV) {
+                return fail(dev, IGX_ERR_UNSUPPORTED, "unsupported light type");
+            }
+            light_remap[l] = (int)lights.size();
+            lights.push_back(d);
+        }
+    int num_infinite = 0;
+    for (auto& l : lights) num_infinite += l.infinite;
+    std::vector<DevMaterial> mats(desc->num_materials);
+    for (uint32_t i = 0; i < desc->num_materials; ++i) {
+        const igx_material& m = desc->materials[i];
+        DevMaterial d{};
+        d.type = m.bsdf_type == IGX_BSDF_DIELECTRIC ? MAT_DIELECTRIC : MAT_DIFFUSE;
+        if (m.bsdf_type == IGX_BSDF_DIELECTRIC && m.thin) return fail(dev, IGX_ERR_UNSUPPORTED, "thin dielectric is not supported");
+        d.light = m.light >= 0 && (uint32_t)m.light < desc->num_lights ? light_remap[m.light] : -1;
+        for (int c = 0; c < 3; ++c) { d.kd[c] = m.kd[c]; d.ks[c] = m.ks[c]; d.kt[c] = m.kt[c]; }
+        d.ks[3] = m.ext_ior;
+        d.kt[3] = m.int_ior;
+        mats[i] = d;
+    }
+
+    // ---- upload ----------------------------------------------------------
+    std::vector<float4> node4(nodes.size() * 4);
+    if (!nodes.empty()) std::memcpy(node4.data(), nodes.data(), nodes.size() * 64);
+    SceneView sv{};
+    igx_status st;
+    if ((st = upload(dev, node4, &sv.nodes)) || (st = upload(dev, tris, &sv.tris)) || (st = upload(dev, inst, &sv.inst)) ||
+        (st = upload(dev, spheres, &sv.spheres)) || (st = upload(dev, ent, &sv.ent)) || (st = upload(dev, vtx, &sv.vtx)) ||
+        (st = upload(dev, nrm, &sv.nrm)) || (st = upload(dev, idx, &sv.idx)) || (st = upload(dev, mats, &sv.mats)) ||
+        (st = upload(dev, lights, &sv.lights))) {
+        free_scene(dev);
+        return st;
+    }
+    sv.tlas_root = tlas_root;
+    sv.num_lights = (int)lights.size();
+    sv.num_infinite = num_infinite;
+    // bbox_radius(scene_bbox) * 1.01 (light/env.art:75; core/bbox.art:24)
+    float dx = desc->scene_bbox_max[0] - desc->scene_bbox_min[0];
+    float dy = desc->scene_bbox_max[1] - desc->scene_bbox_min[1];
+    float dz = desc->scene_bbox_max[2] - desc->scene_bbox_min[2];
+    sv.scene_radius = std::sqrt(dx * dx + dy * dy + dz * dz) / 2 * 1.01f;
+    sv.max_depth = desc->technique.max_depth;
+    sv.min_depth = desc->technique.min_depth;
+    sv.nee = desc->technique.nee;
+    sv.clamp = desc->technique.clamp;
+    dev->cam_desc = desc->camera;
+    dev->sv = sv;
+    // stack: TLAS depth + BLAS depth + marker + exit sentinel
+    dev->scene_depth = tlas_depth + blas_depth + 2;
+    if (dev->scene_depth > 64) {
+        free_scene(dev);
+        return fail(dev, IGX_ERR_UNSUPPORTED, "BVH too deep for the 64-entry LDS stack (depth " + std::to_string(dev->scene_depth) + ")");
+    }
+    dev->stack_depth = dev->scene_depth <= 32 ? 32 : 64;
+    dev->has_scene = true;
+    return IGX_OK;
+}
+
+static void setup_camera(igx_device* dev, int width, int height) {
+    // make_perspective_camera (camera/perspective.art:29-42), compute_scale_from_{h,v}fov (:2-14)
+    const igx_camera& c = dev->cam_desc;
+    DevCamera& k = dev->sv.cam;
+    float aspect = c.aspect > 0 ? c.aspect : (float)width / (float)height;
+    if (c.vertical_fov) {
+        k.scale_y = std::tan(c.fov / 2);
+        k.scale_x = k.scale_y * aspect;
+    } else {
+        k.scale_x = std::tan(c.fov / 2);
+        k.scale_y = k.scale_x / aspect;
+    }
+    float dir[3] = {c.dir[0], c.dir[1], c.dir[2]}, up[3] = {c.up[0], c.up[1], c.up[2]};
+    float r[3] = {dir[1] * up[2] - dir[2] * up[1], dir[2] * up[0] - dir[0] * up[2], dir[0] * up[1] - dir[1] * up[0]};
+    float rl = std::sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
+    float irl = 1 / rl;
+    for (int i = 0; i < 3; ++i) {
+        k.eye[i] = c.eye[i];
+        k.dir[i] = dir[i];
+        k.up[i] = up[i];
+        k.right[i] = r[i] * irl;
+    }
+    k.tmin = c.near_clip;
+    k.tmax = c.far_clip;
+}
+
+extern "C" igx_status igx_render(igx_device* dev, const igx_render_params* p) {
+    if (!dev || !p) return IGX_ERR_INVALID_ARGUMENT;
+    if (!dev->has_scene) return fail(dev, IGX_ERR_NO_SCENE, "no scene uploaded");
+    if (p->spi < 1) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "spi must be >= 1");
+    auto t_start = std::chrono::steady_clock::now();
+    HIPCHK(hipSetDevice(dev->hip_device));
+    const bool list_mode = p->num_rays > 0;
+    int width = list_mode ? p->num_rays : p->width;
+    int height = list_mode ? 1 : p->height;
+    if (width < 1 || height < 1) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "film size must be positive");
+    if (p->tile_size > 0 && (p->tile_stride < 1 || p->tile_offset < 0 || p->tile_offset >= p->tile_stride))
+        return fail(dev, IGX_ERR_INVALID_ARGUMENT, "invalid tile sharding parameters");
+    if (list_mode && p->tile_size > 0) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "ray-list mode cannot be tile-sharded");
+
+    // framebuffer (resize clears, as Device::resize)
+    size_t fbc = (size_t)width * height * 3;
+    if (dev->fb_w != width || dev->fb_h != height || !dev->fb) {
+        if (dev->fb) HIPCHK(hipFree(dev->fb));
+        dev->fb = nullptr;
+        HIPCHK(hipMalloc((void**)&dev->fb, fbc * sizeof(float)));
+        HIPCHK(hipMemsetAsync(dev->fb, 0, fbc * sizeof(float), dev->stream));
+        dev->fb_w = width;
+        dev->fb_h = height;
+        dev->fb_count = fbc;
+        dev->iteration_count = 0;
+    }
+    setup_camera(dev, width, height);
+
+    FrameArgs fa{};
+    fa.width = width;
+    fa.height = height;
+    fa.spi = p->spi;
+    fa.iter = p->iteration;
+    fa.frame = p->frame;
+    fa.seed = p->seed;
+    fa.inv_spi = 1.0f / (float)p->spi;
+    long long local_pixels;
+    if (list_mode) {
+        size_t need = (size_t)p->num_rays * 8;
+        if (dev->ray_list_cap < need) {
+            if (dev->ray_list) HIPCHK(hipFree(dev->ray_list));
+            HIPCHK(hipMalloc((void**)&dev->ray_list, need * sizeof(float)));
+            dev->ray_list_cap = need;
+        }
+        HIPCHK(hipMemcpyAsync(dev->ray_list, p->rays, need * sizeof(float), hipMemcpyHostToDevice, dev->stream));
+        fa.num_rays = p->num_rays;
+        fa.rays = dev->ray_list;
+        local_pixels = p->num_rays;
+    } else if (p->tile_size > 0) {
+        fa.tile_size = p->tile_size;
+        fa.tile_offset = p->tile_offset;
+        fa.tile_stride = p->tile_stride;
+        fa.tiles_x = (width + p->tile_size - 1) / p->tile_size;
+        int tiles_y = (height + p->tile_size - 1) / p->tile_size;
+        int tiles = fa.tiles_x * tiles_y;
+        int mine = tiles > p->tile_offset ? (tiles - p->tile_offset + p->tile_stride - 1) / p->tile_stride : 0;
+        local_pixels = (long long)mine * p->tile_size * p->tile_size;
+    } else {
+        local_pixels = (long long)width * height;
+    }
+    // capacity: whole iteration resident when it fits (<= 16M paths), pixel aligned
+    long long total_paths = local_pixels * p->spi;
+    long long cap = dev->capacity_opt > 0 ? dev->capacity_opt : std::min<long long>(total_paths, 1ll << 24);
+    cap = std::min<long long>(cap, (1ll << 24) - 1);
+    cap = std::max<long long>(p->spi, (cap / p->spi) * p->spi);
+    if (total_paths == 0) {
+        dev->iteration_count++;
+        return IGX_OK;
+    }
+    igx_status st = ensure_streams(dev, (size_t)std::min<long long>(cap, total_paths));
+    if (st != IGX_OK) return st;
+    const long long chunk_pixels_max = std::min<long long>(cap, total_paths) / p->spi;
+
+    int max_bounces = std::min(std::max(dev->sv.max_depth, 1), MAX_BOUNCES - 1);
+    std::vector<TimedLaunch> timed;
+    auto ev = [&](size_t k) -> hipEvent_t {
+        while (dev->ev_pool.size() <= k) {
+            hipEvent_t e;
+            (void)hipEventCreate(&e);
+            dev->ev_pool.push_back(e);
+        }
+        return dev->ev_pool[k];
+    };
+    size_t ev_next = 0;
+    auto begin_timed = [&](int kind) {
+        if (!dev->timing) return;
+        TimedLaunch t{ev(ev_next), ev(ev_next + 1), kind};
+        ev_next += 2;
+        (void)hipEventRecord(t.a, dev->stream);
+        timed.push_back(t);
+    };
+    auto end_timed = [&]() {
+        if (!dev->timing) return;
+        (void)hipEventRecord(timed.back().b, dev->stream);
+    };
+    const int ext_grid_cap = 8;  // blocks per CU for the persistent loops
+
+    for (long long px0 = 0; px0 < local_pixels; px0 += chunk_pixels_max) {
+        int chunk_pixels = (int)std::min<long long>(chunk_pixels_max, local_pixels - px0);
+        fa.chunk_pixel0 = (int)px0;
+        fa.chunk_pixels = chunk_pixels;
+        long long n = (long long)chunk_pixels * p->spi;
+        int* cnt = dev->counters;              // cnt[b]: paths entering bounce b
+        int* scnt = dev->counters + MAX_BOUNCES; // scnt[b]: shadow rays of bounce b
+        HIPCHK(hipMemsetAsync(dev->counters, 0, (2 * MAX_BOUNCES + 4) * sizeof(int), dev->stream));
+        begin_timed(2);
+        hipLaunchKernelGGL(k_generate, dim3(grid_for(dev, n, ext_grid_cap)), dim3(BLOCK), 0, dev->stream, fa, dev->sv, dev->pa,
+                           dev->L, cnt);
+        end_timed();
+        HIPCHK(hipGetLastError());
+        PathBuf in = dev->pa, out = dev->pb;
+        int grid = grid_for(dev, n, ext_grid_cap);
+        // bounce loop; the host stops launching once a bounce two steps back
+        // produced no paths (counts read asynchronously, no per-bounce sync)
+        std::vector<hipEvent_t> bounce_ev;
+        int launched = 0;
+        for (int b = 0; b < max_bounces; ++b) {
+            if (b >= 2) {
+                HIPCHK(hipEventSynchronize(bounce_ev[b - 2]));
+                if (dev->pinned_counts[b - 1] == 0) break; // paths entering bounce b-1 was zero
+            }
+            KernelCounters kc{cnt + b, cnt + b + 1, scnt + b, dev->dstats};
+            begin_timed(0);
+            if (dev->instrument) launch_extend<true>(dev, grid, fa, in, out, kc);
+            else launch_extend<false>(dev, grid, fa, in, out, kc);
+            end_timed();
+            begin_timed(1);
+            if (dev->instrument) launch_shadow<true>(dev, grid, scnt + b);
+            else launch_shadow<false>(dev, grid, scnt + b);
+            end_timed();
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipMemcpyAsync(dev->pinned_counts + b + 1, cnt + b + 1, sizeof(int), hipMemcpyDeviceToHost, dev->stream));
+            hipEvent_t e = ev(ev_next++);
+            (void)hipEventRecord(e, dev->stream);
+            bounce_ev.push_back(e);
+            std::swap(in, out);
+            ++launched;
+        }
+        begin_timed(3);
+        hipLaunchKernelGGL(k_resolve, dim3((chunk_pixels + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, dev->stream, fa, dev->L, dev->fb, width);
+        end_timed();
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(dev->pinned_counts, dev->counters, (2 * MAX_BOUNCES + 4) * sizeof(int), hipMemcpyDeviceToHost, dev->stream));
+        HIPCHK(hipStreamSynchronize(dev->stream));
+        // ray statistics (Statistics.h:56-63; shadow = valid shadow rays only)
+        dev->stats.camera_rays += (uint64_t)dev->pinned_counts[0];
+        for (int b = 1; b <= launched; ++b) dev->stats.bounce_rays += (uint64_t)dev->pinned_counts[b];
+        for (int b = 0; b < launched; ++b) dev->stats.shadow_rays += (uint64_t)dev->pinned_counts[MAX_BOUNCES + b];
+        dev->stats.launches_extend += (uint64_t)launched;
+        dev->stats.launches_shadow += (uint64_t)launched;
+    }
+    if (dev->timing) {
+        for (auto& t : timed) {
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, t.a, t.b);
+            if (t.kind == 0) dev->stats.ms_extend += ms;
+            else if (t.kind == 1) dev->stats.ms_shadow += ms;
+            else if (t.kind == 2) dev->stats.ms_generate += ms;
+            else dev->stats.ms_resolve += ms;
+        }
+    }
+    dev->iteration_count++;
+    dev->stats.iterations++;
+    dev->stats.ms_render += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    return IGX_OK;
+}
+
+extern "C" igx_status igx_get_framebuffer(igx_device* dev, float* host_rgb, size_t count, uint64_t* iteration_count) {
+    if (!dev) return IGX_ERR_INVALID_ARGUMENT;
+    if (iteration_count) *iteration_count = dev->iteration_count;
+    if (!host_rgb) return IGX_OK;
+    if (!dev->fb) {
+        std::memset(host_rgb, 0, count * sizeof(float));
+        return IGX_OK;
+    }
+    if (count != dev->fb_count) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "framebuffer size mismatch: expected " + std::to_string(dev->fb_count));
+    HIPCHK(hipSetDevice(dev->hip_device));
+    HIPCHK(hipMemcpyAsync(host_rgb, dev->fb, count * sizeof(float), hipMemcpyDeviceToHost, dev->stream));
+    HIPCHK(hipStreamSynchronize(dev->stream));
+    return IGX_OK;
+}
+
+extern "C" igx_status igx_framebuffer_device_ptr(igx_device* dev, float** ptr, size_t* count) {
+    if (!dev || !ptr) return IGX_ERR_INVALID_ARGUMENT;
+    *ptr = dev->fb;
+    if (count) *count = dev->fb_count;
+    return IGX_OK;
+}
+
+extern "C" igx_status igx_pack_tiles(igx_device* dev, const igx_render_params* p, float* dst, size_t count) {
+    if (!dev || !p || !dst || p->tile_size <= 0) return IGX_ERR_INVALID_ARGUMENT;
+    if (!dev->fb) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "no framebuffer");
+    FrameArgs fa{};
+    fa.width = p->width;
+    fa.height = p->height;
+    fa.tile_size = p->tile_size;
+    fa.tile_offset = p->tile_offset;
+    fa.tile_stride = p->tile_stride;
+    fa.tiles_x = (p->width + p->tile_size - 1) / p->tile_size;
+    int tiles_y = (p->height + p->tile_size - 1) / p->tile_size;
+    int tiles = fa.tiles_x * tiles_y;
+    int mine = tiles > p->tile_offset ? (tiles - p->tile_offset + p->tile_stride - 1) / p->tile_stride : 0;
+    size_t need = (size_t)mine * p->tile_size * p->tile_size * 3;
+    if (count < need) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "pack buffer too small, need " + std::to_string(need));
+    HIPCHK(hipSetDevice(dev->hip_device));
+    hipLaunchKernelGGL(k_pack_tiles, dim3(1024), dim3(256), 0, dev->stream, fa, dev->fb, dst, mine);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(dev->stream));
+    return IGX_OK;
+}
+
+extern "C" igx_status igx_clear(igx_device* dev) {
+    if (!dev) return IGX_ERR_INVALID_ARGUMENT;
+    if (dev->fb) {
+        HIPCHK(hipSetDevice(dev->hip_device));
+        HIPCHK(hipMemsetAsync(dev->fb, 0, dev->fb_count * sizeof(float), dev->stream));
+        HIPCHK(hipStreamSynchronize(dev->stream));
+    }
+    dev->iteration_count = 0;
+    return IGX_OK;
+}
+
+extern "C" igx_status igx_get_stats(igx_device* dev, igx_stats* out) {
+    if (!dev || !out) return IGX_ERR_INVALID_ARGUMENT;
+    *out = dev->stats;
+    unsigned long long h[8] = {0};
+    HIPCHK(hipSetDevice(dev->hip_device));
+    HIPCHK(hipMemcpy(h, dev->dstats, sizeof(h), hipMemcpyDeviceToHost));
+    out->node_visits = h[0];
+    out->leaf_visits = h[1];
+    out->tri_tests = h[2];
+    out->blas_enters = h[3];
+    out->shadow_node_visits = h[4];
+    out->shadow_leaf_visits = h[5];
+    out->shadow_tri_tests = h[6];
+    out->shadow_blas_enters = h[7];
+    return IGX_OK;
+}
+
+extern "C" igx_status igx_reset_stats(igx_device* dev) {
+    if (!dev) return IGX_ERR_INVALID_ARGUMENT;
+    dev->stats = igx_stats{};
+    HIPCHK(hipSetDevice(dev->hip_device));
+    HIPCHK(hipMemset(dev->dstats, 0, 8 * sizeof(unsigned long long)));
+    return IGX_OK;
+}
+
+static igx_status trace_batch(igx_device* dev, const float* rays, int32_t n, uint32_t flags, int32_t* ent_prim, float* tuv, int any) {
+    if (!dev || (n > 0 && (!rays || !ent_prim))) return IGX_ERR_INVALID_ARGUMENT;
+    if (!dev->has_scene) return fail(dev, IGX_ERR_NO_SCENE, "no scene uploaded");
+    if (n <= 0) return IGX_OK;
+    HIPCHK(hipSetDevice(dev->hip_device));
+    float *d_rays = nullptr, *d_tuv = nullptr;
+    int* d_ep = nullptr;
+    HIPCHK(hipMalloc((void**)&d_rays, (size_t)n * 8 * sizeof(float)));
+    HIPCHK(hipMalloc((void**)&d_ep, (size_t)n * 2 * sizeof(int)));
+    HIPCHK(hipMalloc((void**)&d_tuv, (size_t)n * 3 * sizeof(float)));
+    HIPCHK(hipMemcpy(d_rays, rays, (size_t)n * 8 * sizeof(float), hipMemcpyHostToDevice));
+    int grid = (n + BLOCK - 1) / BLOCK;
+    if (dev->stack_depth <= 32)
+        hipLaunchKernelGGL(k_trace_hits<32>, dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, d_rays, n, flags, d_ep, d_tuv, any);
+    else
+        hipLaunchKernelGGL(k_trace_hits<64>, dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, d_rays, n, flags, d_ep, d_tuv, any);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(dev->stream));
+    HIPCHK(hipMemcpy(ent_prim, d_ep, (size_t)n * (any ? 1 : 2) * sizeof(int), hipMemcpyDeviceToHost));
+    if (!any && tuv) HIPCHK(hipMemcpy(tuv, d_tuv, (size_t)n * 3 * sizeof(float), hipMemcpyDeviceToHost));
+    (void)hipFree(d_rays);
+    (void)hipFree(d_ep);
+    (void)hipFree(d_tuv);
+    return IGX_OK;
+}
+
+extern "C" igx_status igx_trace_hits(igx_device* dev, const float* rays, int32_t n, uint32_t flags, int32_t* ent_prim, float* tuv) {
+    return trace_batch(dev, rays, n, flags, ent_prim, tuv, 0);
+}
+
+extern "C" igx_status igx_trace_occlusion(igx_device* dev, const float* rays, int32_t n, uint32_t flags, int32_t* occluded) {
+    return trace_batch(dev, rays, n, flags, occluded, nullptr, 1);
+}

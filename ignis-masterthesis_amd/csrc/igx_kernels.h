@@ -1,0 +1,482 @@
+// Kernel-side building blocks: traversal, surface elements, BSDFs, lights and
+// the path-tracer technique.  Restates (per function comment) the Artic code
+// the reference JIT-specialises into its GPU kernels:
+//   traversal/mapping_gpu.art, traversal/intersection.art, shapes/trimesh.art,
+//   shapes/sphere.art, bsdf/diffuse.art, bsdf/dielectric.art, light/*.art,
+//   technique/pathtracer.art.
+#pragma once
+
+#include "device_math.h"
+#include "device_scene.h"
+
+namespace igxd {
+
+struct SceneView {
+    const float4* nodes;   // unified BVH2 node array: every BLAS, then the TLAS
+    const float4* tris;    // 3 x float4 per triangle slot: (v0, prim id), (e1 = v0-v1), (e2 = v2-v0)
+    const float4* inst;    // 4 x float4 per TLAS leaf slot (see device_scene.h)
+    const float4* spheres; // origin.xyz, radius
+    const float4* ent;     // ENT_STRIDE x float4 per entity
+    const float4* vtx;     // mesh vertices (object space)
+    const float4* nrm;     // mesh vertex normals (object space)
+    const int4* idx;       // faces: local vertex indices
+    const DevMaterial* mats;
+    const DevLight* lights;
+    int tlas_root;         // -1: no entities
+    int num_lights;        // infinite lights first (light/light_selector.art:26-44)
+    int num_infinite;
+    float scene_radius;    // bbox_radius(scene_bbox) * 1.01 (light/env.art:75)
+    DevCamera cam;
+    int max_depth, min_depth, nee;
+    float clamp;
+};
+
+struct TraceStats {
+    uint32_t nodes, leaves, tris, blas;
+};
+
+// Ray flags (traversal/ray.art:19-23)
+constexpr uint32_t RAY_CAMERA = 0x1, RAY_LIGHT = 0x2, RAY_BOUNCE = 0x4, RAY_SHADOW = 0x8, RAY_TYPE_MASK = 0xF;
+
+// ---------------------------------------------------------------------------
+// Two-level traversal: TLAS (entities) -> BLAS (triangles) or analytic sphere.
+// One loop for both levels with a per-lane stack in LDS (column layout: entry
+// k of lane l at stk[k * stride], conflict-free).  Follows gpu_traverse_scene /
+// gpu_traverse_helper / gpu_traverse_prim (traversal/mapping_gpu.art:73-226):
+// slab test intersect_ray_box with ray.tmin folded in (intersection.art:170-181),
+// nearer child first, tmax shrinks on every accepted hit, entity-local rays are
+// NOT renormalised so t stays global (ray.art:53-59), entity visibility flags
+// (ray.art:51), Moeller-Trumbore with -eps barycentric tolerance and u,v clamp
+// (intersection.art:71-101), analytic sphere (shapes/sphere.art:104-130).
+// ---------------------------------------------------------------------------
+template <bool ANY, bool STATS>
+__device__ __forceinline__ bool trace_ray(const SceneView& sv, f3 o, f3 d, float tmin, float& tmax, uint32_t rflags,
+                                          int* stk, int stride, int& hit_ent, int& hit_prim, float& hu, float& hv,
+                                          TraceStats& st) {
+    hit_ent = -1;
+    hit_prim = -1;
+    if (sv.tlas_root < 0) return false;
+
+    // level ray (world at the TLAS, entity-local inside a BLAS)
+    f3 lo = o, ld = d;
+    f3 idir = mk(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
+    f3 iorg = mk(-(o.x * idir.x), -(o.y * idir.y), -(o.z * idir.z));
+    const f3 w_idir = idir, w_iorg = iorg;
+    int cur_ent = -1;
+    bool in_blas = false;
+    bool found = false;
+
+    int sp = 0;
+    stk[0] = REF_EXIT;
+    sp = 1;
+    int node = sv.tlas_root;
+
+    while (true) {
+        // ---- inner nodes -------------------------------------------------
+        while (node >= 0) {
+            if (STATS) st.nodes++;
+            const float4* np = sv.nodes + 4 * node;
+            float4 a = np[0], b = np[1], c = np[2];
+            int4 r = *reinterpret_cast<const int4*>(np + 3);
+            // child 0 box: lo (a.x, a.z, b.x) hi (a.y, a.w, b.y)
+            float t0x = a.x * idir.x + iorg.x, t1x = a.y * idir.x + iorg.x;
+            float t0y = a.z * idir.y + iorg.y, t1y = a.w * idir.y + iorg.y;
+            float t0z = b.x * idir.z + iorg.z, t1z = b.y * idir.z + iorg.z;
+            float en0 = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), tmin));
+            float ex0 = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), tmax));
+            // child 1 box: lo (b.z, c.x, c.z) hi (b.w, c.y, c.w)
+            float s0x = b.z * idir.x + iorg.x, s1x = b.w * idir.x + iorg.x;
+            float s0y = c.x * idir.y + iorg.y, s1y = c.y * idir.y + iorg.y;
+            float s0z = c.z * idir.z + iorg.z, s1z = c.w * idir.z + iorg.z;
+            float en1 = fmaxf(fmaxf(fminf(s0x, s1x), fminf(s0y, s1y)), fmaxf(fminf(s0z, s1z), tmin));
+            float ex1 = fminf(fminf(fmaxf(s0x, s1x), fmaxf(s0y, s1y)), fminf(fmaxf(s0z, s1z), tmax));
+            bool h0 = en0 <= ex0, h1 = en1 <= ex1;
+            if (h0 && h1) {
+                bool first0 = en0 < en1;
+                node = first0 ? r.x : r.y;
+                stk[sp * stride] = first0 ? r.y : r.x;
+                ++sp;
+            } else if (h0) {
+                node = r.x;
+            } else if (h1) {
+                node = r.y;
+            } else {
+                node = stk[(--sp) * stride];
+            }
+        }
+        // ---- leaves, markers, exit ---------------------------------------
+        if (node == REF_EXIT) break;
+        if (node == REF_MARKER) {
+            // back from a BLAS: restore the world ray
+            lo = o; ld = d; idir = w_idir; iorg = w_iorg;
+            in_blas = false;
+            node = stk[(--sp) * stride];
+            continue;
+        }
+        int code = ~node;
+        int first = code >> LEAF_COUNT_BITS;
+        int count = (code & ((1 << LEAF_COUNT_BITS) - 1)) + 1;
+        if (!in_blas) {
+            // TLAS leaf: entity instances
+            int next = 0;
+            bool entered = false;
+            for (int k = 0; k < count; ++k) {
+                if (STATS) st.leaves++;
+                const float4* ip = sv.inst + 4 * (first + k);
+                int4 info = *reinterpret_cast<const int4*>(ip + 3);
+                uint32_t ef = (uint32_t)info.w;
+                if ((rflags & RAY_TYPE_MASK) != ((rflags & ef) & RAY_TYPE_MASK)) continue; // check_ray_visibility
+                float4 m0 = ip[0], m1 = ip[1], m2 = ip[2];
+                // transform_ray (ray.art:53-59): point and direction, no renormalisation
+                f3 lo2 = mk(m0.x * o.x + m0.y * o.y + m0.z * o.z + m0.w,
+                            m1.x * o.x + m1.y * o.y + m1.z * o.z + m1.w,
+                            m2.x * o.x + m2.y * o.y + m2.z * o.z + m2.w);
+                f3 ld2 = mk(m0.x * d.x + m0.y * d.y + m0.z * d.z,
+                            m1.x * d.x + m1.y * d.y + m1.z * d.z,
+                            m2.x * d.x + m2.y * d.y + m2.z * d.z);
+                if (info.y == 1) {
+                    // analytic sphere in entity space (intersect_sphere, shapes/sphere.art:104-130)
+                    float4 sph = sv.spheres[info.z];
+                    f3 L = sub(lo2, f3of(sph));
+                    float S = -dot(L, ld2);
+                    float D2 = dot(ld2, ld2);
+                    float L2 = dot(L, L);
+                    float R2 = sph.w * sph.w * D2;
+                    float M2 = L2 * D2 - S * S;
+                    if (!(S < 0 || M2 > R2)) {
+                        float Q = sqrtf(R2 - M2);
+                        float ta = (S - Q) / D2, tb = (S + Q) / D2;
+                        float t0 = ta > tb ? tb : ta, t1 = ta > tb ? ta : tb;
+                        float th = t0 < tmin ? t1 : t0;
+                        if (th >= tmin && th <= tmax) {
+                            tmax = th;
+                            hit_ent = info.x;
+                            hit_prim = 0;
+                            // prim coords are only texture coordinates for spheres; not needed downstream
+                            hu = 0; hv = 0;
+                            found = true;
+                            if (ANY) return true;
+                        }
+                    }
+                } else {
+                    if (STATS) st.blas++;
+                    // enter the BLAS (count == 1 for TLAS leaves built here)
+                    lo = lo2; ld = ld2;
+                    idir = mk(safe_rcp(ld.x), safe_rcp(ld.y), safe_rcp(ld.z));
+                    iorg = mk(-(lo.x * idir.x), -(lo.y * idir.y), -(lo.z * idir.z));
+                    cur_ent = info.x;
+                    in_blas = true;
+                    next = info.z;
+                    entered = true;
+                    break;
+                }
+            }
+            if (entered) {
+                stk[sp * stride] = REF_MARKER;
+                ++sp;
+                node = next;
+            } else {
+                node = stk[(--sp) * stride];
+            }
+        } else {
+            // BLAS leaf: triangles (make_gpu_tri_prim, shapes/trimesh.art:124-160)
+            for (int k = 0; k < count; ++k) {
+                if (STATS) st.tris++;
+                const float4* tp = sv.tris + 3 * (first + k);
+                float4 q0 = tp[0], q1 = tp[1], q2 = tp[2];
+                f3 v0 = f3of(q0), e1 = f3of(q1), e2 = f3of(q2);
+                f3 n = cross(e1, e2);
+                f3 cc = sub(v0, lo);
+                f3 rr = cross(ld, cc);
+                float det = dot(n, ld);
+                float inv_det = 1.0f / det;
+                float u = dot(rr, e2) * inv_det;
+                float v = dot(rr, e1) * inv_det;
+                float w = 1 - u - v;
+                bool ok = u >= -FLT_EPS_ && v >= -FLT_EPS_ && w >= -FLT_EPS_;
+                if (ok) {
+                    float t = dot(cc, n) * inv_det;
+                    if (t >= tmin && t <= tmax) {
+                        tmax = t;
+                        hit_ent = cur_ent;
+                        hit_prim = __float_as_int(q0.w);
+                        hu = u > 0 ? u : 0;
+                        hv = v > 0 ? v : 0;
+                        found = true;
+                        if (ANY) return true;
+                    }
+                }
+            }
+            node = stk[(--sp) * stride];
+        }
+    }
+    return found;
+}
+
+// ---------------------------------------------------------------------------
+// Surface element (shapes/trimesh.art:14-39, shapes/sphere.art:50-64)
+// ---------------------------------------------------------------------------
+struct Surface {
+    f3 point;
+    f3 face_normal;
+    Frame local;
+    bool entering;
+};
+
+__device__ __forceinline__ f3 xform_point_rows(float4 r0, float4 r1, float4 r2, f3 p) {
+    return mk(r0.x * p.x + r0.y * p.y + r0.z * p.z + r0.w, r1.x * p.x + r1.y * p.y + r1.z * p.z + r1.w,
+              r2.x * p.x + r2.y * p.y + r2.z * p.z + r2.w);
+}
+__device__ __forceinline__ f3 xform_dir_rows(float4 r0, float4 r1, float4 r2, f3 p) {
+    return mk(r0.x * p.x + r0.y * p.y + r0.z * p.z, r1.x * p.x + r1.y * p.y + r1.z * p.z,
+              r2.x * p.x + r2.y * p.y + r2.z * p.z);
+}
+
+__device__ __forceinline__ Surface surface_element(const SceneView& sv, int ent_id, int prim, float t, float hu, float hv,
+                                                   f3 ro, f3 rd, int& material) {
+    const float4* ep = sv.ent + ENT_STRIDE * ent_id;
+    float4 g0 = ep[0], g1 = ep[1], g2 = ep[2];
+    float4 n0 = ep[3], n1 = ep[4], n2 = ep[5];
+    int4 info = *reinterpret_cast<const int4*>(ep + 6); // shape type, material, vtx_off, idx_off|sphere
+    material = info.y;
+    Surface s;
+    s.point = add(ro, mulf(rd, t));
+    if (info.x == 1) {
+        float4 sph = sv.spheres[info.w];
+        f3 dir = sub(s.point, xform_point_rows(g0, g1, g2, f3of(sph)));
+        float l = len(dir);
+        f3 nrm = mulf(dir, 1 / l);
+        s.entering = true;
+        s.face_normal = nrm;
+        s.local = make_frame(nrm);
+        return s;
+    }
+    int4 f = sv.idx[info.w + prim];
+    f3 v0 = xform_point_rows(g0, g1, g2, f3of(sv.vtx[info.z + f.x]));
+    f3 v1 = xform_point_rows(g0, g1, g2, f3of(sv.vtx[info.z + f.y]));
+    f3 v2 = xform_point_rows(g0, g1, g2, f3of(sv.vtx[info.z + f.z]));
+    // make_triangle (core/triangle.art:11-26)
+    f3 e1 = sub(v1, v0), e2 = sub(v2, v0);
+    f3 n = cross(e1, e2);
+    float nn = len(n);
+    f3 fn = mulf(n, 1 / nn);
+    f3 ln = lerp2(f3of(sv.nrm[info.z + f.x]), f3of(sv.nrm[info.z + f.y]), f3of(sv.nrm[info.z + f.z]), hu, hv);
+    f3 normal = normalize(xform_dir_rows(n0, n1, n2, ln));
+    s.entering = dot(rd, fn) <= 0;
+    s.face_normal = s.entering ? fn : neg(fn);
+    s.local = make_frame(s.entering ? normal : neg(normal));
+    return s;
+}
+
+// ---------------------------------------------------------------------------
+// Lights
+// ---------------------------------------------------------------------------
+// compute_sq of make_plane_area_emitter (light/area.art:127-176)
+struct SQ {
+    f3 o, n;
+    float x0, y0, z0, x1, y1, b0, b1, k, s;
+};
+__device__ __forceinline__ float safe_acos(float a) { return acosf(clampf(a, -1, 1)); }
+__device__ __forceinline__ SQ compute_sq(const DevLight& L, f3 from) {
+    f3 origin = mk(L.origin[0], L.origin[1], L.origin[2]);
+    f3 ex = mk(L.ex[0], L.ex[1], L.ex[2]);
+    f3 ey = mk(L.ey[0], L.ey[1], L.ey[2]);
+    f3 normal = mk(L.normal[0], L.normal[1], L.normal[2]);
+    float width = L.origin[3], height = L.ex[3];
+    f3 dir = sub(origin, from);
+    SQ q;
+    q.x0 = dot(dir, ex);
+    q.y0 = dot(dir, ey);
+    float z0_ = dot(dir, normal);
+    q.x1 = q.x0 + width;
+    q.y1 = q.y0 + height;
+    bool nsb = !signbit(z0_);
+    q.z0 = nsb ? -z0_ : z0_;
+    q.n = nsb ? neg(normal) : normal;
+    // diff = (x0, y1, x1, y0) - (x1, y0, x0, y1); nz_ = (y0, x1, y1, x0) * diff
+    float dx = q.x0 - q.x1, dy = q.y1 - q.y0, dz = q.x1 - q.x0, dw = q.y0 - q.y1;
+    float zx = q.y0 * dx, zy = q.x1 * dy, zz = q.y1 * dz, zw = q.x0 * dw;
+    float z02 = q.z0 * q.z0;
+    float nzx = zx / sqrtf((dx * dx) * z02 + zx * zx);
+    float nzy = zy / sqrtf((dy * dy) * z02 + zy * zy);
+    float nzz = zz / sqrtf((dz * dz) * z02 + zz * zz);
+    float nzw = zw / sqrtf((dw * dw) * z02 + zw * zw);
+    float g0 = safe_acos(-nzx * nzy);
+    float g1 = safe_acos(-nzy * nzz);
+    float g2 = safe_acos(-nzz * nzw);
+    float g3 = safe_acos(-nzw * nzx);
+    q.b0 = nzx;
+    q.b1 = nzz;
+    q.k = 2 * PI_ - g2 - g3;
+    q.s = g0 + g1 - q.k;
+    q.o = from;
+    return q;
+}
+
+struct DirectSample {
+    f3 pos, dir;
+    f3 intensity;
+    float pdf_value;
+    bool pdf_solid; // measure of pdf_value: solid angle or area
+    float cos, dist;
+};
+
+__device__ __forceinline__ float pdf_as_solid(float value, bool solid, float cos, float dist2) {
+    return solid ? value : value * dist2 / cos; // driver/pdf.art:15-32
+}
+
+// Light::sample_direct for the light types on the hot path
+__device__ __forceinline__ DirectSample light_sample_direct(const SceneView& sv, const DevLight& L, Rng& rnd,
+                                                            const Surface& from) {
+    DirectSample ds;
+    f3 rad = mk(L.radiance[0], L.radiance[1], L.radiance[2]);
+    if (L.type == LIGHT_PLANE) {
+        // make_area_light.sample_direct (light/area.art:10-27) + plane sampler (area.art:178-224)
+        float ux = rnd.next_f32();
+        float uy = rnd.next_f32();
+        SQ q = compute_sq(L, from.point);
+        f3 ex = mk(L.ex[0], L.ex[1], L.ex[2]);
+        f3 ey = mk(L.ey[0], L.ey[1], L.ey[2]);
+        float au = fmaf(ux, q.s, q.k);
+        float fu = fmaf(cosf(au), q.b0, -q.b1) / sinf(au);
+        float cu = clampf(copysignf(1.0f, fu) / sqrtf(sum_of_prod(fu, fu, q.b0, q.b0)), -1, 1);
+        float xu = clampf(-(cu * q.z0) / sqrtf(fmaf(-cu, cu, 1.0f)), q.x0, q.x1);
+        float dd = sqrtf(sum_of_prod(xu, xu, q.z0, q.z0));
+        float h0 = q.y0 / sqrtf(sum_of_prod(dd, dd, q.y0, q.y0));
+        float h1 = q.y1 / sqrtf(sum_of_prod(dd, dd, q.y1, q.y1));
+        float hv = fmaf(uy, h1 - h0, h0);
+        float hv2 = hv * hv;
+        float yv = hv2 < 1 - 1e-6f ? (hv * dd) / sqrtf(1 - hv2) : q.y1;
+        f3 p = add(q.o, add(mulf(ex, xu), add(mulf(ey, yv), mulf(q.n, q.z0))));
+        float pdf_s = safe_div(1, q.s);
+        f3 dir_ = sub(p, from.point);
+        float dist = len(dir_);
+        f3 dir = mulf(dir_, safe_div(1, dist));
+        f3 normal = mk(L.normal[0], L.normal[1], L.normal[2]);
+        ds.pos = p;
+        ds.dir = dir;
+        ds.intensity = mulf(rad, q.s);
+        ds.pdf_value = pdf_s;
+        ds.pdf_solid = true;
+        ds.cos = dot(dir, normal) * (from.entering ? -1.0f : 1.0f);
+        ds.dist = dist;
+    } else if (L.type == LIGHT_ENV) {
+        // make_environment_light_function_spherical.sample_direct (light/env.art:80-84)
+        float ux = rnd.next_f32();
+        float uy = rnd.next_f32();
+        f3 dir = equal_area_square_to_sphere(ux, uy);
+        float pdf = 1 / (4 * PI_);
+        ds.intensity = mulf(rad, 1 / pdf);
+        ds.pos = add(from.point, mulf(dir, sv.scene_radius));
+        ds.dir = dir;
+        ds.pdf_value = pdf;
+        ds.pdf_solid = true;
+        ds.cos = 1.0f;
+        ds.dist = sv.scene_radius;
+    } else if (L.type == LIGHT_POINT) {
+        // make_point_light.sample_direct (light/point.art:3-8)
+        f3 pos = mk(L.origin[0], L.origin[1], L.origin[2]);
+        f3 dir_ = sub(pos, from.point);
+        float dist = len(dir_);
+        ds.dir = mulf(dir_, safe_div(1, dist));
+        ds.pos = pos;
+        ds.intensity = rad;
+        ds.pdf_value = 1;
+        ds.pdf_solid = false;
+        ds.cos = 1;
+        ds.dist = dist;
+    } else {
+        // make_spot_light.sample_direct (light/spot.art:27-36)
+        f3 pos = mk(L.origin[0], L.origin[1], L.origin[2]);
+        f3 sdir = mk(L.normal[0], L.normal[1], L.normal[2]);
+        f3 od_ = sub(pos, from.point);
+        float dist = len(od_);
+        f3 od = mulf(od_, safe_div(1, dist));
+        float cos_angle = dot(neg(od), sdir);
+        float cos_cut = L.spot[0], blend = L.spot[2];
+        float factor = blend <= FLT_EPS_ ? (cos_angle <= cos_cut ? 0.0f : 1.0f)
+                                         : [&] { float x = clampf((cos_angle - cos_cut) / blend, 0, 1); return x * x * (3 - 2 * x); }();
+        ds.intensity = mulf(rad, factor);
+        ds.pos = pos;
+        ds.dir = od;
+        ds.cos = -dot(od, sdir);
+        ds.pdf_value = dot(neg(od), sdir) > cos_cut ? 1.0f : 0.0f;
+        ds.pdf_solid = false;
+        ds.dist = dist;
+    }
+    return ds;
+}
+
+// Light::pdf_direct for lights that can be hit (area: plane; env)
+__device__ __forceinline__ float light_pdf_direct_solid(const DevLight& L, f3 ray_org, float cos, float dist2) {
+    if (L.type == LIGHT_PLANE) {
+        SQ q = compute_sq(L, ray_org);
+        return safe_div(1, q.s); // solid measure
+    }
+    (void)cos; (void)dist2;
+    return 1 / (4 * PI_); // env spherical: equal_area_sphere_pdf
+}
+
+// ---------------------------------------------------------------------------
+// BSDFs (bsdf/diffuse.art:2-11, bsdf/dielectric.art:2-23) and fresnel
+// (core/fresnel.art:7-28)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float fresnel_factor(float eta, float cos_i, float cos_t) {
+    float rs = safe_div(eta * cos_i - cos_t, eta * cos_i + cos_t);
+    float rp = safe_div(cos_i - eta * cos_t, cos_i + eta * cos_t);
+    return clampf((rs * rs + rp * rp) * 0.5f, 0, 1);
+}
+
+struct BsdfSample {
+    f3 in_dir;
+    float pdf;
+    f3 color;
+    float eta;
+    bool valid;
+};
+
+__device__ __forceinline__ BsdfSample sample_bsdf(const DevMaterial& m, const Surface& s, Rng& rnd, f3 out_dir) {
+    BsdfSample b;
+    b.valid = true;
+    if (m.type == MAT_DIFFUSE) {
+        float u = rnd.next_f32();
+        float v = rnd.next_f32();
+        float pdf;
+        f3 ld = sample_cosine_hemisphere(u, v, &pdf);
+        b.in_dir = frame_to_world(s.local, ld);
+        b.pdf = pdf;
+        b.color = mk(m.kd[0], m.kd[1], m.kd[2]);
+        b.eta = 1;
+        return b;
+    }
+    // make_pure_dielectric_bsdf.sample (adjoint = false)
+    float n1 = m.ks[3], n2 = m.kt[3];
+    float k = s.entering ? n1 / n2 : n2 / n1;
+    f3 n = s.local.n;
+    float cos_o = dot(out_dir, n);
+    // fresnel(k, cos_o), FresnelTerm{cos_t=0, factor=1} when total internal reflection
+    float ft_cos_t = 0, ft_factor = 1;
+    {
+        float eta2 = cos_o < 0 ? 1 / k : k;
+        float cos2_t = 1 - (1 - cos_o * cos_o) * eta2 * eta2;
+        if (!(cos2_t <= 0.0f)) {
+            float ct = sqrtf(cos2_t);
+            ft_cos_t = cos_o < 0 ? -ct : ct;
+            ft_factor = fresnel_factor(eta2, fabsf(cos_o), ct);
+        }
+    }
+    if (rnd.next_f32() > ft_factor) {
+        b.in_dir = refract(out_dir, n, k, cos_o, ft_cos_t);
+        b.pdf = 1;
+        b.color = mk(m.kt[0], m.kt[1], m.kt[2]);
+        b.eta = k;
+    } else {
+        b.in_dir = reflect(out_dir, n);
+        b.pdf = 1;
+        b.color = mk(m.ks[0], m.ks[1], m.ks[2]);
+        b.eta = 1;
+    }
+    return b;
+}
+
+} // namespace igxd

@@ -1,0 +1,202 @@
+// Binned-SAH BVH2 builder; see bvh_build.h.
+#include "bvh_build.h"
+
+#include <algorithm>
+#include <cmath>
+#include <limits>
+#include <stdexcept>
+#include <thread>
+#include <future>
+
+namespace igx {
+
+namespace {
+
+struct Box {
+    float lo[3] = {std::numeric_limits<float>::max(), std::numeric_limits<float>::max(), std::numeric_limits<float>::max()};
+    float hi[3] = {-std::numeric_limits<float>::max(), -std::numeric_limits<float>::max(), -std::numeric_limits<float>::max()};
+    void grow(const float* a, const float* b) {
+        for (int i = 0; i < 3; ++i) { lo[i] = std::min(lo[i], a[i]); hi[i] = std::max(hi[i], b[i]); }
+    }
+    void grow(const Box& o) { grow(o.lo, o.hi); }
+    void grow_point(const float* p) { grow(p, p); }
+    float half_area() const {
+        float dx = std::max(hi[0] - lo[0], 0.f), dy = std::max(hi[1] - lo[1], 0.f), dz = std::max(hi[2] - lo[2], 0.f);
+        return dx * (dy + dz) + dy * dz;
+    }
+    bool valid() const { return lo[0] <= hi[0]; }
+};
+
+struct TmpNode {
+    Box box;
+    int32_t left = -1, right = -1; // children (tmp indices), -1 for leaf
+    uint32_t first = 0, count = 0;
+};
+
+struct Builder {
+    const BvhBuildInput& in;
+    int max_leaf;
+    int bins;
+    std::vector<uint32_t> idx;
+    std::vector<TmpNode> nodes;
+
+    Builder(const BvhBuildInput& i, int ml, int b) : in(i), max_leaf(ml), bins(b) {}
+
+    Box prim_box(uint32_t p) const { Box b; b.grow(&in.bmin[3 * p], &in.bmax[3 * p]); return b; }
+
+    // Returns tmp node index of a subtree over idx[first, first+count).
+    int32_t build(uint32_t first, uint32_t count, int depth) {
+        int32_t me = (int32_t)nodes.size();
+        nodes.emplace_back();
+        Box box, cbox;
+        for (uint32_t i = first; i < first + count; ++i) {
+            uint32_t p = idx[i];
+            box.grow(&in.bmin[3 * p], &in.bmax[3 * p]);
+            cbox.grow_point(&in.centroid[3 * p]);
+        }
+        nodes[me].box = box;
+        nodes[me].first = first;
+        nodes[me].count = count;
+        if (count == 1) return me;
+
+        // best binned SAH split
+        float best_cost = std::numeric_limits<float>::max();
+        int best_axis = -1, best_bin = -1;
+        std::vector<Box> bbox(bins);
+        std::vector<uint32_t> bcnt(bins);
+        std::vector<float> right_area(bins);
+        std::vector<uint32_t> right_cnt(bins);
+        for (int axis = 0; axis < 3; ++axis) {
+            float ext = cbox.hi[axis] - cbox.lo[axis];
+            if (!(ext > 0)) continue;
+            float scale = bins / ext;
+            for (int b = 0; b < bins; ++b) { bbox[b] = Box(); bcnt[b] = 0; }
+            for (uint32_t i = first; i < first + count; ++i) {
+                uint32_t p = idx[i];
+                int b = std::min(bins - 1, (int)((in.centroid[3 * p + axis] - cbox.lo[axis]) * scale));
+                bbox[b].grow(&in.bmin[3 * p], &in.bmax[3 * p]);
+                bcnt[b]++;
+            }
+            Box acc;
+            uint32_t c = 0;
+            for (int b = bins - 1; b > 0; --b) {
+                acc.grow(bbox[b]);
+                c += bcnt[b];
+                right_area[b] = acc.valid() ? acc.half_area() : 0.f;
+                right_cnt[b] = c;
+            }
+            acc = Box();
+            c = 0;
+            for (int b = 0; b < bins - 1; ++b) {
+                acc.grow(bbox[b]);
+                c += bcnt[b];
+                if (c == 0 || right_cnt[b + 1] == 0) continue;
+                float cost = acc.half_area() * c + right_area[b + 1] * right_cnt[b + 1];
+                if (cost < best_cost) { best_cost = cost; best_axis = axis; best_bin = b; }
+            }
+        }
+        float parent_area = box.half_area();
+        // leaf vs split: traversal cost 1, intersection cost 1 per primitive (relative)
+        float leaf_cost = (float)count;
+        float split_cost = best_axis >= 0 ? 1.0f + best_cost / std::max(parent_area, 1e-30f) : std::numeric_limits<float>::max();
+        if ((int)count <= max_leaf && leaf_cost <= split_cost) return me;
+
+        uint32_t mid;
+        if (best_axis < 0) {
+            mid = first + count / 2; // all centroids coincide: split in the middle
+        } else {
+            float ext = cbox.hi[best_axis] - cbox.lo[best_axis];
+            float scale = bins / ext;
+            auto it = std::partition(idx.begin() + first, idx.begin() + first + count, [&](uint32_t p) {
+                int b = std::min(bins - 1, (int)((in.centroid[3 * p + best_axis] - cbox.lo[best_axis]) * scale));
+                return b <= best_bin;
+            });
+            mid = (uint32_t)(it - idx.begin());
+            if (mid == first || mid == first + count) mid = first + count / 2;
+        }
+        int32_t l = build(first, mid - first, depth + 1);
+        int32_t r = build(mid, first + count - mid, depth + 1);
+        nodes[me].left = l;
+        nodes[me].right = r;
+        return me;
+    }
+};
+
+void set_child(BvhNode& n, int k, const Box& b, int32_t ref) {
+    int o = k == 0 ? 0 : 6;
+    // c0: [0]=lo.x [1]=hi.x [2]=lo.y [3]=hi.y [4]=lo.z [5]=hi.z ; c1 likewise at +6
+    n.b[o + 0] = b.lo[0]; n.b[o + 1] = b.hi[0];
+    n.b[o + 2] = b.lo[1]; n.b[o + 3] = b.hi[1];
+    n.b[o + 4] = b.lo[2]; n.b[o + 5] = b.hi[2];
+    n.ref[k] = ref;
+}
+
+void set_empty(BvhNode& n, int k) {
+    Box e; // inverted box: lo = +max, hi = -max
+    set_child(n, k, e, -1);
+}
+
+} // namespace
+
+BvhBuildResult build_bvh2(const BvhBuildInput& in, int max_leaf, int bins) {
+    if (max_leaf < 1 || max_leaf > (1 << kLeafCountBits)) throw std::invalid_argument("max_leaf out of range");
+    BvhBuildResult res;
+    const size_t n = in.count();
+    res.max_leaf = max_leaf;
+    if (n == 0) {
+        BvhNode root{};
+        set_empty(root, 0);
+        set_empty(root, 1);
+        res.nodes.push_back(root);
+        res.depth = 1;
+        return res;
+    }
+    if (n >= (size_t)kMaxLeafFirst) throw std::invalid_argument("too many primitives for the leaf encoding");
+    Builder b(in, max_leaf, bins);
+    b.idx.resize(n);
+    for (size_t i = 0; i < n; ++i) b.idx[i] = (uint32_t)i;
+    b.nodes.reserve(2 * n / std::max(1, max_leaf) + 4);
+    int32_t root = b.build(0, (uint32_t)n, 0);
+    res.prim_order = b.idx;
+
+    // Flatten: BvhNodes in DFS pre-order; each inner tmp node becomes one BvhNode.
+    auto leaf_ref = [&](const TmpNode& t) { return encode_leaf((int32_t)t.first, (int32_t)t.count); };
+    struct Item { int32_t tmp; int32_t out; int depth; };
+    std::vector<Item> stack;
+    res.nodes.emplace_back();
+    if (b.nodes[root].left < 0) {
+        // root itself is a leaf: both children reference it (an empty child
+        // box would pass the min/max slab test; a duplicate leaf is harmless
+        // for closest and any hit)
+        set_child(res.nodes[0], 0, b.nodes[root].box, leaf_ref(b.nodes[root]));
+        set_child(res.nodes[0], 1, b.nodes[root].box, leaf_ref(b.nodes[root]));
+        res.depth = 1;
+        return res;
+    }
+    stack.push_back({root, 0, 1});
+    while (!stack.empty()) {
+        Item it = stack.back();
+        stack.pop_back();
+        res.depth = std::max(res.depth, it.depth);
+        const TmpNode& t = b.nodes[it.tmp];
+        int32_t kids[2] = {t.left, t.right};
+        // push right first so the left subtree is laid out right after its parent
+        int32_t out_idx[2] = {-1, -1};
+        for (int k = 0; k < 2; ++k) {
+            const TmpNode& c = b.nodes[kids[k]];
+            if (c.left < 0) {
+                set_child(res.nodes[it.out], k, c.box, leaf_ref(c));
+            } else {
+                out_idx[k] = (int32_t)res.nodes.size();
+                res.nodes.emplace_back();
+                set_child(res.nodes[it.out], k, c.box, out_idx[k]);
+            }
+            res.nodes[it.out].pad[k] = 0;
+        }
+        for (int k = 1; k >= 0; --k)
+            if (out_idx[k] >= 0) stack.push_back({kids[k], out_idx[k], it.depth + 1});
+    }
+    return res;
+}
+
+} // namespace igx

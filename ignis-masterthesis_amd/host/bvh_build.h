@@ -1,0 +1,53 @@
+// Host-side binned-SAH BVH2 builder.
+//
+// Replaces madmann91/bvh (GIT_TAG v1, not vendored and unavailable offline),
+// which the reference calls from build_bvh (src/runtime/bvh/TriBVHAdapter.h:163-202)
+// for per-shape BLAS and from build_scene_bvh (src/runtime/bvh/SceneBVHAdapter.h:109-135)
+// for the entity TLAS.  Topology differs from the reference's SBVH (parity of
+// BVH topology is unpinned); closest-hit results do not depend
+// on it.
+//
+// Output node layout = the device's 64-byte BVH2 node (DESIGN.md "HBM layout"):
+//   float lo_hi[12]: c0.lo.x c0.hi.x c0.lo.y c0.hi.y | c0.lo.z c0.hi.z c1.lo.x c1.hi.x |
+//                    c1.lo.y c1.hi.y c1.lo.z c1.hi.z          (Node2 interleaving,
+//                    traversal/mapping_gpu.art:3-7)
+//   int32 ref[2]:    >= 0 inner node index; < 0 leaf, ~ref = (first << 4) | (count - 1)
+//   int32 pad[2]
+// An absent child has an inverted (empty) box so its slab test always fails.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+namespace igx {
+
+struct BvhNode {
+    float b[12];
+    int32_t ref[2];
+    int32_t pad[2];
+};
+static_assert(sizeof(BvhNode) == 64, "BvhNode must be 64 bytes");
+
+constexpr int kLeafCountBits = 4;               // up to 16 primitives per leaf
+constexpr int32_t kMaxLeafFirst = 1 << 26;      // keeps ~ref above the stack sentinels
+
+inline int32_t encode_leaf(int32_t first, int32_t count) { return ~((first << kLeafCountBits) | (count - 1)); }
+
+struct BvhBuildInput {
+    // per primitive: bounds min/max and centroid
+    std::vector<float> bmin, bmax, centroid; // 3 floats each
+    size_t count() const { return bmin.size() / 3; }
+};
+
+struct BvhBuildResult {
+    std::vector<BvhNode> nodes;         // nodes[0] is the root (always an inner node)
+    std::vector<uint32_t> prim_order;   // leaf slot -> original primitive index
+    int depth = 0;                      // maximum root-to-leaf depth (number of inner levels)
+    int max_leaf = 0;
+};
+
+// Build a BVH2 with binned SAH.  `max_leaf` caps primitives per leaf (<= 16).
+BvhBuildResult build_bvh2(const BvhBuildInput& in, int max_leaf, int bins = 32);
+
+} // namespace igx

@@ -1,0 +1,93 @@
+// igcli-style frontend over the HIP device (src/frontend/cli/main.cpp:54-179):
+// loads a scene, renders spp samples in iterations of spi on one GPU, prints
+// Msamples/s like the reference (cli/main.cpp:135, 172-178) plus Mrays/s, and
+// writes the averaged image as PFM (the reference writes EXR, out of scope).
+#include "Device.h"
+#include "igx_scene.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+static void usage() {
+    std::fprintf(stderr,
+                 "usage: igcli SCENE.json [--spp N] [--spi N] [--seed N] [--gpu-device N] [-o out.pfm]\n");
+}
+
+int main(int argc, char** argv) {
+    std::string scene_path, out_path;
+    int spp = 0, spi = 8, seed = 0, device = 0;
+    for (int i = 1; i < argc; ++i) {
+        std::string a = argv[i];
+        auto next = [&]() -> const char* {
+            if (i + 1 >= argc) { usage(); std::exit(2); }
+            return argv[++i];
+        };
+        if (a == "--spp") spp = std::atoi(next());
+        else if (a == "--spi") spi = std::atoi(next());
+        else if (a == "--seed") seed = std::atoi(next());
+        else if (a == "--gpu-device") device = std::atoi(next());
+        else if (a == "-o" || a == "--output") out_path = next();
+        else if (a == "--gpu") {}
+        else if (a == "-h" || a == "--help") { usage(); return 0; }
+        else if (!a.empty() && a[0] == '-') { usage(); return 2; }
+        else scene_path = a;
+    }
+    if (scene_path.empty()) { usage(); return 2; }
+    char err[1024] = {0};
+    igx_scene* scene = igx_scene_load_file(scene_path.c_str(), err, sizeof(err));
+    if (!scene) { std::fprintf(stderr, "failed to load scene: %s\n", err); return 1; }
+    const igx_scene_desc* desc = igx_scene_get_desc(scene);
+    if (spp <= 0) spp = spi;
+    int iters = (spp + spi - 1) / spi; // igcli rounds spp up to a multiple of spi (cli/main.cpp:110-113)
+    try {
+        IG::SetupSettings ss;
+        ss.Device = device;
+        IG::Device dev(ss);
+        IG::SceneSettings sc;
+        sc.Database = desc;
+        dev.assignScene(sc);
+        std::vector<double> rates;
+        for (int it = 0; it < iters; ++it) {
+            IG::RenderSettings rs;
+            rs.spi = spi;
+            rs.width = desc->film_width;
+            rs.height = desc->film_height;
+            rs.iteration = it;
+            rs.user_seed = seed;
+            auto t0 = std::chrono::steady_clock::now();
+            dev.render(rs);
+            double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            rates.push_back((double)spi * desc->film_width * desc->film_height / s / 1e6);
+        }
+        igx_stats st = dev.getStatistics();
+        std::sort(rates.begin(), rates.end());
+        double rays = (double)(st.camera_rays + st.bounce_rays + st.shadow_rays);
+        std::printf("# %f %f %f Msamples/s\n", rates.front(), rates[rates.size() / 2], rates.back());
+        std::printf("# %.3f Mrays/s (camera %llu, bounce %llu, shadow %llu) over %.3f ms\n", rays / (st.ms_render * 1e3), (unsigned long long)st.camera_rays,
+                    (unsigned long long)st.bounce_rays, (unsigned long long)st.shadow_rays, st.ms_render);
+        if (!out_path.empty()) {
+            IG::AOVAccessor acc = dev.getFramebufferForHost();
+            FILE* f = std::fopen(out_path.c_str(), "wb");
+            if (!f) { std::fprintf(stderr, "cannot write %s\n", out_path.c_str()); return 1; }
+            std::fprintf(f, "PF\n%d %d\n-1.0\n", desc->film_width, desc->film_height);
+            float inv = acc.IterationCount ? 1.0f / acc.IterationCount : 0.0f;
+            for (int y = desc->film_height - 1; y >= 0; --y) { // PFM rows go bottom-up
+                std::vector<float> row(3 * desc->film_width);
+                for (int x = 0; x < 3 * desc->film_width; ++x) row[x] = acc.Data[(size_t)y * 3 * desc->film_width + x] * inv;
+                std::fwrite(row.data(), sizeof(float), row.size(), f);
+            }
+            std::fclose(f);
+        }
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "error: %s\n", e.what());
+        igx_scene_free(scene);
+        return 1;
+    }
+    igx_scene_free(scene);
+    return 0;
+}

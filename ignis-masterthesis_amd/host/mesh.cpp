@@ -1,0 +1,616 @@
+// Procedural meshes and mesh readers; see mesh.h for the reference citations.
+#include "mesh.h"
+
+#include <cmath>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <sstream>
+#include <tuple>
+#include <unordered_map>
+
+namespace igx {
+
+static constexpr float kPi = 3.14159265358979323846f;
+static constexpr float kFltEps = 1.1920928955e-07f;
+
+static V3 triangle_normal(V3 v0, V3 v1, V3 v2) { return cross(v1 - v0, v2 - v0); }
+
+BBox TriMesh::compute_bbox() const {
+    BBox b;
+    for (auto& v : vertices) b.extend(v);
+    return b;
+}
+
+void TriMesh::flip_normals() {
+    for (auto& f : faces) std::swap(f[1], f[2]);
+    for (auto& n : normals) n = -n;
+}
+
+void TriMesh::compute_vertex_normals() {
+    normals.assign(vertices.size(), V3());
+    for (auto& f : faces) {
+        V3 n = normalized(triangle_normal(vertices[f[0]], vertices[f[1]], vertices[f[2]]));
+        normals[f[0]] = normals[f[0]] + n;
+        normals[f[1]] = normals[f[1]] + n;
+        normals[f[2]] = normals[f[2]] + n;
+    }
+    for (auto& n : normals) n = normalized(n);
+}
+
+void TriMesh::fix_normals(bool* bad) {
+    bool b = false;
+    for (auto& n : normals) {
+        float l2 = norm2(n);
+        if (l2 <= kFltEps || std::isnan(l2)) {
+            b = true;
+            n = V3(0, 1, 0);
+        } else {
+            n = n / std::sqrt(l2);
+        }
+    }
+    if (bad) *bad = b;
+}
+
+void TriMesh::make_texcoords_normalized() {
+    texcoords.resize(vertices.size());
+    BBox bbox = compute_bbox();
+    V3 d = bbox.diameter();
+    for (size_t i = 0; i < vertices.size(); ++i) {
+        V3 t = vertices[i] - bbox.min;
+        std::array<float, 2> p{0, 0};
+        if (d.x > kFltEps) p[0] = t.x / d.x;
+        if (d.y > kFltEps) p[1] = t.y / d.y;
+        texcoords[i] = p;
+    }
+}
+
+void TriMesh::setup_face_normals_as_vertex_normals() {
+    std::vector<V3> nv(faces.size() * 3), nn(faces.size() * 3);
+    std::vector<std::array<float, 2>> nt;
+    if (!texcoords.empty()) nt.resize(faces.size() * 3);
+    for (size_t f = 0; f < faces.size(); ++f) {
+        for (int k = 0; k < 3; ++k) {
+            nv[3 * f + k] = vertices[faces[f][k]];
+            if (!texcoords.empty()) nt[3 * f + k] = texcoords[faces[f][k]];
+        }
+        V3 n = normalized(triangle_normal(nv[3 * f], nv[3 * f + 1], nv[3 * f + 2]));
+        nn[3 * f] = nn[3 * f + 1] = nn[3 * f + 2] = n;
+        faces[f] = {uint32_t(3 * f), uint32_t(3 * f + 1), uint32_t(3 * f + 2)};
+    }
+    vertices = std::move(nv);
+    normals = std::move(nn);
+    if (!texcoords.empty()) texcoords = std::move(nt);
+}
+
+void TriMesh::transform(const M4& t) {
+    if (t.is_identity()) return;
+    M3 nm = transpose3(inverse3(linear_of(t))); // NormalMatrix = L^T^-1 (TriMesh.cpp:245-248)
+    for (auto& v : vertices) v = xform_point(t, v);
+    for (auto& n : normals) n = normalized(mul3(nm, n));
+}
+
+void TriMesh::append(const TriMesh& o) {
+    uint32_t off = (uint32_t)vertices.size();
+    vertices.insert(vertices.end(), o.vertices.begin(), o.vertices.end());
+    normals.insert(normals.end(), o.normals.begin(), o.normals.end());
+    texcoords.insert(texcoords.end(), o.texcoords.begin(), o.texcoords.end());
+    for (auto f : o.faces) faces.push_back({f[0] + off, f[1] + off, f[2] + off});
+}
+
+// ---------------------------------------------------------------------------
+std::optional<PlaneShape> get_as_plane(const TriMesh& mesh) {
+    constexpr float PlaneEPS = 1e-5f;
+    if (mesh.face_count() != 2) return std::nullopt;
+
+    std::array<V3, 4> uv{};
+    std::array<uint32_t, 4> ids{};
+    const auto& vs = mesh.vertices;
+    if (vs.size() != 4) {
+        if (vs.size() > 4 && vs.size() <= 6) {
+            size_t i = 0;
+            uint32_t id = 0;
+            for (const auto& v : vs) {
+                bool found = false;
+                for (const auto& u : uv) {
+                    found = approx(v, u, PlaneEPS);
+                    if (found) break;
+                }
+                if (!found) {
+                    if (i >= 3) return std::nullopt;
+                    ids[i + 1] = id;
+                    uv[i + 1] = v;
+                    ++i;
+                }
+                ++id;
+            }
+            if (i != 4) return std::nullopt;
+        } else {
+            return std::nullopt;
+        }
+    } else {
+        for (size_t i = 0; i < 4; ++i) { uv[i] = vs[i]; ids[i] = (uint32_t)i; }
+    }
+
+    const auto& f0 = mesh.faces[0];
+    const auto& f1 = mesh.faces[1];
+    V3 fn0 = normalized(triangle_normal(vs[f0[0]], vs[f0[1]], vs[f0[2]]));
+    V3 fn1 = normalized(triangle_normal(vs[f1[0]], vs[f1[1]], vs[f1[2]]));
+    if (!approx(fn0, fn1, PlaneEPS)) return std::nullopt;
+
+    float e1 = norm2(vs[f0[0]] - vs[f0[1]]);
+    float e2 = norm2(vs[f0[1]] - vs[f0[2]]);
+    float e3 = norm2(vs[f0[2]] - vs[f0[0]]);
+    float e4 = norm2(vs[f1[0]] - vs[f1[1]]);
+    float e5 = norm2(vs[f1[1]] - vs[f1[2]]);
+    float e6 = norm2(vs[f1[2]] - vs[f1[0]]);
+    auto safe = [&](float a, float b) { return std::abs(a - b) <= PlaneEPS; };
+    if (!safe(e1, e4) && !safe(e2, e4) && !safe(e3, e4)) return std::nullopt;
+    if (!safe(e1, e5) && !safe(e2, e5) && !safe(e3, e5)) return std::nullopt;
+    if (!safe(e1, e6) && !safe(e2, e6) && !safe(e3, e6)) return std::nullopt;
+
+    V3 origin = uv[0];
+    auto angle = [&](size_t start) {
+        V3 x = normalized(uv[(start + 0) % 3 + 1] - origin);
+        V3 y = normalized(uv[(start + 1) % 3 + 1] - origin);
+        return std::acos(dot(x, y));
+    };
+    float a12 = std::abs(angle(0)), a23 = std::abs(angle(1)), a31 = std::abs(angle(2));
+    int sel;
+    if (a12 >= a23 && a12 >= a31) sel = 0;
+    else if (a23 >= a31 && a23 >= a12) sel = 1;
+    else sel = 2;
+
+    PlaneShape shape;
+    shape.origin = origin;
+    shape.x_axis = uv[(sel + 0) % 3 + 1] - origin;
+    shape.y_axis = uv[(sel + 1) % 3 + 1] - origin;
+    V3 n = normalized(cross(shape.x_axis, shape.y_axis));
+    if (dot(fn0, n) < 0) {
+        std::swap(shape.x_axis, shape.y_axis);
+        std::swap(uv[1], uv[2]);
+        std::swap(ids[1], ids[2]);
+    }
+    if (!mesh.texcoords.empty()) {
+        auto put = [&](int slot, uint32_t vid) {
+            shape.tex[slot * 2] = mesh.texcoords[vid][0];
+            shape.tex[slot * 2 + 1] = mesh.texcoords[vid][1];
+        };
+        put(0, ids[0]);
+        put((0 + sel) % 3 + 1, ids[1]);
+        put((1 + sel) % 3 + 1, ids[2]);
+        put((2 + sel) % 3 + 1, ids[3]);
+    } else {
+        shape.tex = {0, 0, 1, 0, 0, 1, 1, 1};
+    }
+    return shape;
+}
+
+// ---------------------------------------------------------------------------
+static void add_triangle(TriMesh& m, V3 origin, V3 xa, V3 ya) {
+    V3 n = normalized(cross(xa, ya));
+    uint32_t off = (uint32_t)m.vertices.size();
+    m.vertices.insert(m.vertices.end(), {origin, origin + xa, origin + ya});
+    m.normals.insert(m.normals.end(), {n, n, n});
+    m.texcoords.insert(m.texcoords.end(), {{0, 0}, {1, 0}, {0, 1}});
+    m.faces.push_back({off, off + 1, off + 2});
+}
+
+static void add_grid(TriMesh& m, V3 origin, V3 xa, V3 ya, uint32_t cx, uint32_t cy) {
+    V3 n = normalized(cross(xa, ya));
+    uint32_t off = (uint32_t)m.vertices.size();
+    for (uint32_t j = 0; j <= cy; ++j)
+        for (uint32_t i = 0; i <= cx; ++i) {
+            float u = i / (float)cx, v = j / (float)cy;
+            m.vertices.push_back(origin + xa * u + ya * v);
+            m.normals.push_back(n);
+            m.texcoords.push_back({u, v});
+        }
+    for (uint32_t j = 0; j < cy; ++j)
+        for (uint32_t i = 0; i < cx; ++i) {
+            uint32_t i1 = j * (cx + 1) + i + off;
+            uint32_t i2 = (j + 1) * (cx + 1) + i + off;
+            m.faces.push_back({i1, i1 + 1, i2 + 1});
+            m.faces.push_back({i1, i2 + 1, i2});
+        }
+}
+
+static void add_disk(TriMesh& m, V3 origin, V3 n, V3 nx, V3 ny, float radius, uint32_t sections, bool fill, bool flip = false) {
+    float step = 1.0f / sections;
+    uint32_t off = (uint32_t)m.vertices.size();
+    if (fill) {
+        m.vertices.push_back(origin);
+        m.normals.push_back(n);
+        m.texcoords.push_back({0, 0});
+    }
+    for (uint32_t i = 0; i < sections; ++i) {
+        float x = std::cos(2 * kPi * step * i);
+        float y = std::sin(2 * kPi * step * i);
+        m.vertices.push_back(nx * (radius * x) + ny * (radius * y) + origin);
+        m.normals.push_back(n);
+        m.texcoords.push_back({0.5f * (x + 1), 0.5f * (y + 1)});
+    }
+    if (!fill) return;
+    for (uint32_t i = 0; i < sections; ++i) {
+        uint32_t c = i + 1;
+        uint32_t nc = (i + 1 < sections ? i + 1 : 0) + 1;
+        if (flip) m.faces.push_back({off, nc + off, c + off});
+        else m.faces.push_back({off, c + off, nc + off});
+    }
+}
+
+void tangent_frame(V3 n, V3& nx, V3& ny) {
+    float sign = std::copysign(1.0f, n.z);
+    float a = -1.0f / (sign + n.z);
+    float b = n.x * n.y * a;
+    nx = V3(1.0f + sign * n.x * n.x * a, sign * b, -sign * n.x);
+    ny = V3(b, sign + n.y * n.y * a, -n.y);
+    nx = normalized(nx);
+    ny = normalized(ny);
+}
+
+TriMesh make_plane(V3 origin, V3 xa, V3 ya) { TriMesh m; add_grid(m, origin, xa, ya, 1, 1); return m; }
+TriMesh make_triangle(V3 p0, V3 p1, V3 p2) { TriMesh m; add_triangle(m, p0, p1 - p0, p2 - p0); return m; }
+TriMesh make_rectangle(V3 p0, V3 p1, V3 p2, V3 p3) {
+    TriMesh m;
+    add_triangle(m, p0, p1 - p0, p3 - p0);
+    add_triangle(m, p1, p2 - p1, p3 - p1);
+    return m;
+}
+TriMesh make_box(V3 o, V3 xa, V3 ya, V3 za) {
+    V3 hhh = o + xa + ya + za;
+    TriMesh m;
+    add_grid(m, o, ya, xa, 1, 1);
+    add_grid(m, o, xa, za, 1, 1);
+    add_grid(m, o, za, ya, 1, 1);
+    add_grid(m, hhh, -xa, -ya, 1, 1);
+    add_grid(m, hhh, -za, -xa, 1, 1);
+    add_grid(m, hhh, -ya, -za, 1, 1);
+    return m;
+}
+
+TriMesh make_uv_sphere(V3 center, float radius, uint32_t stacks, uint32_t slices) {
+    TriMesh m;
+    float drho = 3.141592f / (float)stacks;
+    float dtheta = 2 * 3.141592f / (float)slices;
+    for (uint32_t i = 0; i <= stacks; ++i) {
+        float rho = (float)i * drho;
+        float srho = std::sin(rho), crho = std::cos(rho);
+        for (uint32_t j = 0; j < slices; ++j) {
+            float theta = (j == slices) ? 0.0f : j * dtheta;
+            float stheta = -std::sin(theta), ctheta = std::cos(theta);
+            V3 n(stheta * srho, ctheta * srho, crho);
+            m.vertices.push_back(n * radius + center);
+            m.normals.push_back(n);
+            m.texcoords.push_back({(float)(0.5 * theta / kPi), rho / kPi});
+        }
+    }
+    for (uint32_t i = 0; i <= stacks; ++i) {
+        uint32_t cur = i * slices;
+        uint32_t nxt = ((i + 1) % (stacks + 1)) * slices;
+        for (uint32_t j = 0; j < slices; ++j) {
+            uint32_t nj = (j + 1) % slices;
+            uint32_t id0 = cur + j, id1 = cur + nj, id2 = nxt + j, id3 = nxt + nj;
+            m.faces.push_back({id2, id3, id1});
+            m.faces.push_back({id2, id1, id0});
+        }
+    }
+    return m;
+}
+
+TriMesh make_ico_sphere(V3 center, float radius, uint32_t subdivisions) {
+    TriMesh m;
+    constexpr float Golden = 1.618033989f;
+    for (int d = 0; d < 3; d++)
+        for (int s1 = -1; s1 <= 1; s1 += 2)
+            for (int s2 = -1; s2 <= 1; s2 += 2) {
+                V3 v;
+                v[(d + 1) % 3] = Golden * s1;
+                v[(d + 2) % 3] = 1.0f * s2;
+                m.vertices.push_back(normalized(v));
+            }
+    auto gi = [](int d, int s1, int s2) { return (uint32_t)(d * 4 + (s1 + 1) + ((s2 + 1) >> 1)); };
+    for (int s1 = -1; s1 <= 1; s1 += 2)
+        for (int s2 = -1; s2 <= 1; s2 += 2)
+            for (int s3 = -1; s3 <= 1; s3 += 2) {
+                bool rev = s1 * s2 * s3 == -1;
+                uint32_t i1 = gi(0, s1, s2), i2 = gi(1, s2, s3), i3 = gi(2, s3, s1);
+                m.faces.push_back({i1, rev ? i3 : i2, rev ? i2 : i3});
+            }
+    for (int d = 0; d < 3; d++)
+        for (int s1 = -1; s1 <= 1; s1 += 2)
+            for (int s2 = -1; s2 <= 1; s2 += 2) {
+                bool rev = s1 * s2 == +1;
+                uint32_t i2 = gi(d, s1, -1), i1 = gi(d, s1, +1), i3 = gi((d + 2) % 3, s2, s1);
+                m.faces.push_back({i1, rev ? i3 : i2, rev ? i2 : i3});
+            }
+    for (uint32_t s = 0; s < subdivisions; ++s) {
+        std::unordered_map<uint64_t, uint32_t> edge;
+        uint32_t prev = (uint32_t)m.vertices.size();
+        for (auto& f : m.faces)
+            for (int j = 0; j < 3; ++j) {
+                uint32_t a = f[j], b = f[(j + 1) % 3];
+                if (a >= b) continue;
+                uint64_t key = (uint64_t)a * prev + b;
+                edge[key] = (uint32_t)m.vertices.size();
+                m.vertices.push_back(normalized(m.vertices[a] + m.vertices[b]));
+            }
+        std::vector<std::array<uint32_t, 3>> refined;
+        refined.reserve(m.faces.size() * 4);
+        for (auto& f : m.faces) {
+            uint32_t ec[3];
+            for (int j = 0; j < 3; ++j) {
+                uint32_t a = f[j], b = f[(j + 1) % 3];
+                ec[j] = edge[(uint64_t)std::min(a, b) * prev + std::max(a, b)];
+            }
+            refined.push_back({ec[0], ec[1], ec[2]});
+            for (int j = 0; j < 3; ++j) refined.push_back({f[j], ec[(j + 0) % 3], ec[(j + 2) % 3]});
+        }
+        m.faces = std::move(refined);
+    }
+    m.normals.resize(m.vertices.size());
+    m.texcoords.resize(m.vertices.size());
+    for (size_t i = 0; i < m.vertices.size(); ++i) {
+        V3 n = normalized(m.vertices[i]);
+        m.normals[i] = n;
+        float theta = std::acos(n.z);
+        float phi = std::atan2(-n.x, n.y);
+        if (phi < 0) phi += 2 * kPi;
+        m.texcoords[i] = {phi / (2 * kPi), theta / kPi};
+    }
+    M4 t;
+    if (!(center.x == 0 && center.y == 0 && center.z == 0)) t = t * translation(center);
+    if (radius != 1) t = t * scaling(V3(radius, radius, radius));
+    m.transform(t);
+    return m;
+}
+
+TriMesh make_disk(V3 center, V3 normal, float radius, uint32_t sections) {
+    sections = std::max<uint32_t>(3, sections);
+    V3 nx, ny;
+    tangent_frame(normal, nx, ny);
+    TriMesh m;
+    add_disk(m, center, normal, nx, ny, radius, sections, true);
+    return m;
+}
+
+TriMesh make_cone(V3 base, float base_radius, V3 tip, uint32_t sections, bool fill) {
+    sections = std::max<uint32_t>(3, sections);
+    V3 h = normalized(base - tip);
+    V3 nx, ny;
+    tangent_frame(h, nx, ny);
+    TriMesh m;
+    add_disk(m, base, h, nx, ny, base_radius, sections, fill);
+    m.vertices.push_back(tip);
+    m.normals.push_back(h);
+    m.texcoords.push_back({0, 0});
+    uint32_t start = fill ? 1 : 0;
+    uint32_t tp = (uint32_t)m.vertices.size() - 1;
+    for (uint32_t i = 0; i < sections; ++i) {
+        uint32_t c = i + start, nc = (i + 1 < sections ? i + 1 : 0) + start;
+        m.faces.push_back({c, tp, nc});
+    }
+    m.compute_vertex_normals();
+    return m;
+}
+
+TriMesh make_cylinder(V3 base, float base_radius, V3 top, float top_radius, uint32_t sections, bool fill) {
+    sections = std::max<uint32_t>(3, sections);
+    V3 h = normalized(base - top);
+    V3 nx, ny;
+    tangent_frame(h, nx, ny);
+    TriMesh m;
+    add_disk(m, base, h, nx, ny, base_radius, sections, fill);
+    uint32_t off = (uint32_t)m.vertices.size();
+    add_disk(m, top, h, nx, ny, top_radius, sections, fill, true);
+    uint32_t start = fill ? 1 : 0;
+    for (uint32_t i = 0; i < sections; ++i) {
+        uint32_t c = i + start, nc = (i + 1 < sections ? i + 1 : 0) + start;
+        m.faces.push_back({c, c + off, nc});
+        m.faces.push_back({c + off, nc + off, nc});
+    }
+    m.compute_vertex_normals();
+    return m;
+}
+
+// ---------------------------------------------------------------------------
+// PLY reader (ascii / binary little+big endian), after src/runtime/mesh/PlyFile.cpp.
+// Polygons with more than three corners are fan-triangulated (the reference
+// ear-clips, Triangulation.cpp; identical for convex faces).
+namespace {
+struct PlyProp {
+    std::string name, type, list_count_type, list_item_type;
+    bool is_list = false;
+};
+size_t ply_type_size(const std::string& t) {
+    if (t == "char" || t == "uchar" || t == "int8" || t == "uint8" || t == "uint8_t") return 1;
+    if (t == "short" || t == "ushort" || t == "int16" || t == "uint16") return 2;
+    if (t == "int" || t == "uint" || t == "float" || t == "int32" || t == "uint32" || t == "float32") return 4;
+    if (t == "double" || t == "float64") return 8;
+    return 0;
+}
+double ply_read_bin(std::istream& in, const std::string& t, bool swap) {
+    unsigned char buf[8];
+    size_t n = ply_type_size(t);
+    in.read(reinterpret_cast<char*>(buf), (std::streamsize)n);
+    if (swap) std::reverse(buf, buf + n);
+    if (t == "char" || t == "int8") return (double)(int8_t)buf[0];
+    if (t == "uchar" || t == "uint8" || t == "uint8_t") return (double)buf[0];
+    if (t == "short" || t == "int16") { int16_t v; std::memcpy(&v, buf, 2); return v; }
+    if (t == "ushort" || t == "uint16") { uint16_t v; std::memcpy(&v, buf, 2); return v; }
+    if (t == "int" || t == "int32") { int32_t v; std::memcpy(&v, buf, 4); return v; }
+    if (t == "uint" || t == "uint32") { uint32_t v; std::memcpy(&v, buf, 4); return v; }
+    if (t == "float" || t == "float32") { float v; std::memcpy(&v, buf, 4); return v; }
+    double v; std::memcpy(&v, buf, 8); return v;
+}
+} // namespace
+
+bool load_ply(const std::string& path, TriMesh& out, std::string& err) {
+    std::ifstream in(path, std::ios::binary);
+    if (!in) { err = "cannot open " + path; return false; }
+    std::string line;
+    std::getline(in, line);
+    if (line.rfind("ply", 0) != 0) { err = path + ": not a ply file"; return false; }
+    std::string format;
+    size_t nv = 0, nf = 0;
+    std::vector<PlyProp> vprops, fprops;
+    std::vector<std::pair<std::string, size_t>> elements;
+    std::string cur;
+    while (std::getline(in, line)) {
+        if (!line.empty() && line.back() == '\r') line.pop_back();
+        std::istringstream ss(line);
+        std::string tok;
+        ss >> tok;
+        if (tok == "format") ss >> format;
+        else if (tok == "element") {
+            size_t n; ss >> cur >> n;
+            elements.push_back({cur, n});
+            if (cur == "vertex") nv = n;
+            else if (cur == "face") nf = n;
+        } else if (tok == "property") {
+            PlyProp p;
+            std::string t; ss >> t;
+            if (t == "list") { p.is_list = true; ss >> p.list_count_type >> p.list_item_type >> p.name; }
+            else { p.type = t; ss >> p.name; }
+            if (cur == "vertex") vprops.push_back(p);
+            else if (cur == "face") fprops.push_back(p);
+        } else if (tok == "end_header") break;
+    }
+    bool ascii = format == "ascii";
+    bool swap = format == "binary_big_endian";
+    if (!ascii && format != "binary_little_endian" && !swap) { err = path + ": unknown ply format " + format; return false; }
+
+    int ix = -1, iy = -1, iz = -1, inx = -1, iny = -1, inz = -1, iu = -1, ivv = -1;
+    for (size_t i = 0; i < vprops.size(); ++i) {
+        const auto& n = vprops[i].name;
+        if (n == "x") ix = (int)i; else if (n == "y") iy = (int)i; else if (n == "z") iz = (int)i;
+        else if (n == "nx") inx = (int)i; else if (n == "ny") iny = (int)i; else if (n == "nz") inz = (int)i;
+        else if (n == "u" || n == "s" || n == "texture_u" || n == "texture_s") iu = (int)i;
+        else if (n == "v" || n == "t" || n == "texture_v" || n == "texture_t") ivv = (int)i;
+    }
+    bool has_n = inx >= 0 && iny >= 0 && inz >= 0;
+    bool has_uv = iu >= 0 && ivv >= 0;
+
+    TriMesh m;
+    std::vector<double> vals(vprops.size());
+    for (auto& el : elements) {
+        if (el.first == "vertex") {
+            for (size_t i = 0; i < nv; ++i) {
+                if (ascii) {
+                    for (auto& v : vals) in >> v;
+                } else {
+                    for (size_t k = 0; k < vprops.size(); ++k) vals[k] = ply_read_bin(in, vprops[k].type, swap);
+                }
+                m.vertices.push_back(V3((float)vals[ix], (float)vals[iy], (float)vals[iz]));
+                if (has_n) {
+                    float nx = (float)vals[inx], ny = (float)vals[iny], nz = (float)vals[inz];
+                    float l = std::sqrt(nx * nx + ny * ny + nz * nz);
+                    if (l == 0.0f) l = 1.0f;
+                    m.normals.push_back(V3(nx / l, ny / l, nz / l));
+                }
+                if (has_uv) m.texcoords.push_back({(float)vals[iu], (float)vals[ivv]});
+            }
+        } else if (el.first == "face") {
+            for (size_t i = 0; i < nf; ++i) {
+                std::vector<uint32_t> poly;
+                for (auto& p : fprops) {
+                    if (p.is_list) {
+                        size_t cnt;
+                        if (ascii) { in >> cnt; } else { cnt = (size_t)ply_read_bin(in, p.list_count_type, swap); }
+                        std::vector<uint32_t> items(cnt);
+                        for (size_t k = 0; k < cnt; ++k) {
+                            double v;
+                            if (ascii) in >> v; else v = ply_read_bin(in, p.list_item_type, swap);
+                            items[k] = (uint32_t)v;
+                        }
+                        if (p.name == "vertex_indices" || p.name == "vertex_index") poly = items;
+                    } else {
+                        double v;
+                        if (ascii) in >> v; else v = ply_read_bin(in, p.type, swap);
+                        (void)v;
+                    }
+                }
+                for (size_t k = 1; k + 1 < poly.size(); ++k) m.faces.push_back({poly[0], poly[k], poly[k + 1]});
+            }
+        } else {
+            err = path + ": unsupported ply element " + el.first;
+            return false;
+        }
+        if (!in) { err = path + ": truncated ply"; return false; }
+    }
+    if (m.vertices.empty() || m.faces.empty()) { err = path + ": empty mesh"; return false; }
+    for (auto& f : m.faces)
+        for (auto i : f)
+            if (i >= m.vertices.size()) { err = path + ": index out of range"; return false; }
+    if (m.normals.empty()) m.compute_vertex_normals();
+    else m.fix_normals(nullptr);
+    if (m.texcoords.empty()) m.make_texcoords_normalized();
+    out = std::move(m);
+    return true;
+}
+
+// OBJ reader: positions/texcoords/normals with (v,vt,vn) de-duplication as the
+// reference does over tinyobjloader output (src/runtime/mesh/ObjFile.cpp).
+bool load_obj(const std::string& path, TriMesh& out, std::string& err) {
+    std::ifstream in(path);
+    if (!in) { err = "cannot open " + path; return false; }
+    std::vector<V3> pos, nrm;
+    std::vector<std::array<float, 2>> tex;
+    std::map<std::tuple<int, int, int>, uint32_t> remap;
+    TriMesh m;
+    bool any_normal_missing = false;
+    std::string line;
+    auto fix_index = [](int i, size_t n) { return i < 0 ? (int)n + i : i - 1; };
+    while (std::getline(in, line)) {
+        std::istringstream ss(line);
+        std::string tok;
+        ss >> tok;
+        if (tok == "v") { V3 p; ss >> p.x >> p.y >> p.z; pos.push_back(p); }
+        else if (tok == "vn") { V3 p; ss >> p.x >> p.y >> p.z; nrm.push_back(p); }
+        else if (tok == "vt") { std::array<float, 2> t{0, 0}; ss >> t[0] >> t[1]; tex.push_back(t); }
+        else if (tok == "f") {
+            std::vector<uint32_t> poly;
+            std::string c;
+            while (ss >> c) {
+                int vi = 0, ti = 0, ni = 0;
+                int parsed[3] = {0, 0, 0};
+                int which = 0;
+                std::string num;
+                for (size_t k = 0; k <= c.size(); ++k) {
+                    if (k == c.size() || c[k] == '/') {
+                        if (!num.empty()) parsed[which] = std::stoi(num);
+                        num.clear();
+                        ++which;
+                    } else {
+                        num += c[k];
+                    }
+                }
+                vi = fix_index(parsed[0], pos.size());
+                ti = parsed[1] ? fix_index(parsed[1], tex.size()) : -1;
+                ni = parsed[2] ? fix_index(parsed[2], nrm.size()) : -1;
+                if (ni < 0) any_normal_missing = true;
+                auto key = std::make_tuple(vi, ti, ni);
+                auto it = remap.find(key);
+                uint32_t id;
+                if (it == remap.end()) {
+                    id = (uint32_t)m.vertices.size();
+                    remap[key] = id;
+                    m.vertices.push_back(pos.at(vi));
+                    m.normals.push_back(ni >= 0 ? nrm.at(ni) : V3());
+                    m.texcoords.push_back(ti >= 0 ? tex.at(ti) : std::array<float, 2>{0, 0});
+                } else {
+                    id = it->second;
+                }
+                poly.push_back(id);
+            }
+            for (size_t k = 1; k + 1 < poly.size(); ++k) m.faces.push_back({poly[0], poly[k], poly[k + 1]});
+        }
+    }
+    if (m.vertices.empty() || m.faces.empty()) { err = path + ": empty mesh"; return false; }
+    if (any_normal_missing) m.compute_vertex_normals();
+    else m.fix_normals(nullptr);
+    out = std::move(m);
+    return true;
+}
+
+} // namespace igx

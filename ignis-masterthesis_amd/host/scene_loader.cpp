@@ -1,0 +1,693 @@
+// Scene JSON -> igx_scene_desc (Ignis schema subset used by the hot path).
+//
+// Stand-in for the reference loader chain, which cannot be built offline:
+//   SceneParser (src/runtime/loader/Parser.cpp) -> LoaderShape/TriMeshProvider/
+//   SphereProvider (src/runtime/shape/*.cpp) -> LoaderEntity
+//   (src/runtime/loader/LoaderEntity.cpp:32-205) -> lights/BSDFs.
+// Only the pieces the configs in BASELINE.json exercise are supported; anything
+// else is rejected with a message instead of being silently approximated.
+#include "igx_scene.h"
+
+#include "json.h"
+#include "linalg.h"
+#include "mesh.h"
+
+#include <cstring>
+#include <fstream>
+#include <memory>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+using igx::BBox;
+using igx::M4;
+using igx::TriMesh;
+using igx::V3;
+using igx::json::Value;
+
+namespace {
+
+constexpr float kPi = 3.14159265358979323846f;
+constexpr float kDeg2Rad = kPi / 180.0f;
+
+struct SceneStore {
+    igx_scene_desc desc{};
+    std::vector<std::vector<float>> vtx, nrm, tex;
+    std::vector<std::vector<uint32_t>> idx;
+    std::vector<igx_mesh> meshes;
+    std::vector<igx_shape> shapes;
+    std::vector<igx_entity> entities;
+    std::vector<igx_material> materials;
+    std::vector<igx_light> lights;
+};
+
+[[noreturn]] void fail(const std::string& m) { throw std::runtime_error(m); }
+
+std::string read_file(const std::string& path) {
+    std::ifstream in(path, std::ios::binary);
+    if (!in) fail("cannot open " + path);
+    std::stringstream ss;
+    ss << in.rdbuf();
+    return ss.str();
+}
+
+std::string dir_of(const std::string& p) {
+    auto pos = p.find_last_of('/');
+    return pos == std::string::npos ? std::string(".") : p.substr(0, pos);
+}
+
+std::string join_path(const std::string& base, const std::string& rel) {
+    if (rel.empty() || rel[0] == '/' || base.empty()) return rel;
+    return base + "/" + rel;
+}
+
+// --- property access, after SceneProperty getters (Parser.cpp:281-312) ----
+struct Props {
+    const Value* v;
+    const Value* get(const char* k) const { return v ? v->find(k) : nullptr; }
+    bool has(const char* k) const { return get(k) != nullptr; }
+    float number(const char* k, float def) const {
+        const Value* p = get(k);
+        if (!p) return def;
+        if (p->is_number()) return (float)p->num;
+        if (p->is_bool()) return p->b ? 1.f : 0.f;
+        fail(std::string("property '") + k + "' is not a number");
+    }
+    int integer(const char* k, int def) const { return (int)number(k, (float)def); }
+    bool boolean(const char* k, bool def) const {
+        const Value* p = get(k);
+        if (!p) return def;
+        if (p->is_bool()) return p->b;
+        if (p->is_number()) return p->num != 0;
+        fail(std::string("property '") + k + "' is not a bool");
+    }
+    std::string string(const char* k, const std::string& def = "") const {
+        const Value* p = get(k);
+        if (!p) return def;
+        if (!p->is_string()) fail(std::string("property '") + k + "' is not a string");
+        return p->str;
+    }
+    V3 vec3(const char* k, V3 def) const {
+        const Value* p = get(k);
+        if (!p) return def;
+        if (p->is_number()) return V3((float)p->num, (float)p->num, (float)p->num);
+        if (!p->is_array() || (p->arr.size() != 3 && p->arr.size() != 2)) fail(std::string("property '") + k + "' is not a vec3");
+        V3 r;
+        for (size_t i = 0; i < p->arr.size(); ++i) {
+            if (!p->arr[i].is_number()) fail(std::string("property '") + k + "' has non-number entries");
+            r[(int)i] = (float)p->arr[i].num;
+        }
+        return r;
+    }
+    // colour: a number is a grey value, an array an RGB triple
+    V3 color(const char* k, V3 def) const { return vec3(k, def); }
+};
+
+M4 matrix_from_array(const Value& a) {
+    size_t n = a.arr.size();
+    M4 m;
+    if (n == 9) {
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) m.at(i, j) = (float)a.arr[i * 3 + j].num;
+    } else if (n == 12 || n == 16) {
+        int rows = n == 12 ? 3 : 4;
+        for (int i = 0; i < rows; ++i)
+            for (int j = 0; j < 4; ++j) m.at(i, j) = (float)a.arr[i * 4 + j].num;
+    } else {
+        fail("transform matrix must have 9, 12 or 16 entries");
+    }
+    return m;
+}
+
+// lookAt (Parser.cpp:137-162)
+M4 look_at(V3 eye, V3 center, V3 up) {
+    V3 f = igx::normalized(center - eye);
+    if (igx::norm2(f) <= 1.1920928955e-07f) f = V3(0, 0, 1);
+    V3 u = igx::normalized(up);
+    V3 s = igx::normalized(igx::cross(f, u));
+    u = igx::cross(s, f);
+    if (igx::norm2(u) <= 1.1920928955e-07f) igx::tangent_frame(f, s, u);
+    M4 m;
+    for (int r = 0; r < 3; ++r) {
+        m.at(r, 0) = s[r];
+        m.at(r, 1) = u[r];
+        m.at(r, 2) = f[r];
+        m.at(r, 3) = eye[r];
+    }
+    return m;
+}
+
+// applyTransformProperty (Parser.cpp:164-226): ops right-multiply in order
+void apply_ops(M4& t, const Value& obj) {
+    for (auto& kv : obj.obj) {
+        const std::string& k = kv.first;
+        const Value& v = kv.second;
+        auto vec = [&](const Value& a) {
+            V3 r;
+            if (!a.is_array() || (a.arr.size() != 3 && a.arr.size() != 2)) fail("transform op '" + k + "' expects a vector");
+            for (size_t i = 0; i < a.arr.size(); ++i) r[(int)i] = (float)a.arr[i].num;
+            return r;
+        };
+        if (k == "translate") {
+            t = t * igx::translation(vec(v));
+        } else if (k == "scale") {
+            if (v.is_number()) t = t * igx::scaling(V3((float)v.num, (float)v.num, (float)v.num));
+            else t = t * igx::scaling(vec(v));
+        } else if (k == "rotate") {
+            V3 a = vec(v);
+            t = t * igx::axis_rotation(0, kDeg2Rad * a.x) * igx::axis_rotation(1, kDeg2Rad * a.y) * igx::axis_rotation(2, kDeg2Rad * a.z);
+        } else if (k == "qrotate") {
+            if (!v.is_array() || v.arr.size() != 4) fail("qrotate expects [w,x,y,z]");
+            float w = (float)v.arr[0].num, x = (float)v.arr[1].num, y = (float)v.arr[2].num, z = (float)v.arr[3].num;
+            float n = std::sqrt(w * w + x * x + y * y + z * z);
+            w /= n; x /= n; y /= n; z /= n;
+            M4 r;
+            r.at(0, 0) = 1 - 2 * (y * y + z * z); r.at(0, 1) = 2 * (x * y - z * w); r.at(0, 2) = 2 * (x * z + y * w);
+            r.at(1, 0) = 2 * (x * y + z * w); r.at(1, 1) = 1 - 2 * (x * x + z * z); r.at(1, 2) = 2 * (y * z - x * w);
+            r.at(2, 0) = 2 * (x * z - y * w); r.at(2, 1) = 2 * (y * z + x * w); r.at(2, 2) = 1 - 2 * (x * x + y * y);
+            t = t * r;
+        } else if (k == "lookat") {
+            V3 origin(0, 0, 0), target(0, 1, 0), up(0, 0, 1), dir;
+            bool has_dir = false;
+            for (auto& kv2 : v.obj) {
+                if (kv2.first == "origin") origin = vec(kv2.second);
+                else if (kv2.first == "target") target = vec(kv2.second);
+                else if (kv2.first == "up") up = vec(kv2.second);
+                else if (kv2.first == "direction") { dir = vec(kv2.second); has_dir = true; }
+            }
+            t = t * look_at(origin, has_dir ? dir + origin : target, up);
+        } else if (k == "matrix") {
+            t = t * matrix_from_array(v);
+        } else {
+            fail("unknown transform entry '" + k + "'");
+        }
+    }
+}
+
+M4 get_transform(const Props& p, const char* key = "transform") {
+    const Value* v = p.get(key);
+    M4 t;
+    if (!v) return t;
+    if (v->is_array()) {
+        if (!v->arr.empty() && v->arr[0].is_object()) {
+            for (auto& op : v->arr) apply_ops(t, op);
+        } else {
+            t = matrix_from_array(*v);
+        }
+    } else if (v->is_object()) {
+        apply_ops(t, *v);
+    } else {
+        fail(std::string("invalid transform in '") + key + "'");
+    }
+    // Transformf::makeAffine: bottom row := 0 0 0 1 (LoaderEntity.cpp:134)
+    t.at(3, 0) = t.at(3, 1) = t.at(3, 2) = 0;
+    t.at(3, 3) = 1;
+    return t;
+}
+
+// Merge externals into the main document (Parser.cpp:451-454)
+void merge_into(Value& dst, const Value& src) {
+    for (auto& kv : src.obj) {
+        Value* existing = nullptr;
+        for (auto& d : dst.obj)
+            if (d.first == kv.first) existing = &d.second;
+        if (!existing) {
+            dst.obj.push_back(kv);
+        } else if (existing->is_array() && kv.second.is_array()) {
+            existing->arr.insert(existing->arr.end(), kv.second.arr.begin(), kv.second.arr.end());
+        } else if (existing->is_object() && kv.second.is_object()) {
+            merge_into(*existing, kv.second);
+        }
+    }
+}
+
+Value load_document(const std::string& text, const std::string& base_dir, int depth = 0) {
+    if (depth > 8) fail("externals nested too deep");
+    Value doc = igx::json::parse(text);
+    if (!doc.is_object()) fail("scene root must be an object");
+    if (const Value* ext = doc.find("externals")) {
+        if (!ext->is_array()) fail("externals must be an array");
+        std::vector<Value> extra;
+        for (auto& e : ext->arr) {
+            const Value* fn = e.find("filename");
+            if (!fn || !fn->is_string()) fail("external without filename");
+            std::string path = join_path(base_dir, fn->str);
+            extra.push_back(load_document(read_file(path), dir_of(path), depth + 1));
+        }
+        for (auto& x : extra) merge_into(doc, x);
+    }
+    return doc;
+}
+
+const Value* array_of(const Value& doc, const char* key) {
+    const Value* v = doc.find(key);
+    if (v && !v->is_array()) fail(std::string("'") + key + "' must be an array");
+    return v;
+}
+
+// --- shapes -------------------------------------------------------------
+struct LoadedShape {
+    igx_shape shape{};
+    TriMesh mesh;
+    bool is_mesh = false;
+};
+
+TriMesh setup_trimesh(const std::string& type, const Props& p, const std::string& base_dir, const std::string& name) {
+    TriMesh m;
+    std::string err;
+    if (type == "triangle") {
+        m = igx::make_triangle(p.vec3("p0", V3(0, 0, 0)), p.vec3("p1", V3(1, 0, 0)), p.vec3("p2", V3(0, 1, 0)));
+    } else if (type == "rectangle") {
+        if (!p.has("p0")) {
+            float w = p.number("width", 2.0f), h = p.number("height", 2.0f);
+            V3 o = p.vec3("origin", V3(-w / 2, -h / 2, 0));
+            m = igx::make_plane(o, V3(w, 0, 0), V3(0, h, 0));
+        } else {
+            m = igx::make_rectangle(p.vec3("p0", V3(-1, -1, 0)), p.vec3("p1", V3(1, -1, 0)), p.vec3("p2", V3(1, 1, 0)), p.vec3("p3", V3(-1, 1, 0)));
+        }
+    } else if (type == "cube" || type == "box") {
+        float w = p.number("width", 2.0f), h = p.number("height", 2.0f), d = p.number("depth", 2.0f);
+        V3 o = p.vec3("origin", V3(-w / 2, -h / 2, -d / 2));
+        m = igx::make_box(o, V3(w, 0, 0), V3(0, h, 0), V3(0, 0, d));
+    } else if (type == "icosphere") {
+        m = igx::make_ico_sphere(p.vec3("center", V3()), p.number("radius", 1.0f), (uint32_t)p.integer("subdivisions", 4));
+    } else if (type == "uvsphere") {
+        m = igx::make_uv_sphere(p.vec3("center", V3()), p.number("radius", 1.0f), (uint32_t)p.integer("stacks", 32), (uint32_t)p.integer("slices", 16));
+    } else if (type == "cylinder") {
+        float br, tr;
+        if (p.has("radius")) { br = tr = p.number("radius", 1.0f); }
+        else { br = p.number("bottom_radius", 1.0f); tr = p.number("top_radius", br); }
+        m = igx::make_cylinder(p.vec3("p0", V3()), br, p.vec3("p1", V3(0, 0, 1)), tr, (uint32_t)p.integer("sections", 32), p.boolean("filled", true));
+    } else if (type == "cone") {
+        m = igx::make_cone(p.vec3("p0", V3()), p.number("radius", 1.0f), p.vec3("p1", V3(0, 0, 1)), (uint32_t)p.integer("sections", 32), p.boolean("filled", true));
+    } else if (type == "disk") {
+        m = igx::make_disk(p.vec3("origin", V3()), p.vec3("normal", V3(0, 0, 1)), p.number("radius", 1.0f), (uint32_t)p.integer("sections", 32));
+    } else if (type == "ply" || type == "obj" || type == "external") {
+        std::string fn = join_path(base_dir, p.string("filename"));
+        std::string ext = fn.size() >= 4 ? fn.substr(fn.size() - 4) : "";
+        for (auto& c : ext) c = (char)std::tolower(c);
+        bool ok;
+        if (type == "ply" || (type == "external" && ext == ".ply")) ok = igx::load_ply(fn, m, err);
+        else if (type == "obj" || (type == "external" && ext == ".obj")) ok = igx::load_obj(fn, m, err);
+        else fail("shape '" + name + "': cannot determine mesh type of " + fn);
+        if (!ok) fail("shape '" + name + "': " + err);
+    } else {
+        fail("shape '" + name + "': unsupported shape type '" + type + "'");
+    }
+    if (m.vertices.empty() || m.faces.empty()) fail("shape '" + name + "': no geometry generated");
+
+    // User options (TriMeshProvider.cpp:528-541)
+    if (p.boolean("flip_normals", false)) m.flip_normals();
+    if (p.boolean("face_normals", false)) m.setup_face_normals_as_vertex_normals();
+    else if (p.boolean("smooth_normals", false)) m.compute_vertex_normals();
+    if (p.boolean("generic_uv", false)) m.make_texcoords_normalized();
+    M4 t = get_transform(p);
+    if (!t.is_identity()) m.transform(t);
+    if (m.texcoords.size() != m.vertices.size()) m.make_texcoords_normalized();
+    return m;
+}
+
+} // namespace
+
+struct igx_scene {
+    SceneStore store;
+};
+
+static void build_scene(SceneStore& S, const Value& doc, const std::string& base_dir) {
+    // ---- film (Runtime.cpp:28-44) ----
+    S.desc.film_width = 800;
+    S.desc.film_height = 600;
+    if (const Value* film = doc.find("film")) {
+        Props fp{film};
+        if (const Value* sz = fp.get("size")) {
+            if (!sz->is_array() || sz->arr.size() != 2) fail("film.size must be [w, h]");
+            S.desc.film_width = std::max(1, (int)sz->arr[0].num);
+            S.desc.film_height = std::max(1, (int)sz->arr[1].num);
+        }
+    }
+
+    // ---- technique (PathTechnique.cpp:8-17) ----
+    igx_technique tech{64, 2, 0.0f, 1};
+    if (const Value* t = doc.find("technique")) {
+        Props tp{t};
+        std::string type = tp.string("type", "path");
+        if (type != "path") fail("unsupported technique '" + type + "' (only 'path' is on the hot path)");
+        tech.max_depth = tp.integer("max_depth", 64);
+        tech.min_depth = tp.integer("min_depth", 2);
+        tech.clamp = tp.number("clamp", 0.0f);
+        tech.nee = tp.boolean("nee", true) ? 1 : 0;
+        if (tp.boolean("aov_mis", false)) fail("technique.aov_mis (advanced shadow handling) is not supported");
+    }
+    S.desc.technique = tech;
+
+    // ---- bsdfs ----
+    std::unordered_map<std::string, igx_material> bsdfs;
+    if (const Value* arr = array_of(doc, "bsdfs")) {
+        for (auto& b : arr->arr) {
+            Props bp{&b};
+            std::string name = bp.string("name");
+            std::string type = bp.string("type");
+            igx_material m{};
+            m.light = -1;
+            m.ext_ior = 1.0f;
+            m.int_ior = 1.5046f;
+            m.kd[0] = m.kd[1] = m.kd[2] = 0.8f;
+            for (int i = 0; i < 3; ++i) m.ks[i] = m.kt[i] = 1.0f;
+            if (type == "diffuse") {
+                m.bsdf_type = IGX_BSDF_DIFFUSE;
+                V3 kd = bp.color("reflectance", V3(0.8f, 0.8f, 0.8f)); // DiffuseBSDF.cpp:17
+                m.kd[0] = kd.x; m.kd[1] = kd.y; m.kd[2] = kd.z;
+                if (bp.number("roughness", 0.0f) > 1.1920928955e-07f)
+                    fail("bsdf '" + name + "': rough (Oren-Nayar) diffuse is not supported");
+            } else if (type == "dielectric" || type == "glass") {
+                m.bsdf_type = IGX_BSDF_DIELECTRIC; // DielectricBSDF.cpp:12-38
+                V3 ks = bp.color("specular_reflectance", V3(1, 1, 1));
+                V3 kt = bp.color("specular_transmittance", V3(1, 1, 1));
+                m.ks[0] = ks.x; m.ks[1] = ks.y; m.ks[2] = ks.z;
+                m.kt[0] = kt.x; m.kt[1] = kt.y; m.kt[2] = kt.z;
+                m.ext_ior = bp.number("ext_ior", 1.0f);
+                m.int_ior = bp.number("int_ior", 1.5046f);
+                m.thin = bp.boolean("thin", false) ? 1 : 0;
+                if (bp.number("roughness", 0.0f) > 0.0f || bp.number("roughness_u", 0.0f) > 0.0f || bp.number("roughness_v", 0.0f) > 0.0f)
+                    fail("bsdf '" + name + "': rough dielectric is not supported");
+            } else {
+                fail("bsdf '" + name + "': unsupported bsdf type '" + type + "'");
+            }
+            bsdfs[name] = m;
+        }
+    }
+
+    // ---- shapes ----
+    std::unordered_map<std::string, int> shape_ids;
+    std::vector<LoadedShape> shapes;
+    if (const Value* arr = array_of(doc, "shapes")) {
+        for (auto& s : arr->arr) {
+            Props sp{&s};
+            std::string name = sp.string("name");
+            std::string type = sp.string("type");
+            LoadedShape ls;
+            if (type == "sphere") {
+                // SphereProvider::handle (SphereProvider.cpp:10-53)
+                V3 o = sp.vec3("center", V3());
+                float r = sp.number("radius", 1.0f);
+                if (r <= 0) fail("shape '" + name + "': invalid sphere radius");
+                ls.shape.type = IGX_SHAPE_SPHERE;
+                ls.shape.mesh = -1;
+                ls.shape.sphere[0] = o.x; ls.shape.sphere[1] = o.y; ls.shape.sphere[2] = o.z; ls.shape.sphere[3] = r;
+                BBox b;
+                b.extend(o + V3(r, 0, 0)); b.extend(o - V3(r, 0, 0));
+                b.extend(o + V3(0, r, 0)); b.extend(o - V3(0, r, 0));
+                b.extend(o + V3(0, 0, r)); b.extend(o - V3(0, 0, r));
+                b.inflate(1e-5f);
+                for (int i = 0; i < 3; ++i) { ls.shape.bbox_min[i] = b.min[i]; ls.shape.bbox_max[i] = b.max[i]; }
+            } else {
+                ls.mesh = setup_trimesh(type, sp, base_dir, name);
+                ls.is_mesh = true;
+                ls.shape.type = IGX_SHAPE_TRIMESH;
+                BBox b = ls.mesh.compute_bbox();
+                b.inflate(1e-5f); // TriMeshProvider.cpp:537-538
+                for (int i = 0; i < 3; ++i) { ls.shape.bbox_min[i] = b.min[i]; ls.shape.bbox_max[i] = b.max[i]; }
+                if (auto pl = igx::get_as_plane(ls.mesh)) {
+                    ls.shape.is_plane = 1;
+                    for (int i = 0; i < 3; ++i) {
+                        ls.shape.plane_origin[i] = pl->origin[i];
+                        ls.shape.plane_x[i] = pl->x_axis[i];
+                        ls.shape.plane_y[i] = pl->y_axis[i];
+                    }
+                    for (int i = 0; i < 8; ++i) ls.shape.plane_tex[i] = pl->tex[i];
+                }
+            }
+            if (shape_ids.count(name)) fail("duplicate shape name '" + name + "'");
+            shape_ids[name] = (int)shapes.size();
+            shapes.push_back(std::move(ls));
+        }
+    }
+    // ---- lights: find area-light entities first (LoaderEntity.cpp:82-84) ----
+    std::unordered_map<std::string, const Value*> area_light_of_entity;
+    const Value* lights_arr = array_of(doc, "lights");
+    if (lights_arr)
+        for (auto& l : lights_arr->arr) {
+            Props lp{&l};
+            if (lp.string("type") == "area") area_light_of_entity[lp.string("entity")] = &l;
+        }
+
+    // ---- entities, grouped by material in first-appearance order (LoaderEntity.cpp:42-103) ----
+    struct MatKey { std::string bsdf; std::string light_entity; };
+    std::vector<MatKey> mat_keys;
+    std::vector<std::vector<const Value*>> groups;
+    if (const Value* arr = array_of(doc, "entities")) {
+        for (auto& e : arr->arr) {
+            Props ep{&e};
+            std::string bsdf = ep.string("bsdf");
+            std::string name = ep.string("name");
+            if (bsdf.empty()) fail("entity '" + name + "' has no bsdf");
+            if (!bsdfs.count(bsdf)) fail("entity '" + name + "' has unknown bsdf '" + bsdf + "'");
+            if (area_light_of_entity.count(name)) {
+                mat_keys.push_back({bsdf, name});
+                groups.push_back({&e});
+            } else {
+                size_t k = 0;
+                for (; k < mat_keys.size(); ++k)
+                    if (mat_keys[k].bsdf == bsdf && mat_keys[k].light_entity.empty()) break;
+                if (k == mat_keys.size()) { mat_keys.push_back({bsdf, ""}); groups.push_back({}); }
+                groups[k].push_back(&e);
+            }
+        }
+    }
+    BBox scene_bbox;
+    std::unordered_map<std::string, int> entity_ids;
+    for (size_t mid = 0; mid < groups.size(); ++mid) {
+        igx_material m = bsdfs[mat_keys[mid].bsdf];
+        m.light = -1;
+        S.materials.push_back(m);
+        for (const Value* e : groups[mid]) {
+            Props ep{e};
+            std::string name = ep.string("name");
+            std::string shape = ep.string("shape");
+            if (!shape_ids.count(shape)) fail("entity '" + name + "' has unknown shape '" + shape + "'");
+            int sid = shape_ids[shape];
+            igx_entity ent{};
+            ent.shape = sid;
+            ent.material = (int)mid;
+            uint32_t flags = 0;
+            if (ep.boolean("camera_visible", true)) flags |= 0x1;
+            if (ep.boolean("light_visible", true)) flags |= 0x2;
+            if (ep.boolean("bounce_visible", true)) flags |= 0x4;
+            if (ep.boolean("shadow_visible", true)) flags |= 0x8;
+            ent.flags = flags;
+            M4 t = get_transform(ep);
+            M4 inv = igx::affine_inverse(t);
+            igx::M3 nm = igx::transpose3(igx::inverse3(igx::linear_of(t)));
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 4; ++c) { ent.to_global[r * 4 + c] = t.at(r, c); ent.to_local[r * 4 + c] = inv.at(r, c); }
+            for (int i = 0; i < 9; ++i) ent.normal[i] = nm.m[i];
+            // BoundingBox::transformed (math/BoundingBox.h:84-95)
+            const igx_shape& sh = shapes[sid].shape;
+            BBox eb;
+            for (int c = 0; c < 8; ++c) {
+                V3 p((c & 1) ? sh.bbox_max[0] : sh.bbox_min[0], (c & 2) ? sh.bbox_max[1] : sh.bbox_min[1], (c & 4) ? sh.bbox_max[2] : sh.bbox_min[2]);
+                eb.extend(igx::xform_point(t, p));
+            }
+            for (int i = 0; i < 3; ++i) { ent.bbox_min[i] = eb.min[i]; ent.bbox_max[i] = eb.max[i]; }
+            scene_bbox.extend(eb);
+            entity_ids[name] = (int)S.entities.size();
+            S.entities.push_back(ent);
+        }
+    }
+
+    // ---- lights ----
+    if (lights_arr) {
+        for (auto& l : lights_arr->arr) {
+            Props lp{&l};
+            std::string type = lp.string("type");
+            std::string name = lp.string("name");
+            igx_light L{};
+            L.entity = -1;
+            if (type == "area") {
+                std::string ename = lp.string("entity");
+                if (!entity_ids.count(ename)) fail("area light '" + name + "': no entity named '" + ename + "'");
+                int eid = entity_ids[ename];
+                const igx_entity& ent = S.entities[eid];
+                const igx_shape& sh = shapes[ent.shape].shape;
+                if (lp.has("power")) fail("area light '" + name + "': 'power' is not supported, use 'radiance'");
+                V3 rad = lp.color("radiance", V3(1, 1, 1));
+                if (!sh.is_plane || !lp.boolean("optimize", true))
+                    fail("area light '" + name + "': only planar emitters are supported (make_plane_area_emitter)");
+                // AreaLight.cpp:59-70, 129-145
+                M4 t;
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 0; c < 4; ++c) t.at(r, c) = ent.to_global[r * 4 + c];
+                V3 o = igx::xform_point(t, V3(sh.plane_origin[0], sh.plane_origin[1], sh.plane_origin[2]));
+                V3 xa = igx::xform_dir(t, V3(sh.plane_x[0], sh.plane_x[1], sh.plane_x[2]));
+                V3 ya = igx::xform_dir(t, V3(sh.plane_y[0], sh.plane_y[1], sh.plane_y[2]));
+                V3 n = igx::normalized(igx::cross(xa, ya));
+                L.type = IGX_LIGHT_PLANE;
+                L.entity = eid;
+                for (int i = 0; i < 3; ++i) { L.origin[i] = o[i]; L.x_axis[i] = xa[i]; L.y_axis[i] = ya[i]; L.normal[i] = n[i]; L.radiance[i] = rad[i]; }
+                L.area = igx::norm(igx::cross(xa, ya));
+                S.materials[ent.material].light = (int)S.lights.size();
+            } else if (type == "env" || type == "constant" || type == "uniform") {
+                // EnvironmentLight.cpp:28-78: constant radiance bakes to a 1x1 texture -> make_environment_light
+                V3 rad = lp.color("radiance", V3(1, 1, 1));
+                V3 scale = lp.color("scale", V3(1, 1, 1));
+                if (const Value* r = lp.get("radiance"))
+                    if (r->is_string()) fail("env light '" + name + "': textured environments are not supported");
+                L.type = IGX_LIGHT_ENV;
+                for (int i = 0; i < 3; ++i) L.radiance[i] = rad[i] * scale[i];
+            } else if (type == "point") {
+                if (lp.has("power")) fail("point light '" + name + "': 'power' is not supported");
+                V3 pos = lp.vec3("position", V3());
+                V3 I = lp.color("intensity", V3(1, 1, 1));
+                L.type = IGX_LIGHT_POINT;
+                for (int i = 0; i < 3; ++i) { L.origin[i] = pos[i]; L.radiance[i] = I[i]; }
+            } else if (type == "spot") {
+                if (lp.has("power")) fail("spot light '" + name + "': 'power' is not supported");
+                V3 pos = lp.vec3("position", V3());
+                V3 dir = igx::normalized(lp.vec3("direction", V3(0, 0, 1)));
+                V3 I = lp.color("intensity", V3(1, 1, 1));
+                L.type = IGX_LIGHT_SPOT;
+                for (int i = 0; i < 3; ++i) { L.origin[i] = pos[i]; L.normal[i] = dir[i]; L.radiance[i] = I[i]; }
+                L.cutoff = lp.number("cutoff", 30.0f) * kDeg2Rad;
+                L.falloff = lp.number("falloff", 20.0f) * kDeg2Rad;
+            } else {
+                fail("light '" + name + "': unsupported light type '" + type + "'");
+            }
+            S.lights.push_back(L);
+        }
+    }
+    if (S.lights.size() > 1) {
+        // Multiple lights use the hierarchy/cdf selectors in the reference
+        // (LoaderLight.cpp:423-440); only the uniform selector is restated.
+        if (const Value* t = doc.find("technique")) {
+            Props tp{t};
+            std::string sel = tp.string("light_selector", "uniform");
+            if (sel != "uniform") fail("light_selector '" + sel + "' is not supported (uniform only)");
+        }
+    }
+
+    // ---- meshes into flat arrays ----
+    for (auto& ls : shapes) {
+        if (ls.is_mesh) {
+            ls.shape.mesh = (int)S.vtx.size();
+            std::vector<float> v, n, t;
+            std::vector<uint32_t> ix;
+            v.reserve(ls.mesh.vertices.size() * 3);
+            for (auto& p : ls.mesh.vertices) { v.push_back(p.x); v.push_back(p.y); v.push_back(p.z); }
+            for (auto& p : ls.mesh.normals) { n.push_back(p.x); n.push_back(p.y); n.push_back(p.z); }
+            for (auto& p : ls.mesh.texcoords) { t.push_back(p[0]); t.push_back(p[1]); }
+            for (auto& f : ls.mesh.faces) { ix.push_back(f[0]); ix.push_back(f[1]); ix.push_back(f[2]); }
+            S.vtx.push_back(std::move(v));
+            S.nrm.push_back(std::move(n));
+            S.tex.push_back(std::move(t));
+            S.idx.push_back(std::move(ix));
+        }
+        S.shapes.push_back(ls.shape);
+    }
+    for (size_t i = 0; i < S.vtx.size(); ++i) {
+        igx_mesh m{};
+        m.num_vertices = (uint32_t)(S.vtx[i].size() / 3);
+        m.num_faces = (uint32_t)(S.idx[i].size() / 3);
+        m.vertices = S.vtx[i].data();
+        m.normals = S.nrm[i].data();
+        m.texcoords = S.tex[i].data();
+        m.indices = S.idx[i].data();
+        S.meshes.push_back(m);
+    }
+
+    // ---- camera (PerspectiveCamera.cpp, Camera.cpp:5-15) ----
+    igx_camera cam{};
+    cam.fov = 60.0f * kDeg2Rad;
+    cam.vertical_fov = 0;
+    cam.aspect = -1.0f;
+    cam.near_clip = 0.0f;
+    cam.far_clip = 3.4028234664e+38f;
+    const Value* camv = doc.find("camera");
+    Props cp{camv};
+    if (camv) {
+        std::string type = cp.string("type", "perspective");
+        if (type != "perspective") fail("unsupported camera type '" + type + "'");
+        if (cp.has("vfov")) { cam.vertical_fov = 1; cam.fov = cp.number("vfov", 60) * kDeg2Rad; }
+        else if (cp.has("hfov")) cam.fov = cp.number("hfov", 60) * kDeg2Rad;
+        else cam.fov = cp.number("fov", 60) * kDeg2Rad;
+        if (cp.has("aspect_ratio")) cam.aspect = cp.number("aspect_ratio", 1);
+        cam.near_clip = cp.number("near_clip", 0.0f);
+        cam.far_clip = cp.number("far_clip", 3.4028234664e+38f);
+        if (cam.far_clip < cam.near_clip) std::swap(cam.near_clip, cam.far_clip);
+        if (cp.number("aperture_radius", 0.0f) > 1.1920928955e-07f) fail("depth-of-field camera is not supported");
+    }
+    if (camv && cp.has("transform")) {
+        M4 t = get_transform(cp);
+        V3 eye = igx::xform_point(t, V3());
+        for (int i = 0; i < 3; ++i) { cam.eye[i] = eye[i]; cam.dir[i] = t.at(i, 2); cam.up[i] = t.at(i, 1); }
+    } else if (scene_bbox.empty()) {
+        cam.dir[2] = -1; cam.up[1] = 1;
+    } else {
+        // PerspectiveCamera::getOrientation without a transform
+        float ar = cam.aspect > 0 ? cam.aspect : S.desc.film_width / (float)S.desc.film_height;
+        V3 d = scene_bbox.diameter();
+        float a = d.x / (2 * (cam.vertical_fov ? ar : 1));
+        float b = d.y / (2 * (!cam.vertical_fov ? ar : 1));
+        float s = std::sin(cam.fov / 2);
+        float dist = std::abs(s) <= 1.1920928955e-07f ? 0 : std::max(a, b) * std::sqrt(1 / (s * s) - 1);
+        V3 c = scene_bbox.center();
+        cam.dir[2] = -1; cam.up[1] = 1;
+        cam.eye[0] = c.x; cam.eye[1] = c.y; cam.eye[2] = scene_bbox.max.z + dist;
+    }
+    S.desc.camera = cam;
+
+    for (int i = 0; i < 3; ++i) {
+        S.desc.scene_bbox_min[i] = scene_bbox.empty() ? 0 : scene_bbox.min[i];
+        S.desc.scene_bbox_max[i] = scene_bbox.empty() ? 0 : scene_bbox.max[i];
+    }
+    S.desc.num_meshes = (uint32_t)S.meshes.size();
+    S.desc.meshes = S.meshes.data();
+    S.desc.num_shapes = (uint32_t)S.shapes.size();
+    S.desc.shapes = S.shapes.data();
+    S.desc.num_entities = (uint32_t)S.entities.size();
+    S.desc.entities = S.entities.data();
+    S.desc.num_materials = (uint32_t)S.materials.size();
+    S.desc.materials = S.materials.data();
+    S.desc.num_lights = (uint32_t)S.lights.size();
+    S.desc.lights = S.lights.data();
+}
+
+static void set_err(char* err, size_t len, const std::string& msg) {
+    if (!err || len == 0) return;
+    std::strncpy(err, msg.c_str(), len - 1);
+    err[len - 1] = 0;
+}
+
+extern "C" igx_scene* igx_scene_load_string(const char* json_text, const char* base_dir, char* err, size_t err_len) {
+    if (!json_text) { set_err(err, err_len, "null json"); return nullptr; }
+    try {
+        std::string base = base_dir ? base_dir : ".";
+        Value doc = load_document(json_text, base);
+        auto* s = new igx_scene();
+        try {
+            build_scene(s->store, doc, base);
+        } catch (...) {
+            delete s;
+            throw;
+        }
+        return s;
+    } catch (const std::exception& e) {
+        set_err(err, err_len, e.what());
+        return nullptr;
+    }
+}
+
+extern "C" igx_scene* igx_scene_load_file(const char* path, char* err, size_t err_len) {
+    if (!path) { set_err(err, err_len, "null path"); return nullptr; }
+    try {
+        std::string text = read_file(path);
+        return igx_scene_load_string(text.c_str(), dir_of(path).c_str(), err, err_len);
+    } catch (const std::exception& e) {
+        set_err(err, err_len, e.what());
+        return nullptr;
+    }
+}
+
+extern "C" const igx_scene_desc* igx_scene_get_desc(const igx_scene* s) { return s ? &s->store.desc : nullptr; }
+extern "C" void igx_scene_free(igx_scene* s) { delete s; }

@@ -1,0 +1,283 @@
+"""ignis_amd — Python face of the MI355X wavefront path-tracing device.
+
+Mirrors the reference's Python module surface used by its integration tests
+(src/frontend/python/runtime.cpp:178-260; src/tests/integrator/common/__init__.py:68-90):
+
+    opts = ignis_amd.RuntimeOptions.makeDefault()
+    with ignis_amd.loadFromString(json_text, opts) as runtime:
+        runtime.step()
+        img = runtime.getFramebufferForHost() / runtime.IterationCount
+
+Semantics follow IG::Runtime (src/runtime/Runtime.cpp): SPI defaults to the
+reference's GPU recommendation (8 for a 1000^2 film, Runtime.cpp:61-69), each
+step() renders one iteration (Runtime::step, Runtime.cpp:292-319) and the
+framebuffer holds sum(colour)/spi per pixel until cleared.
+"""
+import ctypes as C
+import json
+import math
+import os
+
+import numpy as np
+
+from . import _native
+from ._native import EXPORTED_SYMBOLS, LIB_PATH, RenderParams, Stats, lib
+
+__all__ = ["RuntimeOptions", "Scene", "Runtime", "loadFromFile", "loadFromString", "version",
+           "EXPORTED_SYMBOLS", "LIB_PATH", "IgxError"]
+
+
+class IgxError(RuntimeError):
+    pass
+
+
+def version():
+    return lib().igx_version().decode()
+
+
+def recommend_spi(width, height, interactive=False):
+    """Runtime.cpp:61-69 for a GPU target."""
+    spi_f = 8
+    if interactive:
+        spi_f //= 2
+    spi = math.ceil(spi_f / ((width / 1000.0) * (height / 1000.0)))
+    return max(1, min(64, spi))
+
+
+class RuntimeOptions:
+    """Subset of IG::RuntimeOptions (src/runtime/RuntimeSettings.h:16-62)."""
+
+    def __init__(self):
+        self.Device = 0          # HIP device ordinal (--gpu-device)
+        self.SPI = 0             # 0 = recommended
+        self.Seed = 0
+        self.AcquireStats = False
+        self.OverrideFilmSize = (0, 0)
+        self.Capacity = 0        # paths in flight; 0 = whole iteration (<= 16M)
+
+    @staticmethod
+    def makeDefault():
+        return RuntimeOptions()
+
+
+class Scene:
+    """A loaded scene (owner of the igx_scene handle)."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    @staticmethod
+    def from_file(path):
+        err = C.create_string_buffer(2048)
+        h = lib().igx_scene_load_file(os.fsencode(path), err, len(err))
+        if not h:
+            raise IgxError(err.value.decode())
+        return Scene(h)
+
+    @staticmethod
+    def from_string(text, base_dir=None):
+        if isinstance(text, dict):
+            text = json.dumps(text)
+        err = C.create_string_buffer(2048)
+        h = lib().igx_scene_load_string(text.encode(), os.fsencode(base_dir) if base_dir else None, err, len(err))
+        if not h:
+            raise IgxError(err.value.decode())
+        return Scene(h)
+
+    @property
+    def desc_ptr(self):
+        """Raw `const igx_scene_desc*` (for C consumers such as the oracle)."""
+        return C.cast(lib().igx_scene_get_desc(self._h), C.c_void_p)
+
+    @property
+    def desc(self):
+        return lib().igx_scene_get_desc(self._h).contents
+
+    @property
+    def film_size(self):
+        d = self.desc
+        return d.film_width, d.film_height
+
+    def close(self):
+        if self._h:
+            lib().igx_scene_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Device:
+    """Thin owner of an igx_device handle (IG::Device, src/runtime/device/Device.h:14-74)."""
+
+    def __init__(self, hip_device=0):
+        self._lib = lib()
+        h = C.c_void_p()
+        st = self._lib.igx_create(int(hip_device), C.byref(h))
+        if st != 0 or not h:
+            raise IgxError(f"igx_create({hip_device}) failed with status {st}")
+        self._h = h
+
+    def _check(self, st):
+        if st != 0:
+            raise IgxError(self._lib.igx_last_error(self._h).decode())
+
+    def set_option(self, key, value):
+        self._check(self._lib.igx_set_option(self._h, key.encode(), int(value)))
+
+    def upload(self, scene):
+        self._check(self._lib.igx_upload_scene(self._h, scene.desc_ptr))
+
+    def render(self, params):
+        self._check(self._lib.igx_render(self._h, C.byref(params)))
+
+    def framebuffer(self, count):
+        out = np.zeros(count, dtype=np.float32)
+        it = C.c_uint64()
+        self._check(self._lib.igx_get_framebuffer(self._h, out.ctypes.data_as(C.POINTER(C.c_float)), count, C.byref(it)))
+        return out, int(it.value)
+
+    def framebuffer_device_ptr(self):
+        p = C.c_void_p()
+        n = C.c_size_t()
+        self._check(self._lib.igx_framebuffer_device_ptr(self._h, C.byref(p), C.byref(n)))
+        return p.value, n.value
+
+    def pack_tiles(self, params, dst_ptr, count):
+        self._check(self._lib.igx_pack_tiles(self._h, C.byref(params), C.c_void_p(dst_ptr), count))
+
+    def clear(self):
+        self._check(self._lib.igx_clear(self._h))
+
+    def stats(self):
+        s = Stats()
+        self._check(self._lib.igx_get_stats(self._h, C.byref(s)))
+        return s.as_dict()
+
+    def reset_stats(self):
+        self._check(self._lib.igx_reset_stats(self._h))
+
+    def trace_hits(self, rays, flags=0x1):
+        rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)
+        n = rays.shape[0]
+        ep = np.zeros((n, 2), dtype=np.int32)
+        tuv = np.zeros((n, 3), dtype=np.float32)
+        self._check(self._lib.igx_trace_hits(self._h, rays.ctypes.data_as(C.POINTER(C.c_float)), n, flags,
+                                             ep.ctypes.data_as(C.POINTER(C.c_int32)),
+                                             tuv.ctypes.data_as(C.POINTER(C.c_float))))
+        return ep, tuv
+
+    def trace_occlusion(self, rays, flags=0x8):
+        rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)
+        n = rays.shape[0]
+        occ = np.zeros(n, dtype=np.int32)
+        self._check(self._lib.igx_trace_occlusion(self._h, rays.ctypes.data_as(C.POINTER(C.c_float)), n, flags,
+                                                  occ.ctypes.data_as(C.POINTER(C.c_int32))))
+        return occ
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.igx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Runtime:
+    """IG::Runtime restricted to the hot path (src/runtime/Runtime.h:19-198)."""
+
+    def __init__(self, scene, opts=None):
+        opts = opts or RuntimeOptions.makeDefault()
+        self.scene = scene
+        self.options = opts
+        w, h = scene.film_size
+        if opts.OverrideFilmSize[0] > 0:
+            w, h = opts.OverrideFilmSize
+        self.FilmWidth, self.FilmHeight = int(w), int(h)
+        self.SamplesPerIteration = opts.SPI if opts.SPI > 0 else recommend_spi(self.FilmWidth, self.FilmHeight)
+        self.Seed = opts.Seed
+        self.device = Device(opts.Device)
+        if opts.AcquireStats:
+            self.device.set_option("timing", 1)
+        if opts.Capacity:
+            self.device.set_option("capacity", opts.Capacity)
+        self.device.upload(scene)
+        self._iteration = 0
+        self._frame = 0
+        self._fb_count = self.FilmWidth * self.FilmHeight * 3
+
+    @property
+    def IterationCount(self):
+        return self._iters
+
+    def _params(self, tile=None):
+        p = RenderParams()
+        p.width, p.height = self.FilmWidth, self.FilmHeight
+        p.spi = self.SamplesPerIteration
+        p.iteration = self._iteration
+        p.frame = self._frame
+        p.seed = self.Seed
+        if tile is not None:
+            p.tile_size, p.tile_offset, p.tile_stride = tile
+        return p
+
+    _iters = 0
+
+    def step(self, tile=None):
+        """Runtime::step: one iteration of SamplesPerIteration samples."""
+        self.device.render(self._params(tile))
+        self._iteration += 1
+        self._iters += 1
+
+    def getFramebufferForHost(self):
+        fb, it = self.device.framebuffer(self._fb_count)
+        self._iters = it
+        return fb.reshape(self.FilmHeight, self.FilmWidth, 3)
+
+    def clearFramebuffer(self):
+        self.device.clear()
+        self._iters = 0
+
+    def reset(self):
+        self.clearFramebuffer()
+        self._iteration = 0
+
+    def trace(self, rays):
+        """Runtime::trace (Runtime.cpp:385-407): radiance per ray, one iteration."""
+        rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)
+        p = self._params()
+        p.num_rays = rays.shape[0]
+        p.rays = rays.ctypes.data_as(C.POINTER(C.c_float))
+        self.device.clear()
+        self.device.render(p)
+        fb, it = self.device.framebuffer(rays.shape[0] * 3)
+        self.device.clear()
+        return fb.reshape(-1, 3) / max(it, 1)
+
+    def getStatistics(self):
+        return self.device.stats()
+
+    def close(self):
+        self.device.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
+
+def loadFromFile(path, opts=None):
+    return Runtime(Scene.from_file(path), opts)
+
+
+def loadFromString(text, opts=None, base_dir=None):
+    return Runtime(Scene.from_string(text, base_dir), opts)

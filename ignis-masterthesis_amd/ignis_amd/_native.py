@@ -1,0 +1,141 @@
+"""ctypes binding of the igx C-ABI (include/igx.h, include/igx_scene.h).
+
+The shared library is built in-tree (``make -C ignis-masterthesis_amd``) and is
+loaded from the package's parent directory.  There is no fallback: if the
+library is missing, importing the runtime raises, so nothing silently runs on
+the CPU.
+"""
+import ctypes as C
+import os
+
+_PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_PKG_DIR), "libigx.so")
+
+# ---- igx_scene.h ----------------------------------------------------------
+
+
+class Mesh(C.Structure):
+    _fields_ = [("num_vertices", C.c_uint32), ("num_faces", C.c_uint32),
+                ("vertices", C.POINTER(C.c_float)), ("normals", C.POINTER(C.c_float)),
+                ("texcoords", C.POINTER(C.c_float)), ("indices", C.POINTER(C.c_uint32))]
+
+
+class Shape(C.Structure):
+    _fields_ = [("type", C.c_int32), ("mesh", C.c_int32), ("sphere", C.c_float * 4),
+                ("bbox_min", C.c_float * 3), ("bbox_max", C.c_float * 3), ("is_plane", C.c_int32),
+                ("plane_origin", C.c_float * 3), ("plane_x", C.c_float * 3), ("plane_y", C.c_float * 3),
+                ("plane_tex", C.c_float * 8)]
+
+
+class Entity(C.Structure):
+    _fields_ = [("shape", C.c_int32), ("material", C.c_int32), ("flags", C.c_uint32),
+                ("to_global", C.c_float * 12), ("to_local", C.c_float * 12), ("normal", C.c_float * 9),
+                ("bbox_min", C.c_float * 3), ("bbox_max", C.c_float * 3)]
+
+
+class Material(C.Structure):
+    _fields_ = [("bsdf_type", C.c_int32), ("light", C.c_int32), ("thin", C.c_int32), ("pad", C.c_int32),
+                ("kd", C.c_float * 3), ("ks", C.c_float * 3), ("kt", C.c_float * 3),
+                ("ext_ior", C.c_float), ("int_ior", C.c_float)]
+
+
+class Light(C.Structure):
+    _fields_ = [("type", C.c_int32), ("entity", C.c_int32), ("radiance", C.c_float * 3),
+                ("origin", C.c_float * 3), ("x_axis", C.c_float * 3), ("y_axis", C.c_float * 3),
+                ("normal", C.c_float * 3), ("area", C.c_float), ("cutoff", C.c_float), ("falloff", C.c_float)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("eye", C.c_float * 3), ("dir", C.c_float * 3), ("up", C.c_float * 3), ("fov", C.c_float),
+                ("vertical_fov", C.c_int32), ("aspect", C.c_float), ("near_clip", C.c_float), ("far_clip", C.c_float)]
+
+
+class Technique(C.Structure):
+    _fields_ = [("max_depth", C.c_int32), ("min_depth", C.c_int32), ("clamp", C.c_float), ("nee", C.c_int32)]
+
+
+class SceneDesc(C.Structure):
+    _fields_ = [("film_width", C.c_int32), ("film_height", C.c_int32), ("camera", Camera),
+                ("technique", Technique),
+                ("num_meshes", C.c_uint32), ("meshes", C.POINTER(Mesh)),
+                ("num_shapes", C.c_uint32), ("shapes", C.POINTER(Shape)),
+                ("num_entities", C.c_uint32), ("entities", C.POINTER(Entity)),
+                ("num_materials", C.c_uint32), ("materials", C.POINTER(Material)),
+                ("num_lights", C.c_uint32), ("lights", C.POINTER(Light)),
+                ("scene_bbox_min", C.c_float * 3), ("scene_bbox_max", C.c_float * 3)]
+
+
+# ---- igx.h ----------------------------------------------------------------
+
+class RenderParams(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("spi", C.c_int32), ("iteration", C.c_int32),
+                ("frame", C.c_int32), ("seed", C.c_int32), ("tile_size", C.c_int32), ("tile_offset", C.c_int32),
+                ("tile_stride", C.c_int32), ("num_rays", C.c_int32), ("rays", C.POINTER(C.c_float))]
+
+
+class Stats(C.Structure):
+    _fields_ = [("camera_rays", C.c_uint64), ("bounce_rays", C.c_uint64), ("shadow_rays", C.c_uint64),
+                ("iterations", C.c_uint64), ("launches_extend", C.c_uint64), ("launches_shadow", C.c_uint64),
+                ("ms_extend", C.c_double), ("ms_shadow", C.c_double), ("ms_generate", C.c_double),
+                ("ms_resolve", C.c_double), ("ms_render", C.c_double),
+                ("node_visits", C.c_uint64), ("leaf_visits", C.c_uint64), ("tri_tests", C.c_uint64),
+                ("blas_enters", C.c_uint64), ("shadow_node_visits", C.c_uint64),
+                ("shadow_leaf_visits", C.c_uint64), ("shadow_tri_tests", C.c_uint64),
+                ("shadow_blas_enters", C.c_uint64)]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+# every symbol include/igx.h and include/igx_scene.h declare
+EXPORTED_SYMBOLS = [
+    "igx_scene_load_file", "igx_scene_load_string", "igx_scene_get_desc", "igx_scene_free",
+    "igx_create", "igx_destroy", "igx_last_error", "igx_version", "igx_set_option", "igx_upload_scene",
+    "igx_render", "igx_get_framebuffer", "igx_framebuffer_device_ptr", "igx_pack_tiles", "igx_clear",
+    "igx_get_stats", "igx_reset_stats", "igx_trace_hits", "igx_trace_occlusion",
+]
+
+_lib = None
+
+
+def lib():
+    """Load libigx.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libigx.so not found at {LIB_PATH}; build it with `make -C ignis-masterthesis_amd`")
+    L = C.CDLL(LIB_PATH)
+    vp = C.c_void_p
+    L.igx_scene_load_file.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t]
+    L.igx_scene_load_file.restype = vp
+    L.igx_scene_load_string.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_size_t]
+    L.igx_scene_load_string.restype = vp
+    L.igx_scene_get_desc.argtypes = [vp]
+    L.igx_scene_get_desc.restype = C.POINTER(SceneDesc)
+    L.igx_scene_free.argtypes = [vp]
+    L.igx_scene_free.restype = None
+    L.igx_create.argtypes = [C.c_int, C.POINTER(vp)]
+    L.igx_destroy.argtypes = [vp]
+    L.igx_last_error.argtypes = [vp]
+    L.igx_last_error.restype = C.c_char_p
+    L.igx_version.argtypes = []
+    L.igx_version.restype = C.c_char_p
+    L.igx_set_option.argtypes = [vp, C.c_char_p, C.c_int64]
+    L.igx_upload_scene.argtypes = [vp, vp]
+    L.igx_render.argtypes = [vp, C.POINTER(RenderParams)]
+    L.igx_get_framebuffer.argtypes = [vp, C.POINTER(C.c_float), C.c_size_t, C.POINTER(C.c_uint64)]
+    L.igx_framebuffer_device_ptr.argtypes = [vp, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
+    L.igx_pack_tiles.argtypes = [vp, C.POINTER(RenderParams), C.c_void_p, C.c_size_t]
+    L.igx_clear.argtypes = [vp]
+    L.igx_get_stats.argtypes = [vp, C.POINTER(Stats)]
+    L.igx_reset_stats.argtypes = [vp]
+    L.igx_trace_hits.argtypes = [vp, C.POINTER(C.c_float), C.c_int32, C.c_uint32, C.POINTER(C.c_int32),
+                                 C.POINTER(C.c_float)]
+    L.igx_trace_occlusion.argtypes = [vp, C.POINTER(C.c_float), C.c_int32, C.c_uint32, C.POINTER(C.c_int32)]
+    for name in ["igx_create", "igx_destroy", "igx_set_option", "igx_upload_scene", "igx_render",
+                 "igx_get_framebuffer", "igx_framebuffer_device_ptr", "igx_pack_tiles", "igx_clear",
+                 "igx_get_stats", "igx_reset_stats", "igx_trace_hits", "igx_trace_occlusion"]:
+        getattr(L, name).restype = C.c_int
+    _lib = L
+    return L

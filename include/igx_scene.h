@@ -1,0 +1,146 @@
+/*
+ * igx_scene.h — scene description handed across the drop-in boundary.
+ *
+ * This is the data the reference's loader hands to its device through
+ * `IG::SceneSettings` (src/runtime/device/Device.h:25-30), restated as plain C
+ * structs.  The reference passes a `SceneDatabase*` whose tables are produced by
+ * `TriMeshProvider::handle` (src/runtime/shape/TriMeshProvider.cpp:480-617),
+ * `SphereProvider::handle` (src/runtime/shape/SphereProvider.cpp:10-53),
+ * `LoaderEntity::load` (src/runtime/loader/LoaderEntity.cpp:32-205) and the
+ * light/BSDF serialisers.  The reference turns materials and lights into JIT
+ * code; here they are data (material and light tables), because there is no
+ * Artic JIT in this build (SURVEY.md §7 "hard parts").
+ *
+ * All pointers inside an igx_scene_desc are owned by the igx_scene handle that
+ * produced them (igx_scene_load_*); igx_upload_scene copies what it needs.
+ */
+#ifndef IGX_SCENE_H
+#define IGX_SCENE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- shapes ------------------------------------------------------------ */
+enum { IGX_SHAPE_TRIMESH = 0, IGX_SHAPE_SPHERE = 1 };
+
+/* Object-space triangle mesh after the shape's own transform and flip_normals
+ * were baked in (TriMeshProvider.cpp:529-541).  Indices are 3 per face. */
+typedef struct igx_mesh {
+    uint32_t num_vertices;
+    uint32_t num_faces;
+    const float* vertices;   /* 3 * num_vertices */
+    const float* normals;    /* 3 * num_vertices (unit) */
+    const float* texcoords;  /* 2 * num_vertices */
+    const uint32_t* indices; /* 3 * num_faces */
+} igx_mesh;
+
+typedef struct igx_shape {
+    int32_t type;        /* IGX_SHAPE_* */
+    int32_t mesh;        /* index into meshes for TRIMESH, -1 otherwise */
+    float sphere[4];     /* origin.xyz, radius for SPHERE */
+    float bbox_min[3];   /* local bbox, inflated by 1e-5 (TriMeshProvider.cpp:537-538) */
+    float bbox_max[3];
+    /* plane representation (TriMesh::getAsPlane, mesh/TriMesh.cpp:520-634) */
+    int32_t is_plane;
+    float plane_origin[3], plane_x[3], plane_y[3];
+    float plane_tex[8];  /* 4 texcoords */
+} igx_shape;
+
+/* ---- entities ---------------------------------------------------------- */
+/* Matrices are 3x4 row-major: m[r*4+c].  normal is 3x3 row-major.  The
+ * reference stores the same three matrices per entity, 36 floats
+ * (LoaderEntity.cpp:150-162), column-major. */
+typedef struct igx_entity {
+    int32_t shape;
+    int32_t material;
+    uint32_t flags;         /* visibility flags 0x1 camera 0x2 light 0x4 bounce 0x8 shadow */
+    float to_global[12];
+    float to_local[12];
+    float normal[9];        /* inverse-transpose of the linear part of to_global */
+    float bbox_min[3];      /* world-space bbox = local bbox transformed (LoaderEntity.cpp:141) */
+    float bbox_max[3];
+} igx_entity;
+
+/* ---- materials --------------------------------------------------------- */
+enum { IGX_BSDF_DIFFUSE = 0, IGX_BSDF_DIELECTRIC = 1 };
+
+typedef struct igx_material {
+    int32_t bsdf_type;     /* IGX_BSDF_* */
+    int32_t light;         /* index of the area light emitting from this material, -1 if none */
+    int32_t thin;          /* dielectric: thin interface */
+    int32_t pad;
+    float kd[3];           /* diffuse reflectance */
+    float ks[3];           /* specular reflectance */
+    float kt[3];           /* specular transmittance */
+    float ext_ior, int_ior;
+} igx_material;
+
+/* ---- lights ------------------------------------------------------------ */
+enum {
+    IGX_LIGHT_PLANE = 1, /* area light on a planar entity: make_plane_area_emitter (light/area.art:107-240) */
+    IGX_LIGHT_ENV   = 2, /* constant environment, spherical sampling (light/env.art:73-98) */
+    IGX_LIGHT_POINT = 3, /* light/point.art:1-18 */
+    IGX_LIGHT_SPOT  = 4  /* light/spot.art:8-60 */
+};
+
+typedef struct igx_light {
+    int32_t type;
+    int32_t entity;        /* area lights: emitting entity, -1 otherwise */
+    float radiance[3];     /* radiance (area/env) or intensity (point/spot) */
+    float origin[3];       /* plane origin / point position / spot position */
+    float x_axis[3];       /* plane */
+    float y_axis[3];       /* plane */
+    float normal[3];       /* plane normal, spot direction */
+    float area;            /* plane area */
+    float cutoff, falloff; /* spot, radians */
+} igx_light;
+
+/* ---- camera / technique ------------------------------------------------ */
+typedef struct igx_camera {
+    float eye[3], dir[3], up[3];
+    float fov;             /* radians */
+    int32_t vertical_fov;  /* 1: fov is vertical (compute_scale_from_vfov) */
+    float aspect;          /* <= 0: use film width / height */
+    float near_clip, far_clip;
+} igx_camera;
+
+typedef struct igx_technique {
+    int32_t max_depth;     /* PathTechnique.cpp:11, default 64 */
+    int32_t min_depth;     /* default 2 */
+    float clamp;           /* <= 0: no clamping */
+    int32_t nee;           /* next-event estimation on */
+} igx_technique;
+
+typedef struct igx_scene_desc {
+    int32_t film_width, film_height;
+    igx_camera camera;
+    igx_technique technique;
+    uint32_t num_meshes;    const igx_mesh* meshes;
+    uint32_t num_shapes;    const igx_shape* shapes;
+    uint32_t num_entities;  const igx_entity* entities;
+    uint32_t num_materials; const igx_material* materials;
+    uint32_t num_lights;    const igx_light* lights;
+    float scene_bbox_min[3], scene_bbox_max[3];
+} igx_scene_desc;
+
+/* ---- loader C-ABI (stand-in for the reference's Loader, src/runtime/loader) */
+typedef struct igx_scene igx_scene;
+
+/* Load a scene JSON file (Ignis schema subset).  Relative mesh paths resolve
+ * against the directory of `path`.  Returns NULL and fills err (if given) on
+ * failure.  Mirrors SceneParser::loadFromFile + Loader::load
+ * (src/runtime/Runtime.cpp:143-163, 202-290). */
+igx_scene* igx_scene_load_file(const char* path, char* err, size_t err_len);
+/* Same, from a JSON string; `base_dir` resolves external files (may be NULL). */
+igx_scene* igx_scene_load_string(const char* json, const char* base_dir, char* err, size_t err_len);
+const igx_scene_desc* igx_scene_get_desc(const igx_scene* scene);
+void igx_scene_free(igx_scene* scene);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,1075 @@
+/*
+ * oracle.c — CPU restatement of the reference path (TEST INFRASTRUCTURE).
+ * See oracle.h for scope and citations.  Plain C11 + pthreads; no code from
+ * the product library (ignis-masterthesis_amd/) is used here.
+ */
+#include "oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <unistd.h>
+
+#define FLT_EPS_ 1.1920928955e-07f   /* core/common.art:3 */
+#define FLT_MAX_ 3.4028234664e+38f   /* core/common.art:4 */
+#define PI_ 3.14159265359f           /* core/common.art:7 */
+#define INV_PI_ 0.31830988618379067154f
+
+#define RAY_CAMERA 0x1u
+#define RAY_BOUNCE 0x4u
+#define RAY_SHADOW 0x8u
+#define RAY_TYPE_MASK 0xFu
+
+/* ------------------------------------------------------------------------ */
+typedef struct { float x, y, z; } v3;
+static inline v3 V(float x, float y, float z) { v3 r = {x, y, z}; return r; }
+static inline v3 vadd(v3 a, v3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline v3 vsub(v3 a, v3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline v3 vneg(v3 a) { return V(-a.x, -a.y, -a.z); }
+static inline v3 vmulf(v3 a, float s) { return V(a.x * s, a.y * s, a.z * s); }
+static inline v3 vmul(v3 a, v3 b) { return V(a.x * b.x, a.y * b.y, a.z * b.z); }
+static inline float vdot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static inline v3 vcross(v3 a, v3 b) { return V(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+static inline float vlen(v3 a) { return sqrtf(vdot(a, a)); }
+static inline v3 vnormalize(v3 a) { return vmulf(a, 1.0f / vlen(a)); }
+
+/* core/common.art:95-98, 167-171 */
+static inline float safe_rcp(float x) {
+    float ax = x > 0 ? x : -x;
+    if (ax < 1e-8f) return copysignf(FLT_MAX_, x);
+    return 1.0f / x;
+}
+static inline float safe_div(float a, float b) { return fabsf(b) <= FLT_EPS_ ? 0.0f : a / b; }
+static inline float safe_sqrt(float a) { return sqrtf(fmaxf(0.0f, a)); }
+static inline float clampf_(float v, float l, float u) { return fminf(u, fmaxf(l, v)); }
+static inline float sum_of_prod(float a, float b, float c, float d) {
+    float cd = c * d;
+    float s = fmaf(a, b, cd);
+    float err = fmaf(c, d, -cd);
+    return s + err;
+}
+static inline float lerp2(float a, float b, float c, float k1, float k2) { return (1 - k1 - k2) * a + k1 * b + k2 * c; }
+
+/* make_orthonormal_mat3x3 (core/matrix.art:20-28) */
+typedef struct { v3 t, b, n; } frame_t;
+static frame_t make_frame(v3 n) {
+    float sign = copysignf(1.0f, n.z);
+    float a = -1.0f / (sign + n.z);
+    float b = n.x * n.y * a;
+    frame_t f;
+    f.t = V(1 + sign * n.x * n.x * a, sign * b, -sign * n.x);
+    f.b = V(b, sign + n.y * n.y * a, -n.y);
+    f.n = n;
+    return f;
+}
+static inline v3 frame_to_world(const frame_t* f, v3 v) {
+    return V(f->t.x * v.x + f->b.x * v.y + f->n.x * v.z, f->t.y * v.x + f->b.y * v.y + f->n.y * v.z,
+             f->t.z * v.x + f->b.z * v.y + f->n.z * v.z);
+}
+
+/* ---- RNG (core/random.art) --------------------------------------------- */
+static inline uint32_t hash_combine(uint32_t h, uint32_t d) {
+    h = (h * 16777619u) ^ (d & 0xFFu);
+    h = (h * 16777619u) ^ ((d >> 8) & 0xFFu);
+    h = (h * 16777619u) ^ ((d >> 16) & 0xFFu);
+    h = (h * 16777619u) ^ ((d >> 24) & 0xFFu);
+    return h;
+}
+uint32_t oracle_random_seed(int32_t sample, int32_t iter, int32_t frame, int32_t x, int32_t y, int32_t user) {
+    uint32_t h = 0x811C9DC5u;
+    h = hash_combine(h, (uint32_t)sample);
+    h = hash_combine(h, (uint32_t)iter);
+    h = hash_combine(h, (uint32_t)frame);
+    h = hash_combine(h, (uint32_t)x);
+    h = hash_combine(h, (uint32_t)y);
+    h = hash_combine(h, (uint32_t)user);
+    return h;
+}
+static inline uint32_t tea(uint32_t v0, uint32_t v1) {
+    uint32_t sum = 0;
+    for (int i = 0; i < 4; ++i) {
+        sum += 0x9e3779b9u;
+        v0 += ((v1 << 4) + 0xa341316cu) ^ (v1 + sum) ^ ((v1 >> 5) + 0xc8013ea4u);
+        v1 += ((v0 << 4) + 0xad90777du) ^ (v0 + sum) ^ ((v0 >> 5) + 0x7e95761eu);
+    }
+    return v1;
+}
+typedef struct { uint32_t seed, counter; } rng_t;
+static inline uint32_t rng_u32(rng_t* r) { return tea(r->seed, r->counter++); }
+static inline float rng_f32(rng_t* r) {
+    uint32_t x = rng_u32(r);
+    uint32_t b = (x & 0x7FFFFFu) | 0x3F800000u;
+    float f;
+    memcpy(&f, &b, 4);
+    return f - 1.0f;
+}
+static inline int rng_i32(rng_t* r, int s, int e) {
+    uint32_t range = (uint32_t)(e - s);
+    if (range == 0xFFFFFFFFu) return (int)rng_u32(r) + s;
+    uint32_t erange = range + 1;
+    uint32_t scaling = 0xFFFFFFFFu / erange;
+    uint32_t past = erange * scaling;
+    uint32_t ret = rng_u32(r);
+    while (ret >= past) ret = rng_u32(r);
+    return (int)(ret / scaling) + s;
+}
+float oracle_next_f32(uint32_t seed, uint32_t* counter) {
+    rng_t r = {seed, *counter};
+    float f = rng_f32(&r);
+    *counter = r.counter;
+    return f;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Scene                                                                     */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    float lo[3], hi[3];
+    int32_t ref; /* >= 0 inner node, < 0 leaf: ~(first << 4 | (count-1)) */
+} ochild;
+typedef struct { ochild c[2]; } onode;
+
+typedef struct {
+    onode* nodes;
+    int num_nodes;
+    int32_t* order; /* leaf slot -> primitive */
+} obvh;
+
+typedef struct {
+    int type; /* 0 mesh, 1 sphere */
+    int mesh;
+    float sphere[4];
+    obvh bvh;
+    /* Tri with e1 = v0 - v1, e2 = v2 - v0, n = cross(e1, e2) per slot (shapes/trimesh.art:116-122) */
+    float* tri; /* 12 floats per slot */
+} oshape;
+
+typedef struct {
+    int type, infinite, delta;
+    float rad[3];
+    float origin[3], ex[3], ey[3], normal[3];
+    float width, height, area;
+    float cos_cut, blend;
+} olight;
+
+struct oracle_scene {
+    igx_scene_desc desc;        /* borrowed pointers for meshes/entities/materials */
+    oshape* shapes;
+    obvh tlas;
+    olight* lights;
+    int num_lights, num_infinite;
+    int* mat_light;             /* remapped light index per material */
+    float scene_radius;
+};
+
+/* ---- simple object-median BVH2 builder (independent of the product's SAH builder) */
+typedef struct {
+    const float* bmin;
+    const float* bmax;
+    int32_t* idx;
+    onode* nodes;
+    int num_nodes, cap;
+    int max_leaf;
+    int axis;
+} obuild;
+
+static obuild* g_sort_ctx; /* qsort context (builders run single-threaded) */
+static int cmp_centroid(const void* a, const void* b) {
+    int32_t ia = *(const int32_t*)a, ib = *(const int32_t*)b;
+    int ax = g_sort_ctx->axis;
+    float ca = g_sort_ctx->bmin[3 * ia + ax] + g_sort_ctx->bmax[3 * ia + ax];
+    float cb = g_sort_ctx->bmin[3 * ib + ax] + g_sort_ctx->bmax[3 * ib + ax];
+    if (ca < cb) return -1;
+    if (ca > cb) return 1;
+    return ia < ib ? -1 : (ia > ib);
+}
+static void range_box(obuild* b, int first, int count, float* lo, float* hi) {
+    for (int k = 0; k < 3; ++k) { lo[k] = FLT_MAX_; hi[k] = -FLT_MAX_; }
+    for (int i = first; i < first + count; ++i) {
+        int p = b->idx[i];
+        for (int k = 0; k < 3; ++k) {
+            if (b->bmin[3 * p + k] < lo[k]) lo[k] = b->bmin[3 * p + k];
+            if (b->bmax[3 * p + k] > hi[k]) hi[k] = b->bmax[3 * p + k];
+        }
+    }
+}
+/* returns child ref for range */
+static int32_t build_range(obuild* b, int first, int count) {
+    if (count <= b->max_leaf) return ~((first << 4) | (count - 1));
+    float lo[3], hi[3];
+    for (int k = 0; k < 3; ++k) { lo[k] = FLT_MAX_; hi[k] = -FLT_MAX_; }
+    for (int i = first; i < first + count; ++i) {
+        int p = b->idx[i];
+        for (int k = 0; k < 3; ++k) {
+            float c = 0.5f * (b->bmin[3 * p + k] + b->bmax[3 * p + k]);
+            if (c < lo[k]) lo[k] = c;
+            if (c > hi[k]) hi[k] = c;
+        }
+    }
+    int axis = 0;
+    if (hi[1] - lo[1] > hi[axis] - lo[axis]) axis = 1;
+    if (hi[2] - lo[2] > hi[axis] - lo[axis]) axis = 2;
+    b->axis = axis;
+    g_sort_ctx = b;
+    qsort(b->idx + first, (size_t)count, sizeof(int32_t), cmp_centroid);
+    int mid = count / 2;
+    if (b->num_nodes == b->cap) {
+        b->cap = b->cap * 2 + 16;
+        b->nodes = (onode*)realloc(b->nodes, sizeof(onode) * (size_t)b->cap);
+    }
+    int me = b->num_nodes++;
+    int32_t l = build_range(b, first, mid);
+    int32_t r = build_range(b, first + mid, count - mid);
+    onode* n = &b->nodes[me];
+    range_box(b, first, mid, n->c[0].lo, n->c[0].hi);
+    range_box(b, first + mid, count - mid, n->c[1].lo, n->c[1].hi);
+    n->c[0].ref = l;
+    n->c[1].ref = r;
+    return me;
+}
+static obvh build_bvh(const float* bmin, const float* bmax, int n, int max_leaf) {
+    obuild b;
+    memset(&b, 0, sizeof(b));
+    b.bmin = bmin;
+    b.bmax = bmax;
+    b.max_leaf = max_leaf;
+    b.idx = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+    for (int i = 0; i < n; ++i) b.idx[i] = i;
+    obvh out;
+    int32_t root = n > max_leaf ? build_range(&b, 0, n) : -1;
+    if (root < 0) {
+        /* a single leaf: root node with the leaf duplicated in both children */
+        b.nodes = (onode*)malloc(sizeof(onode));
+        b.num_nodes = 1;
+        for (int k = 0; k < 2; ++k) {
+            range_box(&b, 0, n, b.nodes[0].c[k].lo, b.nodes[0].c[k].hi);
+            b.nodes[0].c[k].ref = ~((0 << 4) | (n - 1));
+        }
+    }
+    out.nodes = b.nodes;
+    out.num_nodes = b.num_nodes;
+    out.order = b.idx;
+    return out;
+}
+
+oracle_scene* oracle_scene_create(const igx_scene_desc* desc) {
+    if (!desc) return NULL;
+    oracle_scene* s = (oracle_scene*)calloc(1, sizeof(oracle_scene));
+    s->desc = *desc;
+    s->shapes = (oshape*)calloc(desc->num_shapes ? desc->num_shapes : 1, sizeof(oshape));
+    for (uint32_t i = 0; i < desc->num_shapes; ++i) {
+        const igx_shape* sh = &desc->shapes[i];
+        oshape* o = &s->shapes[i];
+        o->type = sh->type;
+        o->mesh = sh->mesh;
+        memcpy(o->sphere, sh->sphere, sizeof(o->sphere));
+        if (sh->type != IGX_SHAPE_TRIMESH) continue;
+        const igx_mesh* m = &desc->meshes[sh->mesh];
+        int nf = (int)m->num_faces;
+        float* bmin = (float*)malloc(sizeof(float) * 3 * (size_t)nf);
+        float* bmax = (float*)malloc(sizeof(float) * 3 * (size_t)nf);
+        for (int f = 0; f < nf; ++f)
+            for (int k = 0; k < 3; ++k) {
+                float lo = FLT_MAX_, hi = -FLT_MAX_;
+                for (int j = 0; j < 3; ++j) {
+                    float v = m->vertices[3 * m->indices[3 * f + j] + k];
+                    lo = fminf(lo, v);
+                    hi = fmaxf(hi, v);
+                }
+                bmin[3 * f + k] = lo;
+                bmax[3 * f + k] = hi;
+            }
+        o->bvh = build_bvh(bmin, bmax, nf, 4);
+        free(bmin);
+        free(bmax);
+        o->tri = (float*)malloc(sizeof(float) * 12 * (size_t)nf);
+        for (int slot = 0; slot < nf; ++slot) {
+            int f = o->bvh.order[slot];
+            const float* v0 = m->vertices + 3 * m->indices[3 * f];
+            const float* v1 = m->vertices + 3 * m->indices[3 * f + 1];
+            const float* v2 = m->vertices + 3 * m->indices[3 * f + 2];
+            v3 a = V(v0[0], v0[1], v0[2]);
+            v3 e1 = V(v0[0] - v1[0], v0[1] - v1[1], v0[2] - v1[2]);
+            v3 e2 = V(v2[0] - v0[0], v2[1] - v0[1], v2[2] - v0[2]);
+            v3 n = vcross(e1, e2);
+            float* t = o->tri + 12 * slot;
+            t[0] = a.x; t[1] = a.y; t[2] = a.z;
+            t[3] = e1.x; t[4] = e1.y; t[5] = e1.z;
+            t[6] = e2.x; t[7] = e2.y; t[8] = e2.z;
+            t[9] = n.x; t[10] = n.y; t[11] = n.z;
+        }
+    }
+    int ne = (int)desc->num_entities;
+    if (ne > 0) {
+        float* bmin = (float*)malloc(sizeof(float) * 3 * (size_t)ne);
+        float* bmax = (float*)malloc(sizeof(float) * 3 * (size_t)ne);
+        for (int e = 0; e < ne; ++e)
+            for (int k = 0; k < 3; ++k) {
+                bmin[3 * e + k] = desc->entities[e].bbox_min[k];
+                bmax[3 * e + k] = desc->entities[e].bbox_max[k];
+            }
+        s->tlas = build_bvh(bmin, bmax, ne, 1);
+        free(bmin);
+        free(bmax);
+    }
+    /* lights: infinite first (light/light_selector.art:26-44) */
+    s->lights = (olight*)calloc(desc->num_lights ? desc->num_lights : 1, sizeof(olight));
+    int* remap = (int*)malloc(sizeof(int) * (desc->num_lights ? desc->num_lights : 1));
+    int k = 0;
+    for (int pass = 0; pass < 2; ++pass)
+        for (uint32_t l = 0; l < desc->num_lights; ++l) {
+            const igx_light* L = &desc->lights[l];
+            int inf = L->type == IGX_LIGHT_ENV;
+            if ((pass == 0) != inf) continue;
+            olight* o = &s->lights[k];
+            o->type = L->type;
+            o->infinite = inf;
+            o->delta = L->type == IGX_LIGHT_POINT || L->type == IGX_LIGHT_SPOT;
+            memcpy(o->rad, L->radiance, sizeof(o->rad));
+            memcpy(o->origin, L->origin, sizeof(o->origin));
+            memcpy(o->normal, L->normal, sizeof(o->normal));
+            if (L->type == IGX_LIGHT_PLANE) {
+                /* make_plane_area_emitter (light/area.art:107-115) */
+                v3 xa = V(L->x_axis[0], L->x_axis[1], L->x_axis[2]);
+                v3 ya = V(L->y_axis[0], L->y_axis[1], L->y_axis[2]);
+                o->width = vlen(xa);
+                o->height = vlen(ya);
+                v3 ex = vmulf(xa, 1 / o->width), ey = vmulf(ya, 1 / o->height);
+                o->ex[0] = ex.x; o->ex[1] = ex.y; o->ex[2] = ex.z;
+                o->ey[0] = ey.x; o->ey[1] = ey.y; o->ey[2] = ey.z;
+                o->area = L->area;
+            } else if (L->type == IGX_LIGHT_SPOT) {
+                float cc = cosf(L->cutoff), cf = cosf(L->falloff);
+                o->cos_cut = cc;
+                o->blend = cf - cc;
+            }
+            remap[l] = k++;
+        }
+    s->num_lights = k;
+    s->num_infinite = 0;
+    for (int i = 0; i < k; ++i) s->num_infinite += s->lights[i].infinite;
+    s->mat_light = (int*)malloc(sizeof(int) * (desc->num_materials ? desc->num_materials : 1));
+    for (uint32_t m = 0; m < desc->num_materials; ++m) {
+        int l = desc->materials[m].light;
+        s->mat_light[m] = (l >= 0 && (uint32_t)l < desc->num_lights) ? remap[l] : -1;
+    }
+    free(remap);
+    float dx = desc->scene_bbox_max[0] - desc->scene_bbox_min[0];
+    float dy = desc->scene_bbox_max[1] - desc->scene_bbox_min[1];
+    float dz = desc->scene_bbox_max[2] - desc->scene_bbox_min[2];
+    s->scene_radius = sqrtf(dx * dx + dy * dy + dz * dz) / 2 * 1.01f;
+    return s;
+}
+
+void oracle_scene_free(oracle_scene* s) {
+    if (!s) return;
+    for (uint32_t i = 0; i < s->desc.num_shapes; ++i) {
+        free(s->shapes[i].bvh.nodes);
+        free(s->shapes[i].bvh.order);
+        free(s->shapes[i].tri);
+    }
+    free(s->shapes);
+    free(s->tlas.nodes);
+    free(s->tlas.order);
+    free(s->lights);
+    free(s->mat_light);
+    free(s);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Traversal (traversal/mapping_cpu.art:398-495 semantics, scalar)          */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    v3 org, dir, inv_dir, inv_org;
+    float tmin, tmax;
+    uint32_t flags;
+} oray;
+typedef struct {
+    float t, u, v;
+    int prim, ent;
+} ohit;
+typedef struct {
+    uint64_t nodes, leaves, tris;
+} otstats;
+
+/* make_ray (traversal/ray.art:27-39) */
+static oray make_ray(v3 org, v3 dir, float tmin, float tmax, uint32_t flags) {
+    oray r;
+    r.org = org;
+    r.dir = dir;
+    r.inv_dir = V(safe_rcp(dir.x), safe_rcp(dir.y), safe_rcp(dir.z));
+    r.inv_org = vneg(vmul(org, r.inv_dir));
+    r.tmin = tmin;
+    r.tmax = tmax;
+    r.flags = flags;
+    return r;
+}
+
+/* intersect_ray_box, unordered, make_default_min_max (intersection.art:46-50, 170-181) */
+static inline float dmin(float x, float y) { return x < y ? x : y; }
+static inline float dmax(float x, float y) { return x > y ? x : y; }
+static inline void ray_box(const oray* r, const float* lo, const float* hi, float* entry, float* exit) {
+    float t0x = lo[0] * r->inv_dir.x + r->inv_org.x, t1x = hi[0] * r->inv_dir.x + r->inv_org.x;
+    float t0y = lo[1] * r->inv_dir.y + r->inv_org.y, t1y = hi[1] * r->inv_dir.y + r->inv_org.y;
+    float t0z = lo[2] * r->inv_dir.z + r->inv_org.z, t1z = hi[2] * r->inv_dir.z + r->inv_org.z;
+    *entry = dmax(dmax(dmin(t0x, t1x), dmin(t0y, t1y)), dmax(dmin(t0z, t1z), r->tmin));
+    *exit = dmin(dmin(dmax(t0x, t1x), dmax(t0y, t1y)), dmin(dmax(t0z, t1z), r->tmax));
+}
+
+/* Moeller-Trumbore (intersection.art:71-101) */
+static int tri_test(const oray* r, const float* t, float* tt, float* uu, float* vv) {
+    v3 v0 = V(t[0], t[1], t[2]), e1 = V(t[3], t[4], t[5]), e2 = V(t[6], t[7], t[8]), n = V(t[9], t[10], t[11]);
+    v3 c = vsub(v0, r->org);
+    v3 rr = vcross(r->dir, c);
+    float det = vdot(n, r->dir);
+    float inv_det = 1 / det;
+    float u = vdot(rr, e2) * inv_det;
+    float v = vdot(rr, e1) * inv_det;
+    float w = 1 - u - v;
+    int mask = u >= -FLT_EPS_ && v >= -FLT_EPS_ && w >= -FLT_EPS_;
+    if (!mask) return 0;
+    float tv = vdot(c, n) * inv_det;
+    if (!(tv >= r->tmin && tv <= r->tmax)) return 0;
+    *tt = tv;
+    *uu = u > 0 ? u : 0;
+    *vv = v > 0 ? v : 0;
+    return 1;
+}
+
+/* intersect_sphere (shapes/sphere.art:104-130) */
+static int sphere_test(const oray* r, const float* sph, float* tt) {
+    v3 L = vsub(r->org, V(sph[0], sph[1], sph[2]));
+    float S = -vdot(L, r->dir);
+    float D2 = vdot(r->dir, r->dir);
+    float L2 = vdot(L, L);
+    float R2 = sph[3] * sph[3] * D2;
+    float M2 = L2 * D2 - S * S;
+    if (S < 0 || M2 > R2) return 0;
+    float Q = sqrtf(R2 - M2);
+    float ta = (S - Q) / D2, tb = (S + Q) / D2;
+    float t0 = ta > tb ? tb : ta, t1 = ta > tb ? ta : tb;
+    float th = t0 < r->tmin ? t1 : t0;
+    if (th >= r->tmin && th <= r->tmax) { *tt = th; return 1; }
+    return 0;
+}
+
+#define OSTACK 128
+typedef struct { int32_t ref; float tmin; } sentry;
+
+/* BLAS traversal in entity space (cpu_traverse_helper_prim) */
+static int traverse_blas(const oshape* sh, oray* r, int any, ohit* h, otstats* st) {
+    sentry stack[OSTACK];
+    int sp = 0;
+    int found = 0;
+    stack[sp++] = (sentry){0, r->tmin};
+    while (sp > 0) {
+        sentry e = stack[--sp];
+        if (e.tmin > r->tmax) continue; /* cull */
+        if (e.ref >= 0) {
+            st->nodes++;
+            const onode* n = &sh->bvh.nodes[e.ref];
+            float en[2], ex[2];
+            int hitc[2];
+            for (int k = 0; k < 2; ++k) {
+                ray_box(r, n->c[k].lo, n->c[k].hi, &en[k], &ex[k]);
+                hitc[k] = !(ex[k] < en[k]);
+            }
+            /* nearer child on top */
+            if (hitc[0] && hitc[1]) {
+                int first = en[0] <= en[1] ? 0 : 1;
+                stack[sp++] = (sentry){n->c[1 - first].ref, en[1 - first]};
+                stack[sp++] = (sentry){n->c[first].ref, en[first]};
+            } else if (hitc[0]) {
+                stack[sp++] = (sentry){n->c[0].ref, en[0]};
+            } else if (hitc[1]) {
+                stack[sp++] = (sentry){n->c[1].ref, en[1]};
+            }
+        } else {
+            int code = ~e.ref;
+            int first = code >> 4, count = (code & 15) + 1;
+            for (int k = 0; k < count; ++k) {
+                st->tris++;
+                float t, u, v;
+                if (tri_test(r, sh->tri + 12 * (first + k), &t, &u, &v)) {
+                    r->tmax = t;
+                    h->t = t;
+                    h->u = u;
+                    h->v = v;
+                    h->prim = sh->bvh.order[first + k];
+                    found = 1;
+                    if (any) return 1;
+                }
+            }
+        }
+    }
+    return found;
+}
+
+static int trace_scene(const oracle_scene* s, const oray* ray_in, int any, ohit* hit, otstats* st) {
+    hit->ent = -1;
+    hit->prim = -1;
+    hit->t = ray_in->tmax;
+    hit->u = hit->v = 0;
+    if (s->desc.num_entities == 0) return 0;
+    oray ray = *ray_in;
+    sentry stack[OSTACK];
+    int sp = 0;
+    stack[sp++] = (sentry){0, ray.tmin};
+    while (sp > 0) {
+        sentry e = stack[--sp];
+        if (e.tmin > ray.tmax) continue;
+        if (e.ref >= 0) {
+            st->nodes++;
+            const onode* n = &s->tlas.nodes[e.ref];
+            float en[2], ex[2];
+            int hitc[2];
+            for (int k = 0; k < 2; ++k) {
+                ray_box(&ray, n->c[k].lo, n->c[k].hi, &en[k], &ex[k]);
+                hitc[k] = !(ex[k] < en[k]);
+            }
+            if (hitc[0] && hitc[1]) {
+                int first = en[0] <= en[1] ? 0 : 1;
+                stack[sp++] = (sentry){n->c[1 - first].ref, en[1 - first]};
+                stack[sp++] = (sentry){n->c[first].ref, en[first]};
+            } else if (hitc[0]) {
+                stack[sp++] = (sentry){n->c[0].ref, en[0]};
+            } else if (hitc[1]) {
+                stack[sp++] = (sentry){n->c[1].ref, en[1]};
+            }
+            continue;
+        }
+        int code = ~e.ref;
+        int first = code >> 4, count = (code & 15) + 1;
+        for (int k = 0; k < count; ++k) {
+            st->leaves++;
+            int eid = s->tlas.order[first + k];
+            const igx_entity* ent = &s->desc.entities[eid];
+            /* check_ray_visibility (ray.art:51) */
+            if ((ray.flags & RAY_TYPE_MASK) != ((ray.flags & ent->flags) & RAY_TYPE_MASK)) continue;
+            /* intersect_ray_box_single_section on the entity box + tmin <= hit.distance */
+            float en, ex;
+            ray_box(&ray, ent->bbox_min, ent->bbox_max, &en, &ex);
+            if (!((en <= ex) && (ex >= 0))) continue;
+            if (!(en <= hit->t)) continue;
+            /* transform_ray (ray.art:53-59): no renormalisation */
+            const float* m = ent->to_local;
+            v3 lo = V(m[0] * ray.org.x + m[1] * ray.org.y + m[2] * ray.org.z + m[3],
+                      m[4] * ray.org.x + m[5] * ray.org.y + m[6] * ray.org.z + m[7],
+                      m[8] * ray.org.x + m[9] * ray.org.y + m[10] * ray.org.z + m[11]);
+            v3 ld = V(m[0] * ray.dir.x + m[1] * ray.dir.y + m[2] * ray.dir.z,
+                      m[4] * ray.dir.x + m[5] * ray.dir.y + m[6] * ray.dir.z,
+                      m[8] * ray.dir.x + m[9] * ray.dir.y + m[10] * ray.dir.z);
+            oray lr = make_ray(lo, ld, ray.tmin, ray.tmax, ray.flags);
+            const oshape* sh = &s->shapes[ent->shape];
+            ohit lh = {lr.tmax, 0, 0, -1, -1};
+            int got;
+            if (sh->type == IGX_SHAPE_SPHERE) {
+                float t;
+                got = sphere_test(&lr, sh->sphere, &t);
+                if (got) { lh.t = t; lh.prim = 0; }
+            } else {
+                got = traverse_blas(sh, &lr, any, &lh, st);
+            }
+            if (got && lh.prim != -1 && lh.t <= hit->t) {
+                hit->ent = eid;
+                hit->prim = lh.prim;
+                hit->t = lh.t;
+                hit->u = lh.u;
+                hit->v = lh.v;
+                ray.tmax = lh.t;
+                if (any) return 1;
+            }
+        }
+    }
+    return hit->ent >= 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Shading                                                                   */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    v3 point, face_normal;
+    frame_t local;
+    int entering;
+} osurf;
+
+static inline v3 xf_point(const float* m, v3 p) {
+    return V(m[0] * p.x + m[1] * p.y + m[2] * p.z + m[3], m[4] * p.x + m[5] * p.y + m[6] * p.z + m[7],
+             m[8] * p.x + m[9] * p.y + m[10] * p.z + m[11]);
+}
+static inline v3 xf_normal(const float* n, v3 p) {
+    return V(n[0] * p.x + n[1] * p.y + n[2] * p.z, n[3] * p.x + n[4] * p.y + n[5] * p.z, n[6] * p.x + n[7] * p.y + n[8] * p.z);
+}
+
+/* make_trimesh_shape.surface_element (shapes/trimesh.art:14-39); sphere (shapes/sphere.art:50-64) */
+static osurf surface_element(const oracle_scene* s, const ohit* h, const oray* r) {
+    const igx_entity* ent = &s->desc.entities[h->ent];
+    const oshape* sh = &s->shapes[ent->shape];
+    osurf out;
+    out.point = vadd(r->org, vmulf(r->dir, h->t));
+    if (sh->type == IGX_SHAPE_SPHERE) {
+        v3 dir = vsub(out.point, xf_point(ent->to_global, V(sh->sphere[0], sh->sphere[1], sh->sphere[2])));
+        float l = vlen(dir);
+        v3 n = vmulf(dir, 1 / l);
+        out.entering = 1;
+        out.face_normal = n;
+        out.local = make_frame(n);
+        return out;
+    }
+    const igx_mesh* m = &s->desc.meshes[sh->mesh];
+    const uint32_t* f = m->indices + 3 * h->prim;
+    v3 p0 = V(m->vertices[3 * f[0]], m->vertices[3 * f[0] + 1], m->vertices[3 * f[0] + 2]);
+    v3 p1 = V(m->vertices[3 * f[1]], m->vertices[3 * f[1] + 1], m->vertices[3 * f[1] + 2]);
+    v3 p2 = V(m->vertices[3 * f[2]], m->vertices[3 * f[2] + 1], m->vertices[3 * f[2] + 2]);
+    v3 v0 = xf_point(ent->to_global, p0), v1 = xf_point(ent->to_global, p1), v2 = xf_point(ent->to_global, p2);
+    v3 e1 = vsub(v1, v0), e2 = vsub(v2, v0);
+    v3 n = vcross(e1, e2);
+    float nn = vlen(n);
+    v3 fn = vmulf(n, 1 / nn);
+    v3 n0 = V(m->normals[3 * f[0]], m->normals[3 * f[0] + 1], m->normals[3 * f[0] + 2]);
+    v3 n1 = V(m->normals[3 * f[1]], m->normals[3 * f[1] + 1], m->normals[3 * f[1] + 2]);
+    v3 n2 = V(m->normals[3 * f[2]], m->normals[3 * f[2] + 1], m->normals[3 * f[2] + 2]);
+    v3 ln = V(lerp2(n0.x, n1.x, n2.x, h->u, h->v), lerp2(n0.y, n1.y, n2.y, h->u, h->v), lerp2(n0.z, n1.z, n2.z, h->u, h->v));
+    v3 normal = vnormalize(xf_normal(ent->normal, ln));
+    out.entering = vdot(r->dir, fn) <= 0;
+    out.face_normal = out.entering ? fn : vneg(fn);
+    out.local = make_frame(out.entering ? normal : vneg(normal));
+    return out;
+}
+
+/* compute_sq (light/area.art:127-176) */
+typedef struct { v3 o, n; float x0, y0, z0, x1, y1, b0, b1, k, s; } sq_t;
+static inline float safe_acos(float a) { return acosf(clampf_(a, -1, 1)); }
+static sq_t compute_sq(const olight* L, v3 from) {
+    v3 origin = V(L->origin[0], L->origin[1], L->origin[2]);
+    v3 ex = V(L->ex[0], L->ex[1], L->ex[2]), ey = V(L->ey[0], L->ey[1], L->ey[2]);
+    v3 normal = V(L->normal[0], L->normal[1], L->normal[2]);
+    v3 dir = vsub(origin, from);
+    sq_t q;
+    q.x0 = vdot(dir, ex);
+    q.y0 = vdot(dir, ey);
+    float z0_ = vdot(dir, normal);
+    q.x1 = q.x0 + L->width;
+    q.y1 = q.y0 + L->height;
+    int nsb = !signbit(z0_);
+    q.z0 = nsb ? -z0_ : z0_;
+    q.n = nsb ? vneg(normal) : normal;
+    float dx = q.x0 - q.x1, dy = q.y1 - q.y0, dz = q.x1 - q.x0, dw = q.y0 - q.y1;
+    float zx = q.y0 * dx, zy = q.x1 * dy, zz = q.y1 * dz, zw = q.x0 * dw;
+    float z02 = q.z0 * q.z0;
+    float nzx = zx / sqrtf((dx * dx) * z02 + zx * zx);
+    float nzy = zy / sqrtf((dy * dy) * z02 + zy * zy);
+    float nzz = zz / sqrtf((dz * dz) * z02 + zz * zz);
+    float nzw = zw / sqrtf((dw * dw) * z02 + zw * zw);
+    float g0 = safe_acos(-nzx * nzy);
+    float g1 = safe_acos(-nzy * nzz);
+    float g2 = safe_acos(-nzz * nzw);
+    float g3 = safe_acos(-nzw * nzx);
+    q.b0 = nzx;
+    q.b1 = nzz;
+    q.k = 2 * PI_ - g2 - g3;
+    q.s = g0 + g1 - q.k;
+    q.o = from;
+    return q;
+}
+
+typedef struct {
+    v3 pos, dir, intensity;
+    float pdf_value;
+    int pdf_solid;
+    float cos, dist;
+} odirect;
+
+static odirect light_sample_direct(const oracle_scene* s, const olight* L, rng_t* rnd, const osurf* from) {
+    odirect d;
+    v3 rad = V(L->rad[0], L->rad[1], L->rad[2]);
+    if (L->type == IGX_LIGHT_PLANE) {
+        float ux = rng_f32(rnd);
+        float uy = rng_f32(rnd);
+        sq_t q = compute_sq(L, from->point);
+        v3 ex = V(L->ex[0], L->ex[1], L->ex[2]), ey = V(L->ey[0], L->ey[1], L->ey[2]);
+        float au = fmaf(ux, q.s, q.k);
+        float fu = fmaf(cosf(au), q.b0, -q.b1) / sinf(au);
+        float cu = clampf_(copysignf(1.0f, fu) / sqrtf(sum_of_prod(fu, fu, q.b0, q.b0)), -1, 1);
+        float xu = clampf_(-(cu * q.z0) / sqrtf(fmaf(-cu, cu, 1.0f)), q.x0, q.x1);
+        float dd = sqrtf(sum_of_prod(xu, xu, q.z0, q.z0));
+        float h0 = q.y0 / sqrtf(sum_of_prod(dd, dd, q.y0, q.y0));
+        float h1 = q.y1 / sqrtf(sum_of_prod(dd, dd, q.y1, q.y1));
+        float hv = fmaf(uy, h1 - h0, h0);
+        float hv2 = hv * hv;
+        float yv = hv2 < 1 - 1e-6f ? (hv * dd) / sqrtf(1 - hv2) : q.y1;
+        v3 p = vadd(q.o, vadd(vmulf(ex, xu), vadd(vmulf(ey, yv), vmulf(q.n, q.z0))));
+        v3 dir_ = vsub(p, from->point);
+        float dist = vlen(dir_);
+        v3 dir = vmulf(dir_, safe_div(1, dist));
+        v3 normal = V(L->normal[0], L->normal[1], L->normal[2]);
+        d.pos = p;
+        d.dir = dir;
+        d.intensity = vmulf(rad, q.s);
+        d.pdf_value = safe_div(1, q.s);
+        d.pdf_solid = 1;
+        d.cos = vdot(dir, normal) * (from->entering ? -1.0f : 1.0f);
+        d.dist = dist;
+    } else if (L->type == IGX_LIGHT_ENV) {
+        float ux = rng_f32(rnd);
+        float uy = rng_f32(rnd);
+        /* equal_area_square_to_sphere (core/warp.art:63-91) */
+        float u = 2 * ux - 1, v = 2 * uy - 1;
+        float au = fabsf(u), av = fabsf(v);
+        float sd = 1 - (au + av);
+        float dd = fabsf(sd);
+        float r = 1 - dd;
+        float phi = (r == 0 ? 1.0f : (av - au) / r + 1) * PI_ / 4;
+        float ct = copysignf(1 - r * r, sd);
+        float st = safe_sqrt(2 - r * r) * r;
+        float cp = copysignf(cosf(phi), u);
+        float sp = copysignf(sinf(phi), v);
+        v3 dir = V(cp * st, sp * st, ct);
+        float pdf = 1 / (4 * PI_);
+        d.intensity = vmulf(rad, 1 / pdf);
+        d.pos = vadd(from->point, vmulf(dir, s->scene_radius));
+        d.dir = dir;
+        d.pdf_value = pdf;
+        d.pdf_solid = 1;
+        d.cos = 1.0f;
+        d.dist = s->scene_radius;
+    } else if (L->type == IGX_LIGHT_POINT) {
+        v3 pos = V(L->origin[0], L->origin[1], L->origin[2]);
+        v3 dir_ = vsub(pos, from->point);
+        float dist = vlen(dir_);
+        d.dir = vmulf(dir_, safe_div(1, dist));
+        d.pos = pos;
+        d.intensity = rad;
+        d.pdf_value = 1;
+        d.pdf_solid = 0;
+        d.cos = 1;
+        d.dist = dist;
+    } else {
+        v3 pos = V(L->origin[0], L->origin[1], L->origin[2]);
+        v3 sdir = V(L->normal[0], L->normal[1], L->normal[2]);
+        v3 od_ = vsub(pos, from->point);
+        float dist = vlen(od_);
+        v3 od = vmulf(od_, safe_div(1, dist));
+        float cos_angle = vdot(vneg(od), sdir);
+        float factor;
+        if (L->blend <= FLT_EPS_) factor = cos_angle <= L->cos_cut ? 0.0f : 1.0f;
+        else {
+            float x = clampf_((cos_angle - L->cos_cut) / L->blend, 0, 1);
+            factor = x * x * (3 - 2 * x);
+        }
+        d.intensity = vmulf(rad, factor);
+        d.pos = pos;
+        d.dir = od;
+        d.cos = -vdot(od, sdir);
+        d.pdf_value = vdot(vneg(od), sdir) > L->cos_cut ? 1.0f : 0.0f;
+        d.pdf_solid = 0;
+        d.dist = dist;
+    }
+    return d;
+}
+
+static inline float fresnel_factor(float eta, float cos_i, float cos_t) {
+    float rs = safe_div(eta * cos_i - cos_t, eta * cos_i + cos_t);
+    float rp = safe_div(cos_i - eta * cos_t, cos_i + eta * cos_t);
+    return clampf_((rs * rs + rp * rp) * 0.5f, 0, 1);
+}
+
+static inline v3 handle_color(const oracle_scene* s, v3 c) {
+    float cl = s->desc.technique.clamp;
+    if (cl > 0) return V(fminf(c.x, cl), fminf(c.y, cl), fminf(c.z, cl));
+    return c;
+}
+
+typedef struct {
+    uint64_t camera, bounce, shadow;
+    otstats tr;
+} pstats;
+
+/* One path: technique/pathtracer.art:52-200 driven bounce by bounce */
+static v3 trace_path(const oracle_scene* s, const oracle_params* p, int x, int y, int sample, int list_index, pstats* ps) {
+    const igx_technique* tech = &s->desc.technique;
+    const igx_camera* cam = &s->desc.camera;
+    int width = p->num_rays > 0 ? p->num_rays : p->width;
+    int height = p->num_rays > 0 ? 1 : p->height;
+    uint32_t seed = oracle_random_seed(sample, p->iteration, p->frame, x, y, p->seed);
+    rng_t rnd = {seed, 1};
+    oray ray;
+    if (p->num_rays > 0) {
+        const float* r = p->rays + 8 * list_index;
+        ray = make_ray(V(r[0], r[1], r[2]), V(r[3], r[4], r[5]), r[6], r[7], 0);
+    } else {
+        /* make_camera_emitter + make_perspective_camera */
+        float rx = rng_f32(&rnd);
+        float ry = rng_f32(&rnd);
+        float nx = 2 * ((float)x + rx) / (float)width - 1;
+        float ny = 1 - 2 * ((float)y + ry) / (float)height;
+        float aspect = cam->aspect > 0 ? cam->aspect : (float)width / (float)height;
+        float sx, sy;
+        if (cam->vertical_fov) { sy = tanf(cam->fov / 2); sx = sy * aspect; }
+        else { sx = tanf(cam->fov / 2); sy = sx / aspect; }
+        v3 dir = V(cam->dir[0], cam->dir[1], cam->dir[2]), up = V(cam->up[0], cam->up[1], cam->up[2]);
+        v3 right = vcross(dir, up);
+        right = vmulf(right, 1 / vlen(right));
+        v3 v = V(sx * nx, sy * ny, 1);
+        v3 w = V(right.x * v.x + up.x * v.y + dir.x * v.z, right.y * v.x + up.y * v.y + dir.y * v.z,
+                 right.z * v.x + up.z * v.y + dir.z * v.z);
+        ray = make_ray(V(cam->eye[0], cam->eye[1], cam->eye[2]), vnormalize(w), cam->near_clip, cam->far_clip, RAY_CAMERA);
+    }
+    ps->camera++;
+    uint32_t counter = rnd.counter;
+    /* init_pt_raypayload */
+    float inv_pdf = 0, eta = 1;
+    v3 contrib = V(1, 1, 1);
+    int depth = 1;
+    v3 Lsum = V(0, 0, 0);
+    float sel_pdf = s->num_lights == 0 ? 1.0f : 1.0f / (float)s->num_lights;
+    for (;;) {
+        ohit h;
+        trace_scene(s, &ray, 0, &h, &ps->tr);
+        v3 Lacc = V(0, 0, 0);
+        if (h.ent < 0) {
+            for (int li = 0; li < s->num_infinite; ++li) {
+                const olight* L = &s->lights[li];
+                if (L->delta) continue;
+                v3 emit = V(L->rad[0], L->rad[1], L->rad[2]);
+                float pdf_s = 1 / (4 * PI_);
+                float mis = tech->nee ? 1 / (1 + inv_pdf * sel_pdf * pdf_s) : 1.0f;
+                Lacc = vadd(Lacc, handle_color(s, vmulf(vmul(contrib, emit), mis)));
+            }
+            Lsum = vadd(Lsum, Lacc);
+            break;
+        }
+        osurf surf = surface_element(s, &h, &ray);
+        const igx_entity* ent = &s->desc.entities[h.ent];
+        const igx_material* mat = &s->desc.materials[ent->material];
+        int mlight = s->mat_light[ent->material];
+        if (mlight >= 0 && surf.entering) {
+            float dt = -vdot(ray.dir, surf.local.n);
+            if (dt > FLT_EPS_) {
+                const olight* L = &s->lights[mlight];
+                v3 emit = V(L->rad[0], L->rad[1], L->rad[2]);
+                float pdf_s;
+                if (L->type == IGX_LIGHT_PLANE) { sq_t q = compute_sq(L, ray.org); pdf_s = safe_div(1, q.s); }
+                else pdf_s = 1 / (4 * PI_);
+                float mis = tech->nee ? 1 / (1 + inv_pdf * sel_pdf * pdf_s) : 1.0f;
+                Lacc = vadd(Lacc, handle_color(s, vmulf(vmul(contrib, emit), mis)));
+            }
+        }
+        Lsum = vadd(Lsum, Lacc);
+        rng_t r2 = {seed, counter};
+        v3 out_dir = vneg(ray.dir);
+        int specular = mat->bsdf_type == IGX_BSDF_DIELECTRIC;
+        /* on_shadow */
+        if (tech->nee && !specular && s->num_lights > 0 && depth + 1 <= tech->max_depth) {
+            int lid = s->num_lights <= 1 ? 0 : rng_i32(&r2, 0, s->num_lights - 1);
+            const olight* L = &s->lights[lid];
+            odirect ls = light_sample_direct(s, L, &r2, &surf);
+            float pdf_l_s = (ls.pdf_solid ? ls.pdf_value : ls.pdf_value * (ls.dist * ls.dist) / ls.cos) * sel_pdf;
+            if (pdf_l_s > FLT_EPS_ && ls.cos > FLT_EPS_) {
+                v3 kd = V(mat->kd[0], mat->kd[1], mat->kd[2]);
+                float mis;
+                if (L->delta) mis = 1.0f;
+                else {
+                    float c = vdot(ls.dir, surf.local.n);
+                    float pdf_e_s = (c >= 0 ? c : 0) / PI_;
+                    mis = 1 / (1 + pdf_e_s / pdf_l_s);
+                }
+                float factor = ls.pdf_value / pdf_l_s;
+                v3 ev = vmulf(kd, fabsf(vdot(ls.dir, surf.local.n)) * INV_PI_);
+                v3 scol = handle_color(s, vmulf(vmul(ls.intensity, vmul(contrib, ev)), mis * factor));
+                oray sr = L->infinite ? make_ray(surf.point, ls.dir, 0.001f, FLT_MAX_, RAY_SHADOW)
+                                      : make_ray(surf.point, vsub(ls.pos, surf.point), 0.001f, 1 - 0.001f, RAY_SHADOW);
+                ps->shadow++;
+                ohit sh;
+                if (!trace_scene(s, &sr, 1, &sh, &ps->tr)) Lsum = vadd(Lsum, scol);
+            }
+        }
+        /* on_bounce */
+        if (!(depth + 1 <= tech->max_depth)) break;
+        v3 in_dir, bcol;
+        float bpdf, beta;
+        if (!specular) {
+            float u = rng_f32(&r2);
+            float v = rng_f32(&r2);
+            float c = safe_sqrt(v), sn = safe_sqrt(1 - v), phi = 2 * PI_ * u;
+            bpdf = c / PI_;
+            in_dir = frame_to_world(&surf.local, V(sn * cosf(phi), sn * sinf(phi), c));
+            bcol = V(mat->kd[0], mat->kd[1], mat->kd[2]);
+            beta = 1;
+        } else {
+            float n1 = mat->ext_ior, n2 = mat->int_ior;
+            float k = surf.entering ? n1 / n2 : n2 / n1;
+            v3 n = surf.local.n;
+            float cos_o = vdot(out_dir, n);
+            float ft_cos_t = 0, ft_factor = 1;
+            float eta2 = cos_o < 0 ? 1 / k : k;
+            float cos2_t = 1 - (1 - cos_o * cos_o) * eta2 * eta2;
+            if (!(cos2_t <= 0.0f)) {
+                float ct = sqrtf(cos2_t);
+                ft_cos_t = cos_o < 0 ? -ct : ct;
+                ft_factor = fresnel_factor(eta2, fabsf(cos_o), ct);
+            }
+            if (rng_f32(&r2) > ft_factor) {
+                in_dir = vsub(vmulf(n, k * cos_o - ft_cos_t), vmulf(out_dir, k));
+                bcol = V(mat->kt[0], mat->kt[1], mat->kt[2]);
+                beta = k;
+            } else {
+                in_dir = vsub(vmulf(n, 2 * vdot(n, out_dir)), out_dir);
+                bcol = V(mat->ks[0], mat->ks[1], mat->ks[2]);
+                beta = 1;
+            }
+            bpdf = 1;
+        }
+        v3 c2 = vmul(contrib, bcol);
+        float rr = 1.0f;
+        if (depth + 1 > tech->min_depth) {
+            v3 e = vmulf(c2, eta * eta);
+            rr = clampf_(fmaxf(fmaxf(e.x, e.y), e.z), 0.05f, 0.95f);
+        }
+        if (rng_f32(&r2) >= rr) break;
+        inv_pdf = specular ? 0 : 1 / bpdf;
+        contrib = vmulf(c2, 1 / rr);
+        eta = eta * beta;
+        depth = depth + 1;
+        counter = r2.counter;
+        ray = make_ray(surf.point, in_dir, 0.001f, FLT_MAX_, RAY_BOUNCE);
+        ps->bounce++;
+    }
+    return Lsum;
+}
+
+/* ------------------------------------------------------------------------ */
+/* cpu_trace: 16x16 tiles scheduled over threads (driver/mapping_cpu.art:694-836) */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    const oracle_scene* s;
+    const oracle_params* p;
+    float* fb;
+    int x0, y0, x1, y1, tiles_x, num_tiles;
+    atomic_int next;
+    pthread_mutex_t lock;
+    pstats total;
+} job_t;
+
+static void* worker(void* arg) {
+    job_t* j = (job_t*)arg;
+    pstats ps;
+    memset(&ps, 0, sizeof(ps));
+    const int T = 16;
+    int width = j->p->num_rays > 0 ? j->p->num_rays : j->p->width;
+    float inv = 1.0f / (float)j->p->spi;
+    for (;;) {
+        int t = atomic_fetch_add(&j->next, 1);
+        if (t >= j->num_tiles) break;
+        int tx = t % j->tiles_x, ty = t / j->tiles_x;
+        int xs = j->x0 + tx * T, ys = j->y0 + ty * T;
+        for (int y = ys; y < ys + T && y < j->y1; ++y)
+            for (int x = xs; x < xs + T && x < j->x1; ++x) {
+                float r = 0, g = 0, b = 0;
+                for (int smp = 0; smp < j->p->spi; ++smp) {
+                    v3 L = trace_path(j->s, j->p, x, y, smp, x, &ps);
+                    r += L.x * inv;
+                    g += L.y * inv;
+                    b += L.z * inv;
+                }
+                size_t o = 3 * ((size_t)y * width + x);
+                j->fb[o] += r;
+                j->fb[o + 1] += g;
+                j->fb[o + 2] += b;
+            }
+    }
+    pthread_mutex_lock(&j->lock);
+    j->total.camera += ps.camera;
+    j->total.bounce += ps.bounce;
+    j->total.shadow += ps.shadow;
+    j->total.tr.nodes += ps.tr.nodes;
+    j->total.tr.leaves += ps.tr.leaves;
+    j->total.tr.tris += ps.tr.tris;
+    pthread_mutex_unlock(&j->lock);
+    return NULL;
+}
+
+int oracle_render(const oracle_scene* s, const oracle_params* p, float* fb, oracle_stats* stats) {
+    if (!s || !p || !fb || p->spi < 1) return -1;
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    job_t j;
+    memset(&j, 0, sizeof(j));
+    j.s = s;
+    j.p = p;
+    j.fb = fb;
+    int width = p->num_rays > 0 ? p->num_rays : p->width;
+    int height = p->num_rays > 0 ? 1 : p->height;
+    j.x0 = p->x1 > 0 ? p->x0 : 0;
+    j.y0 = p->x1 > 0 ? p->y0 : 0;
+    j.x1 = p->x1 > 0 ? p->x1 : width;
+    j.y1 = p->x1 > 0 ? p->y1 : height;
+    j.tiles_x = (j.x1 - j.x0 + 15) / 16;
+    j.num_tiles = j.tiles_x * ((j.y1 - j.y0 + 15) / 16);
+    atomic_init(&j.next, 0);
+    pthread_mutex_init(&j.lock, NULL);
+    int nt = p->threads > 0 ? p->threads : (int)sysconf(_SC_NPROCESSORS_ONLN);
+    if (nt < 1) nt = 1;
+    if (nt > 256) nt = 256;
+    pthread_t th[256];
+    for (int i = 0; i < nt; ++i) pthread_create(&th[i], NULL, worker, &j);
+    for (int i = 0; i < nt; ++i) pthread_join(th[i], NULL);
+    pthread_mutex_destroy(&j.lock);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    if (stats) {
+        stats->camera_rays = j.total.camera;
+        stats->bounce_rays = j.total.bounce;
+        stats->shadow_rays = j.total.shadow;
+        stats->node_visits = j.total.tr.nodes;
+        stats->leaf_visits = j.total.tr.leaves;
+        stats->tri_tests = j.total.tr.tris;
+        stats->seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+        stats->threads = nt;
+    }
+    return 0;
+}
+
+void oracle_trace_hits(const oracle_scene* s, const float* rays, int32_t n, uint32_t flags, int32_t* ent_prim, float* tuv) {
+    otstats st = {0, 0, 0};
+    for (int i = 0; i < n; ++i) {
+        const float* r = rays + 8 * i;
+        oray ray = make_ray(V(r[0], r[1], r[2]), V(r[3], r[4], r[5]), r[6], r[7], flags);
+        ohit h;
+        trace_scene(s, &ray, 0, &h, &st);
+        ent_prim[2 * i] = h.ent;
+        ent_prim[2 * i + 1] = h.prim;
+        tuv[3 * i] = h.t;
+        tuv[3 * i + 1] = h.ent >= 0 ? h.u : 0;
+        tuv[3 * i + 2] = h.ent >= 0 ? h.v : 0;
+    }
+}
+
+void oracle_trace_occlusion(const oracle_scene* s, const float* rays, int32_t n, uint32_t flags, int32_t* occluded) {
+    otstats st = {0, 0, 0};
+    for (int i = 0; i < n; ++i) {
+        const float* r = rays + 8 * i;
+        oray ray = make_ray(V(r[0], r[1], r[2]), V(r[3], r[4], r[5]), r[6], r[7], flags);
+        ohit h;
+        occluded[i] = trace_scene(s, &ray, 1, &h, &st);
+    }
+}
+
+int oracle_intersect_tri(const float* tri12, const float* ray8, float* tuv) {
+    oray r = make_ray(V(ray8[0], ray8[1], ray8[2]), V(ray8[3], ray8[4], ray8[5]), ray8[6], ray8[7], 0);
+    return tri_test(&r, tri12, &tuv[0], &tuv[1], &tuv[2]);
+}
+
+int oracle_intersect_box(const float* bmin3, const float* bmax3, const float* ray8, float* t) {
+    /* intersect_ray_box_single (intersection.art:183-192) */
+    oray r = make_ray(V(ray8[0], ray8[1], ray8[2]), V(ray8[3], ray8[4], ray8[5]), ray8[6], ray8[7], 0);
+    float en, ex;
+    ray_box(&r, bmin3, bmax3, &en, &ex);
+    if ((en <= ex) && (ex >= 0)) {
+        *t = en < 1e-5f ? ex : en;
+        return 1;
+    }
+    return 0;
+}

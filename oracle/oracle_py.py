@@ -1,0 +1,134 @@
+"""ctypes wrapper of liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module, and only as the checker or the timed CPU baseline (see oracle.h).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+
+class Params(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("spi", C.c_int32), ("iteration", C.c_int32),
+                ("frame", C.c_int32), ("seed", C.c_int32), ("threads", C.c_int32),
+                ("x0", C.c_int32), ("y0", C.c_int32), ("x1", C.c_int32), ("y1", C.c_int32),
+                ("num_rays", C.c_int32), ("rays", C.POINTER(C.c_float))]
+
+
+class OStats(C.Structure):
+    _fields_ = [("camera_rays", C.c_uint64), ("bounce_rays", C.c_uint64), ("shadow_rays", C.c_uint64),
+                ("node_visits", C.c_uint64), ("leaf_visits", C.c_uint64), ("tri_tests", C.c_uint64),
+                ("seconds", C.c_double), ("threads", C.c_int32)]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing; build it with `make -C oracle`")
+        L = C.CDLL(LIB_PATH)
+        L.oracle_scene_create.argtypes = [C.c_void_p]
+        L.oracle_scene_create.restype = C.c_void_p
+        L.oracle_scene_free.argtypes = [C.c_void_p]
+        L.oracle_render.argtypes = [C.c_void_p, C.POINTER(Params), C.POINTER(C.c_float), C.POINTER(OStats)]
+        L.oracle_trace_hits.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.c_int32, C.c_uint32,
+                                        C.POINTER(C.c_int32), C.POINTER(C.c_float)]
+        L.oracle_trace_occlusion.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.c_int32, C.c_uint32,
+                                             C.POINTER(C.c_int32)]
+        L.oracle_intersect_tri.argtypes = [C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        L.oracle_intersect_box.argtypes = [C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                           C.POINTER(C.c_float)]
+        L.oracle_random_seed.argtypes = [C.c_int32] * 6
+        L.oracle_random_seed.restype = C.c_uint32
+        L.oracle_next_f32.argtypes = [C.c_uint32, C.POINTER(C.c_uint32)]
+        L.oracle_next_f32.restype = C.c_float
+        _lib = L
+    return _lib
+
+
+def fptr(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+class OracleScene:
+    """Oracle view of a scene loaded by ignis_amd.Scene (borrowed desc pointer)."""
+
+    def __init__(self, scene):
+        self.scene = scene  # keep the owner alive
+        self._h = lib().oracle_scene_create(scene.desc_ptr)
+        if not self._h:
+            raise RuntimeError("oracle_scene_create failed")
+
+    def render(self, width, height, spi, iteration=0, frame=0, seed=0, threads=0, window=None, fb=None,
+               rays=None):
+        p = Params()
+        p.width, p.height, p.spi = width, height, spi
+        p.iteration, p.frame, p.seed, p.threads = iteration, frame, seed, threads
+        if window is not None:
+            p.x0, p.y0, p.x1, p.y1 = window
+        n = width * height
+        if rays is not None:
+            rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)
+            p.num_rays = rays.shape[0]
+            p.rays = fptr(rays)
+            n = rays.shape[0]
+        if fb is None:
+            fb = np.zeros(n * 3, dtype=np.float32)
+        st = OStats()
+        rc = lib().oracle_render(self._h, C.byref(p), fptr(fb), C.byref(st))
+        if rc != 0:
+            raise RuntimeError("oracle_render failed")
+        return fb, st.as_dict()
+
+    def trace_hits(self, rays, flags=0x1):
+        rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)
+        n = rays.shape[0]
+        ep = np.zeros((n, 2), dtype=np.int32)
+        tuv = np.zeros((n, 3), dtype=np.float32)
+        lib().oracle_trace_hits(self._h, fptr(rays), n, flags, ep.ctypes.data_as(C.POINTER(C.c_int32)), fptr(tuv))
+        return ep, tuv
+
+    def trace_occlusion(self, rays, flags=0x8):
+        rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)
+        n = rays.shape[0]
+        occ = np.zeros(n, dtype=np.int32)
+        lib().oracle_trace_occlusion(self._h, fptr(rays), n, flags, occ.ctypes.data_as(C.POINTER(C.c_int32)))
+        return occ
+
+    def close(self):
+        if self._h:
+            lib().oracle_scene_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def intersect_tri(tri12, ray8):
+    t = np.ascontiguousarray(tri12, dtype=np.float32)
+    r = np.ascontiguousarray(ray8, dtype=np.float32)
+    out = np.zeros(3, dtype=np.float32)
+    hit = lib().oracle_intersect_tri(fptr(t), fptr(r), fptr(out))
+    return bool(hit), out
+
+
+def intersect_box(bmin, bmax, ray8):
+    a = np.ascontiguousarray(bmin, dtype=np.float32)
+    b = np.ascontiguousarray(bmax, dtype=np.float32)
+    r = np.ascontiguousarray(ray8, dtype=np.float32)
+    t = C.c_float()
+    hit = lib().oracle_intersect_box(fptr(a), fptr(b), fptr(r), C.byref(t))
+    return bool(hit), t.value
