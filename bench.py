@@ -1,0 +1,289 @@
+#!/usr/bin/env python3
+"""Benchmark of the wavefront traversal-and-shade loop on MI355X.
+
+Metric (BASELINE.json): Mrays/s (primary + secondary) at fixed spp, per-pixel
+L2 vs the CPU reference.  Workload = BASELINE config 2: scenes/diamond_scene.json,
+1000x1000 film, 256 spp as 32 iterations of spi 8, path tracer max_depth 64,
+seed 0.  One "step" = one full 256-spp frame.  Rays = camera rays + bounce rays
+(closest-hit traversals) + valid shadow rays (any-hit traversals), counted on
+the device.
+
+Multi-GPU (torchrun, one rank per GPU): the film is cut into 64x64 tiles dealt
+round-robin to the ranks (tile t -> rank t % N); every rank renders all 32
+iterations of its tiles, packs them, and an RCCL all_gather over xGMI assembles
+the frame.  Total work is fixed, so scaling is "strong".
+
+Output: ONE JSON line on rank 0.
+"""
+import argparse
+import ctypes as C
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ignis-masterthesis_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+TILE = 64
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", default=os.path.join(ROOT, "scenes", "diamond_scene.json"))
+    ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--spi", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample length")
+    return ap.parse_args()
+
+
+def algorithmic_bytes(stats_inst, rays_ext, rays_next, rays_shadow):
+    """Algorithmic bytes of the extend kernels (closest hit + shade), DESIGN.md §Roofline.
+
+    Per closest-hit ray: 52 B path state read + 32 B radiance read/write
+    + 64 B per BVH2 node + 64 B per instance record + 48 B per triangle
+    + 288 B of shading fetches per hit (entity 112, face 16, 3 vertices +
+    3 normals 96, material 64); plus 52 B per surviving path and 48 B per
+    shadow ray written.  Visit counts per ray come from an instrumented pass.
+    """
+    n = max(stats_inst["_rays_ext"], 1)
+    per_ray = (52 + 32 + 64.0 * stats_inst["node_visits"] / n + 64.0 * stats_inst["leaf_visits"] / n
+               + 48.0 * stats_inst["tri_tests"] / n + 288.0 * stats_inst["_hits"] / n)
+    return rays_ext * per_ray + rays_next * 52 + rays_shadow * 48, per_ray
+
+
+def load_pmc(n_gpus):
+    """Per-launch HBM traffic of the extend kernel from the committed rocprofv3 PMC summary."""
+    path = os.path.join(ROOT, "profiles", "pmc_extend.json")
+    if n_gpus != 1 or not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return float(d["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    n_gpus = max(world, 1)
+
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", init_method="env://")
+    else:
+        torch.cuda.set_device(0)
+
+    import ignis_amd
+
+    scene = ignis_amd.Scene.from_file(args.scene)
+    W, H = scene.film_size
+    spi = args.spi
+    iters = max(1, math.ceil(args.spp / spi))
+    dev = ignis_amd.Device(local_rank if world > 1 else 0)
+    dev.upload(scene)
+
+    tiles_x, tiles_y = (W + TILE - 1) // TILE, (H + TILE - 1) // TILE
+    n_tiles = tiles_x * tiles_y
+    my_tiles = (n_tiles - rank + n_gpus - 1) // n_gpus if n_gpus > 1 else 0
+    max_tiles = (n_tiles + n_gpus - 1) // n_gpus
+
+    def params(it):
+        p = ignis_amd.RenderParams()
+        p.width, p.height, p.spi, p.iteration, p.frame, p.seed = W, H, spi, it, 0, 0
+        if n_gpus > 1:
+            p.tile_size, p.tile_offset, p.tile_stride = TILE, rank, n_gpus
+        return p
+
+    gather_bufs = None
+    if n_gpus > 1:
+        pack = torch.zeros(max_tiles * TILE * TILE * 3, dtype=torch.float32, device="cuda")
+        gather_bufs = [torch.zeros_like(pack) for _ in range(n_gpus)]
+        frame = torch.zeros((tiles_y * TILE * tiles_x * TILE, 3), dtype=torch.float32, device="cuda")
+        # destination pixel of every packed slot of every rank (computed once)
+        dst = []
+        for r in range(n_gpus):
+            cnt = (n_tiles - r + n_gpus - 1) // n_gpus
+            t = np.arange(cnt) * n_gpus + r
+            ty, tx = t // tiles_x, t % tiles_x
+            yy, xx = np.mgrid[0:TILE, 0:TILE]
+            pix = ((ty[:, None, None] * TILE + yy) * (tiles_x * TILE) + tx[:, None, None] * TILE + xx).reshape(-1)
+            full = np.full(max_tiles * TILE * TILE, -1, np.int64)
+            full[: pix.size] = pix
+            dst.append(full)
+        dst = torch.from_numpy(np.concatenate(dst)).cuda()
+        valid = dst >= 0
+        dst_valid = dst[valid]
+
+    def render_frame():
+        dev.clear()
+        for it in range(iters):
+            dev.render(params(it))
+        if n_gpus > 1:
+            # pack owned tiles, RCCL all_gather over xGMI, assemble on every rank
+            torch.cuda.synchronize()
+            dev.pack_tiles(params(0), pack.data_ptr(), pack.numel())
+            dist.all_gather(gather_bufs, pack)
+            allpix = torch.cat(gather_bufs).view(-1, 3)
+            frame[dst_valid] = allpix[valid]
+
+    for _ in range(args.warmup):
+        render_frame()
+
+    dev.reset_stats()
+    dev.set_option("timing", 1)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        render_frame()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st = dev.stats()
+    dev.set_option("timing", 0)
+
+    rays_ext = st["camera_rays"] + st["bounce_rays"]
+    rays_local = rays_ext + st["shadow_rays"]
+    totals = np.array([rays_local, st["camera_rays"], st["bounce_rays"], st["shadow_rays"]], dtype=np.float64)
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        tt = torch.tensor(totals, dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.SUM)
+        totals = tt.cpu().numpy()
+
+    # ---- roofline of the dominant kernel (extend), live HIP-event timing ----
+    # instrumented (untimed) pass for BVH visit counts per ray
+    dev.reset_stats()
+    dev.set_option("instrument", 1)
+    dev.clear()
+    dev.render(params(0))
+    inst = dev.stats()
+    dev.set_option("instrument", 0)
+    inst["_rays_ext"] = inst["camera_rays"] + inst["bounce_rays"]
+    inst["_hits"] = inst["shaded_hits"]
+    alg_bytes, bytes_per_ray = algorithmic_bytes(inst, rays_ext, st["bounce_rays"], st["shadow_rays"])
+    launches = max(st["launches_extend"], 1)
+    avg_launch_s = st["ms_extend"] / 1e3 / launches
+    achieved = (alg_bytes / launches) / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+    traffic = load_pmc(n_gpus)
+
+    result = None
+    if rank == 0:
+        total_rays = float(totals[0])
+        value = total_rays / elapsed / 1e6
+        samples = float(W * H * iters * spi * args.steps)
+        cpu = None
+        parity = None
+        if n_gpus == 1 and not args.no_cpu_baseline:
+            cpu, parity = cpu_baseline(scene, dev, W, H, spi, args.cpu_seconds)
+        result = {
+            "metric": "Mrays/s (primary+secondary) at fixed spp; per-pixel L2 vs CPU ref",
+            "value": round(value, 2),
+            "unit": "Mrays/s",
+            "n_gpus": n_gpus,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic camera paths over the reference's diamond_scene.json (scene data from the reference checkout)",
+            "config": {
+                "workload": f"diamond_scene.json {W}x{H}, {iters * spi} spp = {iters} iterations x spi {spi}, path tracer max_depth 64, seed 0",
+                "scene": os.path.basename(args.scene),
+                "width": W, "height": H, "spp": iters * spi, "spi": spi,
+                "parallelism": f"tile-shard x{n_gpus} (64x64 tiles round-robin) + RCCL all_gather" if n_gpus > 1 else "single GPU",
+            },
+            "msamples_per_s": round(samples / elapsed / 1e6, 2),
+            "rays": {"camera": int(totals[1]), "bounce": int(totals[2]), "shadow": int(totals[3])},
+            "kernel_ms": {"extend": round(st["ms_extend"], 3), "shadow": round(st["ms_shadow"], 3),
+                          "finish": round(st["ms_finish"], 3),
+                          "generate": round(st["ms_generate"], 3), "resolve": round(st["ms_resolve"], 3)},
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_extend (closest-hit traversal + shading)",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": round(alg_bytes / launches, 1),
+                "bytes_per_ray": round(bytes_per_ray, 1),
+                "avg_launch_us": round(avg_launch_s * 1e6, 2),
+                "launches": launches,
+            },
+            "cpu_baseline": cpu,
+            "parity": parity,
+        }
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+    dev.close()
+    return result
+
+
+def cpu_baseline(scene, dev, W, H, spi, target_s):
+    """Oracle (C restatement of the reference CPU device) on a bounded band of the
+    same frame, timed on this host; also the per-pixel parity of the GPU band."""
+    from oracle import oracle_py as O
+    threads = min(16, os.cpu_count() or 1)
+    orc = O.OracleScene(scene)
+    # calibrate on 8 rows, then size the band for ~target_s seconds
+    y0 = H // 2
+    _, st = orc.render(W, H, spi, iteration=0, threads=threads, window=(0, y0, W, y0 + 8))
+    rows = int(max(8, min(H, 8 * target_s / max(st["seconds"], 1e-3))))
+    y0 = max(0, H // 2 - rows // 2)
+    fb, st = orc.render(W, H, spi, iteration=0, threads=threads, window=(0, y0, W, y0 + rows))
+    rays = st["camera_rays"] + st["bounce_rays"] + st["shadow_rays"]
+    cpu = {
+        "value": round(rays / st["seconds"] / 1e6, 3),
+        "unit": "Mrays/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"oracle/oracle.c (restated reference CPU device) on rows {y0}-{y0 + rows} of the {W}x{H} diamond frame, 1 iteration spi {spi}, {st['seconds']:.1f} s",
+    }
+    # parity: GPU iteration 0 of the same frame vs the oracle band
+    dev.clear()
+    p = __import__("ignis_amd").RenderParams()
+    p.width, p.height, p.spi = W, H, spi
+    dev.render(p)
+    g, _ = dev.framebuffer(W * H * 3)
+    g = g.reshape(H, W, 3)[y0:y0 + rows]
+    o = fb.reshape(H, W, 3)[y0:y0 + rows]
+    e = (g - o) ** 2 / (o ** 2 + 1e-2)
+    e = np.minimum(e, np.percentile(e, 99))
+    parity = {
+        "rows": [y0, y0 + rows],
+        "pixel_l2_rmse": float(np.sqrt(np.mean((g - o) ** 2))),
+        "rel_mse": float(e.mean()),
+        "frac_pixels_rel_1e-2": float(np.mean(np.abs(g - o) <= 1e-2 * np.maximum(np.abs(o), 1e-2))),
+        "mean_gpu": float(g.mean()), "mean_cpu": float(o.mean()),
+    }
+    return cpu, parity
+
+
+if __name__ == "__main__":
+    main()

@@ -101,243 +101,368 @@ __device__ __forceinline__ T uniform_load(const T* p) {
 // ---------------------------------------------------------------------------
 // generate: camera rays (gpu_generate_rays, mapping_gpu.art:618-667;
 // make_camera_emitter, driver/emitter.art:6-16; perspective camera,
-// camera/perspective.art:29-42; uniform pixel sampler, sampler/pixel_sampler.art:4-10)
+// camera/perspective.art:29-42; uniform pixel sampler, sampler/pixel_sampler.art:4-10).
+// Slot i of the chunk holds path i; no compaction (tile padding slots are
+// written as dead paths with depth 0), so no atomics.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(BLOCK) k_generate(FrameArgs fa, SceneView sv, PathBuf out, float4* L, int* cnt0) {
     const int n = fa.chunk_pixels * fa.spi;
-    const int total_waves = gridDim.x * (BLOCK / 64);
-    const int wave = blockIdx.x * (BLOCK / 64) + threadIdx.x / 64;
-    for (int base = wave * 64; base < n; base += total_waves * 64) {
-        int i = base + lane_id();
-        bool alive = false;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *cnt0 = n;
+    for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+        L[i] = make_float4(0, 0, 0, 0);
+        int lp = fa.chunk_pixel0 + i / fa.spi;
+        int sample = i - (i / fa.spi) * fa.spi;
+        int x, y;
         f3 o = mk(0, 0, 0), d = mk(0, 0, 1);
         uint32_t counter = 1;
-        if (i < n) {
-            L[i] = make_float4(0, 0, 0, 0);
-            int lp = fa.chunk_pixel0 + i / fa.spi;
-            int sample = i - (i / fa.spi) * fa.spi;
-            int x, y;
-            if (local_to_global(fa, lp, x, y)) {
-                alive = true;
-                Rng rnd{create_random_seed(sample, fa.iter, fa.frame, x, y, fa.seed), 1};
-                if (fa.num_rays > 0) {
-                    // make_list_emitter (driver/emitter.art:18-30): no random draws
-                    const float* r = fa.rays + 8 * x;
-                    o = mk(r[0], r[1], r[2]);
-                    d = mk(r[3], r[4], r[5]);
-                } else {
-                    float rx = rnd.next_f32();
-                    float ry = rnd.next_f32();
-                    float nx = 2 * ((float)x + rx) / (float)fa.width - 1;
-                    float ny = 1 - 2 * ((float)y + ry) / (float)fa.height;
-                    const DevCamera& c = sv.cam;
-                    f3 v = mk(c.scale_x * nx, c.scale_y * ny, 1);
-                    f3 w = mk(c.right[0] * v.x + c.up[0] * v.y + c.dir[0] * v.z,
-                              c.right[1] * v.x + c.up[1] * v.y + c.dir[1] * v.z,
-                              c.right[2] * v.x + c.up[2] * v.y + c.dir[2] * v.z);
-                    o = mk(c.eye[0], c.eye[1], c.eye[2]);
-                    d = normalize(w);
-                }
-                counter = rnd.counter;
+        int depth = 0; // dead
+        if (local_to_global(fa, lp, x, y)) {
+            depth = 1;
+            Rng rnd{create_random_seed(sample, fa.iter, fa.frame, x, y, fa.seed), 1};
+            if (fa.num_rays > 0) {
+                // make_list_emitter (driver/emitter.art:18-30): no random draws
+                const float* r = fa.rays + 8 * x;
+                o = mk(r[0], r[1], r[2]);
+                d = mk(r[3], r[4], r[5]);
+            } else {
+                float rx = rnd.next_f32();
+                float ry = rnd.next_f32();
+                float nx = 2 * ((float)x + rx) / (float)fa.width - 1;
+                float ny = 1 - 2 * ((float)y + ry) / (float)fa.height;
+                const DevCamera& c = sv.cam;
+                f3 v = mk(c.scale_x * nx, c.scale_y * ny, 1);
+                f3 w = mk(c.right[0] * v.x + c.up[0] * v.y + c.dir[0] * v.z,
+                          c.right[1] * v.x + c.up[1] * v.y + c.dir[1] * v.z,
+                          c.right[2] * v.x + c.up[2] * v.y + c.dir[2] * v.z);
+                o = mk(c.eye[0], c.eye[1], c.eye[2]);
+                d = normalize(w);
             }
+            counter = rnd.counter;
         }
-        int dst = wave_append(alive, cnt0);
-        if (alive) {
-            out.p0[dst] = make_float4(o.x, o.y, o.z, __int_as_float(i | (1 << 24)));
-            out.p1[dst] = make_float4(d.x, d.y, d.z, __uint_as_float(counter));
-            out.p2[dst] = make_float4(1, 1, 1, 0); // init_pt_raypayload (technique/pathtracer.art:33-38)
-            out.p3[dst] = 1.0f;
-        }
+        out.p0[i] = make_float4(o.x, o.y, o.z, __int_as_float(i | (depth << 24)));
+        out.p1[i] = make_float4(d.x, d.y, d.z, __uint_as_float(counter));
+        out.p2[i] = make_float4(1, 1, 1, 0); // init_pt_raypayload (technique/pathtracer.art:33-38)
+        out.p3[i] = 1.0f;
     }
 }
 
 // ---------------------------------------------------------------------------
-// extend: closest hit + shading for every live path of one bounce
-// (gpu_traverse_primary + gpu_hit_shade + gpu_miss_shade, restating
-// technique/pathtracer.art:52-200 on_hit / on_shadow / on_bounce / on_miss)
+// One bounce of one path: closest hit + technique (gpu_traverse_primary +
+// gpu_hit_shade + gpu_miss_shade, restating technique/pathtracer.art:52-200
+// on_hit / on_shadow / on_bounce / on_miss).  Shared by the wavefront extend
+// kernel and the tail kernel, so both produce bit-identical paths.
 // ---------------------------------------------------------------------------
 struct KernelCounters {
     int* cnt_in;
     int* cnt_out;
     int* cnt_shadow;
-    unsigned long long* stats; // 8 counters (instrumentation)
+    unsigned long long* stats; // 9 counters (instrumentation)
 };
+
+struct PathState {
+    f3 o, d;
+    uint32_t counter;
+    f3 contrib;
+    float inv_pdf, eta;
+    int slot, depth;
+};
+
+struct ShadowRec {
+    f3 o, d, color;
+    float tmax;
+};
+
+__device__ __forceinline__ PathState load_path(const PathBuf& in, int i) {
+    float4 p0 = in.p0[i], p1 = in.p1[i], p2 = in.p2[i];
+    PathState s;
+    s.o = f3of(p0);
+    s.d = f3of(p1);
+    int sd = __float_as_int(p0.w);
+    s.slot = sd & 0xFFFFFF;
+    s.depth = sd >> 24;
+    s.counter = __float_as_uint(p1.w);
+    s.contrib = f3of(p2);
+    s.inv_pdf = p2.w;
+    s.eta = in.p3[i];
+    return s;
+}
+
+__device__ __forceinline__ void store_path(const PathBuf& out, int i, const PathState& s) {
+    out.p0[i] = make_float4(s.o.x, s.o.y, s.o.z, __int_as_float(s.slot | (s.depth << 24)));
+    out.p1[i] = make_float4(s.d.x, s.d.y, s.d.z, __uint_as_float(s.counter));
+    out.p2[i] = make_float4(s.contrib.x, s.contrib.y, s.contrib.z, s.inv_pdf);
+    out.p3[i] = s.eta;
+}
 
 __device__ __forceinline__ f3 handle_color(const SceneView& sv, f3 c) {
     if (sv.clamp > 0) return mk(fminf(c.x, sv.clamp), fminf(c.y, sv.clamp), fminf(c.z, sv.clamp));
     return c;
 }
 
-template <int STACK, bool STATS>
-__global__ void __launch_bounds__(BLOCK) k_extend(FrameArgs fa, SceneView sv, PathBuf in, PathBuf out, ShadowBuf sh,
-                                                  float4* L, KernelCounters kc) {
-    __shared__ int stack_mem[STACK * BLOCK];
-    int* stk = stack_mem + threadIdx.x;
-    const int n = uniform_load(kc.cnt_in);
-    const int total_waves = gridDim.x * (BLOCK / 64);
-    const int wave = blockIdx.x * (BLOCK / 64) + threadIdx.x / 64;
-    TraceStats st{0, 0, 0, 0};
-    for (int base = wave * 64; base < n; base += total_waves * 64) {
-        int i = base + lane_id();
-        bool alive = false, shadow = false;
-        f3 no = mk(0, 0, 0), nd = mk(0, 0, 0), ncontrib = mk(0, 0, 0);
-        float ninv_pdf = 0, neta = 1;
-        uint32_t ncounter = 0;
-        f3 so = mk(0, 0, 0), sdir = mk(0, 0, 0), scol = mk(0, 0, 0);
-        float stmax = 0;
-        int slot = 0, depth = 0;
-        if (i < n) {
-            float4 p0 = in.p0[i], p1 = in.p1[i], p2 = in.p2[i];
-            float eta = in.p3[i];
-            int sd = __float_as_int(p0.w);
-            slot = sd & 0xFFFFFF;
-            depth = sd >> 24;
-            f3 ro = f3of(p0), rd = f3of(p1);
-            uint32_t counter = __float_as_uint(p1.w);
-            f3 contrib = f3of(p2);
-            float inv_pdf = p2.w;
-            float tmin, tmax;
-            uint32_t rflags;
-            if (depth == 1) {
-                if (fa.num_rays > 0) {
-                    int lp = fa.chunk_pixel0 + slot / fa.spi;
-                    tmin = fa.rays[8 * lp + 6];
-                    tmax = fa.rays[8 * lp + 7];
-                    rflags = 0;
-                } else {
-                    tmin = sv.cam.tmin;
-                    tmax = sv.cam.tmax;
-                    rflags = RAY_CAMERA;
-                }
-            } else {
-                tmin = 0.001f; // offset (pathtracer.art:41)
-                tmax = FLT_MAX_;
-                rflags = RAY_BOUNCE;
-            }
-            int hit_ent, hit_prim;
-            float hu = 0, hv = 0;
-            trace_ray<false, STATS>(sv, ro, rd, tmin, tmax, rflags, stk, BLOCK, hit_ent, hit_prim, hu, hv, st);
+// Advances `ps` by one bounce.  Returns whether the path continues (ps then
+// holds the bounced ray); fills the radiance gathered at this vertex (Lacc,
+// has_l) and the NEE shadow ray (has_shadow, sr).
+template <bool STATS>
+__device__ __forceinline__ bool extend_step(const FrameArgs& fa, const SceneView& sv, int* stk, PathState& ps, f3& Lacc,
+                                            bool& has_l, bool& has_shadow, ShadowRec& sr, TraceStats& st) {
+    float tmin, tmax;
+    uint32_t rflags;
+    if (ps.depth == 1) {
+        if (fa.num_rays > 0) {
+            int lp = fa.chunk_pixel0 + ps.slot / fa.spi;
+            tmin = fa.rays[8 * lp + 6];
+            tmax = fa.rays[8 * lp + 7];
+            rflags = 0;
+        } else {
+            tmin = sv.cam.tmin;
+            tmax = sv.cam.tmax;
+            rflags = RAY_CAMERA;
+        }
+    } else {
+        tmin = 0.001f; // offset (pathtracer.art:41)
+        tmax = FLT_MAX_;
+        rflags = RAY_BOUNCE;
+    }
+    int hit_ent, hit_prim;
+    float hu = 0, hv = 0;
+    trace_ray<false, STATS>(sv, ps.o, ps.d, tmin, tmax, rflags, stk, BLOCK, hit_ent, hit_prim, hu, hv, st);
+    if (STATS && hit_ent >= 0) st.hits++;
 
-            f3 Lacc = mk(0, 0, 0);
-            bool has_l = false;
-            if (hit_ent < 0) {
-                // on_miss (pathtracer.art:136-163): every infinite, non-delta light
-                for (int li = 0; li < sv.num_infinite; ++li) {
-                    const DevLight& Lt = sv.lights[li];
-                    if (Lt.delta) continue;
-                    f3 emit = mk(Lt.radiance[0], Lt.radiance[1], Lt.radiance[2]);
-                    float pdf_s = 1 / (4 * PI_);
-                    float mis = sv.nee ? 1 / (1 + inv_pdf * (1.0f / (float)sv.num_lights) * pdf_s) : 1.0f;
-                    Lacc = add(Lacc, handle_color(sv, mulf(mul(contrib, emit), mis)));
-                    has_l = true;
-                }
-            } else {
-                int mat_id;
-                Surface s = surface_element(sv, hit_ent, hit_prim, tmax, hu, hv, ro, rd, mat_id);
-                const DevMaterial& m = sv.mats[mat_id];
-                // on_hit (pathtracer.art:114-134)
-                if (m.light >= 0 && s.entering) {
-                    float dt = -dot(rd, s.local.n);
-                    if (dt > FLT_EPS_) {
-                        const DevLight& Lt = sv.lights[m.light];
-                        f3 emit = mk(Lt.radiance[0], Lt.radiance[1], Lt.radiance[2]);
-                        float pdf_s = light_pdf_direct_solid(Lt, ro, dt, tmax * tmax);
-                        float mis = sv.nee ? 1 / (1 + inv_pdf * (1.0f / (float)sv.num_lights) * pdf_s) : 1.0f;
-                        Lacc = add(Lacc, handle_color(sv, mulf(mul(contrib, emit), mis)));
-                        has_l = true;
-                    }
-                }
-                int sample = slot - (slot / fa.spi) * fa.spi;
-                int px, py;
-                local_to_global(fa, fa.chunk_pixel0 + slot / fa.spi, px, py);
-                Rng rnd{create_random_seed(sample, fa.iter, fa.frame, px, py, fa.seed), counter};
-                f3 out_dir = neg(rd);
-                bool specular = m.type == MAT_DIELECTRIC;
-                // on_shadow (pathtracer.art:52-112)
-                if (sv.nee && !specular && sv.num_lights > 0 && depth + 1 <= sv.max_depth) {
-                    int lid = sv.num_lights <= 1 ? 0 : rnd.next_i32(0, sv.num_lights - 1);
-                    float sel_pdf = sv.num_lights == 0 ? 1.0f : 1.0f / (float)sv.num_lights;
-                    const DevLight& Lt = sv.lights[lid];
-                    DirectSample ls = light_sample_direct(sv, Lt, rnd, s);
-                    float pdf_l_s = pdf_as_solid(ls.pdf_value, ls.pdf_solid, ls.cos, ls.dist * ls.dist) * sel_pdf;
-                    if (pdf_l_s > FLT_EPS_ && ls.cos > FLT_EPS_) {
-                        f3 in_dir = ls.dir;
-                        f3 kd = mk(m.kd[0], m.kd[1], m.kd[2]);
-                        float mis;
-                        if (Lt.delta) {
-                            mis = 1.0f;
-                        } else {
-                            float c = dot(in_dir, s.local.n);
-                            float pdf_e_s = (c >= 0 ? c : 0) / PI_; // cosine_hemisphere_pdf(positive_cos)
-                            mis = 1 / (1 + pdf_e_s / pdf_l_s);
-                        }
-                        float factor = ls.pdf_value / pdf_l_s;
-                        f3 ev = mulf(kd, fabsf(dot(in_dir, s.local.n)) * INV_PI_); // Lambert eval
-                        scol = handle_color(sv, mulf(mul(ls.intensity, mul(contrib, ev)), mis * factor));
-                        so = s.point;
-                        if (Lt.infinite) {
-                            sdir = in_dir;
-                            stmax = FLT_MAX_;
-                        } else {
-                            sdir = sub(ls.pos, s.point);
-                            stmax = 1 - 0.001f;
-                        }
-                        shadow = true;
-                    }
-                }
-                // on_bounce (pathtracer.art:165-200)
-                if (depth + 1 <= sv.max_depth) {
-                    BsdfSample bs = sample_bsdf(m, s, rnd, out_dir);
-                    f3 c2 = mul(contrib, bs.color);
-                    float rr = 1.0f;
-                    if (depth + 1 > sv.min_depth) {
-                        f3 e = mulf(c2, eta * eta);
-                        rr = clampf(fmaxf(fmaxf(e.x, e.y), e.z), 0.05f, 0.95f); // russian_roulette_pbrt
-                    }
-                    if (!(rnd.next_f32() >= rr)) {
-                        alive = true;
-                        ninv_pdf = specular ? 0 : 1 / bs.pdf;
-                        ncontrib = mulf(c2, 1 / rr);
-                        neta = eta * bs.eta;
-                        no = s.point;
-                        nd = bs.in_dir;
-                        ncounter = rnd.counter;
-                    }
-                }
-            }
-            if (has_l) {
-                float4 l = L[slot];
-                L[slot] = make_float4(l.x + Lacc.x, l.y + Lacc.y, l.z + Lacc.z, 0);
-            }
+    Lacc = mk(0, 0, 0);
+    has_l = false;
+    has_shadow = false;
+    const f3 rd = ps.d;
+    if (hit_ent < 0) {
+        // on_miss (pathtracer.art:136-163): every infinite, non-delta light
+        for (int li = 0; li < sv.num_infinite; ++li) {
+            const DevLight& Lt = sv.lights[li];
+            if (Lt.delta) continue;
+            f3 emit = mk(Lt.radiance[0], Lt.radiance[1], Lt.radiance[2]);
+            float pdf_s = 1 / (4 * PI_);
+            float mis = sv.nee ? 1 / (1 + ps.inv_pdf * (1.0f / (float)sv.num_lights) * pdf_s) : 1.0f;
+            Lacc = add(Lacc, handle_color(sv, mulf(mul(ps.contrib, emit), mis)));
+            has_l = true;
         }
-        int dst = wave_append(alive, kc.cnt_out);
-        if (alive) {
-            out.p0[dst] = make_float4(no.x, no.y, no.z, __int_as_float(slot | ((depth + 1) << 24)));
-            out.p1[dst] = make_float4(nd.x, nd.y, nd.z, __uint_as_float(ncounter));
-            out.p2[dst] = make_float4(ncontrib.x, ncontrib.y, ncontrib.z, ninv_pdf);
-            out.p3[dst] = neta;
-        }
-        int sdst = wave_append(shadow, kc.cnt_shadow);
-        if (shadow) {
-            sh.s0[sdst] = make_float4(so.x, so.y, so.z, __int_as_float(slot));
-            sh.s1[sdst] = make_float4(sdir.x, sdir.y, sdir.z, stmax);
-            sh.s2[sdst] = make_float4(scol.x, scol.y, scol.z, 0);
+        return false;
+    }
+    int mat_id;
+    Surface s = surface_element(sv, hit_ent, hit_prim, tmax, hu, hv, ps.o, rd, mat_id);
+    const DevMaterial& m = sv.mats[mat_id];
+    // on_hit (pathtracer.art:114-134)
+    if (m.light >= 0 && s.entering) {
+        float dt = -dot(rd, s.local.n);
+        if (dt > FLT_EPS_) {
+            const DevLight& Lt = sv.lights[m.light];
+            f3 emit = mk(Lt.radiance[0], Lt.radiance[1], Lt.radiance[2]);
+            float pdf_s = light_pdf_direct_solid(Lt, ps.o, dt, tmax * tmax);
+            float mis = sv.nee ? 1 / (1 + ps.inv_pdf * (1.0f / (float)sv.num_lights) * pdf_s) : 1.0f;
+            Lacc = add(Lacc, handle_color(sv, mulf(mul(ps.contrib, emit), mis)));
+            has_l = true;
         }
     }
+    int sample = ps.slot - (ps.slot / fa.spi) * fa.spi;
+    int px, py;
+    local_to_global(fa, fa.chunk_pixel0 + ps.slot / fa.spi, px, py);
+    Rng rnd{create_random_seed(sample, fa.iter, fa.frame, px, py, fa.seed), ps.counter};
+    f3 out_dir = neg(rd);
+    bool specular = m.type == MAT_DIELECTRIC;
+    // on_shadow (pathtracer.art:52-112)
+    if (sv.nee && !specular && sv.num_lights > 0 && ps.depth + 1 <= sv.max_depth) {
+        int lid = sv.num_lights <= 1 ? 0 : rnd.next_i32(0, sv.num_lights - 1);
+        float sel_pdf = 1.0f / (float)sv.num_lights;
+        const DevLight& Lt = sv.lights[lid];
+        DirectSample ls = light_sample_direct(sv, Lt, rnd, s);
+        float pdf_l_s = pdf_as_solid(ls.pdf_value, ls.pdf_solid, ls.cos, ls.dist * ls.dist) * sel_pdf;
+        if (pdf_l_s > FLT_EPS_ && ls.cos > FLT_EPS_) {
+            f3 in_dir = ls.dir;
+            f3 kd = mk(m.kd[0], m.kd[1], m.kd[2]);
+            float mis;
+            if (Lt.delta) {
+                mis = 1.0f;
+            } else {
+                float c = dot(in_dir, s.local.n);
+                float pdf_e_s = (c >= 0 ? c : 0) / PI_; // cosine_hemisphere_pdf(positive_cos)
+                mis = 1 / (1 + pdf_e_s / pdf_l_s);
+            }
+            float factor = ls.pdf_value / pdf_l_s;
+            f3 ev = mulf(kd, fabsf(dot(in_dir, s.local.n)) * INV_PI_); // Lambert eval
+            sr.color = handle_color(sv, mulf(mul(ls.intensity, mul(ps.contrib, ev)), mis * factor));
+            sr.o = s.point;
+            if (Lt.infinite) {
+                sr.d = in_dir;
+                sr.tmax = FLT_MAX_;
+            } else {
+                sr.d = sub(ls.pos, s.point);
+                sr.tmax = 1 - 0.001f;
+            }
+            has_shadow = true;
+        }
+    }
+    // on_bounce (pathtracer.art:165-200)
+    if (!(ps.depth + 1 <= sv.max_depth)) return false;
+    BsdfSample bs = sample_bsdf(m, s, rnd, out_dir);
+    f3 c2 = mul(ps.contrib, bs.color);
+    float rr = 1.0f;
+    if (ps.depth + 1 > sv.min_depth) {
+        f3 e = mulf(c2, ps.eta * ps.eta);
+        rr = clampf(fmaxf(fmaxf(e.x, e.y), e.z), 0.05f, 0.95f); // russian_roulette_pbrt
+    }
+    if (rnd.next_f32() >= rr) return false;
+    ps.inv_pdf = specular ? 0 : 1 / bs.pdf;
+    ps.contrib = mulf(c2, 1 / rr);
+    ps.eta = ps.eta * bs.eta;
+    ps.o = s.point;
+    ps.d = bs.in_dir;
+    ps.counter = rnd.counter;
+    ps.depth = ps.depth + 1;
+    return true;
+}
+
+__device__ __forceinline__ void add_radiance(float4* L, int slot, f3 c) {
+    float4 l = L[slot];
+    L[slot] = make_float4(l.x + c.x, l.y + c.y, l.z + c.z, 0);
+}
+
+template <bool STATS>
+__device__ __forceinline__ void flush_stats(const TraceStats& st, unsigned long long* stats, int base, bool with_hits) {
+    unsigned long long a = st.nodes, b = st.leaves, c = st.tris, e = st.blas, h = st.hits;
+    for (int off = 32; off > 0; off >>= 1) {
+        a += __shfl_down(a, off);
+        b += __shfl_down(b, off);
+        c += __shfl_down(c, off);
+        e += __shfl_down(e, off);
+        h += __shfl_down(h, off);
+    }
+    if (lane_id() == 0) {
+        atomicAdd(&stats[base + 0], a);
+        atomicAdd(&stats[base + 1], b);
+        atomicAdd(&stats[base + 2], c);
+        atomicAdd(&stats[base + 3], e);
+        if (with_hits) atomicAdd(&stats[8], h);
+    }
+}
+
+// Block-wide stream compaction: one atomic per block and stream per
+// iteration (the per-wave form is bound by a single word's atomic rate,
+// MI355X_MICROARCH.md "dequeue": ~88 atomics/us).  Order inside a block is
+// preserved.  `sh` holds 2 * (BLOCK/64) + 2 ints of LDS.
+__device__ __forceinline__ void block_append2(bool a, bool b, int* ca, int* cb, int* sh, int& ia, int& ib) {
+    const int wave = threadIdx.x / 64;
+    const int lane = lane_id();
+    uint64_t ma = __ballot(a), mb = __ballot(b);
+    uint64_t below = (1ull << lane) - 1ull;
+    if (lane == 0) {
+        sh[wave] = __popcll(ma);
+        sh[BLOCK / 64 + wave] = __popcll(mb);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int ta = 0, tb = 0;
+        for (int w = 0; w < BLOCK / 64; ++w) {
+            int x = sh[w], y = sh[BLOCK / 64 + w];
+            sh[w] = ta;
+            sh[BLOCK / 64 + w] = tb;
+            ta += x;
+            tb += y;
+        }
+        sh[2 * (BLOCK / 64)] = ta ? atomicAdd(ca, ta) : 0;
+        sh[2 * (BLOCK / 64) + 1] = tb ? atomicAdd(cb, tb) : 0;
+    }
+    __syncthreads();
+    ia = sh[2 * (BLOCK / 64)] + sh[wave] + __popcll(ma & below);
+    ib = sh[2 * (BLOCK / 64) + 1] + sh[BLOCK / 64 + wave] + __popcll(mb & below);
+    __syncthreads(); // sh is reused by the next iteration
+}
+
+// ---------------------------------------------------------------------------
+// extend kernel: one bounce for every live path, compacted outputs
+// ---------------------------------------------------------------------------
+template <int STACK, bool STATS>
+__global__ void __launch_bounds__(BLOCK) k_extend(FrameArgs fa, SceneView sv, PathBuf in, PathBuf out, ShadowBuf sh,
+                                                  float4* L, KernelCounters kc, int tail_threshold) {
+    __shared__ int stack_mem[STACK * BLOCK + 2 * (BLOCK / 64) + 2];
+    int* stk = stack_mem + threadIdx.x;
+    int* scan = stack_mem + STACK * BLOCK;
+    const int n = uniform_load(kc.cnt_in);
+    if (n <= tail_threshold) return; // k_finish takes the remaining paths
+    TraceStats st{0, 0, 0, 0, 0};
+    for (int base = blockIdx.x * BLOCK; base < n; base += gridDim.x * BLOCK) {
+        int i = base + threadIdx.x;
+        bool alive = false, has_shadow = false;
+        PathState ps;
+        ShadowRec sr;
+        ps.depth = 0;
+        if (i < n) {
+            ps = load_path(in, i);
+            if (ps.depth > 0) {
+                f3 Lacc;
+                bool has_l;
+                alive = extend_step<STATS>(fa, sv, stk, ps, Lacc, has_l, has_shadow, sr, st);
+                if (has_l) add_radiance(L, ps.slot, Lacc);
+            }
+        }
+        int dst, sdst;
+        block_append2(alive, has_shadow, kc.cnt_out, kc.cnt_shadow, scan, dst, sdst);
+        if (alive) store_path(out, dst, ps);
+        if (has_shadow) {
+            sh.s0[sdst] = make_float4(sr.o.x, sr.o.y, sr.o.z, __int_as_float(ps.slot));
+            sh.s1[sdst] = make_float4(sr.d.x, sr.d.y, sr.d.z, sr.tmax);
+            sh.s2[sdst] = make_float4(sr.color.x, sr.color.y, sr.color.z, 0);
+        }
+    }
+    if (STATS) flush_stats<STATS>(st, kc.stats, 0, true);
+}
+
+// ---------------------------------------------------------------------------
+// tail kernel: once few paths remain, each lane runs its path to the end
+// (extend + inline any-hit shadow ray per bounce), replacing dozens of nearly
+// empty per-bounce launches.  Same per-path arithmetic and the same radiance
+// accumulation order as the wavefront kernels.
+// ---------------------------------------------------------------------------
+template <int STACK, bool STATS>
+__global__ void __launch_bounds__(BLOCK) k_finish(FrameArgs fa, SceneView sv, PathBuf in, float4* L, const int* cnt,
+                                                  int tail_threshold, unsigned long long* stats,
+                                                  unsigned long long* tail_counts) {
+    __shared__ int stack_mem[STACK * BLOCK];
+    int* stk = stack_mem + threadIdx.x;
+    const int n = uniform_load(cnt);
+    if (n > tail_threshold) return; // the wavefront kernels own this bounce
+    TraceStats st{0, 0, 0, 0, 0};
+    TraceStats sst{0, 0, 0, 0, 0};
+    unsigned long long bounces = 0, shadows = 0;
+    for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+        PathState ps = load_path(in, i);
+        if (ps.depth <= 0) continue;
+        for (;;) {
+            f3 Lacc;
+            bool has_l, has_shadow;
+            ShadowRec sr;
+            bool alive = extend_step<STATS>(fa, sv, stk, ps, Lacc, has_l, has_shadow, sr, st);
+            if (has_l) add_radiance(L, ps.slot, Lacc);
+            if (has_shadow) {
+                ++shadows;
+                float tm = sr.tmax;
+                int e, p;
+                float u, v;
+                if (!trace_ray<true, STATS>(sv, sr.o, sr.d, 0.001f, tm, RAY_SHADOW, stk, BLOCK, e, p, u, v, sst))
+                    add_radiance(L, ps.slot, sr.color);
+            }
+            if (!alive) break;
+            ++bounces;
+        }
+    }
+    // ray statistics of the tail (continuation rays, valid shadow rays): one atomic per wave
+    for (int off = 32; off > 0; off >>= 1) {
+        bounces += __shfl_down(bounces, off);
+        shadows += __shfl_down(shadows, off);
+    }
+    if (lane_id() == 0 && (bounces | shadows)) {
+        atomicAdd(&tail_counts[0], bounces);
+        atomicAdd(&tail_counts[1], shadows);
+    }
     if (STATS) {
-        unsigned long long a = st.nodes, b = st.leaves, c = st.tris, e = st.blas;
-        for (int off = 32; off > 0; off >>= 1) {
-            a += __shfl_down(a, off);
-            b += __shfl_down(b, off);
-            c += __shfl_down(c, off);
-            e += __shfl_down(e, off);
-        }
-        if (lane_id() == 0) {
-            atomicAdd(&kc.stats[0], a);
-            atomicAdd(&kc.stats[1], b);
-            atomicAdd(&kc.stats[2], c);
-            atomicAdd(&kc.stats[3], e);
-        }
+        flush_stats<STATS>(st, stats, 0, true);
+        flush_stats<STATS>(sst, stats, 4, false);
     }
 }
 
@@ -351,40 +476,19 @@ __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView sv, ShadowBuf sh, fl
     __shared__ int stack_mem[STACK * BLOCK];
     int* stk = stack_mem + threadIdx.x;
     const int n = uniform_load(cnt);
-    const int total_waves = gridDim.x * (BLOCK / 64);
-    const int wave = blockIdx.x * (BLOCK / 64) + threadIdx.x / 64;
-    TraceStats st{0, 0, 0, 0};
-    for (int base = wave * 64; base < n; base += total_waves * 64) {
-        int i = base + lane_id();
-        if (i < n) {
-            float4 s0 = sh.s0[i], s1 = sh.s1[i];
-            float tmax = s1.w;
-            int e, p;
-            float u, v;
-            bool occluded = trace_ray<true, STATS>(sv, f3of(s0), f3of(s1), 0.001f, tmax, RAY_SHADOW, stk, BLOCK, e, p, u, v, st);
-            if (!occluded) {
-                int slot = __float_as_int(s0.w);
-                float4 c = sh.s2[i];
-                float4 l = L[slot];
-                L[slot] = make_float4(l.x + c.x, l.y + c.y, l.z + c.z, 0);
-            }
+    TraceStats st{0, 0, 0, 0, 0};
+    for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+        float4 s0 = sh.s0[i], s1 = sh.s1[i];
+        float tmax = s1.w;
+        int e, p;
+        float u, v;
+        bool occluded = trace_ray<true, STATS>(sv, f3of(s0), f3of(s1), 0.001f, tmax, RAY_SHADOW, stk, BLOCK, e, p, u, v, st);
+        if (!occluded) {
+            float4 c = sh.s2[i];
+            add_radiance(L, __float_as_int(s0.w), f3of(c));
         }
     }
-    if (STATS) {
-        unsigned long long a = st.nodes, b = st.leaves, c = st.tris, e = st.blas;
-        for (int off = 32; off > 0; off >>= 1) {
-            a += __shfl_down(a, off);
-            b += __shfl_down(b, off);
-            c += __shfl_down(c, off);
-            e += __shfl_down(e, off);
-        }
-        if (lane_id() == 0) {
-            atomicAdd(&stats[4], a);
-            atomicAdd(&stats[5], b);
-            atomicAdd(&stats[6], c);
-            atomicAdd(&stats[7], e);
-        }
-    }
+    if (STATS) flush_stats<STATS>(st, stats, 4, false);
 }
 
 // resolve: fb += sum_s L_s / spi (driver/accumulator.art:13-19, make_standard_accumulator)
@@ -428,7 +532,7 @@ __global__ void __launch_bounds__(BLOCK) k_trace_hits(SceneView sv, const float*
     float tmax = r[7];
     int e, p;
     float u = 0, v = 0;
-    TraceStats st{0, 0, 0, 0};
+    TraceStats st{0, 0, 0, 0, 0};
     if (any) {
         bool occ = trace_ray<true, false>(sv, mk(r[0], r[1], r[2]), mk(r[3], r[4], r[5]), r[6], tmax, flags, stk, BLOCK, e, p, u, v, st);
         ent_prim[i] = occ ? 1 : 0;
@@ -471,6 +575,8 @@ struct igx_device {
     igx_camera cam_desc{};
     int stack_depth = 32;
     int scene_depth = 0;
+    int64_t tail_opt = -1;            // paths below which k_finish takes over (-1 = auto)
+    unsigned long long* tail_counts = nullptr; // [2]: tail continuation rays, tail shadow rays
     // streams
     size_t capacity = 0;
     PathBuf pa{}, pb{};
@@ -555,25 +661,65 @@ int grid_for(igx_device* dev, long long items, int blocks_per_cu) {
     return (int)std::max<long long>(1, std::min(need, cap));
 }
 
-// Launch helpers dispatching on the traversal stack depth
+// Launch helpers dispatching on the traversal stack depth (LDS per block =
+// STACK * BLOCK * 4 bytes, so a shallow scene gets a small stack and more
+// resident blocks).
+#define IGX_DISPATCH_STACK(depth, MACRO) \
+    do {                                  \
+        if ((depth) <= 16) { MACRO(16); }  \
+        else if ((depth) <= 32) { MACRO(32); } \
+        else { MACRO(64); }               \
+    } while (0)
+
 template <bool STATS>
-void launch_extend(igx_device* dev, int grid, const FrameArgs& fa, const PathBuf& in, const PathBuf& out, const KernelCounters& kc) {
-    if (dev->stack_depth <= 32)
-        hipLaunchKernelGGL((k_extend<32, STATS>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, out, dev->sh, dev->L, kc);
-    else
-        hipLaunchKernelGGL((k_extend<64, STATS>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, out, dev->sh, dev->L, kc);
+void launch_extend(igx_device* dev, int grid, const FrameArgs& fa, const PathBuf& in, const PathBuf& out, const KernelCounters& kc, int tail) {
+#define L_EXT(S) hipLaunchKernelGGL((k_extend<S, STATS>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, out, dev->sh, dev->L, kc, tail)
+    IGX_DISPATCH_STACK(dev->stack_depth, L_EXT);
+#undef L_EXT
 }
 template <bool STATS>
 void launch_shadow(igx_device* dev, int grid, const int* cnt) {
-    if (dev->stack_depth <= 32)
-        hipLaunchKernelGGL((k_shadow<32, STATS>), dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, dev->sh, dev->L, cnt, dev->dstats);
-    else
-        hipLaunchKernelGGL((k_shadow<64, STATS>), dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, dev->sh, dev->L, cnt, dev->dstats);
+#define L_SH(S) hipLaunchKernelGGL((k_shadow<S, STATS>), dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, dev->sh, dev->L, cnt, dev->dstats)
+    IGX_DISPATCH_STACK(dev->stack_depth, L_SH);
+#undef L_SH
+}
+template <bool STATS>
+void launch_finish(igx_device* dev, int grid, const FrameArgs& fa, const PathBuf& in, const int* cnt, int tail) {
+#define L_FIN(S) hipLaunchKernelGGL((k_finish<S, STATS>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, dev->L, cnt, tail, dev->dstats, dev->tail_counts)
+    IGX_DISPATCH_STACK(dev->stack_depth, L_FIN);
+#undef L_FIN
+}
+
+// resident blocks per CU of a kernel (persistent grid sizing)
+template <typename K>
+int resident_blocks(K kernel) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, BLOCK, 0) != hipSuccess || nb < 1) nb = 1;
+    return nb;
+}
+template <bool STATS>
+int extend_blocks_per_cu(int depth) {
+    if (depth <= 16) return resident_blocks(k_extend<16, STATS>);
+    if (depth <= 32) return resident_blocks(k_extend<32, STATS>);
+    return resident_blocks(k_extend<64, STATS>);
+}
+template <bool STATS>
+int shadow_blocks_per_cu(int depth) {
+    if (depth <= 16) return resident_blocks(k_shadow<16, STATS>);
+    if (depth <= 32) return resident_blocks(k_shadow<32, STATS>);
+    return resident_blocks(k_shadow<64, STATS>);
+}
+template <bool STATS>
+int finish_blocks_per_cu(int depth) {
+    if (depth <= 16) return resident_blocks(k_finish<16, STATS>);
+    if (depth <= 32) return resident_blocks(k_finish<32, STATS>);
+    return resident_blocks(k_finish<64, STATS>);
 }
 
 struct TimedLaunch {
     hipEvent_t a, b;
-    int kind; // 0 extend, 1 shadow, 2 generate, 3 resolve
+    int kind; // 0 extend, 1 shadow, 2 generate, 3 resolve, 4 finish
+    int bounce;
 };
 
 } // namespace
@@ -600,12 +746,13 @@ extern "C" igx_status igx_create(int hip_device, igx_device** out) {
         return IGX_ERR_HIP;
     }
     if (hipMalloc((void**)&dev->counters, (2 * MAX_BOUNCES + 4) * sizeof(int)) != hipSuccess ||
-        hipMalloc((void**)&dev->dstats, 8 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc((void**)&dev->dstats, 16 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc((void**)&dev->tail_counts, 2 * sizeof(unsigned long long)) != hipSuccess ||
         hipHostMalloc((void**)&dev->pinned_counts, (2 * MAX_BOUNCES + 4) * sizeof(int), hipHostMallocDefault) != hipSuccess) {
         delete dev;
         return IGX_ERR_OUT_OF_MEMORY;
     }
-    (void)hipMemset(dev->dstats, 0, 8 * sizeof(unsigned long long));
+    (void)hipMemset(dev->dstats, 0, 16 * sizeof(unsigned long long));
     *out = dev;
     return IGX_OK;
 }
@@ -619,6 +766,7 @@ extern "C" igx_status igx_destroy(igx_device* dev) {
     if (dev->fb) (void)hipFree(dev->fb);
     if (dev->counters) (void)hipFree(dev->counters);
     if (dev->dstats) (void)hipFree(dev->dstats);
+    if (dev->tail_counts) (void)hipFree(dev->tail_counts);
     if (dev->pinned_counts) (void)hipHostFree(dev->pinned_counts);
     if (dev->ray_list) (void)hipFree(dev->ray_list);
     for (auto& e : dev->ev_pool) (void)hipEventDestroy(e);
@@ -635,6 +783,7 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     if (k == "timing") dev->timing = value != 0;
     else if (k == "instrument") dev->instrument = value != 0;
     else if (k == "capacity") dev->capacity_opt = value;
+    else if (k == "tail_threshold") dev->tail_opt = value;
     else if (k == "bvh_leaf_size") {
         if (value < 1 || value > 16) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "bvh_leaf_size must be in [1, 16]");
         dev->leaf_size = (int)value;
@@ -871,9 +1020,29 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
         free_scene(dev);
         return fail(dev, IGX_ERR_UNSUPPORTED, "BVH too deep for the 64-entry LDS stack (depth " + std::to_string(dev->scene_depth) + ")");
     }
-    dev->stack_depth = dev->scene_depth <= 32 ? 32 : 64;
+    dev->stack_depth = dev->scene_depth <= 16 ? 16 : (dev->scene_depth <= 32 ? 32 : 64);
     dev->has_scene = true;
     return IGX_OK;
+}
+
+static long long valid_pixels_in_chunk(const FrameArgs& fa) {
+    if (fa.num_rays > 0 || fa.tile_size <= 0) return fa.chunk_pixels;
+    long long v = 0;
+    const int T = fa.tile_size;
+    for (int lp0 = fa.chunk_pixel0; lp0 < fa.chunk_pixel0 + fa.chunk_pixels;) {
+        int k = lp0 / (T * T);
+        int t = fa.tile_offset + k * fa.tile_stride;
+        int ty = t / fa.tiles_x, tx = t - ty * fa.tiles_x;
+        int w = std::max(0, std::min(T, fa.width - tx * T)), h = std::max(0, std::min(T, fa.height - ty * T));
+        int tile_end = (k + 1) * T * T;
+        int end = std::min(tile_end, fa.chunk_pixel0 + fa.chunk_pixels);
+        for (int lp = lp0; lp < end; ++lp) {
+            int r = lp - k * T * T;
+            if (r / T < h && r % T < w) ++v;
+        }
+        lp0 = end;
+    }
+    return v;
 }
 
 static void setup_camera(igx_device* dev, int width, int height) {
@@ -986,9 +1155,9 @@ extern "C" igx_status igx_render(igx_device* dev, const igx_render_params* p) {
         return dev->ev_pool[k];
     };
     size_t ev_next = 0;
-    auto begin_timed = [&](int kind) {
+    auto begin_timed = [&](int kind, int bounce) {
         if (!dev->timing) return;
-        TimedLaunch t{ev(ev_next), ev(ev_next + 1), kind};
+        TimedLaunch t{ev(ev_next), ev(ev_next + 1), kind, bounce};
         ev_next += 2;
         (void)hipEventRecord(t.a, dev->stream);
         timed.push_back(t);
@@ -997,40 +1166,55 @@ extern "C" igx_status igx_render(igx_device* dev, const igx_render_params* p) {
         if (!dev->timing) return;
         (void)hipEventRecord(timed.back().b, dev->stream);
     };
-    const int ext_grid_cap = 8;  // blocks per CU for the persistent loops
+    const bool inst = dev->instrument;
+    const int sd = dev->stack_depth;
+    const int ext_bpc = inst ? extend_blocks_per_cu<true>(sd) : extend_blocks_per_cu<false>(sd);
+    const int sh_bpc = inst ? shadow_blocks_per_cu<true>(sd) : shadow_blocks_per_cu<false>(sd);
+    const int fin_bpc = inst ? finish_blocks_per_cu<true>(sd) : finish_blocks_per_cu<false>(sd);
+    HIPCHK(hipMemsetAsync(dev->tail_counts, 0, 2 * sizeof(unsigned long long), dev->stream));
 
     for (long long px0 = 0; px0 < local_pixels; px0 += chunk_pixels_max) {
         int chunk_pixels = (int)std::min<long long>(chunk_pixels_max, local_pixels - px0);
         fa.chunk_pixel0 = (int)px0;
         fa.chunk_pixels = chunk_pixels;
         long long n = (long long)chunk_pixels * p->spi;
-        int* cnt = dev->counters;              // cnt[b]: paths entering bounce b
+        int tail = dev->tail_opt >= 0 ? (int)std::min<int64_t>(dev->tail_opt, 1 << 30)
+                                      : (int)std::max<long long>(32768, n / 16);
+        int* cnt = dev->counters;                // cnt[b]: paths entering bounce b
         int* scnt = dev->counters + MAX_BOUNCES; // scnt[b]: shadow rays of bounce b
         HIPCHK(hipMemsetAsync(dev->counters, 0, (2 * MAX_BOUNCES + 4) * sizeof(int), dev->stream));
-        begin_timed(2);
-        hipLaunchKernelGGL(k_generate, dim3(grid_for(dev, n, ext_grid_cap)), dim3(BLOCK), 0, dev->stream, fa, dev->sv, dev->pa,
+        begin_timed(2, -1);
+        hipLaunchKernelGGL(k_generate, dim3(grid_for(dev, n, 8)), dim3(BLOCK), 0, dev->stream, fa, dev->sv, dev->pa,
                            dev->L, cnt);
         end_timed();
         HIPCHK(hipGetLastError());
         PathBuf in = dev->pa, out = dev->pb;
-        int grid = grid_for(dev, n, ext_grid_cap);
+        const int ext_grid = grid_for(dev, n, ext_bpc);
+        const int sh_grid = grid_for(dev, n, sh_bpc);
+        const int fin_grid = grid_for(dev, std::min<long long>(n, tail), fin_bpc);
         // bounce loop; the host stops launching once a bounce two steps back
-        // produced no paths (counts read asynchronously, no per-bounce sync)
+        // produced no paths (counts read asynchronously, no per-bounce sync).
+        // Above `tail` live paths a bounce runs as extend + shadow; at or
+        // below it k_finish runs every remaining path to its end.
         std::vector<hipEvent_t> bounce_ev;
         int launched = 0;
         for (int b = 0; b < max_bounces; ++b) {
             if (b >= 2) {
                 HIPCHK(hipEventSynchronize(bounce_ev[b - 2]));
-                if (dev->pinned_counts[b - 1] == 0) break; // paths entering bounce b-1 was zero
+                if (dev->pinned_counts[b - 1] == 0) break; // no path entered bounce b-1
             }
             KernelCounters kc{cnt + b, cnt + b + 1, scnt + b, dev->dstats};
-            begin_timed(0);
-            if (dev->instrument) launch_extend<true>(dev, grid, fa, in, out, kc);
-            else launch_extend<false>(dev, grid, fa, in, out, kc);
+            begin_timed(0, b);
+            if (inst) launch_extend<true>(dev, ext_grid, fa, in, out, kc, tail);
+            else launch_extend<false>(dev, ext_grid, fa, in, out, kc, tail);
             end_timed();
-            begin_timed(1);
-            if (dev->instrument) launch_shadow<true>(dev, grid, scnt + b);
-            else launch_shadow<false>(dev, grid, scnt + b);
+            begin_timed(1, b);
+            if (inst) launch_shadow<true>(dev, sh_grid, scnt + b);
+            else launch_shadow<false>(dev, sh_grid, scnt + b);
+            end_timed();
+            begin_timed(4, b);
+            if (inst) launch_finish<true>(dev, fin_grid, fa, in, cnt + b, tail);
+            else launch_finish<false>(dev, fin_grid, fa, in, cnt + b, tail);
             end_timed();
             HIPCHK(hipGetLastError());
             HIPCHK(hipMemcpyAsync(dev->pinned_counts + b + 1, cnt + b + 1, sizeof(int), hipMemcpyDeviceToHost, dev->stream));
@@ -1040,28 +1224,46 @@ extern "C" igx_status igx_render(igx_device* dev, const igx_render_params* p) {
             std::swap(in, out);
             ++launched;
         }
-        begin_timed(3);
+        begin_timed(3, -1);
         hipLaunchKernelGGL(k_resolve, dim3((chunk_pixels + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, dev->stream, fa, dev->L, dev->fb, width);
         end_timed();
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(dev->pinned_counts, dev->counters, (2 * MAX_BOUNCES + 4) * sizeof(int), hipMemcpyDeviceToHost, dev->stream));
         HIPCHK(hipStreamSynchronize(dev->stream));
         // ray statistics (Statistics.h:56-63; shadow = valid shadow rays only)
-        dev->stats.camera_rays += (uint64_t)dev->pinned_counts[0];
+        dev->stats.camera_rays += (uint64_t)valid_pixels_in_chunk(fa) * p->spi;
+        int wavefront_bounces = 0;
         for (int b = 1; b <= launched; ++b) dev->stats.bounce_rays += (uint64_t)dev->pinned_counts[b];
-        for (int b = 0; b < launched; ++b) dev->stats.shadow_rays += (uint64_t)dev->pinned_counts[MAX_BOUNCES + b];
-        dev->stats.launches_extend += (uint64_t)launched;
-        dev->stats.launches_shadow += (uint64_t)launched;
-    }
-    if (dev->timing) {
-        for (auto& t : timed) {
-            float ms = 0;
-            (void)hipEventElapsedTime(&ms, t.a, t.b);
-            if (t.kind == 0) dev->stats.ms_extend += ms;
-            else if (t.kind == 1) dev->stats.ms_shadow += ms;
-            else if (t.kind == 2) dev->stats.ms_generate += ms;
-            else dev->stats.ms_resolve += ms;
+        for (int b = 0; b < launched; ++b) {
+            dev->stats.shadow_rays += (uint64_t)dev->pinned_counts[MAX_BOUNCES + b];
+            if (dev->pinned_counts[b] > tail) ++wavefront_bounces;
         }
+        dev->stats.launches_extend += (uint64_t)wavefront_bounces;
+        dev->stats.launches_shadow += (uint64_t)wavefront_bounces;
+        dev->stats.launches_finish += wavefront_bounces < launched ? 1 : 0;
+        // timing: attribute only launches that did work
+        if (dev->timing) {
+            for (auto& t : timed) {
+                float ms = 0;
+                (void)hipEventElapsedTime(&ms, t.a, t.b);
+                bool wf = t.bounce >= 0 && dev->pinned_counts[t.bounce] > tail;
+                if (t.kind == 0 && wf) dev->stats.ms_extend += ms;
+                else if (t.kind == 1 && wf) dev->stats.ms_shadow += ms;
+                else if (t.kind == 4 && !wf && t.bounce >= 0 && dev->pinned_counts[t.bounce] > 0) dev->stats.ms_finish += ms;
+                else if (t.kind == 2) dev->stats.ms_generate += ms;
+                else if (t.kind == 3) dev->stats.ms_resolve += ms;
+            }
+            timed.clear();
+            ev_next = 0;
+        }
+    }
+    {
+        unsigned long long tc[2] = {0, 0};
+        HIPCHK(hipMemcpy(tc, dev->tail_counts, sizeof(tc), hipMemcpyDeviceToHost));
+        dev->stats.bounce_rays += tc[0];
+        dev->stats.shadow_rays += tc[1];
+        dev->stats.tail_bounce_rays += tc[0];
+        dev->stats.tail_shadow_rays += tc[1];
     }
     dev->iteration_count++;
     dev->stats.iterations++;
@@ -1127,7 +1329,9 @@ extern "C" igx_status igx_clear(igx_device* dev) {
 extern "C" igx_status igx_get_stats(igx_device* dev, igx_stats* out) {
     if (!dev || !out) return IGX_ERR_INVALID_ARGUMENT;
     *out = dev->stats;
-    unsigned long long h[8] = {0};
+    out->bvh_depth = dev->scene_depth;
+    out->stack_entries = dev->stack_depth <= 16 ? 16 : (dev->stack_depth <= 32 ? 32 : 64);
+    unsigned long long h[16] = {0};
     HIPCHK(hipSetDevice(dev->hip_device));
     HIPCHK(hipMemcpy(h, dev->dstats, sizeof(h), hipMemcpyDeviceToHost));
     out->node_visits = h[0];
@@ -1138,6 +1342,7 @@ extern "C" igx_status igx_get_stats(igx_device* dev, igx_stats* out) {
     out->shadow_leaf_visits = h[5];
     out->shadow_tri_tests = h[6];
     out->shadow_blas_enters = h[7];
+    out->shaded_hits = h[8];
     return IGX_OK;
 }
 
@@ -1145,7 +1350,7 @@ extern "C" igx_status igx_reset_stats(igx_device* dev) {
     if (!dev) return IGX_ERR_INVALID_ARGUMENT;
     dev->stats = igx_stats{};
     HIPCHK(hipSetDevice(dev->hip_device));
-    HIPCHK(hipMemset(dev->dstats, 0, 8 * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(dev->dstats, 0, 16 * sizeof(unsigned long long)));
     return IGX_OK;
 }
 
@@ -1161,10 +1366,9 @@ static igx_status trace_batch(igx_device* dev, const float* rays, int32_t n, uin
     HIPCHK(hipMalloc((void**)&d_tuv, (size_t)n * 3 * sizeof(float)));
     HIPCHK(hipMemcpy(d_rays, rays, (size_t)n * 8 * sizeof(float), hipMemcpyHostToDevice));
     int grid = (n + BLOCK - 1) / BLOCK;
-    if (dev->stack_depth <= 32)
-        hipLaunchKernelGGL(k_trace_hits<32>, dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, d_rays, n, flags, d_ep, d_tuv, any);
-    else
-        hipLaunchKernelGGL(k_trace_hits<64>, dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, d_rays, n, flags, d_ep, d_tuv, any);
+#define L_TH(S) hipLaunchKernelGGL(k_trace_hits<S>, dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, d_rays, n, flags, d_ep, d_tuv, any)
+    IGX_DISPATCH_STACK(dev->stack_depth, L_TH);
+#undef L_TH
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(dev->stream));
     HIPCHK(hipMemcpy(ent_prim, d_ep, (size_t)n * (any ? 1 : 2) * sizeof(int), hipMemcpyDeviceToHost));

@@ -32,7 +32,7 @@ struct SceneView {
 };
 
 struct TraceStats {
-    uint32_t nodes, leaves, tris, blas;
+    uint32_t nodes, leaves, tris, blas, hits;
 };
 
 // Ray flags (traversal/ray.art:19-23)
@@ -79,15 +79,17 @@ __device__ __forceinline__ bool trace_ray(const SceneView& sv, f3 o, f3 d, float
             float4 a = np[0], b = np[1], c = np[2];
             int4 r = *reinterpret_cast<const int4*>(np + 3);
             // child 0 box: lo (a.x, a.z, b.x) hi (a.y, a.w, b.y)
-            float t0x = a.x * idir.x + iorg.x, t1x = a.y * idir.x + iorg.x;
-            float t0y = a.z * idir.y + iorg.y, t1y = a.w * idir.y + iorg.y;
-            float t0z = b.x * idir.z + iorg.z, t1z = b.y * idir.z + iorg.z;
+            // slab distances with explicit FMAs (the only contracted arithmetic
+            // in the device code, built with -ffp-contract=off)
+            float t0x = fmaf(a.x, idir.x, iorg.x), t1x = fmaf(a.y, idir.x, iorg.x);
+            float t0y = fmaf(a.z, idir.y, iorg.y), t1y = fmaf(a.w, idir.y, iorg.y);
+            float t0z = fmaf(b.x, idir.z, iorg.z), t1z = fmaf(b.y, idir.z, iorg.z);
             float en0 = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), tmin));
             float ex0 = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), tmax));
             // child 1 box: lo (b.z, c.x, c.z) hi (b.w, c.y, c.w)
-            float s0x = b.z * idir.x + iorg.x, s1x = b.w * idir.x + iorg.x;
-            float s0y = c.x * idir.y + iorg.y, s1y = c.y * idir.y + iorg.y;
-            float s0z = c.z * idir.z + iorg.z, s1z = c.w * idir.z + iorg.z;
+            float s0x = fmaf(b.z, idir.x, iorg.x), s1x = fmaf(b.w, idir.x, iorg.x);
+            float s0y = fmaf(c.x, idir.y, iorg.y), s1y = fmaf(c.y, idir.y, iorg.y);
+            float s0z = fmaf(c.z, idir.z, iorg.z), s1z = fmaf(c.w, idir.z, iorg.z);
             float en1 = fmaxf(fmaxf(fminf(s0x, s1x), fminf(s0y, s1y)), fmaxf(fminf(s0z, s1z), tmin));
             float ex1 = fminf(fminf(fmaxf(s0x, s1x), fmaxf(s0y, s1y)), fminf(fmaxf(s0z, s1z), tmax));
             bool h0 = en0 <= ex0, h1 = en1 <= ex1;

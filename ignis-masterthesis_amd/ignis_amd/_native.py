@@ -81,7 +81,9 @@ class Stats(C.Structure):
                 ("node_visits", C.c_uint64), ("leaf_visits", C.c_uint64), ("tri_tests", C.c_uint64),
                 ("blas_enters", C.c_uint64), ("shadow_node_visits", C.c_uint64),
                 ("shadow_leaf_visits", C.c_uint64), ("shadow_tri_tests", C.c_uint64),
-                ("shadow_blas_enters", C.c_uint64)]
+                ("shadow_blas_enters", C.c_uint64), ("shaded_hits", C.c_uint64),
+                ("launches_finish", C.c_uint64), ("ms_finish", C.c_double), ("tail_bounce_rays", C.c_uint64),
+                ("tail_shadow_rays", C.c_uint64), ("bvh_depth", C.c_int32), ("stack_entries", C.c_int32)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

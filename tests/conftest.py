@@ -1,0 +1,52 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "ignis-masterthesis_amd")
+for p in (PKG, ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+SCENES = os.path.join(ROOT, "scenes")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
+    config.addinivalue_line("markers", "slow: long-running")
+
+
+@pytest.fixture(scope="session")
+def root():
+    return ROOT
+
+
+@pytest.fixture(scope="session")
+def diamond_path():
+    return os.path.join(SCENES, "diamond_scene.json")
+
+
+@pytest.fixture(scope="session")
+def primitives_path():
+    return os.path.join(SCENES, "primitives.json")
+
+
+def flat_scene(lights=None, max_depth=2, size=1000):
+    """create_flat_scene (src/tests/integrator/common/__init__.py:37-66)."""
+    return {
+        "technique": {"type": "path", "max_depth": max_depth},
+        "camera": {"type": "perspective", "fov": 90, "near_clip": 0.01, "far_clip": 100,
+                   "transform": [1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, -1]},
+        "film": {"size": [size, size]},
+        "bsdfs": [{"type": "diffuse", "name": "ground", "reflectance": [1, 1, 1]}],
+        "shapes": [{"type": "rectangle", "name": "Bottom", "width": 2, "height": 2, "flip_normals": True}],
+        "entities": [{"name": "Bottom", "shape": "Bottom", "bsdf": "ground"}],
+        "lights": list(lights or []),
+    }
+
+
+POINT_LIGHT = {"type": "point", "name": "_light", "position": [0, 0, -2], "intensity": [1, 1, 1]}
+SPOT_LIGHT = {"type": "spot", "name": "_light", "cutoff": 45, "falloff": 45, "position": [0, 0, -2],
+              "direction": [0, 0, 1], "intensity": [1, 1, 1]}
+ENV_LIGHT = {"type": "env", "name": "_light", "radiance": [1, 1, 1]}

@@ -1,0 +1,114 @@
+"""Scene ingestion and the C-ABI surface (CPU only: no GPU calls)."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+import ignis_amd
+from ignis_amd import _native
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    names = set()
+    for hdr in ("igx.h", "igx_scene.h"):
+        text = open(os.path.join(ROOT, "include", hdr)).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        for m in re.finditer(r"\b(igx_[a-z_0-9]+)\s*\(", text):
+            names.add(m.group(1))
+    return sorted(names)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = C.CDLL(_native.LIB_PATH)
+    decl = declared_functions()
+    assert len(decl) >= 15
+    missing = [n for n in decl if not hasattr(lib, n)]
+    assert not missing, missing
+    assert sorted(_native.EXPORTED_SYMBOLS) == decl
+
+
+def test_version_without_gpu():
+    assert "gfx950" in ignis_amd.version()
+
+
+def test_diamond_scene_tables(diamond_path):
+    sc = ignis_amd.Scene.from_file(diamond_path)
+    d = sc.desc
+    assert (d.film_width, d.film_height) == (1000, 1000)
+    assert d.num_entities == 9 and d.num_shapes == 7 and d.num_lights == 1
+    # materials grouped per LoaderEntity.cpp:42-103: AreaLight gets its own
+    assert d.num_materials == 4
+    faces = [d.meshes[i].num_faces for i in range(d.num_meshes)]
+    assert sum(faces) == 282  # 270 diamond + 5 walls x 2 + light 2
+    inst = sum(d.meshes[d.shapes[d.entities[e].shape].mesh].num_faces for e in range(d.num_entities))
+    assert inst == 822
+    L = d.lights[0]
+    assert L.type == 1  # plane emitter
+    assert L.area == pytest.approx(0.04, rel=1e-3)
+    n = np.array(L.normal[:])
+    assert np.linalg.norm(n) == pytest.approx(1, abs=1e-6)
+    # the area-light material references the light
+    assert sum(1 for i in range(d.num_materials) if d.materials[i].light == 0) == 1
+    assert d.technique.max_depth == 64 and d.technique.min_depth == 2
+    cam = d.camera
+    np.testing.assert_allclose(cam.eye[:], [0, 0, 3.85], atol=1e-6)
+    np.testing.assert_allclose(cam.dir[:], [0, 0, -1])
+    assert cam.fov == pytest.approx(np.deg2rad(40))
+
+
+def test_primitives_scene_tables(primitives_path):
+    sc = ignis_amd.Scene.from_file(primitives_path)
+    d = sc.desc
+    assert d.num_entities == 11 and d.num_lights == 1
+    types = [d.shapes[i].type for i in range(d.num_shapes)]
+    assert types.count(1) == 1  # "sphere" -> analytic SphereProvider (LoaderShape.cpp:24-40)
+    assert d.lights[0].type == 2  # constant env
+    assert d.technique.max_depth == 2
+    # entity transform [{"translate":[-4,0,0]}, {"scale":0.5}] = T * S
+    e = d.entities[4]
+    m = np.array(e.to_global[:]).reshape(3, 4)
+    np.testing.assert_allclose(m[:, :3], np.eye(3) * 0.5, atol=1e-7)
+    np.testing.assert_allclose(m[:, 3], [-4, 0, 0], atol=1e-7)
+
+
+def test_loader_errors_are_reported():
+    with pytest.raises(ignis_amd.IgxError, match="unsupported shape type"):
+        ignis_amd.Scene.from_string({"shapes": [{"type": "teapot", "name": "x"}]})
+    with pytest.raises(ignis_amd.IgxError, match="unknown bsdf"):
+        ignis_amd.Scene.from_string({"shapes": [{"type": "cube", "name": "c"}],
+                                     "entities": [{"name": "e", "shape": "c", "bsdf": "nope"}]})
+    with pytest.raises(ignis_amd.IgxError, match="JSON parse error"):
+        ignis_amd.Scene.from_string("{ not json")
+    with pytest.raises(ignis_amd.IgxError, match="cannot open"):
+        ignis_amd.Scene.from_file("/nonexistent/scene.json")
+
+
+def test_rectangle_flip_and_plane_detection():
+    sc = ignis_amd.Scene.from_string({"shapes": [{"type": "rectangle", "name": "r", "flip_normals": True}]})
+    d = sc.desc
+    m = d.meshes[0]
+    nrm = np.ctypeslib.as_array(m.normals, shape=(m.num_vertices * 3,)).reshape(-1, 3)
+    np.testing.assert_allclose(nrm, np.tile([0, 0, -1], (4, 1)))
+    s = d.shapes[0]
+    assert s.is_plane == 1
+    x = np.array(s.plane_x[:]); y = np.array(s.plane_y[:])
+    assert np.cross(x, y) @ np.array([0, 0, -1]) > 0  # plane normal follows the (flipped) faces
+
+
+def test_procedural_shapes_load():
+    shapes = [{"type": t, "name": t} for t in ["cube", "icosphere", "uvsphere", "cylinder", "cone", "disk", "triangle"]]
+    sc = ignis_amd.Scene.from_string({"shapes": shapes})
+    d = sc.desc
+    faces = {shapes[i]["type"]: d.meshes[d.shapes[i].mesh].num_faces for i in range(len(shapes))}
+    assert faces["cube"] == 12
+    assert faces["icosphere"] == 20 * 4 ** 4
+    assert faces["triangle"] == 1
+    assert faces["disk"] == 32
+    for i in range(d.num_meshes):
+        m = d.meshes[i]
+        n = np.ctypeslib.as_array(m.normals, shape=(m.num_vertices * 3,)).reshape(-1, 3)
+        np.testing.assert_allclose(np.linalg.norm(n, axis=1), 1, atol=1e-5)
