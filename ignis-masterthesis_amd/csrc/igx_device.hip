@@ -81,18 +81,6 @@ __device__ __forceinline__ bool local_to_global(const FrameArgs& fa, int lp, int
 
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 
-// wave-level stream compaction: returns the output index for lanes with `take`
-__device__ __forceinline__ int wave_append(bool take, int* counter) {
-    uint64_t mask = __ballot(take);
-    int lane = lane_id();
-    int prefix = __popcll(mask & ((1ull << lane) - 1ull));
-    int total = __popcll(mask);
-    int base = 0;
-    if (lane == 0 && total > 0) base = atomicAdd(counter, total);
-    base = __shfl(base, 0);
-    return base + prefix;
-}
-
 template <typename T>
 __device__ __forceinline__ T uniform_load(const T* p) {
     return __builtin_amdgcn_readfirstlane(*p);
@@ -549,42 +537,66 @@ __global__ void __launch_bounds__(BLOCK) k_trace_hits(SceneView sv, const float*
 // ---------------------------------------------------------------------------
 // Host side
 // ---------------------------------------------------------------------------
-template <typename T>
-struct DevArray {
-    T* ptr = nullptr;
-    size_t count = 0;
+// Two stream "slots" (path double-buffer, shadow stream, radiance, counters)
+// alternate between chunks (a chunk = one iteration, or a capacity-sized part
+// of it).  The wavefront bounces of chunk k run on the main stream; when the
+// live-path count falls to the tail threshold, k_finish and the resolve of
+// chunk k are queued on the tail stream and the host moves on to chunk k+1 in
+// the other slot, so the latency-bound tail of one chunk overlaps the next
+// chunk's full bounces.
+struct TimedLaunch {
+    hipEvent_t a, b;
+    int kind; // 0 extend, 1 shadow, 2 generate, 3 resolve, 4 finish
+    int bounce;
 };
+
+struct Slot {
+    size_t cap = 0;
+    PathBuf pa{}, pb{};
+    ShadowBuf sh{};
+    float4* L = nullptr;
+    int* ctr = nullptr;        // device counters: ctr[2b] = paths entering bounce b, ctr[2b+1] = shadow rays of bounce b
+    int* pinned = nullptr;     // host mirror
+    hipEvent_t done = nullptr; // recorded on the tail stream after the resolve
+    std::vector<hipEvent_t> bounce_ev;
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_next = 0;
+    std::vector<TimedLaunch> timed;
+    // pending statistics of the chunk last run in this slot
+    bool pending = false;
+    int switch_bounce = 0;     // first bounce handled by k_finish
+    int tail = 0;
+    long long camera = 0;
+};
+
+constexpr int CTR_INTS = 2 * MAX_BOUNCES + 4;
 
 } // namespace
 
 struct igx_device {
     int hip_device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;  // main (wavefront) stream
+    hipStream_t tail_stream = nullptr;
     std::string last_error;
     int num_cus = 256;
     // options
     bool timing = false;
     bool instrument = false;
     int64_t capacity_opt = 0;
+    int64_t tail_opt = -1;   // paths at or below which k_finish takes over (-1 = auto)
     int leaf_size = 4;
     // scene
     bool has_scene = false;
     std::vector<void*> scene_allocs;
     SceneView sv{};
-    igxd::DevCamera cam_base{};
     igx_camera cam_desc{};
     int stack_depth = 32;
     int scene_depth = 0;
-    int64_t tail_opt = -1;            // paths below which k_finish takes over (-1 = auto)
-    unsigned long long* tail_counts = nullptr; // [2]: tail continuation rays, tail shadow rays
     // streams
-    size_t capacity = 0;
-    PathBuf pa{}, pb{};
-    ShadowBuf sh{};
-    float4* L = nullptr;
-    int* counters = nullptr;          // [2*MAX_BOUNCES+4]
-    unsigned long long* dstats = nullptr;
-    int* pinned_counts = nullptr;     // host pinned mirror of counters
+    Slot slots[2];
+    int next_slot = 0;
+    unsigned long long* dstats = nullptr;      // instrumentation counters
+    unsigned long long* tail_counts = nullptr; // [2]: tail continuation rays, tail shadow rays
     float* ray_list = nullptr;
     size_t ray_list_cap = 0;
     // framebuffer
@@ -594,7 +606,6 @@ struct igx_device {
     uint64_t iteration_count = 0;
     // stats
     igx_stats stats{};
-    std::vector<hipEvent_t> ev_pool;
 };
 
 namespace {
@@ -629,30 +640,44 @@ void free_scene(igx_device* dev) {
     dev->has_scene = false;
 }
 
-void free_streams(igx_device* dev) {
-    void* ptrs[] = {dev->pa.p0, dev->pa.p1, dev->pa.p2, dev->pa.p3, dev->pb.p0, dev->pb.p1, dev->pb.p2, dev->pb.p3,
-                    dev->sh.s0, dev->sh.s1, dev->sh.s2, dev->L};
+void free_slot_buffers(Slot& s) {
+    void* ptrs[] = {s.pa.p0, s.pa.p1, s.pa.p2, s.pa.p3, s.pb.p0, s.pb.p1, s.pb.p2, s.pb.p3, s.sh.s0, s.sh.s1, s.sh.s2, s.L};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
-    dev->pa = PathBuf{};
-    dev->pb = PathBuf{};
-    dev->sh = ShadowBuf{};
-    dev->L = nullptr;
-    dev->capacity = 0;
+    s.pa = PathBuf{};
+    s.pb = PathBuf{};
+    s.sh = ShadowBuf{};
+    s.L = nullptr;
+    s.cap = 0;
 }
 
-igx_status ensure_streams(igx_device* dev, size_t cap) {
-    if (dev->capacity >= cap) return IGX_OK;
-    free_streams(dev);
+igx_status ensure_slot(igx_device* dev, Slot& s, size_t cap) {
+    if (!s.ctr) {
+        HIPCHK(hipMalloc((void**)&s.ctr, CTR_INTS * sizeof(int)));
+        HIPCHK(hipHostMalloc((void**)&s.pinned, CTR_INTS * sizeof(int), hipHostMallocDefault));
+        HIPCHK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+        std::memset(s.pinned, 0, CTR_INTS * sizeof(int));
+    }
+    if (s.cap >= cap) return IGX_OK;
+    free_slot_buffers(s);
     auto alloc4 = [&](float4** p) -> igx_status { HIPCHK(hipMalloc((void**)p, cap * sizeof(float4))); return IGX_OK; };
-    igx_status s;
-    if ((s = alloc4(&dev->pa.p0)) || (s = alloc4(&dev->pa.p1)) || (s = alloc4(&dev->pa.p2))) return s;
-    HIPCHK(hipMalloc((void**)&dev->pa.p3, cap * sizeof(float)));
-    if ((s = alloc4(&dev->pb.p0)) || (s = alloc4(&dev->pb.p1)) || (s = alloc4(&dev->pb.p2))) return s;
-    HIPCHK(hipMalloc((void**)&dev->pb.p3, cap * sizeof(float)));
-    if ((s = alloc4(&dev->sh.s0)) || (s = alloc4(&dev->sh.s1)) || (s = alloc4(&dev->sh.s2)) || (s = alloc4(&dev->L))) return s;
-    dev->capacity = cap;
+    igx_status st;
+    if ((st = alloc4(&s.pa.p0)) || (st = alloc4(&s.pa.p1)) || (st = alloc4(&s.pa.p2))) return st;
+    HIPCHK(hipMalloc((void**)&s.pa.p3, cap * sizeof(float)));
+    if ((st = alloc4(&s.pb.p0)) || (st = alloc4(&s.pb.p1)) || (st = alloc4(&s.pb.p2))) return st;
+    HIPCHK(hipMalloc((void**)&s.pb.p3, cap * sizeof(float)));
+    if ((st = alloc4(&s.sh.s0)) || (st = alloc4(&s.sh.s1)) || (st = alloc4(&s.sh.s2)) || (st = alloc4(&s.L))) return st;
+    s.cap = cap;
     return IGX_OK;
+}
+
+hipEvent_t slot_event(Slot& s) {
+    if (s.ev_next >= s.ev_pool.size()) {
+        hipEvent_t e;
+        (void)hipEventCreate(&e);
+        s.ev_pool.push_back(e);
+    }
+    return s.ev_pool[s.ev_next++];
 }
 
 int grid_for(igx_device* dev, long long items, int blocks_per_cu) {
@@ -664,28 +689,29 @@ int grid_for(igx_device* dev, long long items, int blocks_per_cu) {
 // Launch helpers dispatching on the traversal stack depth (LDS per block =
 // STACK * BLOCK * 4 bytes, so a shallow scene gets a small stack and more
 // resident blocks).
-#define IGX_DISPATCH_STACK(depth, MACRO) \
-    do {                                  \
-        if ((depth) <= 16) { MACRO(16); }  \
+#define IGX_DISPATCH_STACK(depth, MACRO)       \
+    do {                                       \
+        if ((depth) <= 16) { MACRO(16); }      \
         else if ((depth) <= 32) { MACRO(32); } \
-        else { MACRO(64); }               \
+        else { MACRO(64); }                    \
     } while (0)
 
 template <bool STATS>
-void launch_extend(igx_device* dev, int grid, const FrameArgs& fa, const PathBuf& in, const PathBuf& out, const KernelCounters& kc, int tail) {
-#define L_EXT(S) hipLaunchKernelGGL((k_extend<S, STATS>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, out, dev->sh, dev->L, kc, tail)
+void launch_extend(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const PathBuf& in, const PathBuf& out,
+                   const KernelCounters& kc, int tail) {
+#define L_EXT(S) hipLaunchKernelGGL((k_extend<S, STATS>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, out, s.sh, s.L, kc, tail)
     IGX_DISPATCH_STACK(dev->stack_depth, L_EXT);
 #undef L_EXT
 }
 template <bool STATS>
-void launch_shadow(igx_device* dev, int grid, const int* cnt) {
-#define L_SH(S) hipLaunchKernelGGL((k_shadow<S, STATS>), dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, dev->sh, dev->L, cnt, dev->dstats)
+void launch_shadow(igx_device* dev, Slot& s, int grid, const int* cnt) {
+#define L_SH(S) hipLaunchKernelGGL((k_shadow<S, STATS>), dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, s.sh, s.L, cnt, dev->dstats)
     IGX_DISPATCH_STACK(dev->stack_depth, L_SH);
 #undef L_SH
 }
 template <bool STATS>
-void launch_finish(igx_device* dev, int grid, const FrameArgs& fa, const PathBuf& in, const int* cnt, int tail) {
-#define L_FIN(S) hipLaunchKernelGGL((k_finish<S, STATS>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, dev->L, cnt, tail, dev->dstats, dev->tail_counts)
+void launch_finish(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const PathBuf& in, const int* cnt, int tail) {
+#define L_FIN(S) hipLaunchKernelGGL((k_finish<S, STATS>), dim3(grid), dim3(BLOCK), 0, dev->tail_stream, fa, dev->sv, in, s.L, cnt, tail, dev->dstats, dev->tail_counts)
     IGX_DISPATCH_STACK(dev->stack_depth, L_FIN);
 #undef L_FIN
 }
@@ -716,18 +742,101 @@ int finish_blocks_per_cu(int depth) {
     return resident_blocks(k_finish<64, STATS>);
 }
 
-struct TimedLaunch {
-    hipEvent_t a, b;
-    int kind; // 0 extend, 1 shadow, 2 generate, 3 resolve, 4 finish
-    int bounce;
-};
+// Wait for the chunk last run in `s` and fold its statistics in.
+igx_status harvest(igx_device* dev, Slot& s) {
+    if (!s.pending) return IGX_OK;
+    HIPCHK(hipEventSynchronize(s.done));
+    const int* c = s.pinned;
+    dev->stats.camera_rays += (uint64_t)s.camera;
+    for (int b = 1; b <= s.switch_bounce; ++b) dev->stats.bounce_rays += (uint64_t)c[2 * b];
+    for (int b = 0; b < s.switch_bounce; ++b) dev->stats.shadow_rays += (uint64_t)c[2 * b + 1];
+    dev->stats.launches_extend += (uint64_t)s.switch_bounce;
+    dev->stats.launches_shadow += (uint64_t)s.switch_bounce;
+    bool finished = s.switch_bounce < MAX_BOUNCES && c[2 * s.switch_bounce] > 0;
+    dev->stats.launches_finish += finished ? 1 : 0;
+    if (dev->timing) {
+        for (auto& t : s.timed) {
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, t.a, t.b);
+            if (t.kind == 0 && t.bounce < s.switch_bounce) dev->stats.ms_extend += ms;
+            else if (t.kind == 1 && t.bounce < s.switch_bounce) dev->stats.ms_shadow += ms;
+            else if (t.kind == 2) dev->stats.ms_generate += ms;
+            else if (t.kind == 3) dev->stats.ms_resolve += ms;
+            else if (t.kind == 4 && finished) dev->stats.ms_finish += ms;
+        }
+    }
+    s.timed.clear();
+    s.ev_next = 0;
+    s.pending = false;
+    return IGX_OK;
+}
+
+igx_status drain(igx_device* dev) {
+    igx_status st;
+    if ((st = harvest(dev, dev->slots[0])) || (st = harvest(dev, dev->slots[1]))) return st;
+    HIPCHK(hipStreamSynchronize(dev->stream));
+    HIPCHK(hipStreamSynchronize(dev->tail_stream));
+    unsigned long long tc[2] = {0, 0};
+    HIPCHK(hipMemcpy(tc, dev->tail_counts, sizeof(tc), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemset(dev->tail_counts, 0, sizeof(tc)));
+    dev->stats.bounce_rays += tc[0];
+    dev->stats.shadow_rays += tc[1];
+    dev->stats.tail_bounce_rays += tc[0];
+    dev->stats.tail_shadow_rays += tc[1];
+    return IGX_OK;
+}
+
+long long valid_pixels_in_chunk(const FrameArgs& fa) {
+    if (fa.num_rays > 0 || fa.tile_size <= 0) return fa.chunk_pixels;
+    long long v = 0;
+    const int T = fa.tile_size;
+    for (int lp0 = fa.chunk_pixel0; lp0 < fa.chunk_pixel0 + fa.chunk_pixels;) {
+        int k = lp0 / (T * T);
+        int t = fa.tile_offset + k * fa.tile_stride;
+        int ty = t / fa.tiles_x, tx = t - ty * fa.tiles_x;
+        int w = std::max(0, std::min(T, fa.width - tx * T)), h = std::max(0, std::min(T, fa.height - ty * T));
+        int end = std::min((k + 1) * T * T, fa.chunk_pixel0 + fa.chunk_pixels);
+        for (int lp = lp0; lp < end; ++lp) {
+            int r = lp - k * T * T;
+            if (r / T < h && r % T < w) ++v;
+        }
+        lp0 = end;
+    }
+    return v;
+}
+
+void setup_camera(igx_device* dev, int width, int height) {
+    // make_perspective_camera (camera/perspective.art:29-42), compute_scale_from_{h,v}fov (:2-14)
+    const igx_camera& c = dev->cam_desc;
+    DevCamera& k = dev->sv.cam;
+    float aspect = c.aspect > 0 ? c.aspect : (float)width / (float)height;
+    if (c.vertical_fov) {
+        k.scale_y = std::tan(c.fov / 2);
+        k.scale_x = k.scale_y * aspect;
+    } else {
+        k.scale_x = std::tan(c.fov / 2);
+        k.scale_y = k.scale_x / aspect;
+    }
+    float dir[3] = {c.dir[0], c.dir[1], c.dir[2]}, up[3] = {c.up[0], c.up[1], c.up[2]};
+    float r[3] = {dir[1] * up[2] - dir[2] * up[1], dir[2] * up[0] - dir[0] * up[2], dir[0] * up[1] - dir[1] * up[0]};
+    float rl = std::sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
+    float irl = 1 / rl;
+    for (int i = 0; i < 3; ++i) {
+        k.eye[i] = c.eye[i];
+        k.dir[i] = dir[i];
+        k.up[i] = up[i];
+        k.right[i] = r[i] * irl;
+    }
+    k.tmin = c.near_clip;
+    k.tmax = c.far_clip;
+}
 
 } // namespace
 
 // ===========================================================================
 // C-ABI
 // ===========================================================================
-extern "C" const char* igx_version(void) { return "igx 0.1 (gfx950 wavefront path tracer)"; }
+extern "C" const char* igx_version(void) { return "igx 0.2 (gfx950 wavefront path tracer)"; }
 
 extern "C" igx_status igx_create(int hip_device, igx_device** out) {
     if (!out) return IGX_ERR_INVALID_ARGUMENT;
@@ -741,18 +850,18 @@ extern "C" igx_status igx_create(int hip_device, igx_device** out) {
     }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, hip_device) == hipSuccess) dev->num_cus = prop.multiProcessorCount;
-    if (hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&dev->tail_stream, hipStreamNonBlocking) != hipSuccess) {
         delete dev;
         return IGX_ERR_HIP;
     }
-    if (hipMalloc((void**)&dev->counters, (2 * MAX_BOUNCES + 4) * sizeof(int)) != hipSuccess ||
-        hipMalloc((void**)&dev->dstats, 16 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc((void**)&dev->tail_counts, 2 * sizeof(unsigned long long)) != hipSuccess ||
-        hipHostMalloc((void**)&dev->pinned_counts, (2 * MAX_BOUNCES + 4) * sizeof(int), hipHostMallocDefault) != hipSuccess) {
+    if (hipMalloc((void**)&dev->dstats, 16 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc((void**)&dev->tail_counts, 2 * sizeof(unsigned long long)) != hipSuccess) {
         delete dev;
         return IGX_ERR_OUT_OF_MEMORY;
     }
     (void)hipMemset(dev->dstats, 0, 16 * sizeof(unsigned long long));
+    (void)hipMemset(dev->tail_counts, 0, 2 * sizeof(unsigned long long));
     *out = dev;
     return IGX_OK;
 }
@@ -761,16 +870,21 @@ extern "C" igx_status igx_destroy(igx_device* dev) {
     if (!dev) return IGX_ERR_INVALID_ARGUMENT;
     (void)hipSetDevice(dev->hip_device);
     if (dev->stream) (void)hipStreamSynchronize(dev->stream);
+    if (dev->tail_stream) (void)hipStreamSynchronize(dev->tail_stream);
     free_scene(dev);
-    free_streams(dev);
+    for (auto& s : dev->slots) {
+        free_slot_buffers(s);
+        if (s.ctr) (void)hipFree(s.ctr);
+        if (s.pinned) (void)hipHostFree(s.pinned);
+        if (s.done) (void)hipEventDestroy(s.done);
+        for (auto& e : s.ev_pool) (void)hipEventDestroy(e);
+    }
     if (dev->fb) (void)hipFree(dev->fb);
-    if (dev->counters) (void)hipFree(dev->counters);
     if (dev->dstats) (void)hipFree(dev->dstats);
     if (dev->tail_counts) (void)hipFree(dev->tail_counts);
-    if (dev->pinned_counts) (void)hipHostFree(dev->pinned_counts);
     if (dev->ray_list) (void)hipFree(dev->ray_list);
-    for (auto& e : dev->ev_pool) (void)hipEventDestroy(e);
     if (dev->stream) (void)hipStreamDestroy(dev->stream);
+    if (dev->tail_stream) (void)hipStreamDestroy(dev->tail_stream);
     delete dev;
     return IGX_OK;
 }
@@ -791,10 +905,17 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     return IGX_OK;
 }
 
+extern "C" igx_status igx_synchronize(igx_device* dev) {
+    if (!dev) return IGX_ERR_INVALID_ARGUMENT;
+    HIPCHK(hipSetDevice(dev->hip_device));
+    return drain(dev);
+}
+
 extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* desc) {
     if (!dev || !desc) return IGX_ERR_INVALID_ARGUMENT;
     HIPCHK(hipSetDevice(dev->hip_device));
-    HIPCHK(hipStreamSynchronize(dev->stream));
+    igx_status dst = drain(dev);
+    if (dst != IGX_OK) return dst;
     free_scene(dev);
 
     // ---- BLAS per trimesh shape, analytic spheres -------------------------
@@ -1025,52 +1146,6 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     return IGX_OK;
 }
 
-static long long valid_pixels_in_chunk(const FrameArgs& fa) {
-    if (fa.num_rays > 0 || fa.tile_size <= 0) return fa.chunk_pixels;
-    long long v = 0;
-    const int T = fa.tile_size;
-    for (int lp0 = fa.chunk_pixel0; lp0 < fa.chunk_pixel0 + fa.chunk_pixels;) {
-        int k = lp0 / (T * T);
-        int t = fa.tile_offset + k * fa.tile_stride;
-        int ty = t / fa.tiles_x, tx = t - ty * fa.tiles_x;
-        int w = std::max(0, std::min(T, fa.width - tx * T)), h = std::max(0, std::min(T, fa.height - ty * T));
-        int tile_end = (k + 1) * T * T;
-        int end = std::min(tile_end, fa.chunk_pixel0 + fa.chunk_pixels);
-        for (int lp = lp0; lp < end; ++lp) {
-            int r = lp - k * T * T;
-            if (r / T < h && r % T < w) ++v;
-        }
-        lp0 = end;
-    }
-    return v;
-}
-
-static void setup_camera(igx_device* dev, int width, int height) {
-    // make_perspective_camera (camera/perspective.art:29-42), compute_scale_from_{h,v}fov (:2-14)
-    const igx_camera& c = dev->cam_desc;
-    DevCamera& k = dev->sv.cam;
-    float aspect = c.aspect > 0 ? c.aspect : (float)width / (float)height;
-    if (c.vertical_fov) {
-        k.scale_y = std::tan(c.fov / 2);
-        k.scale_x = k.scale_y * aspect;
-    } else {
-        k.scale_x = std::tan(c.fov / 2);
-        k.scale_y = k.scale_x / aspect;
-    }
-    float dir[3] = {c.dir[0], c.dir[1], c.dir[2]}, up[3] = {c.up[0], c.up[1], c.up[2]};
-    float r[3] = {dir[1] * up[2] - dir[2] * up[1], dir[2] * up[0] - dir[0] * up[2], dir[0] * up[1] - dir[1] * up[0]};
-    float rl = std::sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
-    float irl = 1 / rl;
-    for (int i = 0; i < 3; ++i) {
-        k.eye[i] = c.eye[i];
-        k.dir[i] = dir[i];
-        k.up[i] = up[i];
-        k.right[i] = r[i] * irl;
-    }
-    k.tmin = c.near_clip;
-    k.tmax = c.far_clip;
-}
-
 extern "C" igx_status igx_render(igx_device* dev, const igx_render_params* p) {
     if (!dev || !p) return IGX_ERR_INVALID_ARGUMENT;
     if (!dev->has_scene) return fail(dev, IGX_ERR_NO_SCENE, "no scene uploaded");
@@ -1088,10 +1163,12 @@ extern "C" igx_status igx_render(igx_device* dev, const igx_render_params* p) {
     // framebuffer (resize clears, as Device::resize)
     size_t fbc = (size_t)width * height * 3;
     if (dev->fb_w != width || dev->fb_h != height || !dev->fb) {
+        igx_status dst = drain(dev);
+        if (dst != IGX_OK) return dst;
         if (dev->fb) HIPCHK(hipFree(dev->fb));
         dev->fb = nullptr;
         HIPCHK(hipMalloc((void**)&dev->fb, fbc * sizeof(float)));
-        HIPCHK(hipMemsetAsync(dev->fb, 0, fbc * sizeof(float), dev->stream));
+        HIPCHK(hipMemsetAsync(dev->fb, 0, fbc * sizeof(float), dev->tail_stream));
         dev->fb_w = width;
         dev->fb_h = height;
         dev->fb_count = fbc;
@@ -1109,13 +1186,16 @@ extern "C" igx_status igx_render(igx_device* dev, const igx_render_params* p) {
     fa.inv_spi = 1.0f / (float)p->spi;
     long long local_pixels;
     if (list_mode) {
+        // the previous ray list may still be read by a queued tail kernel
+        igx_status dst = drain(dev);
+        if (dst != IGX_OK) return dst;
         size_t need = (size_t)p->num_rays * 8;
         if (dev->ray_list_cap < need) {
             if (dev->ray_list) HIPCHK(hipFree(dev->ray_list));
             HIPCHK(hipMalloc((void**)&dev->ray_list, need * sizeof(float)));
             dev->ray_list_cap = need;
         }
-        HIPCHK(hipMemcpyAsync(dev->ray_list, p->rays, need * sizeof(float), hipMemcpyHostToDevice, dev->stream));
+        HIPCHK(hipMemcpy(dev->ray_list, p->rays, need * sizeof(float), hipMemcpyHostToDevice));
         fa.num_rays = p->num_rays;
         fa.rays = dev->ray_list;
         local_pixels = p->num_rays;
@@ -1133,137 +1213,115 @@ extern "C" igx_status igx_render(igx_device* dev, const igx_render_params* p) {
     }
     // capacity: whole iteration resident when it fits (<= 16M paths), pixel aligned
     long long total_paths = local_pixels * p->spi;
-    long long cap = dev->capacity_opt > 0 ? dev->capacity_opt : std::min<long long>(total_paths, 1ll << 24);
-    cap = std::min<long long>(cap, (1ll << 24) - 1);
-    cap = std::max<long long>(p->spi, (cap / p->spi) * p->spi);
     if (total_paths == 0) {
         dev->iteration_count++;
         return IGX_OK;
     }
-    igx_status st = ensure_streams(dev, (size_t)std::min<long long>(cap, total_paths));
-    if (st != IGX_OK) return st;
+    long long cap = dev->capacity_opt > 0 ? dev->capacity_opt : std::min<long long>(total_paths, 1ll << 24);
+    cap = std::min<long long>(cap, (1ll << 24) - 1);
+    cap = std::max<long long>(p->spi, (cap / p->spi) * p->spi);
     const long long chunk_pixels_max = std::min<long long>(cap, total_paths) / p->spi;
+    const size_t slot_cap = (size_t)(chunk_pixels_max * p->spi);
 
-    int max_bounces = std::min(std::max(dev->sv.max_depth, 1), MAX_BOUNCES - 1);
-    std::vector<TimedLaunch> timed;
-    auto ev = [&](size_t k) -> hipEvent_t {
-        while (dev->ev_pool.size() <= k) {
-            hipEvent_t e;
-            (void)hipEventCreate(&e);
-            dev->ev_pool.push_back(e);
-        }
-        return dev->ev_pool[k];
-    };
-    size_t ev_next = 0;
-    auto begin_timed = [&](int kind, int bounce) {
-        if (!dev->timing) return;
-        TimedLaunch t{ev(ev_next), ev(ev_next + 1), kind, bounce};
-        ev_next += 2;
-        (void)hipEventRecord(t.a, dev->stream);
-        timed.push_back(t);
-    };
-    auto end_timed = [&]() {
-        if (!dev->timing) return;
-        (void)hipEventRecord(timed.back().b, dev->stream);
-    };
+    const int max_bounces = std::min(std::max(dev->sv.max_depth, 1), MAX_BOUNCES - 1);
     const bool inst = dev->instrument;
     const int sd = dev->stack_depth;
     const int ext_bpc = inst ? extend_blocks_per_cu<true>(sd) : extend_blocks_per_cu<false>(sd);
     const int sh_bpc = inst ? shadow_blocks_per_cu<true>(sd) : shadow_blocks_per_cu<false>(sd);
     const int fin_bpc = inst ? finish_blocks_per_cu<true>(sd) : finish_blocks_per_cu<false>(sd);
-    HIPCHK(hipMemsetAsync(dev->tail_counts, 0, 2 * sizeof(unsigned long long), dev->stream));
 
     for (long long px0 = 0; px0 < local_pixels; px0 += chunk_pixels_max) {
+        Slot& S = dev->slots[dev->next_slot];
+        dev->next_slot ^= 1;
+        igx_status st = harvest(dev, S); // waits for the chunk that used this slot two chunks ago
+        if (st != IGX_OK) return st;
+        if ((st = ensure_slot(dev, S, slot_cap)) != IGX_OK) return st;
+
+        auto begin_timed = [&](int kind, int bounce, hipStream_t strm) {
+            if (!dev->timing) return;
+            TimedLaunch t{slot_event(S), slot_event(S), kind, bounce};
+            (void)hipEventRecord(t.a, strm);
+            S.timed.push_back(t);
+        };
+        auto end_timed = [&](hipStream_t strm) {
+            if (!dev->timing) return;
+            (void)hipEventRecord(S.timed.back().b, strm);
+        };
+
         int chunk_pixels = (int)std::min<long long>(chunk_pixels_max, local_pixels - px0);
         fa.chunk_pixel0 = (int)px0;
         fa.chunk_pixels = chunk_pixels;
         long long n = (long long)chunk_pixels * p->spi;
-        int tail = dev->tail_opt >= 0 ? (int)std::min<int64_t>(dev->tail_opt, 1 << 30)
-                                      : (int)std::max<long long>(32768, n / 16);
-        int* cnt = dev->counters;                // cnt[b]: paths entering bounce b
-        int* scnt = dev->counters + MAX_BOUNCES; // scnt[b]: shadow rays of bounce b
-        HIPCHK(hipMemsetAsync(dev->counters, 0, (2 * MAX_BOUNCES + 4) * sizeof(int), dev->stream));
-        begin_timed(2, -1);
-        hipLaunchKernelGGL(k_generate, dim3(grid_for(dev, n, 8)), dim3(BLOCK), 0, dev->stream, fa, dev->sv, dev->pa,
-                           dev->L, cnt);
-        end_timed();
+        int tail = dev->tail_opt >= 0 ? (int)std::min<int64_t>(dev->tail_opt, 1 << 30) : (int)std::max<long long>(32768, n / 64);
+        S.tail = tail;
+        S.camera = valid_pixels_in_chunk(fa) * p->spi;
+        int* cnt = S.ctr; // cnt[2b]: paths entering bounce b, cnt[2b+1]: shadow rays of bounce b
+        HIPCHK(hipMemsetAsync(S.ctr, 0, CTR_INTS * sizeof(int), dev->stream));
+        begin_timed(2, -1, dev->stream);
+        hipLaunchKernelGGL(k_generate, dim3(grid_for(dev, n, 8)), dim3(BLOCK), 0, dev->stream, fa, dev->sv, S.pa, S.L, cnt);
+        end_timed(dev->stream);
         HIPCHK(hipGetLastError());
-        PathBuf in = dev->pa, out = dev->pb;
+        S.pinned[0] = (int)n;
         const int ext_grid = grid_for(dev, n, ext_bpc);
         const int sh_grid = grid_for(dev, n, sh_bpc);
         const int fin_grid = grid_for(dev, std::min<long long>(n, tail), fin_bpc);
-        // bounce loop; the host stops launching once a bounce two steps back
-        // produced no paths (counts read asynchronously, no per-bounce sync).
-        // Above `tail` live paths a bounce runs as extend + shadow; at or
-        // below it k_finish runs every remaining path to its end.
-        std::vector<hipEvent_t> bounce_ev;
-        int launched = 0;
-        for (int b = 0; b < max_bounces; ++b) {
+        // Wavefront bounces on the main stream.  The host learns counts two
+        // bounces late (async copies, no per-bounce sync); the device gates
+        // k_extend off once the count is <= tail, and the host then queues
+        // k_finish for that bounce's buffer on the tail stream.
+        S.bounce_ev.clear();
+        int switch_b = -1;
+        if (n <= tail) switch_b = 0;
+        for (int b = 0; switch_b < 0 && b < max_bounces; ++b) {
             if (b >= 2) {
-                HIPCHK(hipEventSynchronize(bounce_ev[b - 2]));
-                if (dev->pinned_counts[b - 1] == 0) break; // no path entered bounce b-1
+                HIPCHK(hipEventSynchronize(S.bounce_ev[b - 2]));
+                if (S.pinned[2 * (b - 1)] <= tail) {
+                    switch_b = b - 1;
+                    break;
+                }
             }
-            KernelCounters kc{cnt + b, cnt + b + 1, scnt + b, dev->dstats};
-            begin_timed(0, b);
-            if (inst) launch_extend<true>(dev, ext_grid, fa, in, out, kc, tail);
-            else launch_extend<false>(dev, ext_grid, fa, in, out, kc, tail);
-            end_timed();
-            begin_timed(1, b);
-            if (inst) launch_shadow<true>(dev, sh_grid, scnt + b);
-            else launch_shadow<false>(dev, sh_grid, scnt + b);
-            end_timed();
-            begin_timed(4, b);
-            if (inst) launch_finish<true>(dev, fin_grid, fa, in, cnt + b, tail);
-            else launch_finish<false>(dev, fin_grid, fa, in, cnt + b, tail);
-            end_timed();
+            PathBuf in = (b & 1) ? S.pb : S.pa, out = (b & 1) ? S.pa : S.pb;
+            KernelCounters kc{cnt + 2 * b, cnt + 2 * (b + 1), cnt + 2 * b + 1, dev->dstats};
+            begin_timed(0, b, dev->stream);
+            if (inst) launch_extend<true>(dev, S, ext_grid, fa, in, out, kc, tail);
+            else launch_extend<false>(dev, S, ext_grid, fa, in, out, kc, tail);
+            end_timed(dev->stream);
+            begin_timed(1, b, dev->stream);
+            if (inst) launch_shadow<true>(dev, S, sh_grid, cnt + 2 * b + 1);
+            else launch_shadow<false>(dev, S, sh_grid, cnt + 2 * b + 1);
+            end_timed(dev->stream);
             HIPCHK(hipGetLastError());
-            HIPCHK(hipMemcpyAsync(dev->pinned_counts + b + 1, cnt + b + 1, sizeof(int), hipMemcpyDeviceToHost, dev->stream));
-            hipEvent_t e = ev(ev_next++);
+            // shadow count of bounce b and path count entering bounce b+1 (adjacent ints)
+            HIPCHK(hipMemcpyAsync(S.pinned + 2 * b + 1, cnt + 2 * b + 1, 2 * sizeof(int), hipMemcpyDeviceToHost, dev->stream));
+            hipEvent_t e = slot_event(S);
             (void)hipEventRecord(e, dev->stream);
-            bounce_ev.push_back(e);
-            std::swap(in, out);
-            ++launched;
+            S.bounce_ev.push_back(e);
         }
-        begin_timed(3, -1);
-        hipLaunchKernelGGL(k_resolve, dim3((chunk_pixels + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, dev->stream, fa, dev->L, dev->fb, width);
-        end_timed();
+        if (switch_b < 0) {
+            // max_bounces launched: drain the lagged counts and find the first bounce at/below tail
+            HIPCHK(hipStreamSynchronize(dev->stream));
+            switch_b = max_bounces;
+            for (int b = 1; b <= max_bounces; ++b)
+                if (S.pinned[2 * b] <= tail) { switch_b = b; break; }
+        }
+        S.switch_bounce = switch_b;
+        // tail + resolve on the tail stream, after the main stream reached this point
+        hipEvent_t reach = slot_event(S);
+        HIPCHK(hipEventRecord(reach, dev->stream));
+        HIPCHK(hipStreamWaitEvent(dev->tail_stream, reach, 0));
+        if (switch_b < MAX_BOUNCES) {
+            PathBuf in = (switch_b & 1) ? S.pb : S.pa;
+            begin_timed(4, switch_b, dev->tail_stream);
+            if (inst) launch_finish<true>(dev, S, fin_grid, fa, in, cnt + 2 * switch_b, tail);
+            else launch_finish<false>(dev, S, fin_grid, fa, in, cnt + 2 * switch_b, tail);
+            end_timed(dev->tail_stream);
+        }
+        begin_timed(3, -1, dev->tail_stream);
+        hipLaunchKernelGGL(k_resolve, dim3((chunk_pixels + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, dev->tail_stream, fa, S.L, dev->fb, width);
+        end_timed(dev->tail_stream);
         HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(dev->pinned_counts, dev->counters, (2 * MAX_BOUNCES + 4) * sizeof(int), hipMemcpyDeviceToHost, dev->stream));
-        HIPCHK(hipStreamSynchronize(dev->stream));
-        // ray statistics (Statistics.h:56-63; shadow = valid shadow rays only)
-        dev->stats.camera_rays += (uint64_t)valid_pixels_in_chunk(fa) * p->spi;
-        int wavefront_bounces = 0;
-        for (int b = 1; b <= launched; ++b) dev->stats.bounce_rays += (uint64_t)dev->pinned_counts[b];
-        for (int b = 0; b < launched; ++b) {
-            dev->stats.shadow_rays += (uint64_t)dev->pinned_counts[MAX_BOUNCES + b];
-            if (dev->pinned_counts[b] > tail) ++wavefront_bounces;
-        }
-        dev->stats.launches_extend += (uint64_t)wavefront_bounces;
-        dev->stats.launches_shadow += (uint64_t)wavefront_bounces;
-        dev->stats.launches_finish += wavefront_bounces < launched ? 1 : 0;
-        // timing: attribute only launches that did work
-        if (dev->timing) {
-            for (auto& t : timed) {
-                float ms = 0;
-                (void)hipEventElapsedTime(&ms, t.a, t.b);
-                bool wf = t.bounce >= 0 && dev->pinned_counts[t.bounce] > tail;
-                if (t.kind == 0 && wf) dev->stats.ms_extend += ms;
-                else if (t.kind == 1 && wf) dev->stats.ms_shadow += ms;
-                else if (t.kind == 4 && !wf && t.bounce >= 0 && dev->pinned_counts[t.bounce] > 0) dev->stats.ms_finish += ms;
-                else if (t.kind == 2) dev->stats.ms_generate += ms;
-                else if (t.kind == 3) dev->stats.ms_resolve += ms;
-            }
-            timed.clear();
-            ev_next = 0;
-        }
-    }
-    {
-        unsigned long long tc[2] = {0, 0};
-        HIPCHK(hipMemcpy(tc, dev->tail_counts, sizeof(tc), hipMemcpyDeviceToHost));
-        dev->stats.bounce_rays += tc[0];
-        dev->stats.shadow_rays += tc[1];
-        dev->stats.tail_bounce_rays += tc[0];
-        dev->stats.tail_shadow_rays += tc[1];
+        HIPCHK(hipEventRecord(S.done, dev->tail_stream));
+        S.pending = true;
     }
     dev->iteration_count++;
     dev->stats.iterations++;
@@ -1281,8 +1339,9 @@ extern "C" igx_status igx_get_framebuffer(igx_device* dev, float* host_rgb, size
     }
     if (count != dev->fb_count) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "framebuffer size mismatch: expected " + std::to_string(dev->fb_count));
     HIPCHK(hipSetDevice(dev->hip_device));
-    HIPCHK(hipMemcpyAsync(host_rgb, dev->fb, count * sizeof(float), hipMemcpyDeviceToHost, dev->stream));
-    HIPCHK(hipStreamSynchronize(dev->stream));
+    igx_status st = drain(dev);
+    if (st != IGX_OK) return st;
+    HIPCHK(hipMemcpy(host_rgb, dev->fb, count * sizeof(float), hipMemcpyDeviceToHost));
     return IGX_OK;
 }
 
@@ -1309,6 +1368,8 @@ extern "C" igx_status igx_pack_tiles(igx_device* dev, const igx_render_params* p
     size_t need = (size_t)mine * p->tile_size * p->tile_size * 3;
     if (count < need) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "pack buffer too small, need " + std::to_string(need));
     HIPCHK(hipSetDevice(dev->hip_device));
+    igx_status st = drain(dev);
+    if (st != IGX_OK) return st;
     hipLaunchKernelGGL(k_pack_tiles, dim3(1024), dim3(256), 0, dev->stream, fa, dev->fb, dst, mine);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(dev->stream));
@@ -1319,8 +1380,8 @@ extern "C" igx_status igx_clear(igx_device* dev) {
     if (!dev) return IGX_ERR_INVALID_ARGUMENT;
     if (dev->fb) {
         HIPCHK(hipSetDevice(dev->hip_device));
-        HIPCHK(hipMemsetAsync(dev->fb, 0, dev->fb_count * sizeof(float), dev->stream));
-        HIPCHK(hipStreamSynchronize(dev->stream));
+        // resolves of queued chunks land on the tail stream; clear behind them
+        HIPCHK(hipMemsetAsync(dev->fb, 0, dev->fb_count * sizeof(float), dev->tail_stream));
     }
     dev->iteration_count = 0;
     return IGX_OK;
@@ -1328,11 +1389,13 @@ extern "C" igx_status igx_clear(igx_device* dev) {
 
 extern "C" igx_status igx_get_stats(igx_device* dev, igx_stats* out) {
     if (!dev || !out) return IGX_ERR_INVALID_ARGUMENT;
+    HIPCHK(hipSetDevice(dev->hip_device));
+    igx_status st = drain(dev);
+    if (st != IGX_OK) return st;
     *out = dev->stats;
     out->bvh_depth = dev->scene_depth;
     out->stack_entries = dev->stack_depth <= 16 ? 16 : (dev->stack_depth <= 32 ? 32 : 64);
     unsigned long long h[16] = {0};
-    HIPCHK(hipSetDevice(dev->hip_device));
     HIPCHK(hipMemcpy(h, dev->dstats, sizeof(h), hipMemcpyDeviceToHost));
     out->node_visits = h[0];
     out->leaf_visits = h[1];
@@ -1348,8 +1411,10 @@ extern "C" igx_status igx_get_stats(igx_device* dev, igx_stats* out) {
 
 extern "C" igx_status igx_reset_stats(igx_device* dev) {
     if (!dev) return IGX_ERR_INVALID_ARGUMENT;
-    dev->stats = igx_stats{};
     HIPCHK(hipSetDevice(dev->hip_device));
+    igx_status st = drain(dev);
+    if (st != IGX_OK) return st;
+    dev->stats = igx_stats{};
     HIPCHK(hipMemset(dev->dstats, 0, 16 * sizeof(unsigned long long)));
     return IGX_OK;
 }
@@ -1359,6 +1424,8 @@ static igx_status trace_batch(igx_device* dev, const float* rays, int32_t n, uin
     if (!dev->has_scene) return fail(dev, IGX_ERR_NO_SCENE, "no scene uploaded");
     if (n <= 0) return IGX_OK;
     HIPCHK(hipSetDevice(dev->hip_device));
+    igx_status st = drain(dev);
+    if (st != IGX_OK) return st;
     float *d_rays = nullptr, *d_tuv = nullptr;
     int* d_ep = nullptr;
     HIPCHK(hipMalloc((void**)&d_rays, (size_t)n * 8 * sizeof(float)));

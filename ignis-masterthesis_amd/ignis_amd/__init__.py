@@ -152,6 +152,9 @@ class Device:
     def clear(self):
         self._check(self._lib.igx_clear(self._h))
 
+    def synchronize(self):
+        self._check(self._lib.igx_synchronize(self._h))
+
     def stats(self):
         s = Stats()
         self._check(self._lib.igx_get_stats(self._h, C.byref(s)))

@@ -19,6 +19,7 @@ for o in opts:
     t = time.perf_counter(); K = 6
     for it in range(K):
         p.iteration = 10 + it; dev.render(p)
+    dev.synchronize()
     dt = (time.perf_counter() - t) / K
     s = dev.stats(); dev.set_option("timing", 0)
     rays = (s["camera_rays"] + s["bounce_rays"] + s["shadow_rays"]) / K
