@@ -565,6 +565,7 @@ struct Slot {
     // pending statistics of the chunk last run in this slot
     bool pending = false;
     int switch_bounce = 0;     // first bounce handled by k_finish
+    int launched = 0;          // extend/shadow launch pairs queued (the last may find its count <= tail and exit at once)
     int tail = 0;
     long long camera = 0;
 };
@@ -750,16 +751,20 @@ igx_status harvest(igx_device* dev, Slot& s) {
     dev->stats.camera_rays += (uint64_t)s.camera;
     for (int b = 1; b <= s.switch_bounce; ++b) dev->stats.bounce_rays += (uint64_t)c[2 * b];
     for (int b = 0; b < s.switch_bounce; ++b) dev->stats.shadow_rays += (uint64_t)c[2 * b + 1];
-    dev->stats.launches_extend += (uint64_t)s.switch_bounce;
-    dev->stats.launches_shadow += (uint64_t)s.switch_bounce;
+    for (int b = 0; b < s.switch_bounce; ++b) dev->stats.extend_rays += (uint64_t)c[2 * b];
+    for (int b = 1; b <= s.switch_bounce; ++b) dev->stats.extend_paths_out += (uint64_t)c[2 * b];
+    // every queued launch counts (as rocprofv3 sees them), including one that
+    // found the live count at or below the tail threshold and exited at once
+    dev->stats.launches_extend += (uint64_t)s.launched;
+    dev->stats.launches_shadow += (uint64_t)s.launched;
     bool finished = s.switch_bounce < MAX_BOUNCES && c[2 * s.switch_bounce] > 0;
     dev->stats.launches_finish += finished ? 1 : 0;
     if (dev->timing) {
         for (auto& t : s.timed) {
             float ms = 0;
             (void)hipEventElapsedTime(&ms, t.a, t.b);
-            if (t.kind == 0 && t.bounce < s.switch_bounce) dev->stats.ms_extend += ms;
-            else if (t.kind == 1 && t.bounce < s.switch_bounce) dev->stats.ms_shadow += ms;
+            if (t.kind == 0) dev->stats.ms_extend += ms;
+            else if (t.kind == 1) dev->stats.ms_shadow += ms;
             else if (t.kind == 2) dev->stats.ms_generate += ms;
             else if (t.kind == 3) dev->stats.ms_resolve += ms;
             else if (t.kind == 4 && finished) dev->stats.ms_finish += ms;
@@ -1271,6 +1276,7 @@ extern "C" igx_status igx_render(igx_device* dev, const igx_render_params* p) {
         // k_finish for that bounce's buffer on the tail stream.
         S.bounce_ev.clear();
         int switch_b = -1;
+        S.launched = 0;
         if (n <= tail) switch_b = 0;
         for (int b = 0; switch_b < 0 && b < max_bounces; ++b) {
             if (b >= 2) {
@@ -1296,6 +1302,7 @@ extern "C" igx_status igx_render(igx_device* dev, const igx_render_params* p) {
             hipEvent_t e = slot_event(S);
             (void)hipEventRecord(e, dev->stream);
             S.bounce_ev.push_back(e);
+            ++S.launched;
         }
         if (switch_b < 0) {
             // max_bounces launched: drain the lagged counts and find the first bounce at/below tail

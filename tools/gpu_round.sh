@@ -1,11 +1,16 @@
 #!/bin/bash
-# GPU-box session: tests, smoke, bench, rocprof kernel trace. Each GPU step has its own limit.
+# GPU-box session: tests, smoke, bench, rocprof kernel trace, PMC passes.
+# Every GPU step has its own time limit; the chain stops at the first failure.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 400 python3 -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1; echo "pytest rc=$?" >> gpurun_out/status.txt
-tail -5 gpurun_out/pytest_gpu.log
-grep -q "passed" gpurun_out/pytest_gpu.log || exit 1
+timeout -k 10 400 python3 -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1 && tail -3 gpurun_out/pytest_gpu.log && \
 timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && tail -2 gpurun_out/smoke.log && \
-timeout -k 10 300 python3 bench.py --steps 2 --warmup 1 > gpurun_out/bench.json 2> gpurun_out/bench.err && cat gpurun_out/bench.json && \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/prof_bench.json 2> gpurun_out/prof.err; echo "prof rc=$?"
+timeout -k 10 400 python3 bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err && cat gpurun_out/bench.json && \
+rm -rf gpurun_out/prof gpurun_out/pmc_fetch gpurun_out/pmc_write && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/prof_bench.json 2> gpurun_out/prof.err && \
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 tools/pmc_run.py 2 > gpurun_out/pmc_fetch.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 tools/pmc_run.py 2 > gpurun_out/pmc_write.log 2>&1
+rc=$?
+echo "rc=$rc"
+exit $rc

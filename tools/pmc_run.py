@@ -1,0 +1,24 @@
+"""Workload for rocprofv3 counter passes: the bench's iterations (diamond
+1000x1000, spi 8) without timing or instrumentation, so every k_extend
+dispatch is the same kernel the bench times."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ignis-masterthesis_amd"))
+import ignis_amd  # noqa: E402
+
+iters = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+scene = ignis_amd.Scene.from_file(os.path.join(ROOT, "scenes", "diamond_scene.json"))
+W, H = scene.film_size
+dev = ignis_amd.Device(0)
+dev.upload(scene)
+p = ignis_amd.RenderParams()
+p.width, p.height, p.spi = W, H, 8
+for it in range(iters):
+    p.iteration = it
+    dev.render(p)
+dev.synchronize()
+st = dev.stats()
+print({k: st[k] for k in ("camera_rays", "bounce_rays", "shadow_rays", "launches_extend", "extend_rays")}, flush=True)
+dev.close()
