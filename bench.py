@@ -102,10 +102,7 @@ def main():
     dev = ignis_amd.Device(local_rank if world > 1 else 0)
     dev.upload(scene)
 
-    tiles_x, tiles_y = (W + TILE - 1) // TILE, (H + TILE - 1) // TILE
-    n_tiles = tiles_x * tiles_y
-    my_tiles = (n_tiles - rank + n_gpus - 1) // n_gpus if n_gpus > 1 else 0
-    max_tiles = (n_tiles + n_gpus - 1) // n_gpus
+    from ignis_amd import shard
 
     def params(it):
         p = ignis_amd.RenderParams()
@@ -116,21 +113,11 @@ def main():
 
     gather_bufs = None
     if n_gpus > 1:
+        max_tiles = shard.max_tiles_per_rank(W, H, TILE, n_gpus)
         pack = torch.zeros(max_tiles * TILE * TILE * 3, dtype=torch.float32, device="cuda")
         gather_bufs = [torch.zeros_like(pack) for _ in range(n_gpus)]
-        frame = torch.zeros((tiles_y * TILE * tiles_x * TILE, 3), dtype=torch.float32, device="cuda")
-        # destination pixel of every packed slot of every rank (computed once)
-        dst = []
-        for r in range(n_gpus):
-            cnt = (n_tiles - r + n_gpus - 1) // n_gpus
-            t = np.arange(cnt) * n_gpus + r
-            ty, tx = t // tiles_x, t % tiles_x
-            yy, xx = np.mgrid[0:TILE, 0:TILE]
-            pix = ((ty[:, None, None] * TILE + yy) * (tiles_x * TILE) + tx[:, None, None] * TILE + xx).reshape(-1)
-            full = np.full(max_tiles * TILE * TILE, -1, np.int64)
-            full[: pix.size] = pix
-            dst.append(full)
-        dst = torch.from_numpy(np.concatenate(dst)).cuda()
+        frame = torch.zeros((W * H, 3), dtype=torch.float32, device="cuda")
+        dst = torch.from_numpy(shard.packed_destinations(W, H, TILE, n_gpus)).cuda()
         valid = dst >= 0
         dst_valid = dst[valid]
 

@@ -1,0 +1,51 @@
+"""Tile sharding of the film across ranks.
+
+The film is cut into T×T tiles, numbered row-major; tile t belongs to rank
+t % N (round-robin, for load balance).  Each rank renders only its tiles
+(igx_render_params.tile_offset = rank, tile_stride = N) and `igx_pack_tiles`
+packs them as [tile k of this rank][row][col][rgb], padded to T×T.  After an
+all_gather of equal-size packed buffers every rank assembles the frame with
+one scatter through the destination table built here.
+"""
+import numpy as np
+
+
+def tile_grid(width, height, tile):
+    return (width + tile - 1) // tile, (height + tile - 1) // tile
+
+
+def owned_tiles(width, height, tile, rank, n_ranks):
+    tx, ty = tile_grid(width, height, tile)
+    return np.arange(rank, tx * ty, n_ranks)
+
+
+def max_tiles_per_rank(width, height, tile, n_ranks):
+    tx, ty = tile_grid(width, height, tile)
+    return (tx * ty + n_ranks - 1) // n_ranks
+
+
+def packed_destinations(width, height, tile, n_ranks):
+    """For the concatenation of every rank's packed buffer (each padded to
+    max_tiles_per_rank tiles), the destination pixel index in the width×height
+    film, or -1 for padding and for tile pixels outside the film."""
+    tx, _ = tile_grid(width, height, tile)
+    per_rank = max_tiles_per_rank(width, height, tile, n_ranks) * tile * tile
+    yy, xx = np.mgrid[0:tile, 0:tile]
+    out = []
+    for r in range(n_ranks):
+        t = owned_tiles(width, height, tile, r, n_ranks)
+        gy = (t // tx)[:, None, None] * tile + yy
+        gx = (t % tx)[:, None, None] * tile + xx
+        pix = np.where((gx < width) & (gy < height), gy * width + gx, -1).reshape(-1)
+        full = np.full(per_rank, -1, np.int64)
+        full[: pix.size] = pix
+        out.append(full)
+    return np.concatenate(out)
+
+
+def assemble(gathered_rgb, dst, frame_rgb):
+    """Scatter the gathered packed pixels ((R*P, 3) rows, torch or numpy) into
+    frame_rgb ((W*H, 3)) through the table from packed_destinations."""
+    valid = dst >= 0
+    frame_rgb[dst[valid]] = gathered_rgb[valid]
+    return frame_rgb

@@ -209,6 +209,30 @@ def test_tile_sharding_equals_full_render(device, diamond_path):
     np.testing.assert_array_equal(acc, full)
 
 
+def test_pack_tiles_and_assemble(device, diamond_path):
+    """The bench's multi-GPU gather: every shard packs its tiles on the device
+    (igx_pack_tiles), the packed buffers are concatenated as all_gather would,
+    and shard.assemble rebuilds the full render bit for bit."""
+    import torch
+    from ignis_amd import shard
+
+    sc = ignis_amd.Scene.from_file(diamond_path)
+    w, h, T, N = 200, 150, 64, 3
+    full = render_gpu(device, sc, w, h, 4)
+    per = shard.max_tiles_per_rank(w, h, T, N) * T * T * 3
+    packs = []
+    for r in range(N):
+        render_gpu(device, sc, w, h, 4, tile=(T, r, N))
+        buf = torch.zeros(per, dtype=torch.float32, device="cuda")
+        p = ignis_amd.RenderParams()
+        p.width, p.height, p.spi, p.tile_size, p.tile_offset, p.tile_stride = w, h, 4, T, r, N
+        device.pack_tiles(p, buf.data_ptr(), buf.numel())
+        packs.append(buf.cpu().numpy())
+    dst = shard.packed_destinations(w, h, T, N)
+    frame = shard.assemble(np.concatenate(packs).reshape(-1, 3), dst, np.zeros((w * h, 3), np.float32))
+    np.testing.assert_array_equal(frame.reshape(-1), full)
+
+
 def test_capacity_chunking_is_exact(device, diamond_path):
     sc = ignis_amd.Scene.from_file(diamond_path)
     a = render_gpu(device, sc, 160, 120, 8)

@@ -1,0 +1,85 @@
+"""Tile sharding and the frame gather on CPU: the destination
+table, and a world-size-2 gloo all_gather + assemble, mirroring bench.py's
+multi-GPU path (which runs the same code over RCCL)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from ignis_amd import shard
+
+
+def pack_host(frame_rgb, width, height, tile, rank, n_ranks):
+    """Host restatement of k_pack_tiles' layout: owned tiles in ascending order,
+    each T×T row-major, pixels outside the film zero, padded to the max tile count."""
+    out = np.zeros((shard.max_tiles_per_rank(width, height, tile, n_ranks), tile, tile, 3), np.float32)
+    tx, _ = shard.tile_grid(width, height, tile)
+    img = frame_rgb.reshape(height, width, 3)
+    for k, t in enumerate(shard.owned_tiles(width, height, tile, rank, n_ranks)):
+        y0, x0 = (t // tx) * tile, (t % tx) * tile
+        blk = img[y0:y0 + tile, x0:x0 + tile]
+        out[k, : blk.shape[0], : blk.shape[1]] = blk
+    return out.reshape(-1)
+
+
+@pytest.mark.parametrize("w,h,T,N", [(200, 150, 64, 3), (1000, 1000, 64, 8), (64, 64, 64, 2), (130, 70, 16, 5)])
+def test_destinations_cover_film_once(w, h, T, N):
+    dst = shard.packed_destinations(w, h, T, N)
+    v = dst[dst >= 0]
+    assert v.size == w * h
+    assert np.array_equal(np.sort(v), np.arange(w * h))
+
+
+@pytest.mark.parametrize("w,h,T,N", [(200, 150, 64, 3), (130, 70, 16, 5)])
+def test_pack_assemble_roundtrip(w, h, T, N):
+    rng = np.random.default_rng(1)
+    frame = rng.random((w * h, 3), dtype=np.float32)
+    packs = np.concatenate([pack_host(frame, w, h, T, r, N) for r in range(N)])
+    out = shard.assemble(packs.reshape(-1, 3), shard.packed_destinations(w, h, T, N), np.zeros_like(frame))
+    np.testing.assert_array_equal(out, frame)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, w, h, T, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(7)
+    frame = rng.random((w * h, 3), dtype=np.float32)   # same "render" on every rank
+    # each rank keeps only its tiles, as the device does under tile sharding
+    pack = torch.from_numpy(pack_host(frame, w, h, T, rank, world))
+    bufs = [torch.zeros_like(pack) for _ in range(world)]
+    dist.all_gather(bufs, pack)
+    dst = torch.from_numpy(shard.packed_destinations(w, h, T, world))
+    out = shard.assemble(torch.cat(bufs).view(-1, 3), dst, torch.zeros((w * h, 3)))
+    ok = bool(torch.equal(out, torch.from_numpy(frame)))
+    # max-over-ranks timing reduction used by bench.py
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    q.put((rank, ok, float(t.item())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_gather_assembles_frame():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    w, h, T, world = 200, 150, 64, 2
+    procs = [ctx.Process(target=_worker, args=(r, world, port, w, h, T, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok, _ in res), res
+    assert all(t == float(world) for _, _, t in res)
