@@ -53,6 +53,10 @@ struct ShadowBuf {
     float4* s1; // dir.xyz, tmax
     float4* s2; // colour.rgb, -
 };
+struct HitBuf {
+    float4* h;  // t, u, v, entity (int bits; -1 = miss)
+    int* prim;  // primitive id
+};
 
 struct FrameArgs {
     int width, height, spi, iter, frame, seed;
@@ -187,17 +191,14 @@ __device__ __forceinline__ f3 handle_color(const SceneView& sv, f3 c) {
     return c;
 }
 
-// Advances `ps` by one bounce.  Returns whether the path continues (ps then
-// holds the bounced ray); fills the radiance gathered at this vertex (Lacc,
-// has_l) and the NEE shadow ray (has_shadow, sr).
-template <bool STATS>
-__device__ __forceinline__ bool extend_step(const FrameArgs& fa, const SceneView& sv, int* stk, PathState& ps, f3& Lacc,
-                                            bool& has_l, bool& has_shadow, ShadowRec& sr, TraceStats& st) {
-    float tmin, tmax;
-    uint32_t rflags;
-    if (ps.depth == 1) {
+// Ray interval and visibility flags of the ray a path traces at its current
+// vertex (camera / list ray at depth 1, bounce ray with the 0.001 offset
+// afterwards; pathtracer.art:41, ray.art:21).
+__device__ __forceinline__ void ray_extent(const FrameArgs& fa, const SceneView& sv, int depth, int slot, float& tmin,
+                                           float& tmax, uint32_t& rflags) {
+    if (depth == 1) {
         if (fa.num_rays > 0) {
-            int lp = fa.chunk_pixel0 + ps.slot / fa.spi;
+            int lp = fa.chunk_pixel0 + slot / fa.spi;
             tmin = fa.rays[8 * lp + 6];
             tmax = fa.rays[8 * lp + 7];
             rflags = 0;
@@ -211,11 +212,15 @@ __device__ __forceinline__ bool extend_step(const FrameArgs& fa, const SceneView
         tmax = FLT_MAX_;
         rflags = RAY_BOUNCE;
     }
-    int hit_ent, hit_prim;
-    float hu = 0, hv = 0;
-    trace_ray<false, STATS>(sv, ps.o, ps.d, tmin, tmax, rflags, stk, BLOCK, hit_ent, hit_prim, hu, hv, st);
-    if (STATS && hit_ent >= 0) st.hits++;
+}
 
+// Shades the closest hit (or miss, hit_ent < 0) of the path's current ray and
+// advances `ps` by one bounce.  Returns whether the path continues (ps then
+// holds the bounced ray); fills the radiance gathered at this vertex (Lacc,
+// has_l) and the NEE shadow ray (has_shadow, sr).
+__device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView& sv, PathState& ps, int hit_ent,
+                                           int hit_prim, float tmax, float hu, float hv, f3& Lacc, bool& has_l,
+                                           bool& has_shadow, ShadowRec& sr) {
     Lacc = mk(0, 0, 0);
     has_l = false;
     has_shadow = false;
@@ -304,6 +309,22 @@ __device__ __forceinline__ bool extend_step(const FrameArgs& fa, const SceneView
     ps.counter = rnd.counter;
     ps.depth = ps.depth + 1;
     return true;
+}
+
+// One bounce of one path: closest hit + shading.  Used by the tail kernel; the
+// wavefront runs the same two halves as k_trace + k_shade, so both produce
+// bit-identical paths.
+template <bool STATS>
+__device__ __forceinline__ bool extend_step(const FrameArgs& fa, const SceneView& sv, int* stk, PathState& ps, f3& Lacc,
+                                            bool& has_l, bool& has_shadow, ShadowRec& sr, TraceStats& st) {
+    float tmin, tmax;
+    uint32_t rflags;
+    ray_extent(fa, sv, ps.depth, ps.slot, tmin, tmax, rflags);
+    int hit_ent, hit_prim;
+    float hu = 0, hv = 0;
+    trace_ray<false, STATS>(sv, ps.o, ps.d, tmin, tmax, rflags, stk, BLOCK, hit_ent, hit_prim, hu, hv, st);
+    if (STATS && hit_ent >= 0) st.hits++;
+    return shade_step(fa, sv, ps, hit_ent, hit_prim, tmax, hu, hv, Lacc, has_l, has_shadow, sr);
 }
 
 __device__ __forceinline__ void add_radiance(float4* L, int slot, f3 c) {
@@ -399,6 +420,78 @@ __global__ void __launch_bounds__(BLOCK) k_extend(FrameArgs fa, SceneView sv, Pa
         }
     }
     if (STATS) flush_stats<STATS>(st, kc.stats, 0, true);
+}
+
+// ---------------------------------------------------------------------------
+// trace: closest hit of every live path's current ray (gpu_traverse_primary,
+// mapping_gpu.art:45-68).  Traversal only, so the kernel stays small enough
+// for high occupancy (the latency of the dependent node loads is what bounds
+// it); each lane writes its own hit record, no block synchronisation.
+// ---------------------------------------------------------------------------
+template <int STACK, bool STATS, int WAVES>
+__global__ void __launch_bounds__(BLOCK, WAVES) k_trace(FrameArgs fa, SceneView sv, PathBuf in, HitBuf hits,
+                                                                     const int* cnt, int tail_threshold,
+                                                                     unsigned long long* stats) {
+    __shared__ int stack_mem[STACK * BLOCK];
+    int* stk = stack_mem + threadIdx.x;
+    const int n = uniform_load(cnt);
+    if (n <= tail_threshold) return; // k_finish takes the remaining paths
+    TraceStats st{0, 0, 0, 0, 0};
+    for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+        float4 p0 = in.p0[i], p1 = in.p1[i];
+        int sd = __float_as_int(p0.w);
+        int depth = sd >> 24;
+        int hit_ent = -1, hit_prim = -1;
+        float hu = 0, hv = 0, tmax = 0;
+        if (depth > 0) {
+            float tmin;
+            uint32_t rflags;
+            ray_extent(fa, sv, depth, sd & 0xFFFFFF, tmin, tmax, rflags);
+            trace_ray<false, STATS>(sv, f3of(p0), f3of(p1), tmin, tmax, rflags, stk, BLOCK, hit_ent, hit_prim, hu, hv, st);
+            if (STATS && hit_ent >= 0) st.hits++;
+        }
+        hits.h[i] = make_float4(tmax, hu, hv, __int_as_float(hit_ent));
+        hits.prim[i] = hit_prim;
+    }
+    if (STATS) flush_stats<STATS>(st, stats, 0, true);
+}
+
+// ---------------------------------------------------------------------------
+// shade: the path-tracer step at every hit / miss (gpu_hit_shade +
+// gpu_miss_shade, mapping_gpu.art:114-266) for all materials at once, with
+// block-aggregated compaction of surviving paths and shadow rays.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(BLOCK) k_shade(FrameArgs fa, SceneView sv, PathBuf in, HitBuf hits, PathBuf out,
+                                                 ShadowBuf sh, float4* L, KernelCounters kc, int tail_threshold) {
+    __shared__ int scan[2 * (BLOCK / 64) + 2];
+    const int n = uniform_load(kc.cnt_in);
+    if (n <= tail_threshold) return;
+    for (int base = blockIdx.x * BLOCK; base < n; base += gridDim.x * BLOCK) {
+        int i = base + threadIdx.x;
+        bool alive = false, has_shadow = false;
+        PathState ps;
+        ShadowRec sr;
+        ps.depth = 0;
+        if (i < n) {
+            ps = load_path(in, i);
+            if (ps.depth > 0) {
+                float4 h = hits.h[i];
+                int prim = hits.prim[i];
+                f3 Lacc;
+                bool has_l;
+                alive = shade_step(fa, sv, ps, __float_as_int(h.w), prim, h.x, h.y, h.z, Lacc, has_l, has_shadow, sr);
+                if (has_l) add_radiance(L, ps.slot, Lacc);
+            }
+        }
+        int dst, sdst;
+        block_append2(alive, has_shadow, kc.cnt_out, kc.cnt_shadow, scan, dst, sdst);
+        if (alive) store_path(out, dst, ps);
+        if (has_shadow) {
+            sh.s0[sdst] = make_float4(sr.o.x, sr.o.y, sr.o.z, __int_as_float(ps.slot));
+            sh.s1[sdst] = make_float4(sr.d.x, sr.d.y, sr.d.z, sr.tmax);
+            sh.s2[sdst] = make_float4(sr.color.x, sr.color.y, sr.color.z, 0);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -546,7 +639,7 @@ __global__ void __launch_bounds__(BLOCK) k_trace_hits(SceneView sv, const float*
 // chunk's full bounces.
 struct TimedLaunch {
     hipEvent_t a, b;
-    int kind; // 0 extend, 1 shadow, 2 generate, 3 resolve, 4 finish
+    int kind; // 0 extend/shade, 1 shadow, 2 generate, 3 resolve, 4 finish, 5 trace
     int bounce;
 };
 
@@ -554,6 +647,7 @@ struct Slot {
     size_t cap = 0;
     PathBuf pa{}, pb{};
     ShadowBuf sh{};
+    HitBuf hb{};
     float4* L = nullptr;
     int* ctr = nullptr;        // device counters: ctr[2b] = paths entering bounce b, ctr[2b+1] = shadow rays of bounce b
     int* pinned = nullptr;     // host mirror
@@ -566,6 +660,7 @@ struct Slot {
     bool pending = false;
     int switch_bounce = 0;     // first bounce handled by k_finish
     int launched = 0;          // extend/shadow launch pairs queued (the last may find its count <= tail and exit at once)
+    bool split = true;         // chunk ran k_trace + k_shade
     int tail = 0;
     long long camera = 0;
 };
@@ -585,6 +680,8 @@ struct igx_device {
     bool instrument = false;
     int64_t capacity_opt = 0;
     int64_t tail_opt = -1;   // paths at or below which k_finish takes over (-1 = auto)
+    bool split = true;       // k_trace + k_shade per bounce (false: fused k_extend)
+    int trace_waves = 5;     // occupancy target of k_trace<16> (0 = compiler's choice; 5, 6, 8)
     int leaf_size = 4;
     // scene
     bool has_scene = false;
@@ -642,12 +739,13 @@ void free_scene(igx_device* dev) {
 }
 
 void free_slot_buffers(Slot& s) {
-    void* ptrs[] = {s.pa.p0, s.pa.p1, s.pa.p2, s.pa.p3, s.pb.p0, s.pb.p1, s.pb.p2, s.pb.p3, s.sh.s0, s.sh.s1, s.sh.s2, s.L};
+    void* ptrs[] = {s.pa.p0, s.pa.p1, s.pa.p2, s.pa.p3, s.pb.p0, s.pb.p1, s.pb.p2, s.pb.p3, s.sh.s0, s.sh.s1, s.sh.s2, s.L, s.hb.h, s.hb.prim};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     s.pa = PathBuf{};
     s.pb = PathBuf{};
     s.sh = ShadowBuf{};
+    s.hb = HitBuf{};
     s.L = nullptr;
     s.cap = 0;
 }
@@ -668,6 +766,8 @@ igx_status ensure_slot(igx_device* dev, Slot& s, size_t cap) {
     if ((st = alloc4(&s.pb.p0)) || (st = alloc4(&s.pb.p1)) || (st = alloc4(&s.pb.p2))) return st;
     HIPCHK(hipMalloc((void**)&s.pb.p3, cap * sizeof(float)));
     if ((st = alloc4(&s.sh.s0)) || (st = alloc4(&s.sh.s1)) || (st = alloc4(&s.sh.s2)) || (st = alloc4(&s.L))) return st;
+    if ((st = alloc4(&s.hb.h))) return st;
+    HIPCHK(hipMalloc((void**)&s.hb.prim, cap * sizeof(int)));
     s.cap = cap;
     return IGX_OK;
 }
@@ -704,6 +804,23 @@ void launch_extend(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, cons
     IGX_DISPATCH_STACK(dev->stack_depth, L_EXT);
 #undef L_EXT
 }
+// k_trace variants: the 16-entry stack build comes with an occupancy target
+// (waves per SIMD, option "trace_waves"); deeper stacks are LDS-limited anyway.
+template <bool STATS, int W>
+void launch_trace_w(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const PathBuf& in, const int* cnt, int tail) {
+#define L_TR(S) hipLaunchKernelGGL((k_trace<S, STATS, (S == 16 ? W : 1)>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, s.hb, cnt, tail, dev->dstats)
+    IGX_DISPATCH_STACK(dev->stack_depth, L_TR);
+#undef L_TR
+}
+template <bool STATS>
+void launch_trace(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const PathBuf& in, const int* cnt, int tail) {
+    switch (dev->trace_waves) {
+    case 5: launch_trace_w<STATS, 5>(dev, s, grid, fa, in, cnt, tail); break;
+    case 6: launch_trace_w<STATS, 6>(dev, s, grid, fa, in, cnt, tail); break;
+    case 8: launch_trace_w<STATS, 8>(dev, s, grid, fa, in, cnt, tail); break;
+    default: launch_trace_w<STATS, 1>(dev, s, grid, fa, in, cnt, tail); break;
+    }
+}
 template <bool STATS>
 void launch_shadow(igx_device* dev, Slot& s, int grid, const int* cnt) {
 #define L_SH(S) hipLaunchKernelGGL((k_shadow<S, STATS>), dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, s.sh, s.L, cnt, dev->dstats)
@@ -729,6 +846,19 @@ int extend_blocks_per_cu(int depth) {
     if (depth <= 16) return resident_blocks(k_extend<16, STATS>);
     if (depth <= 32) return resident_blocks(k_extend<32, STATS>);
     return resident_blocks(k_extend<64, STATS>);
+}
+template <bool STATS>
+int trace_blocks_per_cu(int depth, int waves) {
+    if (depth <= 16) {
+        switch (waves) {
+        case 5: return resident_blocks(k_trace<16, STATS, 5>);
+        case 6: return resident_blocks(k_trace<16, STATS, 6>);
+        case 8: return resident_blocks(k_trace<16, STATS, 8>);
+        default: return resident_blocks(k_trace<16, STATS, 1>);
+        }
+    }
+    if (depth <= 32) return resident_blocks(k_trace<32, STATS, 1>);
+    return resident_blocks(k_trace<64, STATS, 1>);
 }
 template <bool STATS>
 int shadow_blocks_per_cu(int depth) {
@@ -757,6 +887,7 @@ igx_status harvest(igx_device* dev, Slot& s) {
     // found the live count at or below the tail threshold and exited at once
     dev->stats.launches_extend += (uint64_t)s.launched;
     dev->stats.launches_shadow += (uint64_t)s.launched;
+    if (s.split) dev->stats.launches_trace += (uint64_t)s.launched;
     bool finished = s.switch_bounce < MAX_BOUNCES && c[2 * s.switch_bounce] > 0;
     dev->stats.launches_finish += finished ? 1 : 0;
     if (dev->timing) {
@@ -768,6 +899,7 @@ igx_status harvest(igx_device* dev, Slot& s) {
             else if (t.kind == 2) dev->stats.ms_generate += ms;
             else if (t.kind == 3) dev->stats.ms_resolve += ms;
             else if (t.kind == 4 && finished) dev->stats.ms_finish += ms;
+            else if (t.kind == 5) dev->stats.ms_trace += ms;
         }
     }
     s.timed.clear();
@@ -903,6 +1035,8 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     else if (k == "instrument") dev->instrument = value != 0;
     else if (k == "capacity") dev->capacity_opt = value;
     else if (k == "tail_threshold") dev->tail_opt = value;
+    else if (k == "split") dev->split = value != 0;
+    else if (k == "trace_waves") dev->trace_waves = (int)value;
     else if (k == "bvh_leaf_size") {
         if (value < 1 || value > 16) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "bvh_leaf_size must be in [1, 16]");
         dev->leaf_size = (int)value;
@@ -1232,6 +1366,10 @@ extern "C" igx_status igx_render(igx_device* dev, const igx_render_params* p) {
     const bool inst = dev->instrument;
     const int sd = dev->stack_depth;
     const int ext_bpc = inst ? extend_blocks_per_cu<true>(sd) : extend_blocks_per_cu<false>(sd);
+    const int tr_bpc = inst ? trace_blocks_per_cu<true>(sd, dev->trace_waves) : trace_blocks_per_cu<false>(sd, dev->trace_waves);
+    int shade_bpc = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&shade_bpc, k_shade, BLOCK, 0) != hipSuccess || shade_bpc < 1) shade_bpc = 1;
+    const bool split = dev->split;
     const int sh_bpc = inst ? shadow_blocks_per_cu<true>(sd) : shadow_blocks_per_cu<false>(sd);
     const int fin_bpc = inst ? finish_blocks_per_cu<true>(sd) : finish_blocks_per_cu<false>(sd);
 
@@ -1268,6 +1406,9 @@ extern "C" igx_status igx_render(igx_device* dev, const igx_render_params* p) {
         HIPCHK(hipGetLastError());
         S.pinned[0] = (int)n;
         const int ext_grid = grid_for(dev, n, ext_bpc);
+        const int tr_grid = grid_for(dev, n, tr_bpc);
+        const int shade_grid = grid_for(dev, n, shade_bpc);
+        S.split = split;
         const int sh_grid = grid_for(dev, n, sh_bpc);
         const int fin_grid = grid_for(dev, std::min<long long>(n, tail), fin_bpc);
         // Wavefront bounces on the main stream.  The host learns counts two
@@ -1288,10 +1429,20 @@ extern "C" igx_status igx_render(igx_device* dev, const igx_render_params* p) {
             }
             PathBuf in = (b & 1) ? S.pb : S.pa, out = (b & 1) ? S.pa : S.pb;
             KernelCounters kc{cnt + 2 * b, cnt + 2 * (b + 1), cnt + 2 * b + 1, dev->dstats};
-            begin_timed(0, b, dev->stream);
-            if (inst) launch_extend<true>(dev, S, ext_grid, fa, in, out, kc, tail);
-            else launch_extend<false>(dev, S, ext_grid, fa, in, out, kc, tail);
-            end_timed(dev->stream);
+            if (split) {
+                begin_timed(5, b, dev->stream);
+                if (inst) launch_trace<true>(dev, S, tr_grid, fa, in, cnt + 2 * b, tail);
+                else launch_trace<false>(dev, S, tr_grid, fa, in, cnt + 2 * b, tail);
+                end_timed(dev->stream);
+                begin_timed(0, b, dev->stream);
+                hipLaunchKernelGGL(k_shade, dim3(shade_grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, S.hb, out, S.sh, S.L, kc, tail);
+                end_timed(dev->stream);
+            } else {
+                begin_timed(0, b, dev->stream);
+                if (inst) launch_extend<true>(dev, S, ext_grid, fa, in, out, kc, tail);
+                else launch_extend<false>(dev, S, ext_grid, fa, in, out, kc, tail);
+                end_timed(dev->stream);
+            }
             begin_timed(1, b, dev->stream);
             if (inst) launch_shadow<true>(dev, S, sh_grid, cnt + 2 * b + 1);
             else launch_shadow<false>(dev, S, sh_grid, cnt + 2 * b + 1);

@@ -61,7 +61,6 @@ __device__ __forceinline__ bool trace_ray(const SceneView& sv, f3 o, f3 d, float
     f3 lo = o, ld = d;
     f3 idir = mk(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
     f3 iorg = mk(-(o.x * idir.x), -(o.y * idir.y), -(o.z * idir.z));
-    const f3 w_idir = idir, w_iorg = iorg;
     int cur_ent = -1;
     bool in_blas = false;
     bool found = false;
@@ -109,8 +108,11 @@ __device__ __forceinline__ bool trace_ray(const SceneView& sv, f3 o, f3 d, float
         // ---- leaves, markers, exit ---------------------------------------
         if (node == REF_EXIT) break;
         if (node == REF_MARKER) {
-            // back from a BLAS: restore the world ray
-            lo = o; ld = d; idir = w_idir; iorg = w_iorg;
+            // back from a BLAS: restore the world ray (recomputed: cheaper than
+            // keeping six more registers live through the whole traversal)
+            lo = o; ld = d;
+            idir = mk(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
+            iorg = mk(-(o.x * idir.x), -(o.y * idir.y), -(o.z * idir.z));
             in_blas = false;
             node = stk[(--sp) * stride];
             continue;
@@ -122,6 +124,7 @@ __device__ __forceinline__ bool trace_ray(const SceneView& sv, f3 o, f3 d, float
             // TLAS leaf: entity instances
             int next = 0;
             bool entered = false;
+#pragma unroll 1
             for (int k = 0; k < count; ++k) {
                 if (STATS) st.leaves++;
                 const float4* ip = sv.inst + 4 * (first + k);
@@ -182,6 +185,7 @@ __device__ __forceinline__ bool trace_ray(const SceneView& sv, f3 o, f3 d, float
             }
         } else {
             // BLAS leaf: triangles (make_gpu_tri_prim, shapes/trimesh.art:124-160)
+#pragma unroll 1
             for (int k = 0; k < count; ++k) {
                 if (STATS) st.tris++;
                 const float4* tp = sv.tris + 3 * (first + k);

@@ -84,7 +84,8 @@ class Stats(C.Structure):
                 ("shadow_blas_enters", C.c_uint64), ("shaded_hits", C.c_uint64),
                 ("launches_finish", C.c_uint64), ("ms_finish", C.c_double), ("tail_bounce_rays", C.c_uint64),
                 ("tail_shadow_rays", C.c_uint64), ("bvh_depth", C.c_int32), ("stack_entries", C.c_int32),
-                ("extend_rays", C.c_uint64), ("extend_paths_out", C.c_uint64)]
+                ("extend_rays", C.c_uint64), ("extend_paths_out", C.c_uint64),
+                ("launches_trace", C.c_uint64), ("ms_trace", C.c_double)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

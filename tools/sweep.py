@@ -24,7 +24,7 @@ for o in opts:
     s = dev.stats(); dev.set_option("timing", 0)
     rays = (s["camera_rays"] + s["bounce_rays"] + s["shadow_rays"]) / K
     print(json.dumps({"opt": o, "ms_iter": round(dt * 1e3, 3), "Mrays/s": round(rays / dt / 1e6, 1),
-                      "ext": round(s["ms_extend"] / K, 3), "sh": round(s["ms_shadow"] / K, 3), "fin": round(s["ms_finish"] / K, 3),
+                      "tr": round(s["ms_trace"] / K, 3), "ext": round(s["ms_extend"] / K, 3), "sh": round(s["ms_shadow"] / K, 3), "fin": round(s["ms_finish"] / K, 3),
                       "gen": round(s["ms_generate"] / K, 3), "res": round(s["ms_resolve"] / K, 3),
                       "wf_bounces": s["launches_extend"] / K, "tail_rays": (s["tail_bounce_rays"] + s["tail_shadow_rays"]) / K,
                       "depth": s["bvh_depth"], "stack": s["stack_entries"]}), flush=True)
