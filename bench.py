@@ -47,25 +47,30 @@ def parse():
 
 
 def algorithmic_bytes(stats_inst, st):
-    """Algorithmic bytes of the k_extend launches (closest hit + shade), DESIGN.md §Roofline.
+    """Algorithmic bytes of the dominant wavefront kernel's launches, DESIGN.md §4.
 
-    Per closest-hit ray: 52 B path state read + 32 B radiance read/write
-    + 64 B per BVH2 node + 64 B per instance record + 48 B per triangle
-    + 288 B of shading fetches per hit (entity 112, face 16, 3 vertices +
-    3 normals 96, material 64); plus 52 B per surviving path and 48 B per
-    shadow ray written.  Per-ray visit counts come from an instrumented pass;
-    ray counts are the ones k_extend handled in the timed run (the tail
-    kernel's rays are excluded).
+    Per-ray visit counts (BVH2 nodes, instance records, triangles, hits) come
+    from an instrumented pass; ray counts are those the wavefront kernels
+    handled in the timed run (the tail kernel's rays are excluded).
+    * fused k_extend (default): per closest-hit ray 52 B path state read +
+      32 B radiance read/write + 64 B per node + 64 B per instance + 48 B per
+      triangle + 288 B of shading fetches per hit (entity 112, face 16,
+      3 vertices + 3 normals 96, material 64); plus 52 B per surviving path
+      and 48 B per shadow ray written;
+    * split k_trace: 32 B ray read + 20 B hit written + the same BVH terms.
     """
     n = max(stats_inst["_rays_ext"], 1)
-    per_ray = (52 + 32 + 64.0 * stats_inst["node_visits"] / n + 64.0 * stats_inst["leaf_visits"] / n
-               + 48.0 * stats_inst["tri_tests"] / n + 288.0 * stats_inst["_hits"] / n)
+    bvh = 64.0 * stats_inst["node_visits"] / n + 64.0 * stats_inst["leaf_visits"] / n + 48.0 * stats_inst["tri_tests"] / n
+    if st["launches_trace"] > 0:
+        per_ray = 32 + 20 + bvh
+        return st["extend_rays"] * per_ray, per_ray
+    per_ray = 52 + 32 + bvh + 288.0 * stats_inst["_hits"] / n
     shadow_wf = st["shadow_rays"] - st["tail_shadow_rays"]
     return st["extend_rays"] * per_ray + st["extend_paths_out"] * 52 + shadow_wf * 48, per_ray
 
 
 def load_pmc(n_gpus):
-    """Per-launch HBM traffic of the extend kernel from the committed rocprofv3 PMC summary."""
+    """Per-launch HBM traffic of the dominant kernel (k_extend) from the committed rocprofv3 PMC summary."""
     path = os.path.join(ROOT, "profiles", "pmc_extend.json")
     if n_gpus != 1 or not os.path.exists(path):
         return None
@@ -173,8 +178,9 @@ def main():
     inst["_rays_ext"] = inst["camera_rays"] + inst["bounce_rays"]
     inst["_hits"] = inst["shaded_hits"]
     alg_bytes, bytes_per_ray = algorithmic_bytes(inst, st)
-    launches = max(st["launches_extend"], 1)
-    avg_launch_s = st["ms_extend"] / 1e3 / launches
+    split = st["launches_trace"] > 0
+    launches = max(st["launches_trace"] if split else st["launches_extend"], 1)
+    avg_launch_s = (st["ms_trace"] if split else st["ms_extend"]) / 1e3 / launches
     achieved = (alg_bytes / launches) / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
     traffic = load_pmc(n_gpus)
 
@@ -208,12 +214,13 @@ def main():
             },
             "msamples_per_s": round(samples / elapsed / 1e6, 2),
             "rays": {"camera": int(totals[1]), "bounce": int(totals[2]), "shadow": int(totals[3])},
-            "kernel_ms": {"extend": round(st["ms_extend"], 3), "shadow": round(st["ms_shadow"], 3),
+            "kernel_ms": {"trace": round(st["ms_trace"], 3), "extend": round(st["ms_extend"], 3), "shadow": round(st["ms_shadow"], 3),
                           "finish": round(st["ms_finish"], 3),
                           "generate": round(st["ms_generate"], 3), "resolve": round(st["ms_resolve"], 3)},
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_extend (closest-hit traversal + shading)",
+                "kernel": "k_trace (closest-hit traversal)" if split else "k_extend (closest-hit traversal + shading, fused)",
+                "simd_efficiency": round(inst["node_visits"] / max(1, 64 * inst["wave_node_iters"]), 3),
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

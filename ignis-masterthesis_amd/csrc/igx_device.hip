@@ -38,6 +38,9 @@ namespace {
 
 constexpr int BLOCK = 256;
 constexpr int MAX_BOUNCES = 256;
+#ifndef TRAV_STEP
+#define TRAV_STEP trav_step
+#endif
 
 // ---------------------------------------------------------------------------
 // Streams (SoA of 16-byte records)
@@ -88,6 +91,16 @@ __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 template <typename T>
 __device__ __forceinline__ T uniform_load(const T* p) {
     return __builtin_amdgcn_readfirstlane(*p);
+}
+
+__device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << __lane_id()) - 1ull; }
+
+// Contiguous share [begin, end) of n items for the calling wave (wave-uniform).
+__device__ __forceinline__ void wave_range(int n, int& begin, int& end) {
+    const int waves = (int)(gridDim.x * (BLOCK / 64));
+    const int w = (int)(blockIdx.x * (BLOCK / 64) + threadIdx.x / 64);
+    begin = (int)((long long)n * w / waves);
+    end = (int)((long long)n * (w + 1) / waves);
 }
 
 // ---------------------------------------------------------------------------
@@ -334,13 +347,16 @@ __device__ __forceinline__ void add_radiance(float4* L, int slot, f3 c) {
 
 template <bool STATS>
 __device__ __forceinline__ void flush_stats(const TraceStats& st, unsigned long long* stats, int base, bool with_hits) {
-    unsigned long long a = st.nodes, b = st.leaves, c = st.tris, e = st.blas, h = st.hits;
+    // slots: base+0..3 nodes/leaves/tris/blas, 8 hits, 9+base/4*2 .. wave node / leaf iterations
+    unsigned long long a = st.nodes, b = st.leaves, c = st.tris, e = st.blas, h = st.hits, wn = st.wnodes, wl = st.wleaves;
     for (int off = 32; off > 0; off >>= 1) {
         a += __shfl_down(a, off);
         b += __shfl_down(b, off);
         c += __shfl_down(c, off);
         e += __shfl_down(e, off);
         h += __shfl_down(h, off);
+        wn += __shfl_down(wn, off);
+        wl += __shfl_down(wl, off);
     }
     if (lane_id() == 0) {
         atomicAdd(&stats[base + 0], a);
@@ -348,6 +364,8 @@ __device__ __forceinline__ void flush_stats(const TraceStats& st, unsigned long 
         atomicAdd(&stats[base + 2], c);
         atomicAdd(&stats[base + 3], e);
         if (with_hits) atomicAdd(&stats[8], h);
+        atomicAdd(&stats[9 + (base / 4) * 2], wn);
+        atomicAdd(&stats[10 + (base / 4) * 2], wl);
     }
 }
 
@@ -386,15 +404,17 @@ __device__ __forceinline__ void block_append2(bool a, bool b, int* ca, int* cb, 
 // ---------------------------------------------------------------------------
 // extend kernel: one bounce for every live path, compacted outputs
 // ---------------------------------------------------------------------------
-template <int STACK, bool STATS>
-__global__ void __launch_bounds__(BLOCK) k_extend(FrameArgs fa, SceneView sv, PathBuf in, PathBuf out, ShadowBuf sh,
+template <int STACK, bool STATS, bool LDS>
+__global__ void __launch_bounds__(BLOCK) k_extend(FrameArgs fa, SceneView gsv, PathBuf in, PathBuf out, ShadowBuf sh,
                                                   float4* L, KernelCounters kc, int tail_threshold) {
     __shared__ int stack_mem[STACK * BLOCK + 2 * (BLOCK / 64) + 2];
+    extern __shared__ float4 lds_scene[];
     int* stk = stack_mem + threadIdx.x;
     int* scan = stack_mem + STACK * BLOCK;
     const int n = uniform_load(kc.cnt_in);
     if (n <= tail_threshold) return; // k_finish takes the remaining paths
-    TraceStats st{0, 0, 0, 0, 0};
+    const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
+    TraceStats st{0, 0, 0, 0, 0, 0, 0};
     for (int base = blockIdx.x * BLOCK; base < n; base += gridDim.x * BLOCK) {
         int i = base + threadIdx.x;
         bool alive = false, has_shadow = false;
@@ -428,30 +448,59 @@ __global__ void __launch_bounds__(BLOCK) k_extend(FrameArgs fa, SceneView sv, Pa
 // for high occupancy (the latency of the dependent node loads is what bounds
 // it); each lane writes its own hit record, no block synchronisation.
 // ---------------------------------------------------------------------------
-template <int STACK, bool STATS, int WAVES>
-__global__ void __launch_bounds__(BLOCK, WAVES) k_trace(FrameArgs fa, SceneView sv, PathBuf in, HitBuf hits,
-                                                                     const int* cnt, int tail_threshold,
-                                                                     unsigned long long* stats) {
+template <int STACK, bool STATS, int WAVES, bool LDS>
+__global__ void __launch_bounds__(BLOCK, WAVES) k_trace(FrameArgs fa, SceneView gsv, PathBuf in, HitBuf hits,
+                                                      const int* cnt, int tail_threshold, unsigned long long* stats) {
     __shared__ int stack_mem[STACK * BLOCK];
+    extern __shared__ float4 lds_scene[];
     int* stk = stack_mem + threadIdx.x;
     const int n = uniform_load(cnt);
     if (n <= tail_threshold) return; // k_finish takes the remaining paths
-    TraceStats st{0, 0, 0, 0, 0};
-    for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
-        float4 p0 = in.p0[i], p1 = in.p1[i];
-        int sd = __float_as_int(p0.w);
-        int depth = sd >> 24;
-        int hit_ent = -1, hit_prim = -1;
-        float hu = 0, hv = 0, tmax = 0;
-        if (depth > 0) {
-            float tmin;
-            uint32_t rflags;
-            ray_extent(fa, sv, depth, sd & 0xFFFFFF, tmin, tmax, rflags);
-            trace_ray<false, STATS>(sv, f3of(p0), f3of(p1), tmin, tmax, rflags, stk, BLOCK, hit_ent, hit_prim, hu, hv, st);
-            if (STATS && hit_ent >= 0) st.hits++;
+    const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
+    TraceStats st{0, 0, 0, 0, 0, 0, 0};
+    // Persistent wave with lane refill: each wave owns a contiguous range of
+    // rays; a lane whose ray finished takes the next one at once, so the wave
+    // does not idle behind its longest ray (Aila & Laine 2009).
+    int next, end;
+    wave_range(n, next, end);
+    Trav t;
+    int ri = -1; // ray index; -1 wants a ray, -2 range exhausted
+    for (;;) {
+        const bool need = ri == -1;
+        const uint64_t m = __ballot(need);
+        if (m) {
+            const int idx = next + __popcll(m & lanemask_lt());
+            next += __popcll(m);
+            if (need) {
+                if (idx < end) {
+                    float4 p0 = in.p0[idx], p1 = in.p1[idx];
+                    int sd = __float_as_int(p0.w);
+                    int depth = sd >> 24;
+                    if (depth > 0) {
+                        float tmin, tmax;
+                        uint32_t rflags;
+                        ray_extent(fa, sv, depth, sd & 0xFFFFFF, tmin, tmax, rflags);
+                        trav_init(sv, t, f3of(p0), f3of(p1), tmin, tmax, rflags, stk);
+                        ri = idx;
+                    } else {
+                        hits.h[idx] = make_float4(0, 0, 0, __int_as_float(-1)); // dead slot
+                        hits.prim[idx] = -1;
+                    }
+                } else {
+                    ri = -2;
+                }
+            }
         }
-        hits.h[i] = make_float4(tmax, hu, hv, __int_as_float(hit_ent));
-        hits.prim[i] = hit_prim;
+        if (__ballot(ri >= 0) == 0) {
+            if (__ballot(ri == -1) == 0) break;
+            continue;
+        }
+        if (ri >= 0 && TRAV_STEP<false, STATS>(sv, t, stk, BLOCK, st)) {
+            if (STATS && t.hit_ent >= 0) st.hits++;
+            hits.h[ri] = make_float4(t.tmax, t.hu, t.hv, __int_as_float(t.hit_ent));
+            hits.prim[ri] = t.hit_prim;
+            ri = -1;
+        }
     }
     if (STATS) flush_stats<STATS>(st, stats, 0, true);
 }
@@ -500,16 +549,18 @@ __global__ void __launch_bounds__(BLOCK) k_shade(FrameArgs fa, SceneView sv, Pat
 // empty per-bounce launches.  Same per-path arithmetic and the same radiance
 // accumulation order as the wavefront kernels.
 // ---------------------------------------------------------------------------
-template <int STACK, bool STATS>
-__global__ void __launch_bounds__(BLOCK) k_finish(FrameArgs fa, SceneView sv, PathBuf in, float4* L, const int* cnt,
+template <int STACK, bool STATS, bool LDS>
+__global__ void __launch_bounds__(BLOCK) k_finish(FrameArgs fa, SceneView gsv, PathBuf in, float4* L, const int* cnt,
                                                   int tail_threshold, unsigned long long* stats,
                                                   unsigned long long* tail_counts) {
     __shared__ int stack_mem[STACK * BLOCK];
+    extern __shared__ float4 lds_scene[];
     int* stk = stack_mem + threadIdx.x;
     const int n = uniform_load(cnt);
-    if (n > tail_threshold) return; // the wavefront kernels own this bounce
-    TraceStats st{0, 0, 0, 0, 0};
-    TraceStats sst{0, 0, 0, 0, 0};
+    if (n > tail_threshold || n == 0) return; // the wavefront kernels own this bounce
+    const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
+    TraceStats st{0, 0, 0, 0, 0, 0, 0};
+    TraceStats sst{0, 0, 0, 0, 0, 0, 0};
     unsigned long long bounces = 0, shadows = 0;
     for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
         PathState ps = load_path(in, i);
@@ -551,22 +602,41 @@ __global__ void __launch_bounds__(BLOCK) k_finish(FrameArgs fa, SceneView sv, Pa
 // shadow: any-hit traversal; on miss add the NEE contribution
 // (gpu_traverse_secondary, mapping_gpu.art:70-112; on_shadow_miss, pathtracer.art:202-209)
 // ---------------------------------------------------------------------------
-template <int STACK, bool STATS>
-__global__ void __launch_bounds__(BLOCK) k_shadow(SceneView sv, ShadowBuf sh, float4* L, const int* cnt,
+template <int STACK, bool STATS, bool LDS>
+__global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, float4* L, const int* cnt,
                                                   unsigned long long* stats) {
     __shared__ int stack_mem[STACK * BLOCK];
+    extern __shared__ float4 lds_scene[];
     int* stk = stack_mem + threadIdx.x;
     const int n = uniform_load(cnt);
-    TraceStats st{0, 0, 0, 0, 0};
-    for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
-        float4 s0 = sh.s0[i], s1 = sh.s1[i];
-        float tmax = s1.w;
-        int e, p;
-        float u, v;
-        bool occluded = trace_ray<true, STATS>(sv, f3of(s0), f3of(s1), 0.001f, tmax, RAY_SHADOW, stk, BLOCK, e, p, u, v, st);
-        if (!occluded) {
-            float4 c = sh.s2[i];
-            add_radiance(L, __float_as_int(s0.w), f3of(c));
+    if (n == 0) return;
+    const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
+    TraceStats st{0, 0, 0, 0, 0, 0, 0};
+    int next, end;
+    wave_range(n, next, end);
+    Trav t;
+    int ri = -1, slot = 0;
+    for (;;) {
+        const bool need = ri == -1;
+        const uint64_t m = __ballot(need);
+        if (m) {
+            const int idx = next + __popcll(m & lanemask_lt());
+            next += __popcll(m);
+            if (need) {
+                if (idx < end) {
+                    float4 s0 = sh.s0[idx], s1 = sh.s1[idx];
+                    slot = __float_as_int(s0.w);
+                    trav_init(sv, t, f3of(s0), f3of(s1), 0.001f, s1.w, RAY_SHADOW, stk);
+                    ri = idx;
+                } else {
+                    ri = -2;
+                }
+            }
+        }
+        if (__ballot(ri >= 0) == 0) break;
+        if (ri >= 0 && TRAV_STEP<true, STATS>(sv, t, stk, BLOCK, st)) {
+            if (!t.found) add_radiance(L, slot, f3of(sh.s2[ri]));
+            ri = -1;
         }
     }
     if (STATS) flush_stats<STATS>(st, stats, 4, false);
@@ -613,7 +683,7 @@ __global__ void __launch_bounds__(BLOCK) k_trace_hits(SceneView sv, const float*
     float tmax = r[7];
     int e, p;
     float u = 0, v = 0;
-    TraceStats st{0, 0, 0, 0, 0};
+    TraceStats st{0, 0, 0, 0, 0, 0, 0};
     if (any) {
         bool occ = trace_ray<true, false>(sv, mk(r[0], r[1], r[2]), mk(r[3], r[4], r[5]), r[6], tmax, flags, stk, BLOCK, e, p, u, v, st);
         ent_prim[i] = occ ? 1 : 0;
@@ -680,8 +750,10 @@ struct igx_device {
     bool instrument = false;
     int64_t capacity_opt = 0;
     int64_t tail_opt = -1;   // paths at or below which k_finish takes over (-1 = auto)
-    bool split = true;       // k_trace + k_shade per bounce (false: fused k_extend)
+    bool split = false;      // k_trace + k_shade per bounce (default: fused k_extend)
     int trace_waves = 5;     // occupancy target of k_trace<16> (0 = compiler's choice; 5, 6, 8)
+    int64_t lds_scene_max = 48 * 1024; // stage traversal tables in LDS when they fit (0 = never)
+    size_t lds_scene_bytes = 0;        // bytes staged per block for the current scene (0 = global tables)
     int leaf_size = 4;
     // scene
     bool has_scene = false;
@@ -800,20 +872,33 @@ int grid_for(igx_device* dev, long long items, int blocks_per_cu) {
 template <bool STATS>
 void launch_extend(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const PathBuf& in, const PathBuf& out,
                    const KernelCounters& kc, int tail) {
-#define L_EXT(S) hipLaunchKernelGGL((k_extend<S, STATS>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, out, s.sh, s.L, kc, tail)
+    if (dev->lds_scene_bytes) {
+#define L_EXTL(S) hipLaunchKernelGGL((k_extend<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->stream, fa, dev->sv, in, out, s.sh, s.L, kc, tail)
+        IGX_DISPATCH_STACK(dev->stack_depth, L_EXTL);
+#undef L_EXTL
+        return;
+    }
+#define L_EXT(S) hipLaunchKernelGGL((k_extend<S, STATS, false>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, out, s.sh, s.L, kc, tail)
     IGX_DISPATCH_STACK(dev->stack_depth, L_EXT);
 #undef L_EXT
 }
 // k_trace variants: the 16-entry stack build comes with an occupancy target
 // (waves per SIMD, option "trace_waves"); deeper stacks are LDS-limited anyway.
+// With the traversal tables staged in LDS (small scenes) LDS sets occupancy.
 template <bool STATS, int W>
 void launch_trace_w(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const PathBuf& in, const int* cnt, int tail) {
-#define L_TR(S) hipLaunchKernelGGL((k_trace<S, STATS, (S == 16 ? W : 1)>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, s.hb, cnt, tail, dev->dstats)
+#define L_TR(S) hipLaunchKernelGGL((k_trace<S, STATS, (S == 16 ? W : 1), false>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, s.hb, cnt, tail, dev->dstats)
     IGX_DISPATCH_STACK(dev->stack_depth, L_TR);
 #undef L_TR
 }
 template <bool STATS>
 void launch_trace(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const PathBuf& in, const int* cnt, int tail) {
+    if (dev->lds_scene_bytes) {
+#define L_TRL(S) hipLaunchKernelGGL((k_trace<S, STATS, 1, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->stream, fa, dev->sv, in, s.hb, cnt, tail, dev->dstats)
+        IGX_DISPATCH_STACK(dev->stack_depth, L_TRL);
+#undef L_TRL
+        return;
+    }
     switch (dev->trace_waves) {
     case 5: launch_trace_w<STATS, 5>(dev, s, grid, fa, in, cnt, tail); break;
     case 6: launch_trace_w<STATS, 6>(dev, s, grid, fa, in, cnt, tail); break;
@@ -823,54 +908,86 @@ void launch_trace(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const
 }
 template <bool STATS>
 void launch_shadow(igx_device* dev, Slot& s, int grid, const int* cnt) {
-#define L_SH(S) hipLaunchKernelGGL((k_shadow<S, STATS>), dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, s.sh, s.L, cnt, dev->dstats)
+    if (dev->lds_scene_bytes) {
+#define L_SHL(S) hipLaunchKernelGGL((k_shadow<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->stream, dev->sv, s.sh, s.L, cnt, dev->dstats)
+        IGX_DISPATCH_STACK(dev->stack_depth, L_SHL);
+#undef L_SHL
+        return;
+    }
+#define L_SH(S) hipLaunchKernelGGL((k_shadow<S, STATS, false>), dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, s.sh, s.L, cnt, dev->dstats)
     IGX_DISPATCH_STACK(dev->stack_depth, L_SH);
 #undef L_SH
 }
 template <bool STATS>
 void launch_finish(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const PathBuf& in, const int* cnt, int tail) {
-#define L_FIN(S) hipLaunchKernelGGL((k_finish<S, STATS>), dim3(grid), dim3(BLOCK), 0, dev->tail_stream, fa, dev->sv, in, s.L, cnt, tail, dev->dstats, dev->tail_counts)
+    if (dev->lds_scene_bytes) {
+#define L_FINL(S) hipLaunchKernelGGL((k_finish<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->tail_stream, fa, dev->sv, in, s.L, cnt, tail, dev->dstats, dev->tail_counts)
+        IGX_DISPATCH_STACK(dev->stack_depth, L_FINL);
+#undef L_FINL
+        return;
+    }
+#define L_FIN(S) hipLaunchKernelGGL((k_finish<S, STATS, false>), dim3(grid), dim3(BLOCK), 0, dev->tail_stream, fa, dev->sv, in, s.L, cnt, tail, dev->dstats, dev->tail_counts)
     IGX_DISPATCH_STACK(dev->stack_depth, L_FIN);
 #undef L_FIN
 }
 
 // resident blocks per CU of a kernel (persistent grid sizing)
 template <typename K>
-int resident_blocks(K kernel) {
+int resident_blocks(K kernel, size_t dyn_lds = 0) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, BLOCK, 0) != hipSuccess || nb < 1) nb = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, BLOCK, dyn_lds) != hipSuccess || nb < 1) nb = 1;
     return nb;
 }
 template <bool STATS>
-int extend_blocks_per_cu(int depth) {
-    if (depth <= 16) return resident_blocks(k_extend<16, STATS>);
-    if (depth <= 32) return resident_blocks(k_extend<32, STATS>);
-    return resident_blocks(k_extend<64, STATS>);
+int extend_blocks_per_cu(int depth, size_t lds) {
+    if (lds) {
+        if (depth <= 16) return resident_blocks(k_extend<16, STATS, true>, lds);
+        if (depth <= 32) return resident_blocks(k_extend<32, STATS, true>, lds);
+        return resident_blocks(k_extend<64, STATS, true>, lds);
+    }
+    if (depth <= 16) return resident_blocks(k_extend<16, STATS, false>);
+    if (depth <= 32) return resident_blocks(k_extend<32, STATS, false>);
+    return resident_blocks(k_extend<64, STATS, false>);
 }
 template <bool STATS>
-int trace_blocks_per_cu(int depth, int waves) {
+int trace_blocks_per_cu(int depth, int waves, size_t lds) {
+    if (lds) {
+        if (depth <= 16) return resident_blocks(k_trace<16, STATS, 1, true>, lds);
+        if (depth <= 32) return resident_blocks(k_trace<32, STATS, 1, true>, lds);
+        return resident_blocks(k_trace<64, STATS, 1, true>, lds);
+    }
     if (depth <= 16) {
         switch (waves) {
-        case 5: return resident_blocks(k_trace<16, STATS, 5>);
-        case 6: return resident_blocks(k_trace<16, STATS, 6>);
-        case 8: return resident_blocks(k_trace<16, STATS, 8>);
-        default: return resident_blocks(k_trace<16, STATS, 1>);
+        case 5: return resident_blocks(k_trace<16, STATS, 5, false>);
+        case 6: return resident_blocks(k_trace<16, STATS, 6, false>);
+        case 8: return resident_blocks(k_trace<16, STATS, 8, false>);
+        default: return resident_blocks(k_trace<16, STATS, 1, false>);
         }
     }
-    if (depth <= 32) return resident_blocks(k_trace<32, STATS, 1>);
-    return resident_blocks(k_trace<64, STATS, 1>);
+    if (depth <= 32) return resident_blocks(k_trace<32, STATS, 1, false>);
+    return resident_blocks(k_trace<64, STATS, 1, false>);
 }
 template <bool STATS>
-int shadow_blocks_per_cu(int depth) {
-    if (depth <= 16) return resident_blocks(k_shadow<16, STATS>);
-    if (depth <= 32) return resident_blocks(k_shadow<32, STATS>);
-    return resident_blocks(k_shadow<64, STATS>);
+int shadow_blocks_per_cu(int depth, size_t lds) {
+    if (lds) {
+        if (depth <= 16) return resident_blocks(k_shadow<16, STATS, true>, lds);
+        if (depth <= 32) return resident_blocks(k_shadow<32, STATS, true>, lds);
+        return resident_blocks(k_shadow<64, STATS, true>, lds);
+    }
+    if (depth <= 16) return resident_blocks(k_shadow<16, STATS, false>);
+    if (depth <= 32) return resident_blocks(k_shadow<32, STATS, false>);
+    return resident_blocks(k_shadow<64, STATS, false>);
 }
 template <bool STATS>
-int finish_blocks_per_cu(int depth) {
-    if (depth <= 16) return resident_blocks(k_finish<16, STATS>);
-    if (depth <= 32) return resident_blocks(k_finish<32, STATS>);
-    return resident_blocks(k_finish<64, STATS>);
+int finish_blocks_per_cu(int depth, size_t lds) {
+    if (lds) {
+        if (depth <= 16) return resident_blocks(k_finish<16, STATS, true>, lds);
+        if (depth <= 32) return resident_blocks(k_finish<32, STATS, true>, lds);
+        return resident_blocks(k_finish<64, STATS, true>, lds);
+    }
+    if (depth <= 16) return resident_blocks(k_finish<16, STATS, false>);
+    if (depth <= 32) return resident_blocks(k_finish<32, STATS, false>);
+    return resident_blocks(k_finish<64, STATS, false>);
 }
 
 // Wait for the chunk last run in `s` and fold its statistics in.
@@ -1037,6 +1154,11 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     else if (k == "tail_threshold") dev->tail_opt = value;
     else if (k == "split") dev->split = value != 0;
     else if (k == "trace_waves") dev->trace_waves = (int)value;
+    else if (k == "lds_scene_max") {
+        dev->lds_scene_max = value;
+        size_t b = ((size_t)dev->sv.num_nodes * 4 + (size_t)dev->sv.num_inst * 4 + (size_t)dev->sv.num_tris * 3) * 16;
+        dev->lds_scene_bytes = dev->has_scene && (int64_t)b <= value ? b : 0;
+    }
     else if (k == "bvh_leaf_size") {
         if (value < 1 || value > 16) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "bvh_leaf_size must be in [1, 16]");
         dev->leaf_size = (int)value;
@@ -1261,6 +1383,13 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
         return st;
     }
     sv.tlas_root = tlas_root;
+    sv.num_nodes = (int)nodes.size();
+    sv.num_inst = (int)(inst.size() / 4);
+    sv.num_tris = (int)(tris.size() / 3);
+    {
+        size_t b = ((size_t)sv.num_nodes * 4 + (size_t)sv.num_inst * 4 + (size_t)sv.num_tris * 3) * 16;
+        dev->lds_scene_bytes = (int64_t)b <= dev->lds_scene_max ? b : 0;
+    }
     sv.num_lights = (int)lights.size();
     sv.num_infinite = num_infinite;
     // bbox_radius(scene_bbox) * 1.01 (light/env.art:75; core/bbox.art:24)
@@ -1274,8 +1403,8 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     sv.clamp = desc->technique.clamp;
     dev->cam_desc = desc->camera;
     dev->sv = sv;
-    // stack: TLAS depth + BLAS depth + marker + exit sentinel
-    dev->scene_depth = tlas_depth + blas_depth + 2;
+    // stack: TLAS depth + BLAS depth + marker + resume entry + exit sentinel
+    dev->scene_depth = tlas_depth + blas_depth + 3;
     if (dev->scene_depth > 64) {
         free_scene(dev);
         return fail(dev, IGX_ERR_UNSUPPORTED, "BVH too deep for the 64-entry LDS stack (depth " + std::to_string(dev->scene_depth) + ")");
@@ -1365,13 +1494,15 @@ extern "C" igx_status igx_render(igx_device* dev, const igx_render_params* p) {
     const int max_bounces = std::min(std::max(dev->sv.max_depth, 1), MAX_BOUNCES - 1);
     const bool inst = dev->instrument;
     const int sd = dev->stack_depth;
-    const int ext_bpc = inst ? extend_blocks_per_cu<true>(sd) : extend_blocks_per_cu<false>(sd);
-    const int tr_bpc = inst ? trace_blocks_per_cu<true>(sd, dev->trace_waves) : trace_blocks_per_cu<false>(sd, dev->trace_waves);
+    const size_t ldsb = dev->lds_scene_bytes;
+    const int ext_bpc = inst ? extend_blocks_per_cu<true>(sd, ldsb) : extend_blocks_per_cu<false>(sd, ldsb);
+    const int tr_bpc = inst ? trace_blocks_per_cu<true>(sd, dev->trace_waves, dev->lds_scene_bytes)
+                            : trace_blocks_per_cu<false>(sd, dev->trace_waves, dev->lds_scene_bytes);
     int shade_bpc = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&shade_bpc, k_shade, BLOCK, 0) != hipSuccess || shade_bpc < 1) shade_bpc = 1;
     const bool split = dev->split;
-    const int sh_bpc = inst ? shadow_blocks_per_cu<true>(sd) : shadow_blocks_per_cu<false>(sd);
-    const int fin_bpc = inst ? finish_blocks_per_cu<true>(sd) : finish_blocks_per_cu<false>(sd);
+    const int sh_bpc = inst ? shadow_blocks_per_cu<true>(sd, dev->lds_scene_bytes) : shadow_blocks_per_cu<false>(sd, dev->lds_scene_bytes);
+    const int fin_bpc = inst ? finish_blocks_per_cu<true>(sd, ldsb) : finish_blocks_per_cu<false>(sd, ldsb);
 
     for (long long px0 = 0; px0 < local_pixels; px0 += chunk_pixels_max) {
         Slot& S = dev->slots[dev->next_slot];
@@ -1564,6 +1695,10 @@ extern "C" igx_status igx_get_stats(igx_device* dev, igx_stats* out) {
     out->shadow_tri_tests = h[6];
     out->shadow_blas_enters = h[7];
     out->shaded_hits = h[8];
+    out->wave_node_iters = h[9];
+    out->wave_leaf_iters = h[10];
+    out->shadow_wave_node_iters = h[11];
+    out->shadow_wave_leaf_iters = h[12];
     return IGX_OK;
 }
 

@@ -29,11 +29,36 @@ struct SceneView {
     DevCamera cam;
     int max_depth, min_depth, nee;
     float clamp;
+    int num_nodes, num_inst, num_tris; // table sizes (for staging the traversal tables in LDS)
 };
+
+// Copy the traversal tables (nodes, instances, triangles) of a small scene
+// into LDS, laid out back to back, and point a block-local view at them: the
+// node loop then reads LDS (~50-cycle ds_read) instead of the vector-memory
+// path, which the divergent node fetches otherwise keep busy.
+template <int BLOCK_>
+__device__ __forceinline__ SceneView stage_scene_lds(const SceneView& sv, float4* lds) {
+    const int n4 = sv.num_nodes * 4, i4 = sv.num_inst * 4, t3 = sv.num_tris * 3;
+    for (int k = threadIdx.x; k < n4; k += BLOCK_) lds[k] = sv.nodes[k];
+    for (int k = threadIdx.x; k < i4; k += BLOCK_) lds[n4 + k] = sv.inst[k];
+    for (int k = threadIdx.x; k < t3; k += BLOCK_) lds[n4 + i4 + k] = sv.tris[k];
+    __syncthreads();
+    SceneView l = sv;
+    l.nodes = lds;
+    l.inst = lds + n4;
+    l.tris = lds + n4 + i4;
+    return l;
+}
 
 struct TraceStats {
     uint32_t nodes, leaves, tris, blas, hits;
+    uint32_t wnodes, wleaves; // wave-level iterations of the node loop / leaf phase (SIMD efficiency)
 };
+
+// true on the lowest active lane of the wave (counts one event per wave)
+__device__ __forceinline__ bool first_active_lane() {
+    return (int)__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1;
+}
 
 // Ray flags (traversal/ray.art:19-23)
 constexpr uint32_t RAY_CAMERA = 0x1, RAY_LIGHT = 0x2, RAY_BOUNCE = 0x4, RAY_SHADOW = 0x8, RAY_TYPE_MASK = 0xF;
@@ -49,174 +74,312 @@ constexpr uint32_t RAY_CAMERA = 0x1, RAY_LIGHT = 0x2, RAY_BOUNCE = 0x4, RAY_SHAD
 // (ray.art:51), Moeller-Trumbore with -eps barycentric tolerance and u,v clamp
 // (intersection.art:71-101), analytic sphere (shapes/sphere.art:104-130).
 // ---------------------------------------------------------------------------
+// Traversal state of one ray, resumable: trav_step advances it to the next
+// leaf (or the end), so a persistent kernel can refill lanes whose ray ended
+// while the rest of the wave keeps traversing.
+struct Trav {
+    f3 o, d;          // world ray
+    f3 lo, ld;        // ray of the current level (world at the TLAS, entity space in a BLAS)
+    f3 idir, iorg;    // slab-test form of the current-level ray
+    float tmin, tmax; // tmax shrinks on every accepted hit
+    int node, sp;
+    int prim, prim_end; // open leaf range (trav_micro)
+    int cur_ent;
+    int hit_ent, hit_prim;
+    float hu, hv;
+    uint32_t rflags;
+    bool in_blas, found;
+};
+
+__device__ __forceinline__ bool is_leaf_ref(int r) { return r < 0 && r > REF_EXIT; }
+
+// Closest-hit acceptance with an order-independent tie rule: among hits at the
+// same distance the larger (entity, primitive) wins.  The reference keeps the
+// later-visited one (t <= tmax, intersection.art:97), which depends on BVH
+// topology and traversal order; this rule makes the result independent of
+// both (speculative traversal, tile sharding, tail vs wavefront kernel).
+__device__ __forceinline__ bool accept_hit(const Trav& t, float th, int ent, int prim) {
+    return th >= t.tmin && (th < t.tmax || (th == t.tmax && (ent > t.hit_ent || (ent == t.hit_ent && prim > t.hit_prim))));
+}
+
+__device__ __forceinline__ void trav_init(const SceneView& sv, Trav& t, f3 o, f3 d, float tmin, float tmax, uint32_t rflags,
+                                          int* stk) {
+    t.o = o;
+    t.d = d;
+    t.lo = o;
+    t.ld = d;
+    t.idir = mk(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
+    t.iorg = mk(-(o.x * t.idir.x), -(o.y * t.idir.y), -(o.z * t.idir.z));
+    t.tmin = tmin;
+    t.tmax = tmax;
+    t.rflags = rflags;
+    t.cur_ent = -1;
+    t.hit_ent = -1;
+    t.hit_prim = -1;
+    t.hu = 0;
+    t.hv = 0;
+    t.in_blas = false;
+    t.found = false;
+    t.prim = 0;
+    t.prim_end = 0;
+    stk[0] = REF_EXIT;
+    t.sp = 1;
+    t.node = sv.tlas_root < 0 ? REF_EXIT : sv.tlas_root;
+}
+
+// Slab test of both children of BVH2 node `node` (intersect_ray_box,
+// intersection.art:170-181, with ray.tmin folded in).  Returns the next node
+// (nearer child first; the other is pushed) or the popped entry.
+template <bool STATS>
+__device__ __forceinline__ int node_step(const SceneView& sv, const Trav& t, int node, int* stk, int stride, int& sp,
+                                         TraceStats& st) {
+    if (STATS) {
+        st.nodes++;
+        if (first_active_lane()) st.wnodes++;
+    }
+    const float4* np = sv.nodes + 4 * node;
+    float4 a = np[0], b = np[1], c = np[2];
+    int4 r = *reinterpret_cast<const int4*>(np + 3);
+    // child 0 box: lo (a.x, a.z, b.x) hi (a.y, a.w, b.y)
+    // slab distances with explicit FMAs (the only contracted arithmetic
+    // in the device code, built with -ffp-contract=off)
+    float t0x = fmaf(a.x, t.idir.x, t.iorg.x), t1x = fmaf(a.y, t.idir.x, t.iorg.x);
+    float t0y = fmaf(a.z, t.idir.y, t.iorg.y), t1y = fmaf(a.w, t.idir.y, t.iorg.y);
+    float t0z = fmaf(b.x, t.idir.z, t.iorg.z), t1z = fmaf(b.y, t.idir.z, t.iorg.z);
+    float en0 = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), t.tmin));
+    float ex0 = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), t.tmax));
+    // child 1 box: lo (b.z, c.x, c.z) hi (b.w, c.y, c.w)
+    float s0x = fmaf(b.z, t.idir.x, t.iorg.x), s1x = fmaf(b.w, t.idir.x, t.iorg.x);
+    float s0y = fmaf(c.x, t.idir.y, t.iorg.y), s1y = fmaf(c.y, t.idir.y, t.iorg.y);
+    float s0z = fmaf(c.z, t.idir.z, t.iorg.z), s1z = fmaf(c.w, t.idir.z, t.iorg.z);
+    float en1 = fmaxf(fmaxf(fminf(s0x, s1x), fminf(s0y, s1y)), fmaxf(fminf(s0z, s1z), t.tmin));
+    float ex1 = fminf(fminf(fmaxf(s0x, s1x), fmaxf(s0y, s1y)), fminf(fmaxf(s0z, s1z), t.tmax));
+    bool h0 = en0 <= ex0, h1 = en1 <= ex1;
+    if (h0 && h1) {
+        bool first0 = en0 < en1;
+        stk[sp * stride] = first0 ? r.y : r.x;
+        ++sp;
+        return first0 ? r.x : r.y;
+    }
+    if (h0) return r.x;
+    if (h1) return r.y;
+    return stk[(--sp) * stride];
+}
+
+// Back from a BLAS: restore the world ray (recomputed: cheaper than keeping
+// six more registers live through the whole traversal).
+__device__ __forceinline__ void leave_blas(Trav& t) {
+    t.lo = t.o;
+    t.ld = t.d;
+    t.idir = mk(safe_rcp(t.d.x), safe_rcp(t.d.y), safe_rcp(t.d.z));
+    t.iorg = mk(-(t.o.x * t.idir.x), -(t.o.y * t.idir.y), -(t.o.z * t.idir.z));
+    t.in_blas = false;
+}
+
+// Test TLAS leaf slot `slot`: analytic sphere hit, or entry into the entity's
+// BLAS (returns true and sets `blas_root`; the ray moves to entity space).
+template <bool STATS>
+__device__ __forceinline__ bool instance_test(const SceneView& sv, Trav& t, int slot, int& blas_root, TraceStats& st) {
+    if (STATS) st.leaves++;
+    const float4* ip = sv.inst + 4 * slot;
+    int4 info = *reinterpret_cast<const int4*>(ip + 3);
+    uint32_t ef = (uint32_t)info.w;
+    if ((t.rflags & RAY_TYPE_MASK) != ((t.rflags & ef) & RAY_TYPE_MASK)) return false; // check_ray_visibility
+    float4 m0 = ip[0], m1 = ip[1], m2 = ip[2];
+    const f3 o = t.o, d = t.d;
+    // transform_ray (ray.art:53-59): point and direction, no renormalisation
+    f3 lo2 = mk(m0.x * o.x + m0.y * o.y + m0.z * o.z + m0.w,
+                m1.x * o.x + m1.y * o.y + m1.z * o.z + m1.w,
+                m2.x * o.x + m2.y * o.y + m2.z * o.z + m2.w);
+    f3 ld2 = mk(m0.x * d.x + m0.y * d.y + m0.z * d.z,
+                m1.x * d.x + m1.y * d.y + m1.z * d.z,
+                m2.x * d.x + m2.y * d.y + m2.z * d.z);
+    if (info.y == 1) {
+        // analytic sphere in entity space (intersect_sphere, shapes/sphere.art:104-130)
+        float4 sph = sv.spheres[info.z];
+        f3 L = sub(lo2, f3of(sph));
+        float S = -dot(L, ld2);
+        float D2 = dot(ld2, ld2);
+        float L2 = dot(L, L);
+        float R2 = sph.w * sph.w * D2;
+        float M2 = L2 * D2 - S * S;
+        if (!(S < 0 || M2 > R2)) {
+            float Q = sqrtf(R2 - M2);
+            float ta = (S - Q) / D2, tb = (S + Q) / D2;
+            float t0 = ta > tb ? tb : ta, t1 = ta > tb ? ta : tb;
+            float th = t0 < t.tmin ? t1 : t0;
+            if (accept_hit(t, th, info.x, 0)) {
+                t.tmax = th;
+                t.hit_ent = info.x;
+                t.hit_prim = 0;
+                // prim coords are only texture coordinates for spheres; not needed downstream
+                t.hu = 0;
+                t.hv = 0;
+                t.found = true;
+            }
+        }
+        return false;
+    }
+    if (STATS) st.blas++;
+    t.lo = lo2;
+    t.ld = ld2;
+    t.idir = mk(safe_rcp(ld2.x), safe_rcp(ld2.y), safe_rcp(ld2.z));
+    t.iorg = mk(-(lo2.x * t.idir.x), -(lo2.y * t.idir.y), -(lo2.z * t.idir.z));
+    t.cur_ent = info.x;
+    t.in_blas = true;
+    blas_root = info.z;
+    return true;
+}
+
+// Moeller-Trumbore against triangle slot `slot` in the current BLAS
+// (make_gpu_tri_prim, shapes/trimesh.art:124-160; intersection.art:71-101).
+template <bool STATS>
+__device__ __forceinline__ void tri_test(const SceneView& sv, Trav& t, int slot, TraceStats& st) {
+    if (STATS) st.tris++;
+    const float4* tp = sv.tris + 3 * slot;
+    float4 q0 = tp[0], q1 = tp[1], q2 = tp[2];
+    f3 v0 = f3of(q0), e1 = f3of(q1), e2 = f3of(q2);
+    f3 n = cross(e1, e2);
+    f3 cc = sub(v0, t.lo);
+    f3 rr = cross(t.ld, cc);
+    float det = dot(n, t.ld);
+    float inv_det = 1.0f / det;
+    float u = dot(rr, e2) * inv_det;
+    float v = dot(rr, e1) * inv_det;
+    float w = 1 - u - v;
+    bool ok = u >= -FLT_EPS_ && v >= -FLT_EPS_ && w >= -FLT_EPS_;
+    if (ok) {
+        float th = dot(cc, n) * inv_det;
+        int prim = __float_as_int(q0.w);
+        if (accept_hit(t, th, t.cur_ent, prim)) {
+            t.tmax = th;
+            t.hit_ent = t.cur_ent;
+            t.hit_prim = prim;
+            t.hu = u > 0 ? u : 0;
+            t.hv = v > 0 ? v : 0;
+            t.found = true;
+        }
+    }
+}
+
+// One traversal step (while-while): inner nodes down to a leaf, then that
+// leaf or the BLAS return marker.  Returns true once the ray is finished
+// (stack exhausted, or the first hit for ANY).
+template <bool ANY, bool STATS>
+__device__ __forceinline__ bool trav_step(const SceneView& sv, Trav& t, int* stk, int stride, TraceStats& st) {
+    int node = t.node;
+    int sp = t.sp;
+    while (node >= 0) node = node_step<STATS>(sv, t, node, stk, stride, sp, st);
+    if (node == REF_EXIT) {
+        t.node = node;
+        t.sp = sp;
+        return true;
+    }
+    if (STATS && first_active_lane()) st.wleaves++;
+    if (node == REF_MARKER) {
+        leave_blas(t);
+        t.node = stk[(--sp) * stride];
+        t.sp = sp;
+        return false;
+    }
+    int code = ~node;
+    int first = code >> LEAF_COUNT_BITS;
+    int count = (code & ((1 << LEAF_COUNT_BITS) - 1)) + 1;
+    if (!t.in_blas) {
+        // TLAS leaf: entity instances (one per leaf as built here)
+        int root = 0;
+        bool entered = false;
+#pragma unroll 1
+        for (int k = 0; k < count && !entered; ++k) {
+            entered = instance_test<STATS>(sv, t, first + k, root, st);
+            if (ANY && t.found) {
+                t.node = REF_EXIT;
+                t.sp = sp;
+                return true;
+            }
+        }
+        if (entered) {
+            stk[sp * stride] = REF_MARKER;
+            ++sp;
+            t.node = root;
+        } else {
+            t.node = stk[(--sp) * stride];
+        }
+    } else {
+#pragma unroll 1
+        for (int k = 0; k < count; ++k) {
+            tri_test<STATS>(sv, t, first + k, st);
+            if (ANY && t.found) {
+                t.node = REF_EXIT;
+                t.sp = sp;
+                return true;
+            }
+        }
+        t.node = stk[(--sp) * stride];
+    }
+    t.sp = sp;
+    return false;
+}
+
+// One micro-step (if-if): either one inner node, or one primitive of the
+// current leaf, or a marker.  Every lane of a persistent wave does useful
+// work each step (no wait for the rest of the wave to reach a leaf); the
+// visit order per ray is the same as trav_step's, so results are identical.
+// Returns true once the ray is finished.
+template <bool ANY, bool STATS>
+__device__ __forceinline__ bool trav_micro(const SceneView& sv, Trav& t, int* stk, int stride, TraceStats& st) {
+    int node = t.node;
+    int sp = t.sp;
+    if (t.prim < t.prim_end) {
+        const int slot = t.prim++;
+        if (t.in_blas) {
+            tri_test<STATS>(sv, t, slot, st);
+        } else {
+            int root;
+            if (instance_test<STATS>(sv, t, slot, root, st)) {
+                // TLAS leaves hold one entity: `node` already is the continuation
+                stk[(sp++) * stride] = node;
+                stk[(sp++) * stride] = REF_MARKER;
+                node = root;
+                t.prim_end = t.prim;
+            }
+        }
+        if (ANY && t.found) return true;
+    } else if (node >= 0) {
+        node = node_step<STATS>(sv, t, node, stk, stride, sp, st);
+    } else if (node == REF_MARKER) {
+        leave_blas(t);
+        node = stk[(--sp) * stride];
+    } else if (node == REF_EXIT) {
+        return true;
+    }
+    // a leaf reached: open its primitive range and continue from the stack
+    if (is_leaf_ref(node) && t.prim >= t.prim_end) {
+        const int code = ~node;
+        t.prim = code >> LEAF_COUNT_BITS;
+        t.prim_end = t.prim + (code & ((1 << LEAF_COUNT_BITS) - 1)) + 1;
+        node = stk[(--sp) * stride];
+    }
+    t.node = node;
+    t.sp = sp;
+    return false;
+}
+
+// Whole-ray traversal (used by the tail kernel and the hit-level harness).
 template <bool ANY, bool STATS>
 __device__ __forceinline__ bool trace_ray(const SceneView& sv, f3 o, f3 d, float tmin, float& tmax, uint32_t rflags,
                                           int* stk, int stride, int& hit_ent, int& hit_prim, float& hu, float& hv,
                                           TraceStats& st) {
-    hit_ent = -1;
-    hit_prim = -1;
-    if (sv.tlas_root < 0) return false;
-
-    // level ray (world at the TLAS, entity-local inside a BLAS)
-    f3 lo = o, ld = d;
-    f3 idir = mk(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
-    f3 iorg = mk(-(o.x * idir.x), -(o.y * idir.y), -(o.z * idir.z));
-    int cur_ent = -1;
-    bool in_blas = false;
-    bool found = false;
-
-    int sp = 0;
-    stk[0] = REF_EXIT;
-    sp = 1;
-    int node = sv.tlas_root;
-
-    while (true) {
-        // ---- inner nodes -------------------------------------------------
-        while (node >= 0) {
-            if (STATS) st.nodes++;
-            const float4* np = sv.nodes + 4 * node;
-            float4 a = np[0], b = np[1], c = np[2];
-            int4 r = *reinterpret_cast<const int4*>(np + 3);
-            // child 0 box: lo (a.x, a.z, b.x) hi (a.y, a.w, b.y)
-            // slab distances with explicit FMAs (the only contracted arithmetic
-            // in the device code, built with -ffp-contract=off)
-            float t0x = fmaf(a.x, idir.x, iorg.x), t1x = fmaf(a.y, idir.x, iorg.x);
-            float t0y = fmaf(a.z, idir.y, iorg.y), t1y = fmaf(a.w, idir.y, iorg.y);
-            float t0z = fmaf(b.x, idir.z, iorg.z), t1z = fmaf(b.y, idir.z, iorg.z);
-            float en0 = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), tmin));
-            float ex0 = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), tmax));
-            // child 1 box: lo (b.z, c.x, c.z) hi (b.w, c.y, c.w)
-            float s0x = fmaf(b.z, idir.x, iorg.x), s1x = fmaf(b.w, idir.x, iorg.x);
-            float s0y = fmaf(c.x, idir.y, iorg.y), s1y = fmaf(c.y, idir.y, iorg.y);
-            float s0z = fmaf(c.z, idir.z, iorg.z), s1z = fmaf(c.w, idir.z, iorg.z);
-            float en1 = fmaxf(fmaxf(fminf(s0x, s1x), fminf(s0y, s1y)), fmaxf(fminf(s0z, s1z), tmin));
-            float ex1 = fminf(fminf(fmaxf(s0x, s1x), fmaxf(s0y, s1y)), fminf(fmaxf(s0z, s1z), tmax));
-            bool h0 = en0 <= ex0, h1 = en1 <= ex1;
-            if (h0 && h1) {
-                bool first0 = en0 < en1;
-                node = first0 ? r.x : r.y;
-                stk[sp * stride] = first0 ? r.y : r.x;
-                ++sp;
-            } else if (h0) {
-                node = r.x;
-            } else if (h1) {
-                node = r.y;
-            } else {
-                node = stk[(--sp) * stride];
-            }
-        }
-        // ---- leaves, markers, exit ---------------------------------------
-        if (node == REF_EXIT) break;
-        if (node == REF_MARKER) {
-            // back from a BLAS: restore the world ray (recomputed: cheaper than
-            // keeping six more registers live through the whole traversal)
-            lo = o; ld = d;
-            idir = mk(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
-            iorg = mk(-(o.x * idir.x), -(o.y * idir.y), -(o.z * idir.z));
-            in_blas = false;
-            node = stk[(--sp) * stride];
-            continue;
-        }
-        int code = ~node;
-        int first = code >> LEAF_COUNT_BITS;
-        int count = (code & ((1 << LEAF_COUNT_BITS) - 1)) + 1;
-        if (!in_blas) {
-            // TLAS leaf: entity instances
-            int next = 0;
-            bool entered = false;
-#pragma unroll 1
-            for (int k = 0; k < count; ++k) {
-                if (STATS) st.leaves++;
-                const float4* ip = sv.inst + 4 * (first + k);
-                int4 info = *reinterpret_cast<const int4*>(ip + 3);
-                uint32_t ef = (uint32_t)info.w;
-                if ((rflags & RAY_TYPE_MASK) != ((rflags & ef) & RAY_TYPE_MASK)) continue; // check_ray_visibility
-                float4 m0 = ip[0], m1 = ip[1], m2 = ip[2];
-                // transform_ray (ray.art:53-59): point and direction, no renormalisation
-                f3 lo2 = mk(m0.x * o.x + m0.y * o.y + m0.z * o.z + m0.w,
-                            m1.x * o.x + m1.y * o.y + m1.z * o.z + m1.w,
-                            m2.x * o.x + m2.y * o.y + m2.z * o.z + m2.w);
-                f3 ld2 = mk(m0.x * d.x + m0.y * d.y + m0.z * d.z,
-                            m1.x * d.x + m1.y * d.y + m1.z * d.z,
-                            m2.x * d.x + m2.y * d.y + m2.z * d.z);
-                if (info.y == 1) {
-                    // analytic sphere in entity space (intersect_sphere, shapes/sphere.art:104-130)
-                    float4 sph = sv.spheres[info.z];
-                    f3 L = sub(lo2, f3of(sph));
-                    float S = -dot(L, ld2);
-                    float D2 = dot(ld2, ld2);
-                    float L2 = dot(L, L);
-                    float R2 = sph.w * sph.w * D2;
-                    float M2 = L2 * D2 - S * S;
-                    if (!(S < 0 || M2 > R2)) {
-                        float Q = sqrtf(R2 - M2);
-                        float ta = (S - Q) / D2, tb = (S + Q) / D2;
-                        float t0 = ta > tb ? tb : ta, t1 = ta > tb ? ta : tb;
-                        float th = t0 < tmin ? t1 : t0;
-                        if (th >= tmin && th <= tmax) {
-                            tmax = th;
-                            hit_ent = info.x;
-                            hit_prim = 0;
-                            // prim coords are only texture coordinates for spheres; not needed downstream
-                            hu = 0; hv = 0;
-                            found = true;
-                            if (ANY) return true;
-                        }
-                    }
-                } else {
-                    if (STATS) st.blas++;
-                    // enter the BLAS (count == 1 for TLAS leaves built here)
-                    lo = lo2; ld = ld2;
-                    idir = mk(safe_rcp(ld.x), safe_rcp(ld.y), safe_rcp(ld.z));
-                    iorg = mk(-(lo.x * idir.x), -(lo.y * idir.y), -(lo.z * idir.z));
-                    cur_ent = info.x;
-                    in_blas = true;
-                    next = info.z;
-                    entered = true;
-                    break;
-                }
-            }
-            if (entered) {
-                stk[sp * stride] = REF_MARKER;
-                ++sp;
-                node = next;
-            } else {
-                node = stk[(--sp) * stride];
-            }
-        } else {
-            // BLAS leaf: triangles (make_gpu_tri_prim, shapes/trimesh.art:124-160)
-#pragma unroll 1
-            for (int k = 0; k < count; ++k) {
-                if (STATS) st.tris++;
-                const float4* tp = sv.tris + 3 * (first + k);
-                float4 q0 = tp[0], q1 = tp[1], q2 = tp[2];
-                f3 v0 = f3of(q0), e1 = f3of(q1), e2 = f3of(q2);
-                f3 n = cross(e1, e2);
-                f3 cc = sub(v0, lo);
-                f3 rr = cross(ld, cc);
-                float det = dot(n, ld);
-                float inv_det = 1.0f / det;
-                float u = dot(rr, e2) * inv_det;
-                float v = dot(rr, e1) * inv_det;
-                float w = 1 - u - v;
-                bool ok = u >= -FLT_EPS_ && v >= -FLT_EPS_ && w >= -FLT_EPS_;
-                if (ok) {
-                    float t = dot(cc, n) * inv_det;
-                    if (t >= tmin && t <= tmax) {
-                        tmax = t;
-                        hit_ent = cur_ent;
-                        hit_prim = __float_as_int(q0.w);
-                        hu = u > 0 ? u : 0;
-                        hv = v > 0 ? v : 0;
-                        found = true;
-                        if (ANY) return true;
-                    }
-                }
-            }
-            node = stk[(--sp) * stride];
-        }
+    Trav t;
+    trav_init(sv, t, o, d, tmin, tmax, rflags, stk);
+    while (!trav_step<ANY, STATS>(sv, t, stk, stride, st)) {
     }
-    return found;
+    tmax = t.tmax;
+    hit_ent = t.hit_ent;
+    hit_prim = t.hit_prim;
+    hu = t.hu;
+    hv = t.hv;
+    return t.found;
 }
 
 // ---------------------------------------------------------------------------

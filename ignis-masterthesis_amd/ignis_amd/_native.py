@@ -85,7 +85,9 @@ class Stats(C.Structure):
                 ("launches_finish", C.c_uint64), ("ms_finish", C.c_double), ("tail_bounce_rays", C.c_uint64),
                 ("tail_shadow_rays", C.c_uint64), ("bvh_depth", C.c_int32), ("stack_entries", C.c_int32),
                 ("extend_rays", C.c_uint64), ("extend_paths_out", C.c_uint64),
-                ("launches_trace", C.c_uint64), ("ms_trace", C.c_double)]
+                ("launches_trace", C.c_uint64), ("ms_trace", C.c_double),
+                ("wave_node_iters", C.c_uint64), ("wave_leaf_iters", C.c_uint64),
+                ("shadow_wave_node_iters", C.c_uint64), ("shadow_wave_leaf_iters", C.c_uint64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

@@ -494,6 +494,10 @@ static int traverse_blas(const oshape* sh, oray* r, int any, ohit* h, otstats* s
                 st->tris++;
                 float t, u, v;
                 if (tri_test(r, sh->tri + 12 * (first + k), &t, &u, &v)) {
+                    /* ties at equal distance: the larger primitive id wins (order-independent
+                       rule shared with the device; the reference keeps the later-visited
+                       triangle, intersection.art:97, which depends on BVH topology) */
+                    if (t == r->tmax && !((int)sh->bvh.order[first + k] > h->prim)) continue;
                     r->tmax = t;
                     h->t = t;
                     h->u = u;
@@ -573,7 +577,7 @@ static int trace_scene(const oracle_scene* s, const oray* ray_in, int any, ohit*
             } else {
                 got = traverse_blas(sh, &lr, any, &lh, st);
             }
-            if (got && lh.prim != -1 && lh.t <= hit->t) {
+            if (got && lh.prim != -1 && (lh.t < hit->t || (lh.t == hit->t && eid > hit->ent))) {
                 hit->ent = eid;
                 hit->prim = lh.prim;
                 hit->t = lh.t;
