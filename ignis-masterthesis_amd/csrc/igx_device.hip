@@ -38,9 +38,6 @@ namespace {
 
 constexpr int BLOCK = 256;
 constexpr int MAX_BOUNCES = 256;
-#ifndef TRAV_STEP
-#define TRAV_STEP trav_step
-#endif
 
 // ---------------------------------------------------------------------------
 // Streams (SoA of 16-byte records)
@@ -91,16 +88,6 @@ __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 template <typename T>
 __device__ __forceinline__ T uniform_load(const T* p) {
     return __builtin_amdgcn_readfirstlane(*p);
-}
-
-__device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << __lane_id()) - 1ull; }
-
-// Contiguous share [begin, end) of n items for the calling wave (wave-uniform).
-__device__ __forceinline__ void wave_range(int n, int& begin, int& end) {
-    const int waves = (int)(gridDim.x * (BLOCK / 64));
-    const int w = (int)(blockIdx.x * (BLOCK / 64) + threadIdx.x / 64);
-    begin = (int)((long long)n * w / waves);
-    end = (int)((long long)n * (w + 1) / waves);
 }
 
 // ---------------------------------------------------------------------------
@@ -458,49 +445,21 @@ __global__ void __launch_bounds__(BLOCK, WAVES) k_trace(FrameArgs fa, SceneView 
     if (n <= tail_threshold) return; // k_finish takes the remaining paths
     const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
-    // Persistent wave with lane refill: each wave owns a contiguous range of
-    // rays; a lane whose ray finished takes the next one at once, so the wave
-    // does not idle behind its longest ray (Aila & Laine 2009).
-    int next, end;
-    wave_range(n, next, end);
-    Trav t;
-    int ri = -1; // ray index; -1 wants a ray, -2 range exhausted
-    for (;;) {
-        const bool need = ri == -1;
-        const uint64_t m = __ballot(need);
-        if (m) {
-            const int idx = next + __popcll(m & lanemask_lt());
-            next += __popcll(m);
-            if (need) {
-                if (idx < end) {
-                    float4 p0 = in.p0[idx], p1 = in.p1[idx];
-                    int sd = __float_as_int(p0.w);
-                    int depth = sd >> 24;
-                    if (depth > 0) {
-                        float tmin, tmax;
-                        uint32_t rflags;
-                        ray_extent(fa, sv, depth, sd & 0xFFFFFF, tmin, tmax, rflags);
-                        trav_init(sv, t, f3of(p0), f3of(p1), tmin, tmax, rflags, stk);
-                        ri = idx;
-                    } else {
-                        hits.h[idx] = make_float4(0, 0, 0, __int_as_float(-1)); // dead slot
-                        hits.prim[idx] = -1;
-                    }
-                } else {
-                    ri = -2;
-                }
-            }
+    for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+        float4 p0 = in.p0[i], p1 = in.p1[i];
+        int sd = __float_as_int(p0.w);
+        int depth = sd >> 24;
+        int hit_ent = -1, hit_prim = -1;
+        float hu = 0, hv = 0, tmax = 0;
+        if (depth > 0) {
+            float tmin;
+            uint32_t rflags;
+            ray_extent(fa, sv, depth, sd & 0xFFFFFF, tmin, tmax, rflags);
+            trace_ray<false, STATS>(sv, f3of(p0), f3of(p1), tmin, tmax, rflags, stk, BLOCK, hit_ent, hit_prim, hu, hv, st);
+            if (STATS && hit_ent >= 0) st.hits++;
         }
-        if (__ballot(ri >= 0) == 0) {
-            if (__ballot(ri == -1) == 0) break;
-            continue;
-        }
-        if (ri >= 0 && TRAV_STEP<false, STATS>(sv, t, stk, BLOCK, st)) {
-            if (STATS && t.hit_ent >= 0) st.hits++;
-            hits.h[ri] = make_float4(t.tmax, t.hu, t.hv, __int_as_float(t.hit_ent));
-            hits.prim[ri] = t.hit_prim;
-            ri = -1;
-        }
+        hits.h[i] = make_float4(tmax, hu, hv, __int_as_float(hit_ent));
+        hits.prim[i] = hit_prim;
     }
     if (STATS) flush_stats<STATS>(st, stats, 0, true);
 }
@@ -612,32 +571,13 @@ __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, f
     if (n == 0) return;
     const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
-    int next, end;
-    wave_range(n, next, end);
-    Trav t;
-    int ri = -1, slot = 0;
-    for (;;) {
-        const bool need = ri == -1;
-        const uint64_t m = __ballot(need);
-        if (m) {
-            const int idx = next + __popcll(m & lanemask_lt());
-            next += __popcll(m);
-            if (need) {
-                if (idx < end) {
-                    float4 s0 = sh.s0[idx], s1 = sh.s1[idx];
-                    slot = __float_as_int(s0.w);
-                    trav_init(sv, t, f3of(s0), f3of(s1), 0.001f, s1.w, RAY_SHADOW, stk);
-                    ri = idx;
-                } else {
-                    ri = -2;
-                }
-            }
-        }
-        if (__ballot(ri >= 0) == 0) break;
-        if (ri >= 0 && TRAV_STEP<true, STATS>(sv, t, stk, BLOCK, st)) {
-            if (!t.found) add_radiance(L, slot, f3of(sh.s2[ri]));
-            ri = -1;
-        }
+    for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+        float4 s0 = sh.s0[i], s1 = sh.s1[i];
+        float tmax = s1.w;
+        int e, p;
+        float u, v;
+        if (!trace_ray<true, STATS>(sv, f3of(s0), f3of(s1), 0.001f, tmax, RAY_SHADOW, stk, BLOCK, e, p, u, v, st))
+            add_radiance(L, __float_as_int(s0.w), f3of(sh.s2[i]));
     }
     if (STATS) flush_stats<STATS>(st, stats, 4, false);
 }

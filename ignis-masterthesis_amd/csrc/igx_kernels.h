@@ -74,16 +74,16 @@ constexpr uint32_t RAY_CAMERA = 0x1, RAY_LIGHT = 0x2, RAY_BOUNCE = 0x4, RAY_SHAD
 // (ray.art:51), Moeller-Trumbore with -eps barycentric tolerance and u,v clamp
 // (intersection.art:71-101), analytic sphere (shapes/sphere.art:104-130).
 // ---------------------------------------------------------------------------
-// Traversal state of one ray, resumable: trav_step advances it to the next
-// leaf (or the end), so a persistent kernel can refill lanes whose ray ended
-// while the rest of the wave keeps traversing.
+// Traversal state of one ray; trav_step advances it to the next leaf (or the
+// end).  (Persistent lane-refill and if-if single-step variants built on this
+// were measured slower on gfx950 than the plain grid-stride while-while loop:
+// DESIGN.md §3.)
 struct Trav {
     f3 o, d;          // world ray
     f3 lo, ld;        // ray of the current level (world at the TLAS, entity space in a BLAS)
     f3 idir, iorg;    // slab-test form of the current-level ray
     float tmin, tmax; // tmax shrinks on every accepted hit
     int node, sp;
-    int prim, prim_end; // open leaf range (trav_micro)
     int cur_ent;
     int hit_ent, hit_prim;
     float hu, hv;
@@ -120,8 +120,6 @@ __device__ __forceinline__ void trav_init(const SceneView& sv, Trav& t, f3 o, f3
     t.hv = 0;
     t.in_blas = false;
     t.found = false;
-    t.prim = 0;
-    t.prim_end = 0;
     stk[0] = REF_EXIT;
     t.sp = 1;
     t.node = sv.tlas_root < 0 ? REF_EXIT : sv.tlas_root;
@@ -317,50 +315,6 @@ __device__ __forceinline__ bool trav_step(const SceneView& sv, Trav& t, int* stk
         }
         t.node = stk[(--sp) * stride];
     }
-    t.sp = sp;
-    return false;
-}
-
-// One micro-step (if-if): either one inner node, or one primitive of the
-// current leaf, or a marker.  Every lane of a persistent wave does useful
-// work each step (no wait for the rest of the wave to reach a leaf); the
-// visit order per ray is the same as trav_step's, so results are identical.
-// Returns true once the ray is finished.
-template <bool ANY, bool STATS>
-__device__ __forceinline__ bool trav_micro(const SceneView& sv, Trav& t, int* stk, int stride, TraceStats& st) {
-    int node = t.node;
-    int sp = t.sp;
-    if (t.prim < t.prim_end) {
-        const int slot = t.prim++;
-        if (t.in_blas) {
-            tri_test<STATS>(sv, t, slot, st);
-        } else {
-            int root;
-            if (instance_test<STATS>(sv, t, slot, root, st)) {
-                // TLAS leaves hold one entity: `node` already is the continuation
-                stk[(sp++) * stride] = node;
-                stk[(sp++) * stride] = REF_MARKER;
-                node = root;
-                t.prim_end = t.prim;
-            }
-        }
-        if (ANY && t.found) return true;
-    } else if (node >= 0) {
-        node = node_step<STATS>(sv, t, node, stk, stride, sp, st);
-    } else if (node == REF_MARKER) {
-        leave_blas(t);
-        node = stk[(--sp) * stride];
-    } else if (node == REF_EXIT) {
-        return true;
-    }
-    // a leaf reached: open its primitive range and continue from the stack
-    if (is_leaf_ref(node) && t.prim >= t.prim_end) {
-        const int code = ~node;
-        t.prim = code >> LEAF_COUNT_BITS;
-        t.prim_end = t.prim + (code & ((1 << LEAF_COUNT_BITS) - 1)) + 1;
-        node = stk[(--sp) * stride];
-    }
-    t.node = node;
     t.sp = sp;
     return false;
 }
