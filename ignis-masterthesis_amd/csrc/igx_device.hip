@@ -1191,7 +1191,13 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
             tris.push_back(make_float4(v0[0] - v1[0], v0[1] - v1[1], v0[2] - v1[2], 0));
             tris.push_back(make_float4(v2[0] - v0[0], v2[1] - v0[1], v2[2] - v0[2], 0));
         }
-        sdev[s] = {0, node_off, (int)vtx.size(), (int)idx.size()};
+        // a BLAS that is a single leaf is entered at the leaf itself
+        int root_ref = node_off;
+        if (br.root_is_leaf) {
+            int code = ~br.root_leaf_ref;
+            root_ref = igx::encode_leaf((code >> igx::kLeafCountBits) + tri_off, (code & ((1 << igx::kLeafCountBits) - 1)) + 1);
+        }
+        sdev[s] = {0, root_ref, (int)vtx.size(), (int)idx.size()};
         for (uint32_t v = 0; v < m.num_vertices; ++v) {
             vtx.push_back(make_float4(m.vertices[3 * v], m.vertices[3 * v + 1], m.vertices[3 * v + 2], 0));
             nrm.push_back(make_float4(m.normals[3 * v], m.normals[3 * v + 1], m.normals[3 * v + 2], 0));
@@ -1226,7 +1232,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
                 if (nd.ref[k] >= 0) nd.ref[k] += node_off;
             nodes.push_back(nd);
         }
-        tlas_root = node_off;
+        tlas_root = br.root_is_leaf ? br.root_leaf_ref : node_off; // single entity: start at its leaf
         for (uint32_t slot = 0; slot < br.prim_order.size(); ++slot) {
             uint32_t e = br.prim_order[slot];
             const igx_entity& en = desc->entities[e];

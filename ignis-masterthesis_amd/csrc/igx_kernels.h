@@ -22,7 +22,7 @@ struct SceneView {
     const int4* idx;       // faces: local vertex indices
     const DevMaterial* mats;
     const DevLight* lights;
-    int tlas_root;         // -1: no entities
+    int tlas_root;         // root node of the TLAS, or its only leaf (one entity)
     int num_lights;        // infinite lights first (light/light_selector.art:26-44)
     int num_infinite;
     float scene_radius;    // bbox_radius(scene_bbox) * 1.01 (light/env.art:75)
@@ -122,7 +122,7 @@ __device__ __forceinline__ void trav_init(const SceneView& sv, Trav& t, f3 o, f3
     t.found = false;
     stk[0] = REF_EXIT;
     t.sp = 1;
-    t.node = sv.tlas_root < 0 ? REF_EXIT : sv.tlas_root;
+    t.node = sv.num_inst > 0 ? sv.tlas_root : REF_EXIT; // the root may be a leaf (one entity)
 }
 
 // Slab test of both children of BVH2 node `node` (intersect_ray_box,

@@ -37,12 +37,22 @@ struct Builder {
     const BvhBuildInput& in;
     int max_leaf;
     int bins;
-    std::vector<uint32_t> idx;
+    std::vector<uint32_t>& idx; // shared; each builder only touches its own ranges
     std::vector<TmpNode> nodes;
+    int par_depth;              // subtrees above this depth are built on their own threads
 
-    Builder(const BvhBuildInput& i, int ml, int b) : in(i), max_leaf(ml), bins(b) {}
+    Builder(const BvhBuildInput& i, int ml, int b, std::vector<uint32_t>& ix, int pd)
+        : in(i), max_leaf(ml), bins(b), idx(ix), par_depth(pd) {}
 
-    Box prim_box(uint32_t p) const { Box b; b.grow(&in.bmin[3 * p], &in.bmax[3 * p]); return b; }
+    // Bin idx[first, first+count) by centroid along `axis`.
+    void bin_range(uint32_t first, uint32_t count, int axis, float lo, float scale, Box* bbox, uint32_t* bcnt) const {
+        for (uint32_t i = first; i < first + count; ++i) {
+            uint32_t p = idx[i];
+            int b = std::min(bins - 1, (int)((in.centroid[3 * p + axis] - lo) * scale));
+            bbox[b].grow(&in.bmin[3 * p], &in.bmax[3 * p]);
+            bcnt[b]++;
+        }
+    }
 
     // Returns tmp node index of a subtree over idx[first, first+count).
     int32_t build(uint32_t first, uint32_t count, int depth) {
@@ -71,12 +81,7 @@ struct Builder {
             if (!(ext > 0)) continue;
             float scale = bins / ext;
             for (int b = 0; b < bins; ++b) { bbox[b] = Box(); bcnt[b] = 0; }
-            for (uint32_t i = first; i < first + count; ++i) {
-                uint32_t p = idx[i];
-                int b = std::min(bins - 1, (int)((in.centroid[3 * p + axis] - cbox.lo[axis]) * scale));
-                bbox[b].grow(&in.bmin[3 * p], &in.bmax[3 * p]);
-                bcnt[b]++;
-            }
+            bin_range(first, count, axis, cbox.lo[axis], scale, bbox.data(), bcnt.data());
             Box acc;
             uint32_t c = 0;
             for (int b = bins - 1; b > 0; --b) {
@@ -114,8 +119,23 @@ struct Builder {
             mid = (uint32_t)(it - idx.begin());
             if (mid == first || mid == first + count) mid = first + count / 2;
         }
-        int32_t l = build(first, mid - first, depth + 1);
-        int32_t r = build(mid, first + count - mid, depth + 1);
+        int32_t l, r;
+        if (depth < par_depth && count >= 65536) {
+            // left subtree on its own thread with its own node pool, merged after
+            Builder sub(in, max_leaf, bins, idx, par_depth);
+            auto fut = std::async(std::launch::async, [&sub, first, mid, depth] { return sub.build(first, mid - first, depth + 1); });
+            r = build(mid, first + count - mid, depth + 1);
+            int32_t sroot = fut.get();
+            const int32_t off = (int32_t)nodes.size();
+            for (TmpNode t : sub.nodes) {
+                if (t.left >= 0) { t.left += off; t.right += off; }
+                nodes.push_back(t);
+            }
+            l = sroot + off;
+        } else {
+            l = build(first, mid - first, depth + 1);
+            r = build(mid, first + count - mid, depth + 1);
+        }
         nodes[me].left = l;
         nodes[me].right = r;
         return me;
@@ -152,12 +172,14 @@ BvhBuildResult build_bvh2(const BvhBuildInput& in, int max_leaf, int bins) {
         return res;
     }
     if (n >= (size_t)kMaxLeafFirst) throw std::invalid_argument("too many primitives for the leaf encoding");
-    Builder b(in, max_leaf, bins);
-    b.idx.resize(n);
-    for (size_t i = 0; i < n; ++i) b.idx[i] = (uint32_t)i;
+    std::vector<uint32_t> idx(n);
+    for (size_t i = 0; i < n; ++i) idx[i] = (uint32_t)i;
+    // up to 2^4 concurrent subtree builders for large inputs
+    const int par_depth = n >= 262144 ? 4 : 0;
+    Builder b(in, max_leaf, bins, idx, par_depth);
     b.nodes.reserve(2 * n / std::max(1, max_leaf) + 4);
     int32_t root = b.build(0, (uint32_t)n, 0);
-    res.prim_order = b.idx;
+    res.prim_order = std::move(idx);
 
     // Flatten: BvhNodes in DFS pre-order; each inner tmp node becomes one BvhNode.
     auto leaf_ref = [&](const TmpNode& t) { return encode_leaf((int32_t)t.first, (int32_t)t.count); };
@@ -171,6 +193,8 @@ BvhBuildResult build_bvh2(const BvhBuildInput& in, int max_leaf, int bins) {
         set_child(res.nodes[0], 0, b.nodes[root].box, leaf_ref(b.nodes[root]));
         set_child(res.nodes[0], 1, b.nodes[root].box, leaf_ref(b.nodes[root]));
         res.depth = 1;
+        res.root_is_leaf = true;
+        res.root_leaf_ref = leaf_ref(b.nodes[root]);
         return res;
     }
     stack.push_back({root, 0, 1});

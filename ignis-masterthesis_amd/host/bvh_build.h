@@ -45,6 +45,11 @@ struct BvhBuildResult {
     std::vector<uint32_t> prim_order;   // leaf slot -> original primitive index
     int depth = 0;                      // maximum root-to-leaf depth (number of inner levels)
     int max_leaf = 0;
+    // All primitives fit one leaf: nodes[0] then references that leaf from
+    // both children (keeps the array layout uniform), but traversal should
+    // start at the leaf itself (root_leaf_ref) so it is not visited twice.
+    bool root_is_leaf = false;
+    int32_t root_leaf_ref = 0;
 };
 
 // Build a BVH2 with binned SAH.  `max_leaf` caps primitives per leaf (<= 16).

@@ -298,6 +298,74 @@ TriMesh make_uv_sphere(V3 center, float radius, uint32_t stacks, uint32_t slices
     return m;
 }
 
+namespace {
+// splitmix64: a fixed, platform-independent generator for the synthetic scenes
+struct SplitMix {
+    uint64_t x;
+    uint64_t next() {
+        uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    }
+    float uniform() { return (float)(next() >> 40) * (1.0f / 16777216.0f); } // [0, 1)
+    float range(float a, float b) { return a + (b - a) * uniform(); }
+};
+} // namespace
+
+TriMesh make_soup(uint32_t count, uint64_t seed) {
+    TriMesh m;
+    SplitMix rng{seed};
+    const float e = 0.01f * std::cbrt(1.0e6f / (float)std::max<uint32_t>(count, 1));
+    m.vertices.resize((size_t)count * 3);
+    m.normals.resize((size_t)count * 3);
+    m.faces.resize(count);
+    for (uint32_t i = 0; i < count; ++i) {
+        V3 c(rng.range(-1, 1), rng.range(-1, 1), rng.range(-1, 1));
+        V3 v[3];
+        for (int k = 0; k < 3; ++k) v[k] = c + V3(rng.range(-e, e), rng.range(-e, e), rng.range(-e, e));
+        V3 n = normalized(cross(v[1] - v[0], v[2] - v[0]));
+        for (int k = 0; k < 3; ++k) {
+            m.vertices[3 * (size_t)i + k] = v[k];
+            m.normals[3 * (size_t)i + k] = n;
+        }
+        m.faces[i] = {3 * i, 3 * i + 1, 3 * i + 2};
+    }
+    return m;
+}
+
+TriMesh make_displaced_grid(uint32_t n, float size, float amplitude, uint64_t seed) {
+    TriMesh m;
+    SplitMix rng{seed};
+    constexpr int L = 8; // lattice cells per side
+    float lat[L + 1][L + 1];
+    for (int j = 0; j <= L; ++j)
+        for (int i = 0; i <= L; ++i) lat[j][i] = rng.uniform();
+    auto noise = [&](float u, float v) { // u, v in [0, 1]
+        float x = u * L, y = v * L;
+        int i = std::min((int)x, L - 1), j = std::min((int)y, L - 1);
+        float fx = x - i, fy = y - j;
+        fx = fx * fx * (3 - 2 * fx);
+        fy = fy * fy * (3 - 2 * fy);
+        float a = lat[j][i] + (lat[j][i + 1] - lat[j][i]) * fx;
+        float b = lat[j + 1][i] + (lat[j + 1][i + 1] - lat[j + 1][i]) * fx;
+        return a + (b - a) * fy;
+    };
+    for (uint32_t j = 0; j <= n; ++j)
+        for (uint32_t i = 0; i <= n; ++i) {
+            float u = (float)i / n, v = (float)j / n;
+            m.vertices.push_back(V3((u - 0.5f) * size, (v - 0.5f) * size, amplitude * noise(u, v)));
+        }
+    for (uint32_t j = 0; j < n; ++j)
+        for (uint32_t i = 0; i < n; ++i) {
+            uint32_t a = j * (n + 1) + i, b = a + 1, c = a + (n + 1), d = c + 1;
+            m.faces.push_back({a, b, d});
+            m.faces.push_back({a, d, c});
+        }
+    m.compute_vertex_normals();
+    return m;
+}
+
 TriMesh make_ico_sphere(V3 center, float radius, uint32_t subdivisions) {
     TriMesh m;
     constexpr float Golden = 1.618033989f;

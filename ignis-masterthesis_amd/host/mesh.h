@@ -48,6 +48,15 @@ TriMesh make_disk(V3 center, V3 normal, float radius, uint32_t sections);
 TriMesh make_cone(V3 base_center, float base_radius, V3 tip, uint32_t sections, bool fill_cap);
 TriMesh make_cylinder(V3 base_center, float base_radius, V3 top_center, float top_radius, uint32_t sections, bool fill_cap);
 
+// Synthetic benchmark geometry (not part of the reference's
+// shape set, exposed to scene files as igx extensions):
+// `count` independent triangles, centroids uniform in [-1,1]^3, vertices =
+// centroid + uniform offsets in [-e,e]^3 with e = 0.01 * (1M / count)^(1/3).
+TriMesh make_soup(uint32_t count, uint64_t seed);
+// (n x n)-quad grid over [-size/2, size/2]^2 displaced along z by `amplitude`
+// times bilinear value noise on an 8x8-cell lattice of seeded random heights.
+TriMesh make_displaced_grid(uint32_t n, float size, float amplitude, uint64_t seed);
+
 // Tangent::frame with the Duff et al. basis (src/runtime/math/Tangent.h:52-73)
 void tangent_frame(V3 n, V3& nx, V3& ny);
 

@@ -75,7 +75,13 @@ struct Props {
         if (p->is_bool()) return p->b ? 1.f : 0.f;
         fail(std::string("property '") + k + "' is not a number");
     }
-    int integer(const char* k, int def) const { return (int)number(k, (float)def); }
+    int64_t integer(const char* k, int64_t def) const {
+        const Value* p = get(k);
+        if (!p) return def;
+        if (p->is_number()) return (int64_t)p->num;
+        if (p->is_bool()) return p->b ? 1 : 0;
+        fail(std::string("property '") + k + "' is not an integer");
+    }
     bool boolean(const char* k, bool def) const {
         const Value* p = get(k);
         if (!p) return def;
@@ -284,6 +290,15 @@ TriMesh setup_trimesh(const std::string& type, const Props& p, const std::string
         m = igx::make_cone(p.vec3("p0", V3()), p.number("radius", 1.0f), p.vec3("p1", V3(0, 0, 1)), (uint32_t)p.integer("sections", 32), p.boolean("filled", true));
     } else if (type == "disk") {
         m = igx::make_disk(p.vec3("origin", V3()), p.vec3("normal", V3(0, 0, 1)), p.number("radius", 1.0f), (uint32_t)p.integer("sections", 32));
+    } else if (type == "soup") {
+        // igx extension: synthetic triangle soup of the benchmark suite
+        int64_t cnt = p.integer("count", 1000000);
+        if (cnt < 1 || cnt >= (1ll << 26)) fail("shape '" + name + "': soup count must be in [1, 2^26)");
+        m = igx::make_soup((uint32_t)cnt, (uint64_t)p.integer("seed", 42));
+    } else if (type == "displaced_grid") {
+        // igx extension: value-noise height field of the S-deep scene
+        m = igx::make_displaced_grid((uint32_t)p.integer("quads", 256), p.number("size", 2.0f), p.number("amplitude", 0.25f),
+                                     (uint64_t)p.integer("seed", 7));
     } else if (type == "ply" || type == "obj" || type == "external") {
         std::string fn = join_path(base_dir, p.string("filename"));
         std::string ext = fn.size() >= 4 ? fn.substr(fn.size() - 4) : "";
