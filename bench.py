@@ -43,6 +43,7 @@ def parse():
     ap.add_argument("--spi", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample length")
+    ap.add_argument("--suite", type=int, default=1, help="also measure the other §8d scenes (N=1 only)")
     return ap.parse_args()
 
 
@@ -69,9 +70,11 @@ def algorithmic_bytes(stats_inst, st):
     return st["extend_rays"] * per_ray + st["extend_paths_out"] * 52 + shadow_wf * 48, per_ray
 
 
-def load_pmc(n_gpus):
-    """Per-launch HBM traffic of the dominant kernel (k_extend) from the committed rocprofv3 PMC summary."""
-    path = os.path.join(ROOT, "profiles", "pmc_extend.json")
+def load_pmc(n_gpus, scene="diamond_scene"):
+    """Per-launch HBM traffic of the dominant kernel (k_extend) from the committed
+    rocprofv3 PMC summary of the same workload (profiles/pmc_extend*.json)."""
+    name = "pmc_extend.json" if scene == "diamond_scene" else f"pmc_extend_{scene}.json"
+    path = os.path.join(ROOT, "profiles", name)
     if n_gpus != 1 or not os.path.exists(path):
         return None
     try:
@@ -80,6 +83,76 @@ def load_pmc(n_gpus):
         return float(d["hbm_bytes_per_launch"])
     except Exception:
         return None
+
+
+def roofline(dev, st, render_one, n_gpus, scene_key):
+    """Roofline object of the dominant kernel: algorithmic bytes (visit counts
+    from an instrumented, untimed pass) over its HIP-event launch time."""
+    dev.reset_stats()
+    dev.set_option("instrument", 1)
+    dev.clear()
+    render_one()
+    inst = dev.stats()
+    dev.set_option("instrument", 0)
+    inst["_rays_ext"] = inst["camera_rays"] + inst["bounce_rays"]
+    inst["_hits"] = inst["shaded_hits"]
+    alg_bytes, bytes_per_ray = algorithmic_bytes(inst, st)
+    split = st["launches_trace"] > 0
+    launches = max(st["launches_trace"] if split else st["launches_extend"], 1)
+    avg_launch_s = (st["ms_trace"] if split else st["ms_extend"]) / 1e3 / launches
+    achieved = (alg_bytes / launches) / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+    return {
+        "bound": "hbm",
+        "kernel": "k_trace (closest-hit traversal)" if split else "k_extend (closest-hit traversal + shading, fused)",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": load_pmc(n_gpus, scene_key),
+        "algorithmic_bytes_per_launch": round(alg_bytes / launches, 1),
+        "bytes_per_ray": round(bytes_per_ray, 1),
+        "visits_per_ray": {"nodes": round(inst["node_visits"] / max(1, inst["_rays_ext"]), 2),
+                           "instances": round(inst["leaf_visits"] / max(1, inst["_rays_ext"]), 2),
+                           "triangles": round(inst["tri_tests"] / max(1, inst["_rays_ext"]), 2)},
+        "simd_efficiency": round(inst["node_visits"] / max(1, 64 * inst["wave_node_iters"]), 3),
+        "avg_launch_us": round(avg_launch_s * 1e6, 2),
+        "launches": launches,
+    }
+
+
+def suite_line(ignis_amd, dev_index, path, spi, iters):
+    """Short single-GPU measurement of another scene of SURVEY.md §8d (load and
+    BVH build excluded): Mrays/s over `iters` iterations after one warm-up,
+    plus the dominant kernel's roofline on that scene."""
+    t_load = time.perf_counter()
+    scene = ignis_amd.Scene.from_file(path)
+    W, H = scene.film_size
+    dev = ignis_amd.Device(dev_index)
+    dev.upload(scene)
+    t_load = time.perf_counter() - t_load
+    p = ignis_amd.RenderParams()
+    p.width, p.height, p.spi = W, H, spi
+    dev.render(p)
+    dev.synchronize()
+    dev.reset_stats()
+    dev.set_option("timing", 1)
+    t0 = time.perf_counter()
+    for it in range(iters):
+        p.iteration = 1 + it
+        dev.render(p)
+    dev.synchronize()
+    dt = time.perf_counter() - t0
+    st = dev.stats()
+    dev.set_option("timing", 0)
+    rays = st["camera_rays"] + st["bounce_rays"] + st["shadow_rays"]
+    key = os.path.splitext(os.path.basename(path))[0]
+    line = {"scene": os.path.basename(path), "width": W, "height": H, "spi": spi, "iterations": iters,
+            "value": round(rays / dt / 1e6, 2), "unit": "Mrays/s", "ms_per_iteration": round(dt / iters * 1e3, 3),
+            "load_and_build_s": round(t_load, 2), "bvh_depth": st["bvh_depth"],
+            "roofline": roofline(dev, st, lambda: dev.render(p), 1, key)}
+    dev.close()
+    del scene
+    return line
 
 
 def main():
@@ -167,22 +240,8 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.SUM)
         totals = tt.cpu().numpy()
 
-    # ---- roofline of the dominant kernel (extend), live HIP-event timing ----
-    # instrumented (untimed) pass for BVH visit counts per ray
-    dev.reset_stats()
-    dev.set_option("instrument", 1)
-    dev.clear()
-    dev.render(params(0))
-    inst = dev.stats()
-    dev.set_option("instrument", 0)
-    inst["_rays_ext"] = inst["camera_rays"] + inst["bounce_rays"]
-    inst["_hits"] = inst["shaded_hits"]
-    alg_bytes, bytes_per_ray = algorithmic_bytes(inst, st)
-    split = st["launches_trace"] > 0
-    launches = max(st["launches_trace"] if split else st["launches_extend"], 1)
-    avg_launch_s = (st["ms_trace"] if split else st["ms_extend"]) / 1e3 / launches
-    achieved = (alg_bytes / launches) / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
-    traffic = load_pmc(n_gpus)
+    # ---- roofline of the dominant kernel, live HIP-event timing ----
+    roof = roofline(dev, st, lambda: dev.render(params(0)), n_gpus, os.path.splitext(os.path.basename(args.scene))[0])
 
     result = None
     if rank == 0:
@@ -193,6 +252,11 @@ def main():
         parity = None
         if n_gpus == 1 and not args.no_cpu_baseline:
             cpu, parity = cpu_baseline(scene, dev, W, H, spi, args.cpu_seconds)
+        suite = None
+        if n_gpus == 1 and args.suite:
+            # other scenes of SURVEY.md §8d, incl. the HBM roofline scene of record (S-soup-16M)
+            suite = [suite_line(ignis_amd, 0, os.path.join(ROOT, "scenes", f), spi, n)
+                     for f, n in (("primitives.json", 8), ("s_deep.json", 4), ("s_soup_1m.json", 2), ("s_soup_16m.json", 1))]
         result = {
             "metric": "Mrays/s (primary+secondary) at fixed spp; per-pixel L2 vs CPU ref",
             "value": round(value, 2),
@@ -217,22 +281,10 @@ def main():
             "kernel_ms": {"trace": round(st["ms_trace"], 3), "extend": round(st["ms_extend"], 3), "shadow": round(st["ms_shadow"], 3),
                           "finish": round(st["ms_finish"], 3),
                           "generate": round(st["ms_generate"], 3), "resolve": round(st["ms_resolve"], 3)},
-            "roofline": {
-                "bound": "hbm",
-                "kernel": "k_trace (closest-hit traversal)" if split else "k_extend (closest-hit traversal + shading, fused)",
-                "simd_efficiency": round(inst["node_visits"] / max(1, 64 * inst["wave_node_iters"]), 3),
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "algorithmic_bytes_per_launch": round(alg_bytes / launches, 1),
-                "bytes_per_ray": round(bytes_per_ray, 1),
-                "avg_launch_us": round(avg_launch_s * 1e6, 2),
-                "launches": launches,
-            },
+            "roofline": roof,
             "cpu_baseline": cpu,
             "parity": parity,
+            "suite": suite,
         }
         print(json.dumps(result), flush=True)
     if dist:

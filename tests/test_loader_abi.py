@@ -112,3 +112,36 @@ def test_procedural_shapes_load():
         m = d.meshes[i]
         n = np.ctypeslib.as_array(m.normals, shape=(m.num_vertices * 3,)).reshape(-1, 3)
         np.testing.assert_allclose(np.linalg.norm(n, axis=1), 1, atol=1e-5)
+
+
+def test_synthetic_bench_scenes(root):
+    """SURVEY.md §8d stand-ins: soup size/extent and determinism, S-deep instancing."""
+    soup = ignis_amd.Scene.from_file(os.path.join(root, "scenes", "s_soup_1m.json"))
+    d = soup.desc
+    assert d.num_meshes == 1 and d.meshes[0].num_faces == 1000000
+    assert all(-1.011 < d.scene_bbox_min[i] < -0.99 and 0.99 < d.scene_bbox_max[i] < 1.011 for i in range(3))
+    v = np.ctypeslib.as_array(d.meshes[0].vertices, shape=(9,)).copy()
+    again = ignis_amd.Scene.from_file(os.path.join(root, "scenes", "s_soup_1m.json"))
+    np.testing.assert_array_equal(v, np.ctypeslib.as_array(again.desc.meshes[0].vertices, shape=(9,)))
+    # triangle edge length ~ e = 0.01 for 1M triangles
+    t = v.reshape(3, 3)
+    assert np.abs(t - t.mean(axis=0)).max() <= 0.02 + 1e-6
+    deep = ignis_amd.Scene.from_file(os.path.join(root, "scenes", "s_deep.json"))
+    dd = deep.desc
+    assert dd.num_entities == 4097 and dd.num_meshes == 4
+    faces = sorted(dd.meshes[i].num_faces for i in range(dd.num_meshes))
+    assert faces == [2, 270, 20480, 131072]
+    assert dd.num_lights == 2
+
+
+def test_soup_and_grid_shapes_from_string():
+    doc = {"shapes": [{"type": "soup", "name": "s", "count": 1000, "seed": 1},
+                      {"type": "displaced_grid", "name": "g", "quads": 16, "size": 2.0, "amplitude": 0.5, "seed": 3}],
+           "bsdfs": [{"type": "diffuse", "name": "d"}],
+           "entities": [{"name": "a", "shape": "s", "bsdf": "d"}, {"name": "b", "shape": "g", "bsdf": "d"}]}
+    sc = ignis_amd.Scene.from_string(doc)
+    d = sc.desc
+    counts = sorted(d.meshes[i].num_faces for i in range(d.num_meshes))
+    assert counts == [512, 1000]
+    with pytest.raises(ignis_amd.IgxError):
+        ignis_amd.Scene.from_string({"shapes": [{"type": "soup", "name": "s", "count": 0}]})

@@ -1,6 +1,7 @@
-"""Workload for rocprofv3 counter passes: the bench's iterations (diamond
-1000x1000, spi 8) without timing or instrumentation, so every k_extend
-dispatch is the same kernel the bench times."""
+"""Workload for rocprofv3 counter passes: the bench's iterations of a scene
+(default diamond 1000x1000, spi 8) without timing or instrumentation, so every
+k_extend dispatch is the same kernel the bench times.
+Usage: pmc_run.py [iterations] [scene file under scenes/]"""
 import os
 import sys
 
@@ -9,7 +10,7 @@ sys.path.insert(0, os.path.join(ROOT, "ignis-masterthesis_amd"))
 import ignis_amd  # noqa: E402
 
 iters = int(sys.argv[1]) if len(sys.argv) > 1 else 2
-scene = ignis_amd.Scene.from_file(os.path.join(ROOT, "scenes", "diamond_scene.json"))
+scene = ignis_amd.Scene.from_file(os.path.join(ROOT, "scenes", sys.argv[2] if len(sys.argv) > 2 else "diamond_scene.json"))
 W, H = scene.film_size
 dev = ignis_amd.Device(0)
 dev.upload(scene)

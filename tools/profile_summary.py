@@ -46,7 +46,7 @@ def kernel_stats(src_dir, tag):
     print("\n".join(lines[:14]))
 
 
-def pmc(fetch_dir, write_dir, kernel="k_extend"):
+def pmc(fetch_dir, write_dir, kernel="k_extend", scene="diamond_scene"):
     def per_dispatch(d, counter):
         f = find(d, "*counter_collection.csv")
         if not f:
@@ -66,14 +66,15 @@ def pmc(fetch_dir, write_dir, kernel="k_extend"):
     write = sum(ws.values()) / len(ws)
     res = {
         "kernel": kernel,
-        "workload": "tools/pmc_run.py: diamond_scene.json 1000x1000, spi 8, 2 iterations (the bench's iterations)",
+        "workload": f"tools/pmc_run.py: {scene}.json 1000x1000, spi 8 (the bench's iterations)",
         "dispatches_fetch_pass": len(fs), "dispatches_write_pass": len(ws),
         "fetch_size_kib_per_launch": round(fetch, 1),
         "write_size_kib_per_launch": round(write, 1),
         "hbm_bytes_per_launch": round((2 * fetch + write) * 1024, 1),
         "correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE reports half of wide reads; MI355X_MICROARCH.md HBM section); Infinity-Cache hits are included in the counters",
     }
-    json.dump(res, open(os.path.join(ROOT, "profiles", "pmc_extend.json"), "w"), indent=1)
+    name = "pmc_extend.json" if scene == "diamond_scene" else f"pmc_extend_{scene}.json"
+    json.dump(res, open(os.path.join(ROOT, "profiles", name), "w"), indent=1)
     print(json.dumps(res, indent=1))
 
 
@@ -82,3 +83,5 @@ if __name__ == "__main__":
     out = os.path.join(ROOT, "gpurun_out")
     kernel_stats(os.path.join(out, "prof"), tag)
     pmc(os.path.join(out, "pmc_fetch"), os.path.join(out, "pmc_write"))
+    if os.path.isdir(os.path.join(out, "pmc_fetch_soup")):
+        pmc(os.path.join(out, "pmc_fetch_soup"), os.path.join(out, "pmc_write_soup"), scene="s_soup_16m")
