@@ -399,7 +399,7 @@ __device__ __forceinline__ void block_append2(bool a, bool b, int* ca, int* cb, 
 // extend kernel: one bounce for every live path, compacted outputs
 // ---------------------------------------------------------------------------
 template <int STACK, bool STATS, bool LDS>
-__global__ void __launch_bounds__(BLOCK, EXTEND_WAVES) k_extend(FrameArgs fa, SceneView gsv, PathBuf in, PathBuf out, ShadowBuf sh,
+__global__ void __launch_bounds__(BLOCK, (STACK <= 32 ? EXTEND_WAVES : 1)) k_extend(FrameArgs fa, SceneView gsv, PathBuf in, PathBuf out, ShadowBuf sh,
                                                   float4* L, KernelCounters kc, int tail_threshold) {
     __shared__ int stack_mem[STACK * BLOCK + 2 * (BLOCK / 64) + 2];
     extern __shared__ float4 lds_scene[];
