@@ -5,7 +5,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "ignis-masterthesis_amd"))
 import ignis_amd
 
-scene = ignis_amd.Scene.from_file(os.path.join(ROOT, sys.argv[1] if len(sys.argv) > 1 else "scenes/diamond_scene.json"))
+scene = ignis_amd.Scene.from_file(sys.argv[1] if len(sys.argv) > 1 and os.path.isabs(sys.argv[1]) else os.path.join(ROOT, sys.argv[1] if len(sys.argv) > 1 else "scenes/diamond_scene.json"))
 W, H = scene.film_size
 dev = ignis_amd.Device(0)
 dev.upload(scene)
