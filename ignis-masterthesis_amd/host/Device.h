@@ -88,6 +88,9 @@ public:
 
     void clearFramebuffer() { check(igx_clear(mDev)); }
 
+    // render() only queues work; wait for it (timing, device-side reads)
+    void synchronize() { check(igx_synchronize(mDev)); }
+
     igx_stats getStatistics() {
         igx_stats s{};
         check(igx_get_stats(mDev, &s));

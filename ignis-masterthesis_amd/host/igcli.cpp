@@ -1,7 +1,8 @@
 // igcli-style frontend over the HIP device (src/frontend/cli/main.cpp:54-179):
 // loads a scene, renders spp samples in iterations of spi on one GPU, prints
 // Msamples/s like the reference (cli/main.cpp:135, 172-178) plus Mrays/s, and
-// writes the averaged image as PFM (the reference writes EXR, out of scope).
+// writes the averaged image as EXR (Image::save, Image.h:92-101), or PFM when
+// the output name ends in .pfm.
 #include "Device.h"
 #include "igx_scene.h"
 
@@ -15,7 +16,7 @@
 
 static void usage() {
     std::fprintf(stderr,
-                 "usage: igcli SCENE.json [--spp N] [--spi N] [--seed N] [--gpu-device N] [-o out.pfm]\n");
+                 "usage: igcli SCENE.json [--spp N] [--spi N] [--seed N] [--gpu-device N] [-o out.exr|out.pfm]\n");
 }
 
 int main(int argc, char** argv) {
@@ -61,6 +62,7 @@ int main(int argc, char** argv) {
             rs.user_seed = seed;
             auto t0 = std::chrono::steady_clock::now();
             dev.render(rs);
+            dev.synchronize(); // render() only queues the iteration
             double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
             rates.push_back((double)spi * desc->film_width * desc->film_height / s / 1e6);
         }
@@ -72,16 +74,24 @@ int main(int argc, char** argv) {
                     (unsigned long long)st.bounce_rays, (unsigned long long)st.shadow_rays, st.ms_render);
         if (!out_path.empty()) {
             IG::AOVAccessor acc = dev.getFramebufferForHost();
-            FILE* f = std::fopen(out_path.c_str(), "wb");
-            if (!f) { std::fprintf(stderr, "cannot write %s\n", out_path.c_str()); return 1; }
-            std::fprintf(f, "PF\n%d %d\n-1.0\n", desc->film_width, desc->film_height);
             float inv = acc.IterationCount ? 1.0f / acc.IterationCount : 0.0f;
-            for (int y = desc->film_height - 1; y >= 0; --y) { // PFM rows go bottom-up
-                std::vector<float> row(3 * desc->film_width);
-                for (int x = 0; x < 3 * desc->film_width; ++x) row[x] = acc.Data[(size_t)y * 3 * desc->film_width + x] * inv;
-                std::fwrite(row.data(), sizeof(float), row.size(), f);
+            const bool pfm = out_path.size() >= 4 && out_path.compare(out_path.size() - 4, 4, ".pfm") == 0;
+            if (!pfm) {
+                if (igx_write_exr(out_path.c_str(), acc.Data, desc->film_width, desc->film_height, 3, inv) != 0) {
+                    std::fprintf(stderr, "cannot write %s\n", out_path.c_str());
+                    return 1;
+                }
+            } else {
+                FILE* f = std::fopen(out_path.c_str(), "wb");
+                if (!f) { std::fprintf(stderr, "cannot write %s\n", out_path.c_str()); return 1; }
+                std::fprintf(f, "PF\n%d %d\n-1.0\n", desc->film_width, desc->film_height);
+                for (int y = desc->film_height - 1; y >= 0; --y) { // PFM rows go bottom-up
+                    std::vector<float> row(3 * desc->film_width);
+                    for (int x = 0; x < 3 * desc->film_width; ++x) row[x] = acc.Data[(size_t)y * 3 * desc->film_width + x] * inv;
+                    std::fwrite(row.data(), sizeof(float), row.size(), f);
+                }
+                std::fclose(f);
             }
-            std::fclose(f);
         }
     } catch (const std::exception& e) {
         std::fprintf(stderr, "error: %s\n", e.what());

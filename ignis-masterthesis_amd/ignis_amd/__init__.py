@@ -35,6 +35,17 @@ def version():
     return lib().igx_version().decode()
 
 
+def write_exr(path, rgb, scale=1.0, alpha=False):
+    """Write a (H, W, 3) float image as an uncompressed float OpenEXR file
+    (Image::save, src/runtime/Image.h:92-101)."""
+    rgb = np.ascontiguousarray(rgb, dtype=np.float32)
+    h, w = rgb.shape[0], rgb.shape[1]
+    rc = _native.lib().igx_write_exr(os.fsencode(path), rgb.ctypes.data_as(C.POINTER(C.c_float)), w, h, 4 if alpha else 3,
+                                      float(scale))
+    if rc != 0:
+        raise IgxError(f"cannot write EXR {path} (code {rc})")
+
+
 def recommend_spi(width, height, interactive=False):
     """Runtime.cpp:61-69 for a GPU target."""
     spi_f = 8

@@ -95,7 +95,7 @@ class Stats(C.Structure):
 
 # every symbol include/igx.h and include/igx_scene.h declare
 EXPORTED_SYMBOLS = [
-    "igx_scene_load_file", "igx_scene_load_string", "igx_scene_get_desc", "igx_scene_free",
+    "igx_scene_load_file", "igx_scene_load_string", "igx_scene_get_desc", "igx_scene_free", "igx_write_exr",
     "igx_create", "igx_destroy", "igx_last_error", "igx_version", "igx_set_option", "igx_upload_scene",
     "igx_render", "igx_get_framebuffer", "igx_framebuffer_device_ptr", "igx_pack_tiles", "igx_clear",
     "igx_get_stats", "igx_reset_stats", "igx_trace_hits", "igx_trace_occlusion", "igx_synchronize",
@@ -121,6 +121,8 @@ def lib():
     L.igx_scene_get_desc.restype = C.POINTER(SceneDesc)
     L.igx_scene_free.argtypes = [vp]
     L.igx_scene_free.restype = None
+    L.igx_write_exr.argtypes = [C.c_char_p, C.POINTER(C.c_float), C.c_int32, C.c_int32, C.c_int32, C.c_float]
+    L.igx_write_exr.restype = C.c_int
     L.igx_create.argtypes = [C.c_int, C.POINTER(vp)]
     L.igx_destroy.argtypes = [vp]
     L.igx_last_error.argtypes = [vp]

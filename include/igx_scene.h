@@ -140,6 +140,12 @@ igx_scene* igx_scene_load_string(const char* json, const char* base_dir, char* e
 const igx_scene_desc* igx_scene_get_desc(const igx_scene* scene);
 void igx_scene_free(igx_scene* scene);
 
+/* Write a linear RGB image (row-major, 3 floats per pixel, each multiplied by
+ * `scale`, e.g. 1/iteration count) as an uncompressed float OpenEXR file with
+ * `channels` = 3 (RGB) or 4 (RGB + alpha 1).  Replaces Image::save
+ * (src/runtime/Image.h:92-101) for the framebuffer output.  0 on success. */
+int igx_write_exr(const char* path, const float* rgb, int32_t width, int32_t height, int32_t channels, float scale);
+
 #ifdef __cplusplus
 }
 #endif

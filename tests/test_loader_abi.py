@@ -145,3 +145,22 @@ def test_soup_and_grid_shapes_from_string():
     assert counts == [512, 1000]
     with pytest.raises(ignis_amd.IgxError):
         ignis_amd.Scene.from_string({"shapes": [{"type": "soup", "name": "s", "count": 0}]})
+
+
+def test_write_exr_roundtrip(tmp_path):
+    """Image::save stand-in (Image.h:92-101): float RGB(A) EXR, read back by an independent parser."""
+    from exr_read import read_exr
+    rng = np.random.default_rng(5)
+    img = rng.random((7, 11, 3), dtype=np.float32) * 10
+    p = tmp_path / "out.exr"
+    ignis_amd.write_exr(p, img, scale=0.5)
+    ch, attrs = read_exr(p)
+    assert sorted(ch) == ["B", "G", "R"]
+    np.testing.assert_array_equal(ch["R"], img[..., 0] * 0.5)
+    np.testing.assert_array_equal(ch["G"], img[..., 1] * 0.5)
+    np.testing.assert_array_equal(ch["B"], img[..., 2] * 0.5)
+    ignis_amd.write_exr(p, img, alpha=True)
+    ch, _ = read_exr(p)
+    assert sorted(ch) == ["A", "B", "G", "R"] and np.all(ch["A"] == 1)
+    with pytest.raises(ignis_amd.IgxError):
+        ignis_amd.write_exr(tmp_path / "missing_dir" / "x.exr", img)
