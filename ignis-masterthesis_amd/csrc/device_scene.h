@@ -27,13 +27,18 @@ constexpr int LEAF_COUNT_BITS = 4;
 // info (shape, material, vtx_offset, idx_offset) -> 7 x 16 B.
 constexpr int ENT_STRIDE = 7;
 
-enum : int32_t { MAT_DIFFUSE = 0, MAT_DIELECTRIC = 1 };
-struct DevMaterial {   // 64 B
-    int32_t type, light, thin, pad;
-    float kd[4];
-    float ks[4];
-    float kt[4];        // w unused
-    // n1 = ext_ior in ks[3], n2 = int_ior in kt[3]
+enum : int32_t { MAT_DIFFUSE = 0, MAT_DIELECTRIC = 1, MAT_CONDUCTOR = 2, MAT_PLASTIC = 3 };
+// microfacet distribution of conductor / plastic specular lobes
+// (BSDF::setupRoughness, src/runtime/bsdf/BSDF.cpp:53-99)
+enum : int32_t { MF_DELTA = 0, MF_VNDF_GGX = 1, MF_GGX = 2, MF_BECKMANN = 3 };
+struct DevMaterial {   // 128 B
+    int32_t type, light, dist, mirror; // mirror: delta conductor with eta = 0, k = 1 (make_mirror_bsdf)
+    float kd[4];        // diffuse reflectance; w = Oren-Nayar roughness (0: Lambert)
+    float ks[4];        // specular reflectance; w = n1 (ext ior)
+    float kt[4];        // specular transmittance; w = n2 (int ior)
+    float eta[4];       // conductor eta; w = alpha_u
+    float kappa[4];     // conductor k; w = alpha_v
+    float pad[8];
 };
 
 enum : int32_t { LIGHT_PLANE = 1, LIGHT_ENV = 2, LIGHT_POINT = 3, LIGHT_SPOT = 4 };

@@ -265,7 +265,7 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
     local_to_global(fa, fa.chunk_pixel0 + ps.slot / fa.spi, px, py);
     Rng rnd{create_random_seed(sample, fa.iter, fa.frame, px, py, fa.seed), ps.counter};
     f3 out_dir = neg(rd);
-    bool specular = m.type == MAT_DIELECTRIC;
+    const bool specular = bsdf_is_specular(m);
     // on_shadow (pathtracer.art:52-112)
     if (sv.nee && !specular && sv.num_lights > 0 && ps.depth + 1 <= sv.max_depth) {
         int lid = sv.num_lights <= 1 ? 0 : rnd.next_i32(0, sv.num_lights - 1);
@@ -275,17 +275,15 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
         float pdf_l_s = pdf_as_solid(ls.pdf_value, ls.pdf_solid, ls.cos, ls.dist * ls.dist) * sel_pdf;
         if (pdf_l_s > FLT_EPS_ && ls.cos > FLT_EPS_) {
             f3 in_dir = ls.dir;
-            f3 kd = mk(m.kd[0], m.kd[1], m.kd[2]);
             float mis;
             if (Lt.delta) {
                 mis = 1.0f;
             } else {
-                float c = dot(in_dir, s.local.n);
-                float pdf_e_s = (c >= 0 ? c : 0) / PI_; // cosine_hemisphere_pdf(positive_cos)
+                float pdf_e_s = bsdf_pdf(m, s, in_dir, out_dir); // pdf to sample the light by the bsdf
                 mis = 1 / (1 + pdf_e_s / pdf_l_s);
             }
             float factor = ls.pdf_value / pdf_l_s;
-            f3 ev = mulf(kd, fabsf(dot(in_dir, s.local.n)) * INV_PI_); // Lambert eval
+            f3 ev = bsdf_eval(m, s, in_dir, out_dir);
             sr.color = handle_color(sv, mulf(mul(ls.intensity, mul(ps.contrib, ev)), mis * factor));
             sr.o = s.point;
             if (Lt.infinite) {
@@ -300,7 +298,8 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
     }
     // on_bounce (pathtracer.art:165-200)
     if (!(ps.depth + 1 <= sv.max_depth)) return false;
-    BsdfSample bs = sample_bsdf(m, s, rnd, out_dir);
+    BsdfSample bs = bsdf_sample(m, s, rnd, out_dir);
+    if (!bs.valid) return false;
     f3 c2 = mul(ps.contrib, bs.color);
     float rr = 1.0f;
     if (ps.depth + 1 > sv.min_depth) {
@@ -1314,12 +1313,35 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     for (uint32_t i = 0; i < desc->num_materials; ++i) {
         const igx_material& m = desc->materials[i];
         DevMaterial d{};
-        d.type = m.bsdf_type == IGX_BSDF_DIELECTRIC ? MAT_DIELECTRIC : MAT_DIFFUSE;
+        switch (m.bsdf_type) {
+        case IGX_BSDF_DIFFUSE: d.type = MAT_DIFFUSE; break;
+        case IGX_BSDF_DIELECTRIC: d.type = MAT_DIELECTRIC; break;
+        case IGX_BSDF_CONDUCTOR: d.type = MAT_CONDUCTOR; break;
+        case IGX_BSDF_PLASTIC: d.type = MAT_PLASTIC; break;
+        default: return fail(dev, IGX_ERR_UNSUPPORTED, "unsupported bsdf type " + std::to_string(m.bsdf_type));
+        }
         if (m.bsdf_type == IGX_BSDF_DIELECTRIC && m.thin) return fail(dev, IGX_ERR_UNSUPPORTED, "thin dielectric is not supported");
+        if (m.distribution < IGX_MICROFACET_DELTA || m.distribution > IGX_MICROFACET_BECKMANN)
+            return fail(dev, IGX_ERR_INVALID_ARGUMENT, "invalid microfacet distribution");
         d.light = m.light >= 0 && (uint32_t)m.light < desc->num_lights ? light_remap[m.light] : -1;
-        for (int c = 0; c < 3; ++c) { d.kd[c] = m.kd[c]; d.ks[c] = m.ks[c]; d.kt[c] = m.kt[c]; }
+        // check_if_delta_distribution (core/microfacet.art:272): alpha <= 1e-4 is a delta lobe
+        const bool rough = m.distribution != IGX_MICROFACET_DELTA && m.alpha_u > 1e-4f && m.alpha_v > 1e-4f;
+        d.dist = rough ? m.distribution : MF_DELTA;
+        bool mirror = true; // make_conductor_bsdf: eta ~ black and k ~ white (bsdf/conductor.art:111-121)
+        for (int c = 0; c < 3; ++c) {
+            d.kd[c] = m.kd[c];
+            d.ks[c] = m.ks[c];
+            d.kt[c] = m.kt[c];
+            d.eta[c] = m.eta[c];
+            d.kappa[c] = m.kappa[c];
+            mirror = mirror && std::fabs(m.eta[c]) <= 1e-4f && std::fabs(m.kappa[c] - 1.0f) <= 1e-4f;
+        }
+        d.mirror = mirror ? 1 : 0;
+        d.kd[3] = m.bsdf_type == IGX_BSDF_DIFFUSE ? m.diffuse_alpha : 0.0f;
         d.ks[3] = m.ext_ior;
         d.kt[3] = m.int_ior;
+        d.eta[3] = m.alpha_u;
+        d.kappa[3] = m.alpha_v;
         mats[i] = d;
     }
 

@@ -553,26 +553,320 @@ __device__ __forceinline__ float fresnel_factor(float eta, float cos_i, float co
 struct BsdfSample {
     f3 in_dir;
     float pdf;
-    f3 color;
+    f3 color; // already divided by the pdf, cosine applied (make_bsdf_sample)
     float eta;
     bool valid;
 };
 
-__device__ __forceinline__ BsdfSample sample_bsdf(const DevMaterial& m, const Surface& s, Rng& rnd, f3 out_dir) {
+__device__ __forceinline__ BsdfSample reject_sample() {
     BsdfSample b;
+    b.in_dir = mk(0, 0, 0);
+    b.pdf = 0;
+    b.color = mk(0, 0, 0);
+    b.eta = 1;
+    b.valid = false;
+    return b;
+}
+__device__ __forceinline__ BsdfSample make_sample(f3 dir, float pdf, f3 color, float eta) {
+    BsdfSample b;
+    b.in_dir = dir;
+    b.pdf = pdf;
+    b.color = color;
+    b.eta = eta;
     b.valid = true;
-    if (m.type == MAT_DIFFUSE) {
-        float u = rnd.next_f32();
-        float v = rnd.next_f32();
-        float pdf;
-        f3 ld = sample_cosine_hemisphere(u, v, &pdf);
-        b.in_dir = frame_to_world(s.local, ld);
-        b.pdf = pdf;
-        b.color = mk(m.kd[0], m.kd[1], m.kd[2]);
-        b.eta = 1;
-        return b;
+    return b;
+}
+
+__device__ __forceinline__ float positive_cos(f3 a, f3 b) {
+    float c = dot(a, b);
+    return c >= 0 ? c : 0;
+}
+__device__ __forceinline__ float absolute_cos(f3 a, f3 b) { return fabsf(dot(a, b)); }
+__device__ __forceinline__ f3 lerp3(f3 a, f3 b, float t) { // color_lerp (core/color.art:18-22)
+    return mk((1 - t) * a.x + t * b.x, (1 - t) * a.y + t * b.y, (1 - t) * a.z + t * b.z);
+}
+__device__ __forceinline__ float lerp1(float a, float b, float k) { return (1 - k) * a + k * b; } // common.art:120
+__device__ __forceinline__ f3 to_local(const Frame& f, f3 v) { return mk(dot(f.t, v), dot(f.b, v), dot(f.n, v)); }
+
+// fresnel(eta, cos_i).factor, or 1 on total internal reflection (math::fresnel_dielectric, core/math.art:120)
+__device__ __forceinline__ float fresnel_dielectric(float eta, float cos_i) {
+    float eta2 = cos_i < 0 ? 1 / eta : eta;
+    float cos2_t = 1 - (1 - cos_i * cos_i) * eta2 * eta2; // snell (core/fresnel.art:13)
+    if (cos2_t <= 0.0f) return 1.0f;
+    return fresnel_factor(eta2, fabsf(cos_i), sqrtf(cos2_t));
+}
+// conductor_factor (core/fresnel.art:29-36)
+__device__ __forceinline__ float conductor_factor(float n, float k, float cos_i) {
+    float f = n * n + k * k;
+    float d1 = f * cos_i * cos_i;
+    float d2 = 2.0f * n * cos_i;
+    float rs = safe_div(d1 - d2, d1 + d2);
+    float rp = safe_div(f - d2 + cos_i * cos_i, f + d2 + cos_i * cos_i);
+    return clampf((rs * rs + rp * rp) * 0.5f, 0, 1);
+}
+// fresnel_diffuse_factor (core/fresnel.art:42-64)
+__device__ __forceinline__ float fresnel_diffuse_factor(float eta) {
+    if (eta < 1) return -1.4399f * (eta * eta) + 0.7099f * eta + 0.6681f + 0.0636f / eta;
+    float i1 = 1 / eta, i2 = i1 * i1, i3 = i2 * i1, i4 = i3 * i1, i5 = i4 * i1;
+    return 0.919317f - 3.4793f * i1 + 6.75335f * i2 - 7.80989f * i3 + 4.98554f * i4 - 1.36881f * i5;
+}
+__device__ __forceinline__ float diff_of_prod(float a, float b, float c, float d) { // common.art:132-137
+    float cd = c * d;
+    float diff = fmaf(a, b, -cd);
+    float err = fmaf(-c, d, cd);
+    return diff + err;
+}
+
+// ---- microfacet distributions (core/microfacet.art) ----------------------
+__device__ __forceinline__ float ndf_ggx(const Frame& l, f3 m, float au, float av) { // :187-197
+    float cz = dot(l.n, m), cx = dot(l.t, m), cy = dot(l.b, m);
+    float kx = cx / au, ky = cy / av;
+    float k = kx * kx + ky * ky + cz * cz;
+    return safe_div(1, PI_ * au * av * k * k);
+}
+__device__ __forceinline__ float ndf_beckmann(const Frame& l, f3 m, float au, float av) { // :175-185
+    float cz = dot(l.n, m), cx = dot(l.t, m), cy = dot(l.b, m);
+    float kx = cx / au, ky = cy / av;
+    float k2 = safe_div(kx * kx + ky * ky, cz * cz);
+    return safe_div(expf(-k2), PI_ * au * av * cz * cz * cz * cz);
+}
+__device__ __forceinline__ float g1_smith(const Frame& l, f3 w, float au, float av) { // :157-173
+    float cz = dot(l.n, w);
+    if (fabsf(cz) <= FLT_EPS_) return 0;
+    float cx = dot(l.t, w), cy = dot(l.b, w);
+    float kx = au * cx, ky = av * cy;
+    float a2 = kx * kx + ky * ky;
+    if (a2 <= FLT_EPS_) return 1;
+    float k2 = a2 / (cz * cz);
+    return 2 / (1 + sqrtf(1 + k2));
+}
+__device__ __forceinline__ float g1_walter(const Frame& l, f3 w, float au, float av) { // :136-155
+    float cz = dot(l.n, w);
+    if (fabsf(cz) <= FLT_EPS_) return 0;
+    float cx = dot(l.t, w), cy = dot(l.b, w);
+    float kx = au * cx, ky = av * cy;
+    float k2 = (kx * kx + ky * ky) / (cz * cz);
+    if (k2 <= FLT_EPS_) return 1;
+    float a = 1 / sqrtf(k2), a2 = 1 / k2;
+    return a >= 1.6f ? 1.0f : (3.535f * a + 2.181f * a2) / (1.0f + 2.276f * a + 2.577f * a2);
+}
+__device__ __forceinline__ float mf_D(const DevMaterial& m, const Frame& l, f3 h) {
+    return m.dist == MF_BECKMANN ? ndf_beckmann(l, h, m.eta[3], m.kappa[3]) : ndf_ggx(l, h, m.eta[3], m.kappa[3]);
+}
+__device__ __forceinline__ float mf_G(const DevMaterial& m, const Frame& l, f3 wi, f3 wo) {
+    if (m.dist == MF_BECKMANN) return g1_walter(l, wi, m.eta[3], m.kappa[3]) * g1_walter(l, wo, m.eta[3], m.kappa[3]);
+    return g1_smith(l, wi, m.eta[3], m.kappa[3]) * g1_smith(l, wo, m.eta[3], m.kappa[3]);
+}
+// pdf_vndf_ggx (:337-340)
+__device__ __forceinline__ float pdf_vndf_ggx(const Frame& l, f3 w, f3 h, float au, float av) {
+    float cz = absolute_cos(l.n, w);
+    return safe_div(g1_smith(l, w, au, av) * absolute_cos(w, h) * ndf_ggx(l, h, au, av), cz);
+}
+__device__ __forceinline__ float mf_pdf(const DevMaterial& m, const Frame& l, f3 wo, f3 h) {
+    if (m.dist == MF_VNDF_GGX) return pdf_vndf_ggx(l, wo, h, m.eta[3], m.kappa[3]);
+    return mf_D(m, l, h) * absolute_cos(l.n, h); // make_microfacet_distribution.pdf (:265)
+}
+// square_to_concentric_disk (core/warp.art:2-22)
+__device__ __forceinline__ void concentric_disk(float u, float v, float& x, float& y) {
+    float a = 2 * u - 1, b = 2 * v - 1;
+    if (a == 0 && b == 0) {
+        x = 0;
+        y = 0;
+    } else if (a * a > b * b) {
+        float phi = (PI_ / 4) * safe_div(b, a);
+        x = cosf(phi) * a;
+        y = sinf(phi) * a;
+    } else {
+        float phi = (PI_ / 2) - (PI_ / 4) * safe_div(a, b);
+        x = cosf(phi) * b;
+        y = sinf(phi) * b;
     }
-    // make_pure_dielectric_bsdf.sample (adjoint = false)
+}
+// Microfacet normal sample of the material's distribution for outgoing wo.
+__device__ __forceinline__ f3 mf_sample(const DevMaterial& m, const Frame& l, Rng& rnd, f3 wo, float& pdf) {
+    const float au = m.eta[3], av = m.kappa[3];
+    if (m.dist == MF_VNDF_GGX) {
+        // sample_vndf_ggx (:306-335) with sample_vndf_ggx_11 (:287-304)
+        f3 vl = to_local(l, wo);
+        f3 sl = normalize(mk(au * vl.x, av * vl.y, vl.z));
+        float st = safe_sqrt(1 - sl.z * sl.z); // sin_cos_phi (core/shading.art:46-53)
+        float sin_phi = 0, cos_phi = 1;
+        if (fabsf(st) > FLT_EPS_) {
+            sin_phi = sl.y / st;
+            cos_phi = sl.x / st;
+        }
+        float ct = fabsf(sl.z);
+        float u0 = rnd.next_f32();
+        float u1 = rnd.next_f32();
+        float px, py;
+        concentric_disk(u0, u1, px, py);
+        float sv = 0.5f * (1 + ct);
+        float y = (1 - sv) * safe_sqrt(1 - px * px) + sv * py;
+        float z = safe_sqrt(1 - y * y - px * px);
+        float sin_t = safe_sqrt(1 - ct * ct);
+        float nrm = safe_div(1, sum_of_prod(sin_t, y, ct, z));
+        float slx = diff_of_prod(ct, y, sin_t, z) * nrm, sly = px * nrm;
+        float s2x = (cos_phi * slx - sin_phi * sly) * au;
+        float s2y = (sin_phi * slx + cos_phi * sly) * av;
+        f3 nh = isfinite(s2x) ? normalize(mk(-s2x, -s2y, 1)) : mk(0, 0, 0);
+        f3 h = frame_to_world(l, nh);
+        pdf = pdf_vndf_ggx(l, wo, h, au, av);
+        return h;
+    }
+    float u0 = rnd.next_f32();
+    float u1 = rnd.next_f32();
+    const float ar = av / au;
+    if (m.dist == MF_BECKMANN) {
+        // make_beckmann_model.sample (:211-232)
+        float phi = atanf(ar * tanf(2 * PI_ * u1));
+        float cos_phi = cosf(phi);
+        float sin_phi = sqrtf(1 - cos_phi * cos_phi);
+        float kx = cos_phi / au, ky = sin_phi / av;
+        float k2 = 1 / (kx * kx + ky * ky);
+        float cos_t = 1 / sqrtf(1 - k2 * logf(1.0f - u0));
+        float cos_t2 = cos_t * cos_t;
+        float sin_t = sqrtf(1 - cos_t2);
+        pdf = (1 - u0) / (PI_ * au * av * cos_t2 * cos_t);
+        return frame_to_world(l, mk(sin_t * cos_phi, sin_t * sin_phi, cos_t));
+    }
+    // make_ggx_model.sample (:236-262); the isotropic case uses phi = 2 pi u1
+    float phi = au == av ? 2 * PI_ * u1 : atanf(ar * tanf(2 * PI_ * u1));
+    float cos_phi = cosf(phi);
+    float sin_phi = sqrtf(1 - cos_phi * cos_phi);
+    float kx = cos_phi / au, ky = sin_phi / av;
+    float d2 = kx * kx + ky * ky;
+    float a2 = safe_div(1, d2);
+    float t2 = a2 * u0 / (1 - u0);
+    float cos_t = 1 / sqrtf(1 + t2);
+    float cos_t2 = cos_t * cos_t;
+    float sin_t = sqrtf(1 - cos_t2);
+    float k2 = d2 * (sin_t * sin_t) / cos_t2;
+    pdf = safe_div(1, PI_ * au * av * cos_t2 * cos_t * (1 + k2) * (1 + k2));
+    return frame_to_world(l, mk(sin_t * cos_phi, sin_t * sin_phi, cos_t));
+}
+
+// ---- BSDFs ------------------------------------------------------------------
+// Fresnel term of a conductor lobe: per-channel conductor_factor; plastic's
+// specular lobe is a conductor with eta 0, k 1 (PlasticBSDF.cpp:38-42).
+__device__ __forceinline__ f3 conductor_fresnel(const DevMaterial& m, float c) {
+    if (m.type == MAT_PLASTIC)
+        return mk(conductor_factor(0, 1, c), conductor_factor(0, 1, c), conductor_factor(0, 1, c));
+    return mk(conductor_factor(m.eta[0], m.kappa[0], c), conductor_factor(m.eta[1], m.kappa[1], c),
+              conductor_factor(m.eta[2], m.kappa[2], c));
+}
+// make_rough_base_conductor_bsdf.eval with kd = black (bsdf/conductor.art:57-69)
+__device__ __forceinline__ f3 rough_conductor_eval(const DevMaterial& m, const Surface& s, f3 in, f3 out) {
+    const f3 N = s.local.n;
+    float cos_o = absolute_cos(out, N), cos_i = absolute_cos(in, N);
+    if (cos_o <= FLT_EPS_ || cos_i <= FLT_EPS_) return mk(0, 0, 0);
+    f3 h = normalize(add(in, out));
+    float D = mf_D(m, s.local, h);
+    float G = mf_G(m, s.local, in, out);
+    f3 F = conductor_fresnel(m, absolute_cos(out, h));
+    f3 ks = mk(m.ks[0], m.ks[1], m.ks[2]);
+    return mulf(mul(ks, F), D * G / (4 * cos_o));
+}
+__device__ __forceinline__ float rough_conductor_pdf(const DevMaterial& m, const Surface& s, f3 in, f3 out) {
+    f3 h = normalize(add(in, out));
+    float jacob = safe_div(1, 4 * absolute_cos(out, h));
+    return mf_pdf(m, s.local, out, h) * jacob;
+}
+// conductor / plastic specular lobe sample (bsdf/conductor.art:1-27, 42-55, 71-100)
+__device__ __forceinline__ BsdfSample specular_lobe_sample(const DevMaterial& m, const Surface& s, Rng& rnd, f3 out) {
+    const f3 N = s.local.n;
+    const f3 ks = mk(m.ks[0], m.ks[1], m.ks[2]);
+    if (m.dist == MF_DELTA) {
+        if (m.mirror || m.type == MAT_PLASTIC) return make_sample(reflect(out, N), 1, ks, 1); // make_mirror_bsdf
+        float cos_i = dot(out, N);                                                          // make_pure_conductor_bsdf
+        return make_sample(reflect(out, N), 1, mul(ks, conductor_fresnel(m, cos_i)), 1);
+    }
+    float cos_o = absolute_cos(out, N);
+    if (cos_o <= FLT_EPS_) return reject_sample();
+    float spdf;
+    f3 sn = mf_sample(m, s.local, rnd, out, spdf);
+    if (dot(sn, sn) <= FLT_EPS_) return reject_sample();
+    f3 oh = normalize(sn);
+    f3 h = signbit(dot(oh, out)) ? neg(oh) : oh;
+    f3 in = reflect(out, h);
+    if (absolute_cos(in, N) <= FLT_EPS_) return reject_sample();
+    float jacob = 1 / (4 * absolute_cos(out, h));
+    float pdf = spdf * jacob;
+    return make_sample(in, pdf, mulf(rough_conductor_eval(m, s, in, out), safe_div(1, pdf)), 1);
+}
+__device__ __forceinline__ bool lobe_is_specular(const DevMaterial& m) { return m.dist == MF_DELTA; }
+
+// Diffuse: Lambert, or Oren-Nayar when roughness > eps (bsdf/diffuse.art:2-46)
+__device__ __forceinline__ f3 diffuse_eval(const DevMaterial& m, const Surface& s, f3 in, f3 out) {
+    const f3 N = s.local.n;
+    const f3 kd = mk(m.kd[0], m.kd[1], m.kd[2]);
+    const float alpha = m.kd[3];
+    if (alpha <= FLT_EPS_) return mulf(kd, absolute_cos(in, N) * INV_PI_);
+    float a2 = alpha * alpha;
+    float p1 = absolute_cos(in, N), p2 = absolute_cos(out, N);
+    float sv = -p1 * p2 + positive_cos(out, in);
+    float t = sv <= FLT_EPS_ ? 1.0f : fmaxf(FLT_EPS_, fmaxf(p1, p2));
+    float A = 1 - 0.5f * a2 / (a2 + 0.33f);
+    float B = 0.45f * a2 / (a2 + 0.09f);
+    float C = 0.17f * a2 / (a2 + 0.13f);
+    return mulf(add(mulf(kd, (A + (B * sv / t)) / PI_), mul(kd, mulf(kd, C / PI_))), p1);
+}
+__device__ __forceinline__ BsdfSample diffuse_sample(const DevMaterial& m, const Surface& s, Rng& rnd, f3 out) {
+    float u = rnd.next_f32();
+    float v = rnd.next_f32();
+    float pdf;
+    f3 ld = sample_cosine_hemisphere(u, v, &pdf);
+    f3 dir = frame_to_world(s.local, ld);
+    if (m.kd[3] <= FLT_EPS_) return make_sample(dir, pdf, mk(m.kd[0], m.kd[1], m.kd[2]), 1);
+    return make_sample(dir, pdf, mulf(diffuse_eval(m, s, dir, out), 1 / pdf), 1);
+}
+__device__ __forceinline__ float diffuse_pdf(const Surface& s, f3 in) { return positive_cos(in, s.local.n) / PI_; }
+
+// Plastic (bsdf/plastic.art): Fresnel-weighted variadic mix of a diffuse lobe
+// with inner-scattering term and a conductor(eta 0, k 1) specular lobe.
+__device__ __forceinline__ float plastic_scatter(const DevMaterial& m, float cos_i) {
+    const float eta = m.ks[3] / m.kt[3];
+    const float fdr = fresnel_diffuse_factor(eta);
+    float fi = fresnel_dielectric(eta, cos_i);
+    return (1 - fi) * eta * eta / (1 - fdr);
+}
+__device__ __forceinline__ f3 plastic_diffuse_eval(const DevMaterial& m, const Surface& s, f3 in) {
+    const f3 kd = mk(m.kd[0], m.kd[1], m.kd[2]);
+    return mulf(mulf(kd, absolute_cos(in, s.local.n) * INV_PI_), plastic_scatter(m, absolute_cos(in, s.local.n)));
+}
+__device__ __forceinline__ float plastic_mix(const DevMaterial& m, const Surface& s, f3 out) {
+    return fresnel_dielectric(m.ks[3] / m.kt[3], absolute_cos(out, s.local.n));
+}
+
+__device__ __forceinline__ bool bsdf_is_specular(const DevMaterial& m) {
+    return m.type == MAT_DIELECTRIC || (m.type == MAT_CONDUCTOR && m.dist == MF_DELTA);
+}
+__device__ __forceinline__ f3 bsdf_eval(const DevMaterial& m, const Surface& s, f3 in, f3 out) {
+    switch (m.type) {
+    case MAT_DIFFUSE: return diffuse_eval(m, s, in, out);
+    case MAT_CONDUCTOR: return m.dist == MF_DELTA ? mk(0, 0, 0) : rough_conductor_eval(m, s, in, out);
+    case MAT_PLASTIC: {
+        float k = plastic_mix(m, s, out);
+        f3 spec = m.dist == MF_DELTA ? mk(0, 0, 0) : rough_conductor_eval(m, s, in, out);
+        return lerp3(plastic_diffuse_eval(m, s, in), spec, k);
+    }
+    default: return mk(0, 0, 0);
+    }
+}
+__device__ __forceinline__ float bsdf_pdf(const DevMaterial& m, const Surface& s, f3 in, f3 out) {
+    switch (m.type) {
+    case MAT_DIFFUSE: return diffuse_pdf(s, in);
+    case MAT_CONDUCTOR: return m.dist == MF_DELTA ? 0.0f : rough_conductor_pdf(m, s, in, out);
+    case MAT_PLASTIC: {
+        float k = plastic_mix(m, s, out);
+        float sp = m.dist == MF_DELTA ? 0.0f : rough_conductor_pdf(m, s, in, out);
+        return lerp1(diffuse_pdf(s, in), sp, k);
+    }
+    default: return 0;
+    }
+}
+
+// make_pure_dielectric_bsdf.sample, adjoint = false (bsdf/dielectric.art)
+__device__ __forceinline__ BsdfSample dielectric_sample(const DevMaterial& m, const Surface& s, Rng& rnd, f3 out_dir) {
     float n1 = m.ks[3], n2 = m.kt[3];
     float k = s.entering ? n1 / n2 : n2 / n1;
     f3 n = s.local.n;
@@ -588,18 +882,49 @@ __device__ __forceinline__ BsdfSample sample_bsdf(const DevMaterial& m, const Su
             ft_factor = fresnel_factor(eta2, fabsf(cos_o), ct);
         }
     }
-    if (rnd.next_f32() > ft_factor) {
-        b.in_dir = refract(out_dir, n, k, cos_o, ft_cos_t);
-        b.pdf = 1;
-        b.color = mk(m.kt[0], m.kt[1], m.kt[2]);
-        b.eta = k;
-    } else {
-        b.in_dir = reflect(out_dir, n);
-        b.pdf = 1;
-        b.color = mk(m.ks[0], m.ks[1], m.ks[2]);
-        b.eta = 1;
+    if (rnd.next_f32() > ft_factor)
+        return make_sample(refract(out_dir, n, k, cos_o, ft_cos_t), 1, mk(m.kt[0], m.kt[1], m.kt[2]), k);
+    return make_sample(reflect(out_dir, n), 1, mk(m.ks[0], m.ks[1], m.ks[2]), 1);
+}
+
+__device__ __forceinline__ BsdfSample bsdf_sample(const DevMaterial& m, const Surface& s, Rng& rnd, f3 out) {
+    switch (m.type) {
+    case MAT_DIFFUSE: return diffuse_sample(m, s, rnd, out);
+    case MAT_DIELECTRIC: return dielectric_sample(m, s, rnd, out);
+    case MAT_CONDUCTOR: return specular_lobe_sample(m, s, rnd, out);
+    default: break;
     }
-    return b;
+    // plastic: make_variadic_mix_bsdf(diffuse_extra, specular, mix_f).sample (bsdf/mix.art:29-62)
+    const float k = plastic_mix(m, s, out);
+    const bool spec_delta = lobe_is_specular(m);
+    auto diffuse_extra = [&]() {
+        BsdfSample b = diffuse_sample(m, s, rnd, out); // Lambert lobe (kd, cosine pdf)
+        b.color = mulf(b.color, plastic_scatter(m, absolute_cos(b.in_dir, s.local.n)));
+        return b;
+    };
+    if (k <= 0) return diffuse_extra();
+    if (k >= 1) return specular_lobe_sample(m, s, rnd, out);
+    if (rnd.next_f32() < 1 - k) {
+        BsdfSample b = diffuse_extra(); // sample_mat(diffuse, specular, k)
+        if (b.valid) {
+            if (spec_delta) return b;
+            float p = lerp1(b.pdf, rough_conductor_pdf(m, s, b.in_dir, out), k);
+            f3 c = lerp3(mulf(b.color, b.pdf), rough_conductor_eval(m, s, b.in_dir, out), k);
+            b.pdf = p;
+            b.color = mk(c.x / p, c.y / p, c.z / p);
+            return b;
+        }
+        return specular_lobe_sample(m, s, rnd, out);
+    }
+    BsdfSample b = specular_lobe_sample(m, s, rnd, out); // sample_mat(specular, diffuse, 1 - k)
+    if (b.valid) {
+        float p = lerp1(b.pdf, diffuse_pdf(s, b.in_dir), 1 - k);
+        f3 c = lerp3(mulf(b.color, b.pdf), plastic_diffuse_eval(m, s, b.in_dir), 1 - k);
+        b.pdf = p;
+        b.color = mk(c.x / p, c.y / p, c.z / p);
+        return b;
+    }
+    return diffuse_extra();
 }
 
 } // namespace igxd

@@ -253,6 +253,66 @@ const Value* array_of(const Value& doc, const char* key) {
     return v;
 }
 
+// --- bsdf parameter tables (src/runtime/bsdf/BSDF.cpp:7-51) ----------------
+float dielectric_ior(const std::string& mat, const std::string& bsdf) {
+    static const std::pair<const char*, float> table[] = {
+        {"vacuum", 1.0f}, {"bk7", 1.5046f}, {"glass", 1.5046f}, {"helium", 1.00004f}, {"hydrogen", 1.00013f},
+        {"air", 1.000277f}, {"water", 1.333f}, {"ethanol", 1.361f}, {"diamond", 2.419f}, {"polypropylene", 1.49f}};
+    std::string l = mat;
+    for (auto& c : l) c = (char)std::tolower(c);
+    for (auto& e : table)
+        if (l == e.first) return e.second;
+    fail("bsdf '" + bsdf + "': unknown dielectric material '" + mat + "'");
+}
+
+void conductor_spec(const std::string& mat, const std::string& bsdf, V3& eta, V3& k) {
+    struct Spec { const char* name; float eta[3], k[3]; };
+    static const Spec table[] = {
+        {"aluminum", {1.34560f, 0.96521f, 0.61722f}, {7.47460f, 6.39950f, 5.30310f}},
+        {"brass", {0.44400f, 0.52700f, 1.09400f}, {3.69500f, 2.76500f, 1.82900f}},
+        {"copper", {0.27105f, 0.67693f, 1.31640f}, {3.60920f, 2.62480f, 2.29210f}},
+        {"gold", {0.18299f, 0.42108f, 1.37340f}, {3.4242f, 2.34590f, 1.77040f}},
+        {"iron", {2.91140f, 2.94970f, 2.58450f}, {3.08930f, 2.93180f, 2.76700f}},
+        {"lead", {1.91000f, 1.83000f, 1.44000f}, {3.51000f, 3.40000f, 3.18000f}},
+        {"mercury", {2.07330f, 1.55230f, 1.06060f}, {5.33830f, 4.65100f, 3.86280f}},
+        {"platinum", {2.37570f, 2.08470f, 1.84530f}, {4.26550f, 3.71530f, 3.13650f}},
+        {"silver", {0.15943f, 0.14512f, 0.13547f}, {3.92910f, 3.19000f, 2.38080f}},
+        {"titanium", {2.74070f, 2.54180f, 2.26700f}, {3.81430f, 3.43450f, 3.03850f}},
+        {"none", {0.0f, 0.0f, 0.0f}, {1.0f, 1.0f, 1.0f}}};
+    std::string l = mat;
+    for (auto& c : l) c = (char)std::tolower(c);
+    for (auto& e : table)
+        if (l == e.name) {
+            eta = V3(e.eta[0], e.eta[1], e.eta[2]);
+            k = V3(e.k[0], e.k[1], e.k[2]);
+            return;
+        }
+    fail("bsdf '" + bsdf + "': unknown conductor material '" + mat + "'");
+}
+
+// BSDF::setupRoughness (BSDF.cpp:53-99) and microfacet::compute_explicit
+// (core/microfacet.art:395-402): no roughness property -> delta lobe.
+void setup_roughness(const Props& bp, igx_material& m) {
+    const bool old = bp.has("alpha") || bp.has("alpha_u") || bp.has("alpha_v");
+    const std::string p = old ? "alpha" : "roughness";
+    const std::string pu = p + "_u", pv = p + "_v";
+    if (!bp.has(p.c_str()) && !bp.has(pu.c_str()) && !bp.has(pv.c_str())) {
+        m.distribution = IGX_MICROFACET_DELTA;
+        return;
+    }
+    std::string dist = bp.string("distribution", "");
+    m.distribution = dist == "ggx" ? IGX_MICROFACET_GGX : dist == "beckmann" ? IGX_MICROFACET_BECKMANN : IGX_MICROFACET_VNDF_GGX;
+    if (bp.has(pu.c_str()) || bp.has(pv.c_str())) {
+        m.alpha_u = bp.number(pu.c_str(), 0.1f);
+        m.alpha_v = bp.number(pv.c_str(), 0.1f);
+    } else {
+        float r = bp.number(p.c_str(), 0.1f), an = bp.number("anisotropic", 0.0f);
+        float aspect = an == 0.0f ? 1.0f : std::sqrt(1 - std::min(std::max(an, 0.0f), 1.0f) * 0.99f);
+        m.alpha_u = r / aspect;
+        m.alpha_v = r * aspect;
+    }
+}
+
 // --- shapes -------------------------------------------------------------
 struct LoadedShape {
     igx_shape shape{};
@@ -370,23 +430,44 @@ static void build_scene(SceneStore& S, const Value& doc, const std::string& base
             m.int_ior = 1.5046f;
             m.kd[0] = m.kd[1] = m.kd[2] = 0.8f;
             for (int i = 0; i < 3; ++i) m.ks[i] = m.kt[i] = 1.0f;
-            if (type == "diffuse") {
+            if (type == "diffuse" || type == "roughdiffuse") {
                 m.bsdf_type = IGX_BSDF_DIFFUSE;
                 V3 kd = bp.color("reflectance", V3(0.8f, 0.8f, 0.8f)); // DiffuseBSDF.cpp:17
                 m.kd[0] = kd.x; m.kd[1] = kd.y; m.kd[2] = kd.z;
-                if (bp.number("roughness", 0.0f) > 1.1920928955e-07f)
-                    fail("bsdf '" + name + "': rough (Oren-Nayar) diffuse is not supported");
+                m.diffuse_alpha = bp.number(bp.has("alpha") ? "alpha" : "roughness", 0.0f); // Oren-Nayar above flt_eps
             } else if (type == "dielectric" || type == "glass") {
                 m.bsdf_type = IGX_BSDF_DIELECTRIC; // DielectricBSDF.cpp:12-38
                 V3 ks = bp.color("specular_reflectance", V3(1, 1, 1));
                 V3 kt = bp.color("specular_transmittance", V3(1, 1, 1));
                 m.ks[0] = ks.x; m.ks[1] = ks.y; m.ks[2] = ks.z;
                 m.kt[0] = kt.x; m.kt[1] = kt.y; m.kt[2] = kt.z;
-                m.ext_ior = bp.number("ext_ior", 1.0f);
-                m.int_ior = bp.number("int_ior", 1.5046f);
+                m.ext_ior = bp.number("ext_ior", dielectric_ior(bp.string("ext_ior_material", "vacuum"), name));
+                m.int_ior = bp.number("int_ior", dielectric_ior(bp.string("int_ior_material", "bk7"), name));
                 m.thin = bp.boolean("thin", false) ? 1 : 0;
                 if (bp.number("roughness", 0.0f) > 0.0f || bp.number("roughness_u", 0.0f) > 0.0f || bp.number("roughness_v", 0.0f) > 0.0f)
                     fail("bsdf '" + name + "': rough dielectric is not supported");
+            } else if (type == "conductor" || type == "roughconductor" || type == "mirror") {
+                // ConductorBSDF.cpp:12-33; material table BSDF.cpp:30-51 (default "none": eta 0, k 1)
+                m.bsdf_type = IGX_BSDF_CONDUCTOR;
+                V3 ks = bp.color("specular_reflectance", V3(1, 1, 1));
+                m.ks[0] = ks.x; m.ks[1] = ks.y; m.ks[2] = ks.z;
+                V3 eta(0, 0, 0), k(1, 1, 1);
+                conductor_spec(bp.string("material", "none"), name, eta, k);
+                eta = bp.color("eta", eta);
+                k = bp.color("k", k);
+                for (int c = 0; c < 3; ++c) { m.eta[c] = eta[c]; m.kappa[c] = k[c]; }
+                setup_roughness(bp, m);
+            } else if (type == "plastic" || type == "roughplastic") {
+                // PlasticBSDF.cpp:12-46
+                m.bsdf_type = IGX_BSDF_PLASTIC;
+                V3 ks = bp.color("specular_reflectance", V3(1, 1, 1));
+                V3 kd = bp.color("diffuse_reflectance", V3(0.8f, 0.8f, 0.8f));
+                m.ks[0] = ks.x; m.ks[1] = ks.y; m.ks[2] = ks.z;
+                m.kd[0] = kd.x; m.kd[1] = kd.y; m.kd[2] = kd.z;
+                m.ext_ior = bp.number("ext_ior", dielectric_ior(bp.string("ext_ior_material", "vacuum"), name));
+                m.int_ior = bp.number("int_ior", dielectric_ior(bp.string("int_ior_material", "polypropylene"), name));
+                for (int c = 0; c < 3; ++c) { m.eta[c] = 0; m.kappa[c] = 1; }
+                setup_roughness(bp, m);
             } else {
                 fail("bsdf '" + name + "': unsupported bsdf type '" + type + "'");
             }

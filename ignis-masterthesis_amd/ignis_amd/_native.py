@@ -34,9 +34,10 @@ class Entity(C.Structure):
 
 
 class Material(C.Structure):
-    _fields_ = [("bsdf_type", C.c_int32), ("light", C.c_int32), ("thin", C.c_int32), ("pad", C.c_int32),
+    _fields_ = [("bsdf_type", C.c_int32), ("light", C.c_int32), ("thin", C.c_int32), ("distribution", C.c_int32),
                 ("kd", C.c_float * 3), ("ks", C.c_float * 3), ("kt", C.c_float * 3),
-                ("ext_ior", C.c_float), ("int_ior", C.c_float)]
+                ("ext_ior", C.c_float), ("int_ior", C.c_float), ("eta", C.c_float * 3), ("kappa", C.c_float * 3),
+                ("alpha_u", C.c_float), ("alpha_v", C.c_float), ("diffuse_alpha", C.c_float), ("pad", C.c_float)]
 
 
 class Light(C.Structure):

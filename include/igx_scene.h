@@ -66,17 +66,29 @@ typedef struct igx_entity {
 } igx_entity;
 
 /* ---- materials --------------------------------------------------------- */
-enum { IGX_BSDF_DIFFUSE = 0, IGX_BSDF_DIELECTRIC = 1 };
+enum {
+    IGX_BSDF_DIFFUSE    = 0, /* Lambert / Oren-Nayar (bsdf/diffuse.art) */
+    IGX_BSDF_DIELECTRIC = 1, /* pure (smooth) dielectric (bsdf/dielectric.art) */
+    IGX_BSDF_CONDUCTOR  = 2, /* mirror / pure / rough conductor (bsdf/conductor.art) */
+    IGX_BSDF_PLASTIC    = 3  /* Fresnel mix of diffuse and a conductor lobe (bsdf/plastic.art) */
+};
+/* microfacet distribution of conductor / plastic lobes (BSDF::setupRoughness, BSDF.cpp:53-99) */
+enum { IGX_MICROFACET_DELTA = 0, IGX_MICROFACET_VNDF_GGX = 1, IGX_MICROFACET_GGX = 2, IGX_MICROFACET_BECKMANN = 3 };
 
 typedef struct igx_material {
     int32_t bsdf_type;     /* IGX_BSDF_* */
     int32_t light;         /* index of the area light emitting from this material, -1 if none */
     int32_t thin;          /* dielectric: thin interface */
-    int32_t pad;
+    int32_t distribution;  /* IGX_MICROFACET_* (conductor, plastic) */
     float kd[3];           /* diffuse reflectance */
     float ks[3];           /* specular reflectance */
     float kt[3];           /* specular transmittance */
     float ext_ior, int_ior;
+    float eta[3];          /* conductor complex ior: real part */
+    float kappa[3];        /* conductor complex ior: imaginary part */
+    float alpha_u, alpha_v;/* microfacet roughness (compute_explicit, core/microfacet.art:395-402) */
+    float diffuse_alpha;   /* Oren-Nayar roughness, 0 = Lambert */
+    float pad;
 } igx_material;
 
 /* ---- lights ------------------------------------------------------------ */

@@ -781,6 +781,310 @@ static inline float fresnel_factor(float eta, float cos_i, float cos_t) {
     return clampf_((rs * rs + rp * rp) * 0.5f, 0, 1);
 }
 
+/* ------------------------------------------------------------------------ */
+/* BSDFs: the Artic Bsdf records {eval, pdf, sample, is_specular} built per  */
+/* hit (bsdf/diffuse.art, dielectric.art, conductor.art, plastic.art, mix.art */
+/* and core/microfacet.art), restated as one record + lobe functions.        */
+/* ------------------------------------------------------------------------ */
+enum { LOBE_LAMBERT, LOBE_OREN_NAYAR, LOBE_DIELECTRIC, LOBE_MIRROR, LOBE_PURE_CONDUCTOR, LOBE_ROUGH_CONDUCTOR };
+
+typedef struct {
+    int lobe;          /* primary lobe; plastic = mix(LAMBERT+scatter, spec) */
+    int plastic;
+    int spec;          /* plastic specular lobe: LOBE_MIRROR or LOBE_ROUGH_CONDUCTOR */
+    int model;         /* IGX_MICROFACET_* for rough lobes */
+    float au, av, on_alpha;
+    v3 kd, ks, kt, eta, kap;
+    float n1, n2;
+    const osurf* surf;
+} obsdf;
+
+typedef struct { v3 dir; float pdf; v3 color; float eta; int ok; } osample;
+
+static inline osample osample_make(v3 d, float pdf, v3 c, float eta) { osample r = {d, pdf, c, eta, 1}; return r; }
+static inline osample osample_reject(void) { osample r = {V(0, 0, 0), 0, V(0, 0, 0), 1, 0}; return r; }
+static inline float pos_cos(v3 a, v3 b) { float c = vdot(a, b); return c >= 0 ? c : 0; }
+static inline float abs_cos(v3 a, v3 b) { return fabsf(vdot(a, b)); }
+static inline v3 vreflect(v3 v, v3 n) { return vsub(vmulf(n, 2 * vdot(n, v)), v); }
+static inline v3 vhalf(v3 a, v3 b) { return vnormalize(vadd(a, b)); }
+static inline float lerp1(float a, float b, float k) { return (1 - k) * a + k * b; }
+static inline v3 clerp(v3 a, v3 b, float t) { return V((1 - t) * a.x + t * b.x, (1 - t) * a.y + t * b.y, (1 - t) * a.z + t * b.z); }
+static inline float diff_of_prod(float a, float b, float c, float d) {
+    float cd = c * d;
+    return fmaf(a, b, -cd) + fmaf(-c, d, cd);
+}
+/* core/fresnel.art */
+static float fresnel_dielectric_f(float eta, float cos_i) {
+    float eta2 = cos_i < 0 ? 1 / eta : eta;
+    float c2 = 1 - (1 - cos_i * cos_i) * eta2 * eta2;
+    return c2 <= 0.0f ? 1.0f : fresnel_factor(eta2, fabsf(cos_i), sqrtf(c2));
+}
+static float conductor_f(float n, float k, float ci) {
+    float f = n * n + k * k, d1 = f * ci * ci, d2 = 2.0f * n * ci;
+    float rs = safe_div(d1 - d2, d1 + d2), rp = safe_div(f - d2 + ci * ci, f + d2 + ci * ci);
+    return clampf_((rs * rs + rp * rp) * 0.5f, 0, 1);
+}
+static float diffuse_fresnel(float eta) {
+    if (eta < 1) return -1.4399f * (eta * eta) + 0.7099f * eta + 0.6681f + 0.0636f / eta;
+    float a = 1 / eta, b = a * a, c = b * a, d = c * a, e = d * a;
+    return 0.919317f - 3.4793f * a + 6.75335f * b - 7.80989f * c + 4.98554f * d - 1.36881f * e;
+}
+/* core/microfacet.art */
+static float d_ggx(const frame_t* l, v3 m, float au, float av) {
+    float z = vdot(l->n, m), x = vdot(l->t, m), y = vdot(l->b, m);
+    float kx = x / au, ky = y / av, k = kx * kx + ky * ky + z * z;
+    return safe_div(1, PI_ * au * av * k * k);
+}
+static float d_beckmann(const frame_t* l, v3 m, float au, float av) {
+    float z = vdot(l->n, m), x = vdot(l->t, m), y = vdot(l->b, m);
+    float kx = x / au, ky = y / av;
+    float k2 = safe_div(kx * kx + ky * ky, z * z);
+    return safe_div(expf(-k2), PI_ * au * av * z * z * z * z);
+}
+static float g1_smith_f(const frame_t* l, v3 w, float au, float av) {
+    float z = vdot(l->n, w);
+    if (fabsf(z) <= FLT_EPS_) return 0;
+    float kx = au * vdot(l->t, w), ky = av * vdot(l->b, w), a2 = kx * kx + ky * ky;
+    if (a2 <= FLT_EPS_) return 1;
+    return 2 / (1 + sqrtf(1 + a2 / (z * z)));
+}
+static float g1_walter_f(const frame_t* l, v3 w, float au, float av) {
+    float z = vdot(l->n, w);
+    if (fabsf(z) <= FLT_EPS_) return 0;
+    float kx = au * vdot(l->t, w), ky = av * vdot(l->b, w);
+    float k2 = (kx * kx + ky * ky) / (z * z);
+    if (k2 <= FLT_EPS_) return 1;
+    float a = 1 / sqrtf(k2), a2 = 1 / k2;
+    if (a >= 1.6f) return 1.0f;
+    return (3.535f * a + 2.181f * a2) / (1.0f + 2.276f * a + 2.577f * a2);
+}
+static float mf_d(const obsdf* b, v3 h) {
+    return b->model == IGX_MICROFACET_BECKMANN ? d_beckmann(&b->surf->local, h, b->au, b->av) : d_ggx(&b->surf->local, h, b->au, b->av);
+}
+static float mf_g(const obsdf* b, v3 wi, v3 wo) {
+    const frame_t* l = &b->surf->local;
+    if (b->model == IGX_MICROFACET_BECKMANN) return g1_walter_f(l, wi, b->au, b->av) * g1_walter_f(l, wo, b->au, b->av);
+    return g1_smith_f(l, wi, b->au, b->av) * g1_smith_f(l, wo, b->au, b->av);
+}
+static float vndf_pdf(const frame_t* l, v3 w, v3 h, float au, float av) {
+    return safe_div(g1_smith_f(l, w, au, av) * abs_cos(w, h) * d_ggx(l, h, au, av), abs_cos(l->n, w));
+}
+static float mf_pdf(const obsdf* b, v3 wo, v3 h) {
+    if (b->model == IGX_MICROFACET_VNDF_GGX) return vndf_pdf(&b->surf->local, wo, h, b->au, b->av);
+    return mf_d(b, h) * abs_cos(b->surf->local.n, h);
+}
+static v3 mf_sample(const obsdf* b, rng_t* r, v3 wo, float* pdf) {
+    const frame_t* l = &b->surf->local;
+    const float au = b->au, av = b->av;
+    if (b->model == IGX_MICROFACET_VNDF_GGX) {
+        /* Heitz 2018 (sample_vndf_ggx / sample_vndf_ggx_11) */
+        v3 vl = V(vdot(l->t, wo), vdot(l->b, wo), vdot(l->n, wo));
+        v3 sl = vnormalize(V(au * vl.x, av * vl.y, vl.z));
+        float st = safe_sqrt(1 - sl.z * sl.z);
+        float sphi = 0, cphi = 1;
+        if (fabsf(st) > FLT_EPS_) { sphi = sl.y / st; cphi = sl.x / st; }
+        float ct = fabsf(sl.z);
+        float u0 = rng_f32(r), u1 = rng_f32(r);
+        float a = 2 * u0 - 1, c = 2 * u1 - 1, px, py;
+        if (a == 0 && c == 0) { px = 0; py = 0; }
+        else if (a * a > c * c) { float phi = (PI_ / 4) * safe_div(c, a); px = cosf(phi) * a; py = sinf(phi) * a; }
+        else { float phi = (PI_ / 2) - (PI_ / 4) * safe_div(a, c); px = cosf(phi) * c; py = sinf(phi) * c; }
+        float sv = 0.5f * (1 + ct);
+        float y = (1 - sv) * safe_sqrt(1 - px * px) + sv * py;
+        float z = safe_sqrt(1 - y * y - px * px);
+        float sin_t = safe_sqrt(1 - ct * ct);
+        float norm = safe_div(1, sum_of_prod(sin_t, y, ct, z));
+        float sx = diff_of_prod(ct, y, sin_t, z) * norm, sy = px * norm;
+        float tx = (cphi * sx - sphi * sy) * au, ty = (sphi * sx + cphi * sy) * av;
+        v3 nh = isfinite(tx) ? vnormalize(V(-tx, -ty, 1)) : V(0, 0, 0);
+        v3 h = frame_to_world(l, nh);
+        *pdf = vndf_pdf(l, wo, h, au, av);
+        return h;
+    }
+    float u0 = rng_f32(r), u1 = rng_f32(r), ar = av / au;
+    if (b->model == IGX_MICROFACET_BECKMANN) {
+        float phi = atanf(ar * tanf(2 * PI_ * u1));
+        float cp = cosf(phi), sp = sqrtf(1 - cp * cp);
+        float kx = cp / au, ky = sp / av, k2 = 1 / (kx * kx + ky * ky);
+        float cth = 1 / sqrtf(1 - k2 * logf(1.0f - u0)), c2 = cth * cth, sth = sqrtf(1 - c2);
+        *pdf = (1 - u0) / (PI_ * au * av * c2 * cth);
+        return frame_to_world(l, V(sth * cp, sth * sp, cth));
+    }
+    float phi = au == av ? 2 * PI_ * u1 : atanf(ar * tanf(2 * PI_ * u1));
+    float cp = cosf(phi), sp = sqrtf(1 - cp * cp);
+    float kx = cp / au, ky = sp / av, d2 = kx * kx + ky * ky;
+    float t2 = safe_div(1, d2) * u0 / (1 - u0);
+    float cth = 1 / sqrtf(1 + t2), c2 = cth * cth, sth = sqrtf(1 - c2);
+    float k2 = d2 * (sth * sth) / c2;
+    *pdf = safe_div(1, PI_ * au * av * c2 * cth * (1 + k2) * (1 + k2));
+    return frame_to_world(l, V(sth * cp, sth * sp, cth));
+}
+
+static obsdf obsdf_make(const igx_material* m, const osurf* surf) {
+    obsdf b;
+    memset(&b, 0, sizeof(b));
+    b.surf = surf;
+    b.kd = V(m->kd[0], m->kd[1], m->kd[2]);
+    b.ks = V(m->ks[0], m->ks[1], m->ks[2]);
+    b.kt = V(m->kt[0], m->kt[1], m->kt[2]);
+    b.eta = V(m->eta[0], m->eta[1], m->eta[2]);
+    b.kap = V(m->kappa[0], m->kappa[1], m->kappa[2]);
+    b.n1 = m->ext_ior;
+    b.n2 = m->int_ior;
+    b.au = m->alpha_u;
+    b.av = m->alpha_v;
+    b.on_alpha = m->diffuse_alpha;
+    /* check_if_delta_distribution: alpha <= 1e-4 */
+    int rough = m->distribution != IGX_MICROFACET_DELTA && m->alpha_u > 1e-4f && m->alpha_v > 1e-4f;
+    b.model = rough ? m->distribution : IGX_MICROFACET_DELTA;
+    switch (m->bsdf_type) {
+    case IGX_BSDF_DIELECTRIC: b.lobe = LOBE_DIELECTRIC; break;
+    case IGX_BSDF_CONDUCTOR:
+        if (rough) b.lobe = LOBE_ROUGH_CONDUCTOR;
+        else {
+            int mirror = fabsf(b.eta.x) <= 1e-4f && fabsf(b.eta.y) <= 1e-4f && fabsf(b.eta.z) <= 1e-4f &&
+                         fabsf(b.kap.x - 1) <= 1e-4f && fabsf(b.kap.y - 1) <= 1e-4f && fabsf(b.kap.z - 1) <= 1e-4f;
+            b.lobe = mirror ? LOBE_MIRROR : LOBE_PURE_CONDUCTOR;
+        }
+        break;
+    case IGX_BSDF_PLASTIC:
+        b.plastic = 1;
+        b.lobe = LOBE_LAMBERT;
+        b.spec = rough ? LOBE_ROUGH_CONDUCTOR : LOBE_MIRROR;
+        b.eta = V(0, 0, 0);
+        b.kap = V(1, 1, 1);
+        break;
+    default: b.lobe = m->diffuse_alpha <= FLT_EPS_ ? LOBE_LAMBERT : LOBE_OREN_NAYAR; break;
+    }
+    return b;
+}
+static int obsdf_specular(const obsdf* b) {
+    return !b->plastic && (b->lobe == LOBE_DIELECTRIC || b->lobe == LOBE_MIRROR || b->lobe == LOBE_PURE_CONDUCTOR);
+}
+static int lobe_specular(int lobe) { return lobe == LOBE_DIELECTRIC || lobe == LOBE_MIRROR || lobe == LOBE_PURE_CONDUCTOR; }
+
+static v3 rough_eval(const obsdf* b, v3 in, v3 out) {
+    v3 N = b->surf->local.n;
+    float co = abs_cos(out, N), ci = abs_cos(in, N);
+    if (co <= FLT_EPS_ || ci <= FLT_EPS_) return V(0, 0, 0);
+    v3 h = vhalf(in, out);
+    float D = mf_d(b, h), G = mf_g(b, in, out), ch = abs_cos(out, h);
+    v3 F = V(conductor_f(b->eta.x, b->kap.x, ch), conductor_f(b->eta.y, b->kap.y, ch), conductor_f(b->eta.z, b->kap.z, ch));
+    return vmulf(vmul(b->ks, F), D * G / (4 * co));
+}
+static float rough_pdf(const obsdf* b, v3 in, v3 out) {
+    v3 h = vhalf(in, out);
+    return mf_pdf(b, out, h) * safe_div(1, 4 * abs_cos(out, h));
+}
+/* eval / pdf / sample of one lobe (plastic's diffuse lobe carries the inner scattering term) */
+static float plastic_scatter_f(const obsdf* b, float ci) {
+    float eta = b->n1 / b->n2;
+    return (1 - fresnel_dielectric_f(eta, ci)) * eta * eta / (1 - diffuse_fresnel(eta));
+}
+static v3 lobe_eval(const obsdf* b, int lobe, v3 in, v3 out) {
+    v3 N = b->surf->local.n;
+    switch (lobe) {
+    case LOBE_LAMBERT: {
+        v3 e = vmulf(b->kd, abs_cos(in, N) * INV_PI_);
+        return b->plastic ? vmulf(e, plastic_scatter_f(b, abs_cos(in, N))) : e;
+    }
+    case LOBE_OREN_NAYAR: {
+        float a2 = b->on_alpha * b->on_alpha;
+        float p1 = abs_cos(in, N), p2 = abs_cos(out, N);
+        float sv = -p1 * p2 + pos_cos(out, in);
+        float t = sv <= FLT_EPS_ ? 1.0f : fmaxf(FLT_EPS_, fmaxf(p1, p2));
+        float A = 1 - 0.5f * a2 / (a2 + 0.33f), B = 0.45f * a2 / (a2 + 0.09f), C = 0.17f * a2 / (a2 + 0.13f);
+        return vmulf(vadd(vmulf(b->kd, (A + (B * sv / t)) / PI_), vmul(b->kd, vmulf(b->kd, C / PI_))), p1);
+    }
+    case LOBE_ROUGH_CONDUCTOR: return rough_eval(b, in, out);
+    default: return V(0, 0, 0);
+    }
+}
+static float lobe_pdf(const obsdf* b, int lobe, v3 in, v3 out) {
+    if (lobe == LOBE_LAMBERT || lobe == LOBE_OREN_NAYAR) return pos_cos(in, b->surf->local.n) / PI_;
+    if (lobe == LOBE_ROUGH_CONDUCTOR) return rough_pdf(b, in, out);
+    return 0;
+}
+static osample lobe_sample(const obsdf* b, int lobe, rng_t* r, v3 out) {
+    const osurf* sf = b->surf;
+    v3 N = sf->local.n;
+    switch (lobe) {
+    case LOBE_LAMBERT:
+    case LOBE_OREN_NAYAR: {
+        float u = rng_f32(r), v = rng_f32(r);
+        float c = safe_sqrt(v), sn = safe_sqrt(1 - v), phi = 2 * PI_ * u;
+        float pdf = c / PI_;
+        v3 d = frame_to_world(&sf->local, V(sn * cosf(phi), sn * sinf(phi), c));
+        if (lobe == LOBE_OREN_NAYAR) return osample_make(d, pdf, vmulf(lobe_eval(b, lobe, d, out), 1 / pdf), 1);
+        v3 col = b->plastic ? vmulf(b->kd, plastic_scatter_f(b, abs_cos(d, N))) : b->kd;
+        return osample_make(d, pdf, col, 1);
+    }
+    case LOBE_DIELECTRIC: {
+        float k = sf->entering ? b->n1 / b->n2 : b->n2 / b->n1;
+        float co = vdot(out, N);
+        float ft_cos_t = 0, ft_factor = 1;
+        float eta2 = co < 0 ? 1 / k : k;
+        float c2 = 1 - (1 - co * co) * eta2 * eta2;
+        if (!(c2 <= 0.0f)) {
+            float ct = sqrtf(c2);
+            ft_cos_t = co < 0 ? -ct : ct;
+            ft_factor = fresnel_factor(eta2, fabsf(co), ct);
+        }
+        if (rng_f32(r) > ft_factor) return osample_make(vsub(vmulf(N, k * co - ft_cos_t), vmulf(out, k)), 1, b->kt, k);
+        return osample_make(vreflect(out, N), 1, b->ks, 1);
+    }
+    case LOBE_MIRROR: return osample_make(vreflect(out, N), 1, b->ks, 1);
+    case LOBE_PURE_CONDUCTOR: {
+        float ci = vdot(out, N);
+        v3 F = V(conductor_f(b->eta.x, b->kap.x, ci), conductor_f(b->eta.y, b->kap.y, ci), conductor_f(b->eta.z, b->kap.z, ci));
+        return osample_make(vreflect(out, N), 1, vmul(b->ks, F), 1);
+    }
+    default: { /* rough conductor */
+        if (abs_cos(out, N) <= FLT_EPS_) return osample_reject();
+        float mpdf;
+        v3 mn = mf_sample(b, r, out, &mpdf);
+        if (vdot(mn, mn) <= FLT_EPS_) return osample_reject();
+        v3 oh = vnormalize(mn);
+        v3 h = signbit(vdot(oh, out)) ? vneg(oh) : oh;
+        v3 in = vreflect(out, h);
+        if (abs_cos(in, N) <= FLT_EPS_) return osample_reject();
+        float pdf = mpdf * (1 / (4 * abs_cos(out, h)));
+        return osample_make(in, pdf, vmulf(rough_eval(b, in, out), safe_div(1, pdf)), 1);
+    }
+    }
+}
+/* make_variadic_mix_bsdf (bsdf/mix.art) with k = Fresnel(out) for plastic */
+static float plastic_k(const obsdf* b, v3 out) { return fresnel_dielectric_f(b->n1 / b->n2, abs_cos(out, b->surf->local.n)); }
+static v3 obsdf_eval(const obsdf* b, v3 in, v3 out) {
+    if (!b->plastic) return lobe_eval(b, b->lobe, in, out);
+    return clerp(lobe_eval(b, LOBE_LAMBERT, in, out), lobe_eval(b, b->spec, in, out), plastic_k(b, out));
+}
+static float obsdf_pdf(const obsdf* b, v3 in, v3 out) {
+    if (!b->plastic) return lobe_pdf(b, b->lobe, in, out);
+    return lerp1(lobe_pdf(b, LOBE_LAMBERT, in, out), lobe_pdf(b, b->spec, in, out), plastic_k(b, out));
+}
+static osample mix_sample_first(const obsdf* b, int first, int second, rng_t* r, v3 out, float t) {
+    osample s1 = lobe_sample(b, first, r, out);
+    if (!s1.ok || lobe_specular(second)) return s1;
+    float p = lerp1(s1.pdf, lobe_pdf(b, second, s1.dir, out), t);
+    v3 c = clerp(vmulf(s1.color, s1.pdf), lobe_eval(b, second, s1.dir, out), t);
+    s1.pdf = p;
+    s1.color = V(c.x / p, c.y / p, c.z / p);
+    return s1;
+}
+static osample obsdf_sample(const obsdf* b, rng_t* r, v3 out) {
+    if (!b->plastic) return lobe_sample(b, b->lobe, r, out);
+    float k = plastic_k(b, out);
+    if (k <= 0) return lobe_sample(b, LOBE_LAMBERT, r, out);
+    if (k >= 1) return lobe_sample(b, b->spec, r, out);
+    if (rng_f32(r) < 1 - k) {
+        osample s1 = mix_sample_first(b, LOBE_LAMBERT, b->spec, r, out, k);
+        return s1.ok ? s1 : lobe_sample(b, b->spec, r, out);
+    }
+    osample s1 = mix_sample_first(b, b->spec, LOBE_LAMBERT, r, out, 1 - k);
+    return s1.ok ? s1 : lobe_sample(b, LOBE_LAMBERT, r, out);
+}
+
 static inline v3 handle_color(const oracle_scene* s, v3 c) {
     float cl = s->desc.technique.clamp;
     if (cl > 0) return V(fminf(c.x, cl), fminf(c.y, cl), fminf(c.z, cl));
@@ -865,7 +1169,8 @@ static v3 trace_path(const oracle_scene* s, const oracle_params* p, int x, int y
         Lsum = vadd(Lsum, Lacc);
         rng_t r2 = {seed, counter};
         v3 out_dir = vneg(ray.dir);
-        int specular = mat->bsdf_type == IGX_BSDF_DIELECTRIC;
+        obsdf bs = obsdf_make(mat, &surf);
+        int specular = obsdf_specular(&bs);
         /* on_shadow */
         if (tech->nee && !specular && s->num_lights > 0 && depth + 1 <= tech->max_depth) {
             int lid = s->num_lights <= 1 ? 0 : rng_i32(&r2, 0, s->num_lights - 1);
@@ -873,16 +1178,9 @@ static v3 trace_path(const oracle_scene* s, const oracle_params* p, int x, int y
             odirect ls = light_sample_direct(s, L, &r2, &surf);
             float pdf_l_s = (ls.pdf_solid ? ls.pdf_value : ls.pdf_value * (ls.dist * ls.dist) / ls.cos) * sel_pdf;
             if (pdf_l_s > FLT_EPS_ && ls.cos > FLT_EPS_) {
-                v3 kd = V(mat->kd[0], mat->kd[1], mat->kd[2]);
-                float mis;
-                if (L->delta) mis = 1.0f;
-                else {
-                    float c = vdot(ls.dir, surf.local.n);
-                    float pdf_e_s = (c >= 0 ? c : 0) / PI_;
-                    mis = 1 / (1 + pdf_e_s / pdf_l_s);
-                }
+                float mis = L->delta ? 1.0f : 1 / (1 + obsdf_pdf(&bs, ls.dir, out_dir) / pdf_l_s);
                 float factor = ls.pdf_value / pdf_l_s;
-                v3 ev = vmulf(kd, fabsf(vdot(ls.dir, surf.local.n)) * INV_PI_);
+                v3 ev = obsdf_eval(&bs, ls.dir, out_dir);
                 v3 scol = handle_color(s, vmulf(vmul(ls.intensity, vmul(contrib, ev)), mis * factor));
                 oray sr = L->infinite ? make_ray(surf.point, ls.dir, 0.001f, FLT_MAX_, RAY_SHADOW)
                                       : make_ray(surf.point, vsub(ls.pos, surf.point), 0.001f, 1 - 0.001f, RAY_SHADOW);
@@ -893,40 +1191,10 @@ static v3 trace_path(const oracle_scene* s, const oracle_params* p, int x, int y
         }
         /* on_bounce */
         if (!(depth + 1 <= tech->max_depth)) break;
-        v3 in_dir, bcol;
-        float bpdf, beta;
-        if (!specular) {
-            float u = rng_f32(&r2);
-            float v = rng_f32(&r2);
-            float c = safe_sqrt(v), sn = safe_sqrt(1 - v), phi = 2 * PI_ * u;
-            bpdf = c / PI_;
-            in_dir = frame_to_world(&surf.local, V(sn * cosf(phi), sn * sinf(phi), c));
-            bcol = V(mat->kd[0], mat->kd[1], mat->kd[2]);
-            beta = 1;
-        } else {
-            float n1 = mat->ext_ior, n2 = mat->int_ior;
-            float k = surf.entering ? n1 / n2 : n2 / n1;
-            v3 n = surf.local.n;
-            float cos_o = vdot(out_dir, n);
-            float ft_cos_t = 0, ft_factor = 1;
-            float eta2 = cos_o < 0 ? 1 / k : k;
-            float cos2_t = 1 - (1 - cos_o * cos_o) * eta2 * eta2;
-            if (!(cos2_t <= 0.0f)) {
-                float ct = sqrtf(cos2_t);
-                ft_cos_t = cos_o < 0 ? -ct : ct;
-                ft_factor = fresnel_factor(eta2, fabsf(cos_o), ct);
-            }
-            if (rng_f32(&r2) > ft_factor) {
-                in_dir = vsub(vmulf(n, k * cos_o - ft_cos_t), vmulf(out_dir, k));
-                bcol = V(mat->kt[0], mat->kt[1], mat->kt[2]);
-                beta = k;
-            } else {
-                in_dir = vsub(vmulf(n, 2 * vdot(n, out_dir)), out_dir);
-                bcol = V(mat->ks[0], mat->ks[1], mat->ks[2]);
-                beta = 1;
-            }
-            bpdf = 1;
-        }
+        osample smp = obsdf_sample(&bs, &r2, out_dir);
+        if (!smp.ok) break;
+        v3 in_dir = smp.dir, bcol = smp.color;
+        float bpdf = smp.pdf, beta = smp.eta;
         v3 c2 = vmul(contrib, bcol);
         float rr = 1.0f;
         if (depth + 1 > tech->min_depth) {
