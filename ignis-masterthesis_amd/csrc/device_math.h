@@ -42,6 +42,7 @@ __device__ __forceinline__ float safe_rcp(float x) {
 // safe_div / safe_sqrt / clampf (core/common.art:167-171)
 __device__ __forceinline__ float safe_div(float a, float b) { return fabsf(b) <= FLT_EPS_ ? 0.0f : a / b; }
 __device__ __forceinline__ float safe_sqrt(float a) { return sqrtf(fmaxf(0.0f, a)); }
+__device__ __forceinline__ float safe_div_one(float a, float b) { return fabsf(b) <= FLT_EPS_ ? 1.0f : a / b; }
 __device__ __forceinline__ float clampf(float v, float l, float u) { return fminf(u, fmaxf(l, v)); }
 // sum_of_prod (core/common.art:148-153)
 __device__ __forceinline__ float sum_of_prod(float a, float b, float c, float d) {

@@ -41,7 +41,7 @@ struct DevMaterial {   // 128 B
     float pad[8];
 };
 
-enum : int32_t { LIGHT_PLANE = 1, LIGHT_ENV = 2, LIGHT_POINT = 3, LIGHT_SPOT = 4 };
+enum : int32_t { LIGHT_PLANE = 1, LIGHT_ENV = 2, LIGHT_POINT = 3, LIGHT_SPOT = 4, LIGHT_DIRECTIONAL = 5, LIGHT_SUN = 6 };
 struct DevLight {      // 128 B
     int32_t type, infinite, delta, pad;
     float radiance[4];
@@ -49,7 +49,7 @@ struct DevLight {      // 128 B
     float ex[4];       // plane x axis normalised; w = plane height
     float ey[4];       // plane y axis normalised; w = inv_area
     float normal[4];   // plane normal / spot direction; w = area
-    float spot[4];     // cos_cutoff, cos_falloff, blend range, 0
+    float spot[4];     // spot: cos_cutoff, cos_falloff, blend range; sun: cos_angle, sun_area
     float pad2[4];
 };
 

@@ -1269,12 +1269,13 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     for (int pass = 0; pass < 2; ++pass)
         for (uint32_t l = 0; l < desc->num_lights; ++l) {
             const igx_light& L = desc->lights[l];
-            bool infinite = L.type == IGX_LIGHT_ENV;
+            bool infinite = L.type == IGX_LIGHT_ENV || L.type == IGX_LIGHT_DIRECTIONAL || L.type == IGX_LIGHT_SUN;
             if ((pass == 0) != infinite) continue;
             DevLight d{};
             d.type = L.type;
             d.infinite = infinite ? 1 : 0;
-            d.delta = (L.type == IGX_LIGHT_POINT || L.type == IGX_LIGHT_SPOT) ? 1 : 0;
+            d.delta = (L.type == IGX_LIGHT_POINT || L.type == IGX_LIGHT_SPOT || L.type == IGX_LIGHT_DIRECTIONAL ||
+                       L.type == IGX_LIGHT_SUN) ? 1 : 0;
             for (int i = 0; i < 3; ++i) d.radiance[i] = L.radiance[i];
             if (L.type == IGX_LIGHT_PLANE) {
                 // make_plane_area_emitter constants (light/area.art:107-115)
@@ -1301,6 +1302,15 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
                 d.spot[0] = cc;
                 d.spot[1] = cf;
                 d.spot[2] = cf - cc;
+            } else if (L.type == IGX_LIGHT_DIRECTIONAL) {
+                for (int i = 0; i < 3; ++i) d.normal[i] = L.normal[i];
+            } else if (L.type == IGX_LIGHT_SUN) {
+                // make_sun_light constants (light/sun.art:4-8)
+                for (int i = 0; i < 3; ++i) d.normal[i] = L.normal[i];
+                float c = L.cutoff;
+                float r = std::sqrt(1 - c * c) / c; // sun_radius_from_cos_angle
+                d.spot[0] = c;
+                d.spot[1] = 3.14159265359f * r * r;
             } else if (L.type != IGX_LIGHT_ENV) {
                 return fail(dev, IGX_ERR_UNSUPPORTED, "unsupported light type");
             }

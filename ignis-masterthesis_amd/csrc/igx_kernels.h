@@ -436,6 +436,22 @@ __device__ __forceinline__ SQ compute_sq(const DevLight& L, f3 from) {
     return q;
 }
 
+// square_to_concentric_disk (core/warp.art:2-22)
+__device__ __forceinline__ void concentric_disk(float u, float v, float& x, float& y) {
+    float a = 2 * u - 1, b = 2 * v - 1;
+    if (a == 0 && b == 0) {
+        x = 0;
+        y = 0;
+    } else if (a * a > b * b) {
+        float phi = (PI_ / 4) * safe_div(b, a);
+        x = cosf(phi) * a;
+        y = sinf(phi) * a;
+    } else {
+        float phi = (PI_ / 2) - (PI_ / 4) * safe_div(a, b);
+        x = cosf(phi) * b;
+        y = sinf(phi) * b;
+    }
+}
 struct DirectSample {
     f3 pos, dir;
     f3 intensity;
@@ -496,6 +512,37 @@ __device__ __forceinline__ DirectSample light_sample_direct(const SceneView& sv,
         ds.pdf_solid = true;
         ds.cos = 1.0f;
         ds.dist = sv.scene_radius;
+    } else if (L.type == LIGHT_DIRECTIONAL) {
+        // make_directional_light.sample_direct (light/directional.art:6): delta pdf, cos 1
+        f3 dir = mk(L.normal[0], L.normal[1], L.normal[2]);
+        ds.pos = add(from.point, mulf(dir, -sv.scene_radius));
+        ds.dir = neg(dir);
+        ds.intensity = rad;
+        ds.pdf_value = 1;
+        ds.pdf_solid = true; // delta: as_solid = 1
+        ds.cos = 1;
+        ds.dist = sv.scene_radius;
+    } else if (L.type == LIGHT_SUN) {
+        // make_sun_light.sample_direct (light/sun.art:10-14) with sample_uniform_cone
+        // (core/sampling.art:106-116) in make_orthonormal_mat3x3(dir)
+        const float cos_angle = L.spot[0], sun_area = L.spot[1];
+        float u = rnd.next_f32();
+        float v = rnd.next_f32();
+        float c1 = 1 - cos_angle;
+        float px, py;
+        concentric_disk(u, v, px, py);
+        float n2 = px * px + py * py;
+        float z = cos_angle + c1 * (1 - n2);
+        float sc = safe_sqrt(c1 * (2 - c1 * n2));
+        float pdf = safe_div_one(1, 2 * PI_ * (1 - cos_angle));
+        f3 ndir = frame_to_world(make_frame(mk(L.normal[0], L.normal[1], L.normal[2])), mk(px * sc, py * sc, z));
+        ds.pos = mk(0, 0, 0);
+        ds.dir = neg(ndir);
+        ds.intensity = mulf(rad, 1 / (sun_area * pdf));
+        ds.pdf_value = 1;
+        ds.pdf_solid = true;
+        ds.cos = z;
+        ds.dist = INFINITY;
     } else if (L.type == LIGHT_POINT) {
         // make_point_light.sample_direct (light/point.art:3-8)
         f3 pos = mk(L.origin[0], L.origin[1], L.origin[2]);
@@ -665,22 +712,6 @@ __device__ __forceinline__ float pdf_vndf_ggx(const Frame& l, f3 w, f3 h, float 
 __device__ __forceinline__ float mf_pdf(const DevMaterial& m, const Frame& l, f3 wo, f3 h) {
     if (m.dist == MF_VNDF_GGX) return pdf_vndf_ggx(l, wo, h, m.eta[3], m.kappa[3]);
     return mf_D(m, l, h) * absolute_cos(l.n, h); // make_microfacet_distribution.pdf (:265)
-}
-// square_to_concentric_disk (core/warp.art:2-22)
-__device__ __forceinline__ void concentric_disk(float u, float v, float& x, float& y) {
-    float a = 2 * u - 1, b = 2 * v - 1;
-    if (a == 0 && b == 0) {
-        x = 0;
-        y = 0;
-    } else if (a * a > b * b) {
-        float phi = (PI_ / 4) * safe_div(b, a);
-        x = cosf(phi) * a;
-        y = sinf(phi) * a;
-    } else {
-        float phi = (PI_ / 2) - (PI_ / 4) * safe_div(a, b);
-        x = cosf(phi) * b;
-        y = sinf(phi) * b;
-    }
 }
 // Microfacet normal sample of the material's distribution for outgoing wo.
 __device__ __forceinline__ f3 mf_sample(const DevMaterial& m, const Frame& l, Rng& rnd, f3 wo, float& pdf) {

@@ -647,6 +647,27 @@ static void build_scene(SceneStore& S, const Value& doc, const std::string& base
                 for (int i = 0; i < 3; ++i) { L.origin[i] = pos[i]; L.normal[i] = dir[i]; L.radiance[i] = I[i]; }
                 L.cutoff = lp.number("cutoff", 30.0f) * kDeg2Rad;
                 L.falloff = lp.number("falloff", 20.0f) * kDeg2Rad;
+            } else if (type == "directional" || type == "sun") {
+                // DirectionalLight.cpp:20-32, SunLight.cpp:24-46; direction via
+                // LoaderUtils::getEA(...).toDirectionYUp() (LoaderUtils.cpp:140-156)
+                V3 dir;
+                if (lp.has("direction") || lp.has("sun_direction")) {
+                    V3 d = igx::normalized(lp.vec3(lp.has("direction") ? "direction" : "sun_direction", V3(0, 0, 1)));
+                    float theta = std::acos(d.y), phi = std::atan2(d.x, -d.z); // ElevationAzimuth::fromDirectionYUp
+                    float el = 1.57079632679f - theta, az = phi < 0 ? phi + 6.28318530718f : phi;
+                    dir = V3(std::cos(el) * std::sin(az), std::sin(el), -std::cos(el) * std::cos(az));
+                } else if (lp.has("elevation") || lp.has("azimuth")) {
+                    float el = lp.number("elevation", 0.0f), az = lp.number("azimuth", 0.0f);
+                    dir = V3(std::cos(el) * std::sin(az), std::sin(el), -std::cos(el) * std::cos(az));
+                } else {
+                    fail("light '" + name + "': give 'direction', 'sun_direction' or 'elevation'/'azimuth' (time/location sun positions are not supported)");
+                }
+                V3 E = lp.color("irradiance", V3(1, 1, 1));
+                L.type = type == "sun" ? IGX_LIGHT_SUN : IGX_LIGHT_DIRECTIONAL;
+                for (int i = 0; i < 3; ++i) { L.normal[i] = dir[i]; L.radiance[i] = E[i]; }
+                if (type == "sun")
+                    L.cutoff = lp.has("radius") ? 1 / std::sqrt(lp.number("radius", 1.0f) * lp.number("radius", 1.0f) + 1) // sun_cos_angle_from_radius
+                                                : std::cos(lp.number("angle", 11.4f) * kDeg2Rad / 2);
             } else {
                 fail("light '" + name + "': unsupported light type '" + type + "'");
             }

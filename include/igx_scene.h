@@ -96,19 +96,21 @@ enum {
     IGX_LIGHT_PLANE = 1, /* area light on a planar entity: make_plane_area_emitter (light/area.art:107-240) */
     IGX_LIGHT_ENV   = 2, /* constant environment, spherical sampling (light/env.art:73-98) */
     IGX_LIGHT_POINT = 3, /* light/point.art:1-18 */
-    IGX_LIGHT_SPOT  = 4  /* light/spot.art:8-60 */
+    IGX_LIGHT_SPOT  = 4, /* light/spot.art:8-60 */
+    IGX_LIGHT_DIRECTIONAL = 5, /* light/directional.art:1-19 */
+    IGX_LIGHT_SUN   = 6  /* light/sun.art:4-30 (delta, infinite) */
 };
 
 typedef struct igx_light {
     int32_t type;
     int32_t entity;        /* area lights: emitting entity, -1 otherwise */
-    float radiance[3];     /* radiance (area/env) or intensity (point/spot) */
+    float radiance[3];     /* radiance (area/env), intensity (point/spot), irradiance (directional/sun) */
     float origin[3];       /* plane origin / point position / spot position */
     float x_axis[3];       /* plane */
     float y_axis[3];       /* plane */
-    float normal[3];       /* plane normal, spot direction */
+    float normal[3];       /* plane normal, spot / directional / sun propagation direction */
     float area;            /* plane area */
-    float cutoff, falloff; /* spot, radians */
+    float cutoff, falloff; /* spot, radians; sun: cutoff = cosine of the sun's half angle */
 } igx_light;
 
 /* ---- camera / technique ------------------------------------------------ */

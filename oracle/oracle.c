@@ -153,6 +153,7 @@ typedef struct {
     float origin[3], ex[3], ey[3], normal[3];
     float width, height, area;
     float cos_cut, blend;
+    float sun_cos, sun_area; /* make_sun_light (light/sun.art:4-8) */
 } olight;
 
 struct oracle_scene {
@@ -322,12 +323,13 @@ oracle_scene* oracle_scene_create(const igx_scene_desc* desc) {
     for (int pass = 0; pass < 2; ++pass)
         for (uint32_t l = 0; l < desc->num_lights; ++l) {
             const igx_light* L = &desc->lights[l];
-            int inf = L->type == IGX_LIGHT_ENV;
+            int inf = L->type == IGX_LIGHT_ENV || L->type == IGX_LIGHT_DIRECTIONAL || L->type == IGX_LIGHT_SUN;
             if ((pass == 0) != inf) continue;
             olight* o = &s->lights[k];
             o->type = L->type;
             o->infinite = inf;
-            o->delta = L->type == IGX_LIGHT_POINT || L->type == IGX_LIGHT_SPOT;
+            o->delta = L->type == IGX_LIGHT_POINT || L->type == IGX_LIGHT_SPOT || L->type == IGX_LIGHT_DIRECTIONAL ||
+                       L->type == IGX_LIGHT_SUN;
             memcpy(o->rad, L->radiance, sizeof(o->rad));
             memcpy(o->origin, L->origin, sizeof(o->origin));
             memcpy(o->normal, L->normal, sizeof(o->normal));
@@ -341,6 +343,10 @@ oracle_scene* oracle_scene_create(const igx_scene_desc* desc) {
                 o->ex[0] = ex.x; o->ex[1] = ex.y; o->ex[2] = ex.z;
                 o->ey[0] = ey.x; o->ey[1] = ey.y; o->ey[2] = ey.z;
                 o->area = L->area;
+            } else if (L->type == IGX_LIGHT_SUN) {
+                float c = L->cutoff, r = sqrtf(1 - c * c) / c;
+                o->sun_cos = c;
+                o->sun_area = PI_ * r * r;
             } else if (L->type == IGX_LIGHT_SPOT) {
                 float cc = cosf(L->cutoff), cf = cosf(L->falloff);
                 o->cos_cut = cc;
@@ -740,6 +746,38 @@ static odirect light_sample_direct(const oracle_scene* s, const olight* L, rng_t
         d.pdf_solid = 1;
         d.cos = 1.0f;
         d.dist = s->scene_radius;
+    } else if (L->type == IGX_LIGHT_DIRECTIONAL) {
+        /* light/directional.art:6 */
+        v3 dir = V(L->normal[0], L->normal[1], L->normal[2]);
+        d.pos = vadd(from->point, vmulf(dir, -s->scene_radius));
+        d.dir = vneg(dir);
+        d.intensity = rad;
+        d.pdf_value = 1;
+        d.pdf_solid = 1; /* delta pdf: as_solid = 1 */
+        d.cos = 1;
+        d.dist = s->scene_radius;
+    } else if (L->type == IGX_LIGHT_SUN) {
+        /* light/sun.art:10-14, sample_uniform_cone (core/sampling.art:106-116) */
+        float u = rng_f32(rnd), v = rng_f32(rnd);
+        float c1 = 1 - L->sun_cos;
+        float a = 2 * u - 1, b = 2 * v - 1, px, py;
+        if (a == 0 && b == 0) { px = 0; py = 0; }
+        else if (a * a > b * b) { float phi = (PI_ / 4) * safe_div(b, a); px = cosf(phi) * a; py = sinf(phi) * a; }
+        else { float phi = (PI_ / 2) - (PI_ / 4) * safe_div(a, b); px = cosf(phi) * b; py = sinf(phi) * b; }
+        float n2 = px * px + py * py;
+        float z = L->sun_cos + c1 * (1 - n2);
+        float sc = safe_sqrt(c1 * (2 - c1 * n2));
+        float den = 2 * PI_ * (1 - L->sun_cos);
+        float pdf = fabsf(den) <= FLT_EPS_ ? 1.0f : 1 / den;
+        frame_t fr = make_frame(V(L->normal[0], L->normal[1], L->normal[2]));
+        v3 nd = frame_to_world(&fr, V(px * sc, py * sc, z));
+        d.pos = V(0, 0, 0);
+        d.dir = vneg(nd);
+        d.intensity = vmulf(rad, 1 / (L->sun_area * pdf));
+        d.pdf_value = 1;
+        d.pdf_solid = 1;
+        d.cos = z;
+        d.dist = INFINITY;
     } else if (L->type == IGX_LIGHT_POINT) {
         v3 pos = V(L->origin[0], L->origin[1], L->origin[2]);
         v3 dir_ = vsub(pos, from->point);

@@ -50,3 +50,5 @@ POINT_LIGHT = {"type": "point", "name": "_light", "position": [0, 0, -2], "inten
 SPOT_LIGHT = {"type": "spot", "name": "_light", "cutoff": 45, "falloff": 45, "position": [0, 0, -2],
               "direction": [0, 0, 1], "intensity": [1, 1, 1]}
 ENV_LIGHT = {"type": "env", "name": "_light", "radiance": [1, 1, 1]}
+DIRECTIONAL_LIGHT = {"type": "directional", "name": "_light", "direction": [0, 0, 1], "irradiance": [1, 1, 1]}
+SUN_LIGHT = {"type": "sun", "name": "_light", "direction": [0, 0, 1], "irradiance": [1, 1, 1]}

@@ -19,7 +19,7 @@ import pytest
 
 import ignis_amd
 from oracle import oracle_py as O
-from conftest import ENV_LIGHT, POINT_LIGHT, SPOT_LIGHT, flat_scene
+from conftest import DIRECTIONAL_LIGHT, ENV_LIGHT, POINT_LIGHT, SPOT_LIGHT, SUN_LIGHT, flat_scene
 
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
@@ -184,7 +184,8 @@ def test_full_size_window_parity(device, diamond_path):
 ANALYTIC = json.load(open(os.path.join(GOLDEN, "analytic_kats.json")))["cases"]
 
 
-@pytest.mark.parametrize("name,light", [("no_light", None), ("point", POINT_LIGHT), ("spot", SPOT_LIGHT), ("env", ENV_LIGHT)])
+@pytest.mark.parametrize("name,light", [("no_light", None), ("point", POINT_LIGHT), ("spot", SPOT_LIGHT), ("env", ENV_LIGHT),
+                                        ("directional", DIRECTIONAL_LIGHT), ("sun", SUN_LIGHT)])
 def test_analytic_known_answers(device, name, light):
     """test_lights.py / test_init.py at the reference's 1000^2 film, values re-derived (tests/golden)."""
     sc = ignis_amd.Scene.from_string(flat_scene([light] if light else []))

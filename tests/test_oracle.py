@@ -8,7 +8,7 @@ import pytest
 
 import ignis_amd
 from oracle import oracle_py as O
-from conftest import ENV_LIGHT, POINT_LIGHT, SPOT_LIGHT, flat_scene
+from conftest import DIRECTIONAL_LIGHT, ENV_LIGHT, POINT_LIGHT, SPOT_LIGHT, SUN_LIGHT, flat_scene
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
@@ -93,7 +93,8 @@ def _oracle_mean(scene_dict, size=200, spi=8):
 ANALYTIC = load_golden("analytic_kats.json")["cases"]
 
 
-@pytest.mark.parametrize("name,light", [("no_light", None), ("point", POINT_LIGHT), ("spot", SPOT_LIGHT), ("env", ENV_LIGHT)])
+@pytest.mark.parametrize("name,light", [("no_light", None), ("point", POINT_LIGHT), ("spot", SPOT_LIGHT), ("env", ENV_LIGHT),
+                                        ("directional", DIRECTIONAL_LIGHT), ("sun", SUN_LIGHT)])
 def test_oracle_analytic(name, light):
     mean, se, _ = _oracle_mean(flat_scene([light] if light else []))
     expected = ANALYTIC[name]["value"]
