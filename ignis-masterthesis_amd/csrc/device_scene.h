@@ -41,15 +41,17 @@ struct DevMaterial {   // 128 B
     float pad[8];
 };
 
-enum : int32_t { LIGHT_PLANE = 1, LIGHT_ENV = 2, LIGHT_POINT = 3, LIGHT_SPOT = 4, LIGHT_DIRECTIONAL = 5, LIGHT_SUN = 6 };
+enum : int32_t { LIGHT_PLANE = 1, LIGHT_ENV = 2, LIGHT_POINT = 3, LIGHT_SPOT = 4, LIGHT_DIRECTIONAL = 5, LIGHT_SUN = 6,
+                   LIGHT_SPHERE = 7, LIGHT_MESH = 8 };
 struct DevLight {      // 128 B
-    int32_t type, infinite, delta, pad;
+    int32_t type, infinite, delta, entity; // entity: emitting entity of sphere / mesh area lights
     float radiance[4];
-    float origin[4];   // plane origin / point/spot position; w = plane width
+    float origin[4];   // plane origin / point/spot position; w = plane width; sphere: object-space centre, radius
     float ex[4];       // plane x axis normalised; w = plane height
     float ey[4];       // plane y axis normalised; w = inv_area
     float normal[4];   // plane normal / spot direction; w = area
-    float spot[4];     // spot: cos_cutoff, cos_falloff, blend range; sun: cos_angle, sun_area
+    float spot[4];     // spot: cos_cutoff, cos_falloff, blend range; sun: cos_angle, sun_area;
+                       // sphere: emitter area (compute_ellipsoid_area); mesh: face count
     float pad2[4];
 };
 

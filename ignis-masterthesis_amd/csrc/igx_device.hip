@@ -254,7 +254,7 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
         if (dt > FLT_EPS_) {
             const DevLight& Lt = sv.lights[m.light];
             f3 emit = mk(Lt.radiance[0], Lt.radiance[1], Lt.radiance[2]);
-            float pdf_s = light_pdf_direct_solid(Lt, ps.o, dt, tmax * tmax);
+            float pdf_s = light_pdf_direct_solid(sv, Lt, ps.o, dt, tmax * tmax, hu, hv);
             float mis = sv.nee ? 1 / (1 + ps.inv_pdf * (1.0f / (float)sv.num_lights) * pdf_s) : 1.0f;
             Lacc = add(Lacc, handle_color(sv, mulf(mul(ps.contrib, emit), mis)));
             has_l = true;
@@ -1311,6 +1311,22 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
                 float r = std::sqrt(1 - c * c) / c; // sun_radius_from_cos_angle
                 d.spot[0] = c;
                 d.spot[1] = 3.14159265359f * r * r;
+            } else if (L.type == IGX_LIGHT_SPHERE || L.type == IGX_LIGHT_MESH) {
+                if (L.entity < 0 || (uint32_t)L.entity >= desc->num_entities)
+                    return fail(dev, IGX_ERR_INVALID_ARGUMENT, "area light references an invalid entity");
+                d.entity = L.entity;
+                if (L.type == IGX_LIGHT_SPHERE) {
+                    if (!(L.area > 0) || !(L.radius > 0))
+                        return fail(dev, IGX_ERR_INVALID_ARGUMENT, "sphere light needs a positive radius and area");
+                    for (int i = 0; i < 3; ++i) d.origin[i] = L.origin[i];
+                    d.origin[3] = L.radius;
+                    d.spot[0] = L.area;
+                } else {
+                    const igx_shape& sh = desc->shapes[desc->entities[L.entity].shape];
+                    if (sh.type != IGX_SHAPE_TRIMESH || sh.mesh < 0 || desc->meshes[sh.mesh].num_faces == 0)
+                        return fail(dev, IGX_ERR_INVALID_ARGUMENT, "mesh light needs a non-empty triangle entity");
+                    d.spot[0] = (float)desc->meshes[sh.mesh].num_faces;
+                }
             } else if (L.type != IGX_LIGHT_ENV) {
                 return fail(dev, IGX_ERR_UNSUPPORTED, "unsupported light type");
             }

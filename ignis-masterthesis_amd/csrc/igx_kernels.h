@@ -543,6 +543,63 @@ __device__ __forceinline__ DirectSample light_sample_direct(const SceneView& sv,
         ds.pdf_solid = true;
         ds.cos = z;
         ds.dist = INFINITY;
+    } else if (L.type == LIGHT_SPHERE || L.type == LIGHT_MESH) {
+        // make_area_light.sample_direct (light/area.art:12-27) over the sphere emitter
+        // (area.art:248-274) or the triangle-shape emitter (area.art:48-57)
+        float ux = rnd.next_f32();
+        float uy = rnd.next_f32();
+        const float4* ep = sv.ent + ENT_STRIDE * L.entity;
+        float4 g0 = ep[0], g1 = ep[1], g2 = ep[2];
+        f3 p, fn;
+        float pdf_a, weight;
+        if (L.type == LIGHT_SPHERE) {
+            float4 n0 = ep[3], n1 = ep[4], n2 = ep[5];
+            f3 so = mk(L.origin[0], L.origin[1], L.origin[2]);
+            float r = L.origin[3];
+            float inv_area = 1 / L.spot[0];
+            f3 glb_org = xform_point_rows(g0, g1, g2, so);
+            f3 nrm = equal_area_square_to_sphere(ux, uy);
+            p = xform_point_rows(g0, g1, g2, add(so, mulf(nrm, r)));
+            fn = normalize(xform_dir_rows(n0, n1, n2, nrm));
+            f3 os = sub(from.point, glb_org), pq = sub(from.point, p);
+            if (!(dot(pq, pq) <= dot(os, os))) { // keep the point on the visible side
+                f3 op = sub(p, glb_org);
+                f3 np = sub(p, mulf(op, 2));
+                f3 nn = normalize(sub(np, glb_org));
+                p = xform_point_rows(g0, g1, g2, add(so, mulf(nn, r)));
+                fn = normalize(xform_dir_rows(n0, n1, n2, nn));
+            }
+            pdf_a = 2 * inv_area;
+            weight = 1 / (2 * inv_area);
+        } else {
+            int4 info = *reinterpret_cast<const int4*>(ep + 6);
+            float cnt = L.spot[0];
+            float uxc = ux * cnt;
+            int f = min((int)uxc, (int)cnt - 1);
+            float su = uxc - (float)f, sw = uy;
+            if (su + sw > 1) { su = 1 - su; sw = 1 - sw; } // sample_triangle (core/sampling.art:34-36)
+            int4 fi = sv.idx[info.w + f];
+            f3 v0 = xform_point_rows(g0, g1, g2, f3of(sv.vtx[info.z + fi.x]));
+            f3 v1 = xform_point_rows(g0, g1, g2, f3of(sv.vtx[info.z + fi.y]));
+            f3 v2 = xform_point_rows(g0, g1, g2, f3of(sv.vtx[info.z + fi.z]));
+            f3 n = cross(sub(v1, v0), sub(v2, v0));
+            float nn = len(n);
+            fn = mulf(n, 1 / nn);
+            float inv_area = 1 / (nn / 2);
+            p = lerp2(v0, v1, v2, su, sw);
+            pdf_a = inv_area / cnt;
+            weight = cnt / inv_area;
+        }
+        f3 dir_ = sub(p, from.point);
+        float dist = len(dir_);
+        f3 dir = mulf(dir_, safe_div(1, dist));
+        ds.pos = p;
+        ds.dir = dir;
+        ds.intensity = mulf(rad, weight);
+        ds.pdf_value = pdf_a;
+        ds.pdf_solid = false;
+        ds.cos = dot(dir, fn) * (from.entering ? -1.0f : 1.0f);
+        ds.dist = dist;
     } else if (L.type == LIGHT_POINT) {
         // make_point_light.sample_direct (light/point.art:3-8)
         f3 pos = mk(L.origin[0], L.origin[1], L.origin[2]);
@@ -577,13 +634,31 @@ __device__ __forceinline__ DirectSample light_sample_direct(const SceneView& sv,
     return ds;
 }
 
-// Light::pdf_direct for lights that can be hit (area: plane; env)
-__device__ __forceinline__ float light_pdf_direct_solid(const DevLight& L, f3 ray_org, float cos, float dist2) {
+// Light::pdf_direct for lights that can be hit (area: plane, sphere, mesh; env),
+// in solid-angle measure.  (hu, hv) are the hit's prim_coords, which the
+// shape emitter reuses as its sample coordinates (light/area.art:41, 59-67).
+__device__ __forceinline__ float light_pdf_direct_solid(const SceneView& sv, const DevLight& L, f3 ray_org, float cos,
+                                                        float dist2, float hu, float hv) {
     if (L.type == LIGHT_PLANE) {
         SQ q = compute_sq(L, ray_org);
         return safe_div(1, q.s); // solid measure
     }
-    (void)cos; (void)dist2;
+    if (L.type == LIGHT_SPHERE) return pdf_as_solid(2 / L.spot[0], false, cos, dist2); // area.art:282-284
+    if (L.type == LIGHT_MESH) {
+        const float4* ep = sv.ent + ENT_STRIDE * L.entity;
+        float4 g0 = ep[0], g1 = ep[1], g2 = ep[2];
+        int4 info = *reinterpret_cast<const int4*>(ep + 6);
+        float cnt = L.spot[0];
+        int f = min((int)(hu * cnt), (int)cnt - 1);
+        int4 fi = sv.idx[info.w + f];
+        f3 v0 = xform_point_rows(g0, g1, g2, f3of(sv.vtx[info.z + fi.x]));
+        f3 v1 = xform_point_rows(g0, g1, g2, f3of(sv.vtx[info.z + fi.y]));
+        f3 v2 = xform_point_rows(g0, g1, g2, f3of(sv.vtx[info.z + fi.z]));
+        float inv_area = 1 / (len(cross(sub(v1, v0), sub(v2, v0))) / 2);
+        (void)hv;
+        return pdf_as_solid(inv_area / cnt, false, cos, dist2);
+    }
+    (void)cos; (void)dist2; (void)hu; (void)hv;
     return 1 / (4 * PI_); // env spherical: equal_area_sphere_pdf
 }
 

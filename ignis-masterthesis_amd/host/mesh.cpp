@@ -99,6 +99,35 @@ void TriMesh::append(const TriMesh& o) {
 }
 
 // ---------------------------------------------------------------------------
+std::optional<SphereShape> get_as_sphere(const TriMesh& mesh) {
+    constexpr float kEps = 1e-5f;
+    if (mesh.face_count() < 32 || mesh.vertices.empty()) return std::nullopt; // too coarse to stand for a sphere
+    const BBox b = mesh.compute_bbox();
+    const V3 c = b.center();
+    const V3 d = b.diameter();
+    if (d.x * d.y * d.z <= kEps) return std::nullopt; // flat
+    if (std::fabs(d.x - d.y) > kEps || std::fabs(d.x - d.z) > kEps || std::fabs(d.y - d.z) > kEps) return std::nullopt;
+    auto dist2 = [&](V3 v) { V3 t = c - v; return dot(t, t); };
+    const float r2 = dist2(mesh.vertices[0]);
+    if (r2 <= kEps) return std::nullopt;
+    bool octant[8] = {};
+    for (size_t i = 0; i < mesh.vertices.size(); ++i) {
+        if (i > 0 && std::fabs(dist2(mesh.vertices[i]) - r2) > kEps) return std::nullopt;
+        V3 t = c - mesh.vertices[i];
+        octant[(t.x < 0 ? 1 : 0) | (t.y < 0 ? 2 : 0) | (t.z < 0 ? 4 : 0)] = true;
+    }
+    for (bool o : octant)
+        if (!o) return std::nullopt;
+    return SphereShape{c, std::sqrt(r2)};
+}
+
+float compute_area(const TriMesh& mesh) {
+    float a = 0;
+    for (auto& f : mesh.faces)
+        a += 0.5f * norm(cross(mesh.vertices[f[1]] - mesh.vertices[f[0]], mesh.vertices[f[2]] - mesh.vertices[f[0]]));
+    return a;
+}
+
 std::optional<PlaneShape> get_as_plane(const TriMesh& mesh) {
     constexpr float PlaneEPS = 1e-5f;
     if (mesh.face_count() != 2) return std::nullopt;

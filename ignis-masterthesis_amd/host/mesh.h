@@ -37,6 +37,16 @@ struct PlaneShape {
 // TriMesh::getAsPlane (TriMesh.cpp:520-634)
 std::optional<PlaneShape> get_as_plane(const TriMesh& mesh);
 
+struct SphereShape {
+    V3 origin;
+    float radius;
+};
+// TriMesh::getAsSphere (TriMesh.cpp:636-698): a closed mesh whose vertices all
+// lie on one sphere around its bbox centre
+std::optional<SphereShape> get_as_sphere(const TriMesh& mesh);
+// TriMesh::computeArea (TriMesh.cpp:199-209)
+float compute_area(const TriMesh& mesh);
+
 // Procedural shapes (TriMesh.cpp:700-1058)
 TriMesh make_plane(V3 origin, V3 x_axis, V3 y_axis);
 TriMesh make_triangle(V3 p0, V3 p1, V3 p2);

@@ -12,7 +12,11 @@
 #include "linalg.h"
 #include "mesh.h"
 
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <optional>
 #include <fstream>
 #include <memory>
 #include <sstream>
@@ -607,22 +611,67 @@ static void build_scene(SceneStore& S, const Value& doc, const std::string& base
                 int eid = entity_ids[ename];
                 const igx_entity& ent = S.entities[eid];
                 const igx_shape& sh = shapes[ent.shape].shape;
-                if (lp.has("power")) fail("area light '" + name + "': 'power' is not supported, use 'radiance'");
-                V3 rad = lp.color("radiance", V3(1, 1, 1));
-                if (!sh.is_plane || !lp.boolean("optimize", true))
-                    fail("area light '" + name + "': only planar emitters are supported (make_plane_area_emitter)");
-                // AreaLight.cpp:59-70, 129-145
                 M4 t;
                 for (int r = 0; r < 3; ++r)
                     for (int c = 0; c < 4; ++c) t.at(r, c) = ent.to_global[r * 4 + c];
-                V3 o = igx::xform_point(t, V3(sh.plane_origin[0], sh.plane_origin[1], sh.plane_origin[2]));
-                V3 xa = igx::xform_dir(t, V3(sh.plane_x[0], sh.plane_x[1], sh.plane_x[2]));
-                V3 ya = igx::xform_dir(t, V3(sh.plane_y[0], sh.plane_y[1], sh.plane_y[2]));
-                V3 n = igx::normalized(igx::cross(xa, ya));
-                L.type = IGX_LIGHT_PLANE;
+                // AreaLight::AreaLight (AreaLight.cpp:38-99): choose the emitter representation
+                const bool is_tri = sh.type == IGX_SHAPE_TRIMESH;
+                const bool opt = lp.boolean("optimize", true) || !is_tri;
+                std::optional<igx::SphereShape> sphere;
+                if (sh.type == IGX_SHAPE_SPHERE) sphere = igx::SphereShape{V3(sh.sphere[0], sh.sphere[1], sh.sphere[2]), sh.sphere[3]};
+                else if (!sh.is_plane) sphere = igx::get_as_sphere(shapes[ent.shape].mesh); // TriMeshProvider.cpp:563, 604-611
+                auto scaled_len = [&](V3 axis) { return igx::norm(igx::xform_dir(t, axis)); };
+                float host_area; // AreaLight::mArea, used by 'power'
                 L.entity = eid;
-                for (int i = 0; i < 3; ++i) { L.origin[i] = o[i]; L.x_axis[i] = xa[i]; L.y_axis[i] = ya[i]; L.normal[i] = n[i]; L.radiance[i] = rad[i]; }
-                L.area = igx::norm(igx::cross(xa, ya));
+                if (opt && sh.is_plane) {
+                    // AreaLight.cpp:59-70, 129-145: make_plane_area_emitter
+                    V3 o = igx::xform_point(t, V3(sh.plane_origin[0], sh.plane_origin[1], sh.plane_origin[2]));
+                    V3 xa = igx::xform_dir(t, V3(sh.plane_x[0], sh.plane_x[1], sh.plane_x[2]));
+                    V3 ya = igx::xform_dir(t, V3(sh.plane_y[0], sh.plane_y[1], sh.plane_y[2]));
+                    V3 n = igx::normalized(igx::cross(xa, ya));
+                    L.type = IGX_LIGHT_PLANE;
+                    for (int i = 0; i < 3; ++i) { L.origin[i] = o[i]; L.x_axis[i] = xa[i]; L.y_axis[i] = ya[i]; L.normal[i] = n[i]; }
+                    L.area = igx::norm(igx::cross(xa, ya));
+                    host_area = L.area;
+                } else if (opt && sphere) {
+                    // AreaLight.cpp:71-79, 146-152: make_sphere_area_emitter; the emitter's own
+                    // area is compute_ellipsoid_area (shapes/sphere.art:21-27, P = 1.6)
+                    const float r = sphere->radius;
+                    float l1 = scaled_len(V3(r, 0, 0)), l2 = scaled_len(V3(0, r, 0)), l3 = scaled_len(V3(0, 0, r));
+                    auto ellipsoid = [&](float P) {
+                        return 4 * 3.14159265358979f *
+                               std::pow((std::pow(l1 * l2, P) + std::pow(l1 * l3, P) + std::pow(l2 * l3, P)) / 3, 1 / P);
+                    };
+                    L.type = IGX_LIGHT_SPHERE;
+                    for (int i = 0; i < 3; ++i) L.origin[i] = sphere->origin[i];
+                    L.radius = r;
+                    L.area = ellipsoid(1.6f);
+                    host_area = ellipsoid(1.6075f); // approximate_ellipsoid_area (AreaLight.cpp:24-33)
+                } else if (is_tri) {
+                    // AreaLight.cpp:80-90, 153-168: make_shape_area_emitter over the mesh
+                    const igx::TriMesh& mesh = shapes[ent.shape].mesh;
+                    if (mesh.face_count() == 0) fail("area light '" + name + "': entity '" + ename + "' has no faces");
+                    L.type = IGX_LIGHT_MESH;
+                    // approximate_area_scale (AreaLight.cpp:11-22) over the shape's bbox
+                    V3 ls(sh.bbox_max[0] - sh.bbox_min[0], sh.bbox_max[1] - sh.bbox_min[1], sh.bbox_max[2] - sh.bbox_min[2]);
+                    float w = scaled_len(V3(ls.x, 0, 0)), h = scaled_len(V3(0, ls.y, 0)), d = scaled_len(V3(0, 0, ls.z));
+                    float half_area = ls.x * (ls.y + ls.z) + ls.y * ls.z;
+                    host_area = igx::compute_area(mesh) * ((w * h + w * d + h * d) / half_area);
+                } else {
+                    fail("area light '" + name + "': entity '" + ename + "' is not triangular");
+                }
+                V3 rad;
+                if (lp.has("power")) {
+                    // AreaLight::serialize (AreaLight.cpp:176-179): power * (inv_pi / area), the area
+                    // printed into the generated shader at default stream precision
+                    char buf[64];
+                    std::snprintf(buf, sizeof(buf), "%g", (double)host_area);
+                    const float area_code = std::strtof(buf, nullptr);
+                    rad = lp.color("power", V3(1, 1, 1)) * (0.318309886183791f / area_code);
+                } else {
+                    rad = lp.color("radiance", V3(1, 1, 1));
+                }
+                for (int i = 0; i < 3; ++i) L.radiance[i] = rad[i];
                 S.materials[ent.material].light = (int)S.lights.size();
             } else if (type == "env" || type == "constant" || type == "uniform") {
                 // EnvironmentLight.cpp:28-78: constant radiance bakes to a 1x1 texture -> make_environment_light

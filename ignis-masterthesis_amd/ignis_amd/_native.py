@@ -40,10 +40,15 @@ class Material(C.Structure):
                 ("alpha_u", C.c_float), ("alpha_v", C.c_float), ("diffuse_alpha", C.c_float), ("pad", C.c_float)]
 
 
+# igx_light.type (include/igx_scene.h)
+LIGHT_PLANE, LIGHT_ENV, LIGHT_POINT, LIGHT_SPOT, LIGHT_DIRECTIONAL, LIGHT_SUN, LIGHT_SPHERE, LIGHT_MESH = range(1, 9)
+
+
 class Light(C.Structure):
     _fields_ = [("type", C.c_int32), ("entity", C.c_int32), ("radiance", C.c_float * 3),
                 ("origin", C.c_float * 3), ("x_axis", C.c_float * 3), ("y_axis", C.c_float * 3),
-                ("normal", C.c_float * 3), ("area", C.c_float), ("cutoff", C.c_float), ("falloff", C.c_float)]
+                ("normal", C.c_float * 3), ("area", C.c_float), ("cutoff", C.c_float), ("falloff", C.c_float),
+                ("radius", C.c_float)]
 
 
 class Camera(C.Structure):

@@ -98,19 +98,22 @@ enum {
     IGX_LIGHT_POINT = 3, /* light/point.art:1-18 */
     IGX_LIGHT_SPOT  = 4, /* light/spot.art:8-60 */
     IGX_LIGHT_DIRECTIONAL = 5, /* light/directional.art:1-19 */
-    IGX_LIGHT_SUN   = 6  /* light/sun.art:4-30 (delta, infinite) */
+    IGX_LIGHT_SUN   = 6, /* light/sun.art:4-30 (delta, infinite) */
+    IGX_LIGHT_SPHERE = 7, /* area light on a (near-)spherical entity: make_sphere_area_emitter (light/area.art:240-293) */
+    IGX_LIGHT_MESH  = 8  /* area light on any triangle entity: make_shape_area_emitter (light/area.art:45-105) */
 };
 
 typedef struct igx_light {
     int32_t type;
     int32_t entity;        /* area lights: emitting entity, -1 otherwise */
     float radiance[3];     /* radiance (area/env), intensity (point/spot), irradiance (directional/sun) */
-    float origin[3];       /* plane origin / point position / spot position */
+    float origin[3];       /* plane origin / point position / spot position / sphere centre (object space) */
     float x_axis[3];       /* plane */
     float y_axis[3];       /* plane */
     float normal[3];       /* plane normal, spot / directional / sun propagation direction */
-    float area;            /* plane area */
+    float area;            /* plane area; sphere: emitter area, compute_ellipsoid_area (shapes/sphere.art:21-27) */
     float cutoff, falloff; /* spot, radians; sun: cutoff = cosine of the sun's half angle */
+    float radius;          /* sphere: object-space radius */
 } igx_light;
 
 /* ---- camera / technique ------------------------------------------------ */

@@ -154,6 +154,10 @@ typedef struct {
     float width, height, area;
     float cos_cut, blend;
     float sun_cos, sun_area; /* make_sun_light (light/sun.art:4-8) */
+    int entity;              /* sphere / mesh area lights: emitting entity */
+    float sph[4];            /* sphere emitter: object-space centre, radius */
+    float sph_area;          /* compute_ellipsoid_area (shapes/sphere.art:21-27) */
+    int faces;               /* shape emitter: primitive_count */
 } olight;
 
 struct oracle_scene {
@@ -347,6 +351,21 @@ oracle_scene* oracle_scene_create(const igx_scene_desc* desc) {
                 float c = L->cutoff, r = sqrtf(1 - c * c) / c;
                 o->sun_cos = c;
                 o->sun_area = PI_ * r * r;
+            } else if (L->type == IGX_LIGHT_SPHERE) {
+                /* make_sphere_area_emitter (light/area.art:240-246): the area is
+                 * recomputed here from the entity transform, not taken from the desc */
+                const float* g = desc->entities[L->entity].to_global;
+                float r = L->radius;
+                float l1 = vlen(V(g[0] * r, g[4] * r, g[8] * r));
+                float l2 = vlen(V(g[1] * r, g[5] * r, g[9] * r));
+                float l3 = vlen(V(g[2] * r, g[6] * r, g[10] * r));
+                const float P = 1.6f;
+                o->entity = L->entity;
+                o->sph[0] = L->origin[0]; o->sph[1] = L->origin[1]; o->sph[2] = L->origin[2]; o->sph[3] = r;
+                o->sph_area = 4 * PI_ * powf((powf(l1 * l2, P) + powf(l1 * l3, P) + powf(l2 * l3, P)) / 3, 1 / P);
+            } else if (L->type == IGX_LIGHT_MESH) {
+                o->entity = L->entity;
+                o->faces = (int)desc->meshes[desc->shapes[desc->entities[L->entity].shape].mesh].num_faces;
             } else if (L->type == IGX_LIGHT_SPOT) {
                 float cc = cosf(L->cutoff), cf = cosf(L->falloff);
                 o->cos_cut = cc;
@@ -693,6 +712,63 @@ typedef struct {
     float cos, dist;
 } odirect;
 
+/* equal_area_square_to_sphere (core/warp.art:63-91) */
+static v3 eq_area_sphere(float ux, float uy) {
+    float u = 2 * ux - 1, v = 2 * uy - 1;
+    float au = fabsf(u), av = fabsf(v);
+    float sd = 1 - (au + av);
+    float dd = fabsf(sd);
+    float r = 1 - dd;
+    float phi = (r == 0 ? 1.0f : (av - au) / r + 1) * PI_ / 4;
+    float ct = copysignf(1 - r * r, sd);
+    float st = safe_sqrt(2 - r * r) * r;
+    float cp = copysignf(cosf(phi), u);
+    float sp = copysignf(sinf(phi), v);
+    return V(cp * st, sp * st, ct);
+}
+
+/* world-space triangle `f` of a mesh entity (make_triangle, core/triangle.art:11-26) */
+static void emitter_triangle(const oracle_scene* s, int entity, int f, v3* v0, v3* v1, v3* v2, v3* n, float* area) {
+    const igx_entity* ent = &s->desc.entities[entity];
+    const igx_mesh* m = &s->desc.meshes[s->desc.shapes[ent->shape].mesh];
+    const uint32_t* ix = m->indices + 3 * (size_t)f;
+    *v0 = xf_point(ent->to_global, V(m->vertices[3 * ix[0]], m->vertices[3 * ix[0] + 1], m->vertices[3 * ix[0] + 2]));
+    *v1 = xf_point(ent->to_global, V(m->vertices[3 * ix[1]], m->vertices[3 * ix[1] + 1], m->vertices[3 * ix[1] + 2]));
+    *v2 = xf_point(ent->to_global, V(m->vertices[3 * ix[2]], m->vertices[3 * ix[2] + 1], m->vertices[3 * ix[2] + 2]));
+    v3 c = vcross(vsub(*v1, *v0), vsub(*v2, *v0));
+    float nn = vlen(c);
+    *n = vmulf(c, 1 / nn);
+    *area = nn / 2;
+}
+
+/* face picked by the shape emitter for sample coordinates u (light/area.art:49-50) */
+static int emitter_face(const olight* L, float u) {
+    float ux = u * (float)L->faces;
+    int f = (int)ux;
+    return f < L->faces - 1 ? f : L->faces - 1;
+}
+
+/* sphere emitter point for a local normal (sphere_compute_surface_element_for_normal, shapes/sphere.art:29-42) */
+static void sphere_point(const oracle_scene* s, const olight* L, v3 nrm, v3* p, v3* fn) {
+    const igx_entity* ent = &s->desc.entities[L->entity];
+    v3 o = V(L->sph[0], L->sph[1], L->sph[2]);
+    *p = xf_point(ent->to_global, vadd(o, vmulf(nrm, L->sph[3])));
+    *fn = vnormalize(xf_normal(ent->normal, nrm));
+}
+
+/* Light::pdf_direct of an area light, solid-angle measure (make_area_light, light/area.art:41) */
+static float area_pdf_direct_solid(const oracle_scene* s, const olight* L, v3 org, float cos, float dist2, float u) {
+    if (L->type == IGX_LIGHT_PLANE) { sq_t q = compute_sq(L, org); return safe_div(1, q.s); }
+    if (L->type == IGX_LIGHT_SPHERE) return (2 / L->sph_area) * dist2 / cos;
+    if (L->type == IGX_LIGHT_MESH) {
+        v3 a, b, c, n;
+        float area;
+        emitter_triangle(s, L->entity, emitter_face(L, u), &a, &b, &c, &n, &area);
+        return ((1 / area) / (float)L->faces) * dist2 / cos;
+    }
+    return 1 / (4 * PI_);
+}
+
 static odirect light_sample_direct(const oracle_scene* s, const olight* L, rng_t* rnd, const osurf* from) {
     odirect d;
     v3 rad = V(L->rad[0], L->rad[1], L->rad[2]);
@@ -726,18 +802,7 @@ static odirect light_sample_direct(const oracle_scene* s, const olight* L, rng_t
     } else if (L->type == IGX_LIGHT_ENV) {
         float ux = rng_f32(rnd);
         float uy = rng_f32(rnd);
-        /* equal_area_square_to_sphere (core/warp.art:63-91) */
-        float u = 2 * ux - 1, v = 2 * uy - 1;
-        float au = fabsf(u), av = fabsf(v);
-        float sd = 1 - (au + av);
-        float dd = fabsf(sd);
-        float r = 1 - dd;
-        float phi = (r == 0 ? 1.0f : (av - au) / r + 1) * PI_ / 4;
-        float ct = copysignf(1 - r * r, sd);
-        float st = safe_sqrt(2 - r * r) * r;
-        float cp = copysignf(cosf(phi), u);
-        float sp = copysignf(sinf(phi), v);
-        v3 dir = V(cp * st, sp * st, ct);
+        v3 dir = eq_area_sphere(ux, uy);
         float pdf = 1 / (4 * PI_);
         d.intensity = vmulf(rad, 1 / pdf);
         d.pos = vadd(from->point, vmulf(dir, s->scene_radius));
@@ -778,6 +843,47 @@ static odirect light_sample_direct(const oracle_scene* s, const olight* L, rng_t
         d.pdf_solid = 1;
         d.cos = z;
         d.dist = INFINITY;
+    } else if (L->type == IGX_LIGHT_SPHERE || L->type == IGX_LIGHT_MESH) {
+        float ux = rng_f32(rnd);
+        float uy = rng_f32(rnd);
+        v3 p, fn;
+        float pdf_a, weight;
+        if (L->type == IGX_LIGHT_SPHERE) {
+            /* make_sphere_area_emitter.sample_direct (light/area.art:248-274) */
+            v3 glb = xf_point(s->desc.entities[L->entity].to_global, V(L->sph[0], L->sph[1], L->sph[2]));
+            sphere_point(s, L, eq_area_sphere(ux, uy), &p, &fn);
+            v3 os = vsub(from->point, glb), pq = vsub(from->point, p);
+            if (!(vdot(pq, pq) <= vdot(os, os))) {
+                v3 np = vsub(p, vmulf(vsub(p, glb), 2));
+                sphere_point(s, L, vnormalize(vsub(np, glb)), &p, &fn);
+            }
+            float inv_area = 1 / L->sph_area;
+            pdf_a = 2 * inv_area;
+            weight = 1 / (2 * inv_area);
+        } else {
+            /* make_shape_area_emitter.sample (light/area.art:48-57) */
+            int f = emitter_face(L, ux);
+            float su = ux * (float)L->faces - (float)f, sw = uy;
+            if (su + sw > 1) { su = 1 - su; sw = 1 - sw; }
+            v3 a, b, c;
+            float area;
+            emitter_triangle(s, L->entity, f, &a, &b, &c, &fn, &area);
+            float inv_area = 1 / area;
+            p = V(lerp2(a.x, b.x, c.x, su, sw), lerp2(a.y, b.y, c.y, su, sw), lerp2(a.z, b.z, c.z, su, sw));
+            pdf_a = inv_area / (float)L->faces;
+            weight = (float)L->faces / inv_area;
+        }
+        /* make_area_light.sample_direct (light/area.art:12-27) */
+        v3 dir_ = vsub(p, from->point);
+        float dist = vlen(dir_);
+        v3 dir = vmulf(dir_, safe_div(1, dist));
+        d.pos = p;
+        d.dir = dir;
+        d.intensity = vmulf(rad, weight);
+        d.pdf_value = pdf_a;
+        d.pdf_solid = 0;
+        d.cos = vdot(dir, fn) * (from->entering ? -1.0f : 1.0f);
+        d.dist = dist;
     } else if (L->type == IGX_LIGHT_POINT) {
         v3 pos = V(L->origin[0], L->origin[1], L->origin[2]);
         v3 dir_ = vsub(pos, from->point);
@@ -1197,9 +1303,7 @@ static v3 trace_path(const oracle_scene* s, const oracle_params* p, int x, int y
             if (dt > FLT_EPS_) {
                 const olight* L = &s->lights[mlight];
                 v3 emit = V(L->rad[0], L->rad[1], L->rad[2]);
-                float pdf_s;
-                if (L->type == IGX_LIGHT_PLANE) { sq_t q = compute_sq(L, ray.org); pdf_s = safe_div(1, q.s); }
-                else pdf_s = 1 / (4 * PI_);
+                float pdf_s = area_pdf_direct_solid(s, L, ray.org, dt, h.t * h.t, h.u);
                 float mis = tech->nee ? 1 / (1 + inv_pdf * sel_pdf * pdf_s) : 1.0f;
                 Lacc = vadd(Lacc, handle_color(s, vmulf(vmul(contrib, emit), mis)));
             }

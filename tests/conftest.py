@@ -52,3 +52,21 @@ SPOT_LIGHT = {"type": "spot", "name": "_light", "cutoff": 45, "falloff": 45, "po
 ENV_LIGHT = {"type": "env", "name": "_light", "radiance": [1, 1, 1]}
 DIRECTIONAL_LIGHT = {"type": "directional", "name": "_light", "direction": [0, 0, 1], "irradiance": [1, 1, 1]}
 SUN_LIGHT = {"type": "sun", "name": "_light", "direction": [0, 0, 1], "irradiance": [1, 1, 1]}
+
+
+def emitter_scene(kind, max_depth=2, size=1000):
+    """flat_scene with an emissive entity as the only light (area lights on
+    non-planar shapes, light/area.art:45-105 and 240-293)."""
+    sc = flat_scene([], max_depth=max_depth, size=size)
+    sc["bsdfs"].append({"type": "diffuse", "name": "black", "reflectance": [0, 0, 0]})
+    if kind == "sphere_area":
+        sc["shapes"].append({"type": "sphere", "name": "Ball", "center": [0, 0, -2], "radius": 0.5})
+        sc["entities"].append({"name": "Ball", "shape": "Ball", "bsdf": "black"})
+    elif kind == "mesh_area":
+        sc["shapes"].append({"type": "cube", "name": "Room", "width": 8, "height": 8, "depth": 8, "flip_normals": True})
+        sc["entities"].append({"name": "Room", "shape": "Room", "bsdf": "black"})
+    else:
+        raise ValueError(kind)
+    ent = sc["entities"][-1]["name"]
+    sc["lights"].append({"type": "area", "name": "Emitter", "entity": ent, "radiance": [1, 1, 1]})
+    return sc

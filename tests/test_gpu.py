@@ -19,7 +19,7 @@ import pytest
 
 import ignis_amd
 from oracle import oracle_py as O
-from conftest import DIRECTIONAL_LIGHT, ENV_LIGHT, POINT_LIGHT, SPOT_LIGHT, SUN_LIGHT, flat_scene
+from conftest import DIRECTIONAL_LIGHT, ENV_LIGHT, POINT_LIGHT, SPOT_LIGHT, SUN_LIGHT, emitter_scene, flat_scene
 
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
@@ -342,6 +342,61 @@ def test_image_parity_materials(device, root):
     """§8f wider materials: mirror, smooth / rough conductors (VNDF-GGX, GGX, Beckmann,
     anisotropic), smooth / rough plastic, Oren-Nayar, glass -- GPU vs oracle."""
     sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", "materials.json"))
+    g = render_gpu(device, sc, 192, 192, 8)
+    o, _ = O.OracleScene(sc).render(192, 192, 8)
+    assert abs(g.mean() - o.mean()) / o.mean() < 0.01
+    assert rel_mse(g, o) <= 5e-3
+    close = np.abs(g - o) <= 1e-2 * np.maximum(np.abs(o), 1e-2)
+    assert close.mean() >= 0.99, close.mean()
+
+
+@pytest.mark.parametrize("name", ["sphere_area", "mesh_area"])
+def test_area_emitters_known_answers(device, name):
+    """Sphere and triangle-shape emitters (light/area.art:45-105, 240-293) against closed forms."""
+    sc = ignis_amd.Scene.from_string(emitter_scene(name))
+    fb = render_gpu(device, sc, 1000, 1000, 8)
+    pix = fb.reshape(-1, 3).mean(axis=1)
+    mean, se = float(pix.mean()), float(pix.std() / math.sqrt(pix.size))
+    assert abs(mean - ANALYTIC[name]["value"]) <= 5 * se + 1e-6, (mean, ANALYTIC[name]["value"], se)
+
+
+LIGHTS_SCENE = {
+    "technique": {"type": "path", "max_depth": 8},
+    "camera": {"type": "perspective", "fov": 55, "near_clip": 0.01, "far_clip": 100,
+               "transform": [{"lookat": {"origin": [0, -4.5, 1.6], "target": [0, 0, 0.9], "up": [0, 0, 1]}}]},
+    "bsdfs": [{"type": "diffuse", "name": "white", "reflectance": [0.75, 0.75, 0.75]},
+              {"type": "diffuse", "name": "red", "reflectance": [0.7, 0.15, 0.1]},
+              {"type": "roughconductor", "name": "metal", "material": "gold", "roughness": 0.2},
+              {"type": "diffuse", "name": "black", "reflectance": [0, 0, 0]}],
+    "shapes": [{"type": "rectangle", "name": "floor", "width": 6, "height": 6},
+               {"type": "rectangle", "name": "wall", "width": 6, "height": 3,
+                "transform": [{"translate": [0, 2.5, 1.5]}, {"rotate": [90, 0, 0]}]},
+               {"type": "cube", "name": "block", "width": 0.8, "height": 0.8, "depth": 1.2,
+                "transform": [{"rotate": [0, 0, 25]}, {"translate": [-0.9, 0.6, 0.6]}]},
+               {"type": "sphere", "name": "ball", "center": [0.9, 0.3, 0.5], "radius": 0.5},
+               {"type": "sphere", "name": "lamp", "center": [0.2, -0.6, 2.1], "radius": 0.25},
+               {"type": "cylinder", "name": "tube", "radius": 0.06, "p0": [-1.8, 1.8, 0.2], "p1": [-1.8, 1.8, 2.4]},
+               {"type": "icosphere", "name": "bulb", "center": [1.6, 1.6, 1.8], "radius": 0.2, "subdivisions": 3}],
+    "entities": [{"name": "floor", "shape": "floor", "bsdf": "white"},
+                 {"name": "wall", "shape": "wall", "bsdf": "red"},
+                 {"name": "block", "shape": "block", "bsdf": "white"},
+                 {"name": "ball", "shape": "ball", "bsdf": "metal"},
+                 {"name": "lamp", "shape": "lamp", "bsdf": "black"},
+                 {"name": "tube", "shape": "tube", "bsdf": "black"},
+                 {"name": "bulb", "shape": "bulb", "bsdf": "black"}],
+    "lights": [{"type": "area", "name": "L_lamp", "entity": "lamp", "radiance": [6, 5, 4]},
+               {"type": "area", "name": "L_tube", "entity": "tube", "radiance": [2, 3, 6]},
+               {"type": "area", "name": "L_bulb", "entity": "bulb", "radiance": [5, 5, 5]},
+               {"type": "env", "name": "sky", "radiance": [0.05, 0.05, 0.06]}],
+}
+
+
+def test_image_parity_area_emitters(device):
+    """§8f wider lights: analytic sphere, mesh-detected sphere and triangle-mesh emitters
+    next to an environment, GPU vs oracle."""
+    sc = ignis_amd.Scene.from_string(LIGHTS_SCENE)
+    types = sorted(sc.desc.lights[i].type for i in range(sc.desc.num_lights))
+    assert types == [2, 7, 7, 8]
     g = render_gpu(device, sc, 192, 192, 8)
     o, _ = O.OracleScene(sc).render(192, 192, 8)
     assert abs(g.mean() - o.mean()) / o.mean() < 0.01

@@ -164,3 +164,68 @@ def test_write_exr_roundtrip(tmp_path):
     assert sorted(ch) == ["A", "B", "G", "R"] and np.all(ch["A"] == 1)
     with pytest.raises(ignis_amd.IgxError):
         ignis_amd.write_exr(tmp_path / "missing_dir" / "x.exr", img)
+
+
+def _emitter_doc(shape, light_extra=None, transform=None):
+    ent = {"name": "E", "shape": "S", "bsdf": "d"}
+    if transform:
+        ent["transform"] = transform
+    light = {"type": "area", "name": "L", "entity": "E", "radiance": [1, 2, 3]}
+    light.update(light_extra or {})
+    return {"bsdfs": [{"type": "diffuse", "name": "d"}], "shapes": [dict(shape, name="S")],
+            "entities": [ent], "lights": [light]}
+
+
+def _ellipsoid_area(l1, l2, l3, P):
+    return 4 * np.pi * (((l1 * l2) ** P + (l1 * l3) ** P + (l2 * l3) ** P) / 3) ** (1 / P)
+
+
+def test_area_light_representations():
+    """AreaLight::AreaLight (AreaLight.cpp:38-99): plane -> plane sampler, analytic
+    or mesh-detected sphere -> sphere sampler, any other triangle shape (or
+    optimize=false) -> triangle-shape sampler."""
+    keep = []
+
+    def light_of(doc):
+        sc = ignis_amd.Scene.from_string(doc)
+        keep.append(sc)  # the desc is owned by the scene handle
+        assert sc.desc.num_lights == 1
+        return sc.desc.lights[0], sc.desc
+    L, _ = light_of(_emitter_doc({"type": "rectangle"}))
+    assert L.type == _native.LIGHT_PLANE
+    L, _ = light_of(_emitter_doc({"type": "rectangle"}, {"optimize": False}))
+    assert L.type == _native.LIGHT_MESH and L.entity == 0
+    L, _ = light_of(_emitter_doc({"type": "cylinder"}))
+    assert L.type == _native.LIGHT_MESH
+    # analytic sphere, non-uniformly scaled: the emitter keeps the object-space sphere
+    # and the P = 1.6 ellipsoid area of compute_ellipsoid_area (shapes/sphere.art:21-27)
+    L, _ = light_of(_emitter_doc({"type": "sphere", "center": [1, 2, 3], "radius": 0.5},
+                                 transform=[{"scale": [1, 2, 3]}]))
+    assert L.type == _native.LIGHT_SPHERE
+    np.testing.assert_allclose(L.origin[:], [1, 2, 3])
+    assert L.radius == pytest.approx(0.5)
+    assert L.area == pytest.approx(_ellipsoid_area(0.5, 1.0, 1.5, 1.6), rel=1e-5)
+    # icosphere mesh: TriMesh::getAsSphere (TriMesh.cpp:636-698) detects the sphere
+    L, _ = light_of(_emitter_doc({"type": "icosphere", "center": [0, 0, 1], "radius": 2, "subdivisions": 3}))
+    assert L.type == _native.LIGHT_SPHERE
+    np.testing.assert_allclose(L.origin[:], [0, 0, 1], atol=1e-5)
+    assert L.radius == pytest.approx(2, rel=1e-5)
+    assert L.area == pytest.approx(4 * np.pi * 4, rel=1e-5)
+    # ... unless optimize = false: the mesh itself is sampled
+    L, _ = light_of(_emitter_doc({"type": "icosphere", "subdivisions": 3}, {"optimize": False}))
+    assert L.type == _native.LIGHT_MESH
+
+
+def test_area_light_power():
+    """'power' becomes power * (inv_pi / area) (AreaLight.cpp:170-179), with the area the
+    representation's own: plane |x*y|, sphere 1.6075-ellipsoid, mesh area * bbox scale."""
+    pw = {"power": [10, 10, 10]}
+    sc = ignis_amd.Scene.from_string(_emitter_doc({"type": "rectangle", "width": 2, "height": 3}, pw))
+    assert sc.desc.lights[0].radiance[0] == pytest.approx(10 / (np.pi * 6), rel=1e-5)
+    sc = ignis_amd.Scene.from_string(_emitter_doc({"type": "sphere", "radius": 2}, pw))
+    assert sc.desc.lights[0].radiance[1] == pytest.approx(10 / (np.pi * _ellipsoid_area(2, 2, 2, 1.6075)), rel=1e-5)
+    # unit cube scaled by 2 along x: area 6 * scale (w h + w d + h d) / half_area = 6 * 5 / 3
+    sc = ignis_amd.Scene.from_string(_emitter_doc({"type": "cube", "width": 1, "height": 1, "depth": 1}, pw,
+                                                  transform=[{"scale": [2, 1, 1]}]))
+    assert sc.desc.lights[0].type == _native.LIGHT_MESH
+    assert sc.desc.lights[0].radiance[2] == pytest.approx(10 / (np.pi * 10), rel=1e-4)

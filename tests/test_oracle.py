@@ -8,7 +8,7 @@ import pytest
 
 import ignis_amd
 from oracle import oracle_py as O
-from conftest import DIRECTIONAL_LIGHT, ENV_LIGHT, POINT_LIGHT, SPOT_LIGHT, SUN_LIGHT, flat_scene
+from conftest import DIRECTIONAL_LIGHT, ENV_LIGHT, POINT_LIGHT, SPOT_LIGHT, SUN_LIGHT, emitter_scene, flat_scene
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
@@ -97,6 +97,13 @@ ANALYTIC = load_golden("analytic_kats.json")["cases"]
                                         ("directional", DIRECTIONAL_LIGHT), ("sun", SUN_LIGHT)])
 def test_oracle_analytic(name, light):
     mean, se, _ = _oracle_mean(flat_scene([light] if light else []))
+    expected = ANALYTIC[name]["value"]
+    assert abs(mean - expected) <= 5 * se + 1e-6, (mean, expected, se)
+
+
+@pytest.mark.parametrize("name", ["sphere_area", "mesh_area"])
+def test_oracle_area_emitters_analytic(name):
+    mean, se, _ = _oracle_mean(emitter_scene(name))
     expected = ANALYTIC[name]["value"]
     assert abs(mean - expected) <= 5 * se + 1e-6, (mean, expected, se)
 
