@@ -54,14 +54,15 @@ def algorithmic_bytes(stats_inst, st):
     from an instrumented pass; ray counts are those the wavefront kernels
     handled in the timed run (the tail kernel's rays are excluded).
     * fused k_extend (default): per closest-hit ray 52 B path state read +
-      32 B radiance read/write + 64 B per node + 64 B per instance + 48 B per
+      32 B radiance read/write + 128 B per 4-wide node (64 B per BVH2 node) +
+      64 B per instance + 48 B per
       triangle + 288 B of shading fetches per hit (entity 112, face 16,
       3 vertices + 3 normals 96, material 64); plus 52 B per surviving path
       and 48 B per shadow ray written;
     * split k_trace: 32 B ray read + 20 B hit written + the same BVH terms.
     """
     n = max(stats_inst["_rays_ext"], 1)
-    bvh = 64.0 * stats_inst["node_visits"] / n + 64.0 * stats_inst["leaf_visits"] / n + 48.0 * stats_inst["tri_tests"] / n
+    bvh = float(st.get("node_bytes", 64)) * stats_inst["node_visits"] / n + 64.0 * stats_inst["leaf_visits"] / n + 48.0 * stats_inst["tri_tests"] / n
     if st["launches_trace"] > 0:
         per_ray = 32 + 20 + bvh
         return st["extend_rays"] * per_ray, per_ray

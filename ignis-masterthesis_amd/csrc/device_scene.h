@@ -16,6 +16,15 @@ constexpr int32_t REF_MARKER = (int32_t)0x80000000; // return from a BLAS to the
 constexpr int32_t REF_EXIT = (int32_t)0x80000001;   // bottom of the traversal stack
 constexpr int LEAF_COUNT_BITS = 4;
 
+// Traversal variant V (a kernel template parameter): bit 1 = 4-wide nodes
+// (128-B SoA node, host Bvh4Node) instead of BVH2 (64-B Node2, host BvhNode);
+// bit 0 = the scene's stack need exceeds the LDS stack, so pushes and pops
+// check for the spill area.  The upload picks the width per scene.
+constexpr int LDS_STACK = 16; // LDS traversal-stack entries per lane
+__host__ __device__ constexpr int variant_width(int v) { return (v & 2) ? 4 : 2; }
+__host__ __device__ constexpr bool variant_spill(int v) { return (v & 1) != 0; }
+__host__ __device__ constexpr int node_f4(int width) { return width == 4 ? 8 : 4; }
+
 // Instance record (one per TLAS leaf slot): 64 B
 //   row0..row2: to_local 3x4 (row-major, xyz = linear row, w = translation)
 //   info: x = entity id, y = shape type (0 trimesh, 1 sphere), z = BLAS root node

@@ -37,6 +37,8 @@ using namespace igxd;
 namespace {
 
 constexpr int BLOCK = 256;
+constexpr int MAX_BLOCKS_PER_CU = 8;  // 2048 threads per CU; grids never exceed num_cus * this
+constexpr int MAX_STACK = 128;        // traversal stack entries (LDS + spill) per ray
 constexpr int MAX_BOUNCES = 256;
 // Occupancy target (waves per SIMD) of k_extend: 4 caps it at 128 VGPRs
 // without spills (the compiler's own choice is 142 -> 3 waves); measured
@@ -320,15 +322,15 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
 // One bounce of one path: closest hit + shading.  Used by the tail kernel; the
 // wavefront runs the same two halves as k_trace + k_shade, so both produce
 // bit-identical paths.
-template <bool STATS>
-__device__ __forceinline__ bool extend_step(const FrameArgs& fa, const SceneView& sv, int* stk, PathState& ps, f3& Lacc,
+template <bool STATS, int V>
+__device__ __forceinline__ bool extend_step(const FrameArgs& fa, const SceneView& sv, const TStack& ts, PathState& ps, f3& Lacc,
                                             bool& has_l, bool& has_shadow, ShadowRec& sr, TraceStats& st) {
     float tmin, tmax;
     uint32_t rflags;
     ray_extent(fa, sv, ps.depth, ps.slot, tmin, tmax, rflags);
     int hit_ent, hit_prim;
     float hu = 0, hv = 0;
-    trace_ray<false, STATS>(sv, ps.o, ps.d, tmin, tmax, rflags, stk, BLOCK, hit_ent, hit_prim, hu, hv, st);
+    trace_ray<false, STATS, V>(sv, ps.o, ps.d, tmin, tmax, rflags, ts, hit_ent, hit_prim, hu, hv, st);
     if (STATS && hit_ent >= 0) st.hits++;
     return shade_step(fa, sv, ps, hit_ent, hit_prim, tmax, hu, hv, Lacc, has_l, has_shadow, sr);
 }
@@ -397,13 +399,13 @@ __device__ __forceinline__ void block_append2(bool a, bool b, int* ca, int* cb, 
 // ---------------------------------------------------------------------------
 // extend kernel: one bounce for every live path, compacted outputs
 // ---------------------------------------------------------------------------
-template <int STACK, bool STATS, bool LDS>
-__global__ void __launch_bounds__(BLOCK, (STACK <= 32 ? EXTEND_WAVES : 1)) k_extend(FrameArgs fa, SceneView gsv, PathBuf in, PathBuf out, ShadowBuf sh,
+template <int V, bool STATS, bool LDS>
+__global__ void __launch_bounds__(BLOCK, EXTEND_WAVES) k_extend(FrameArgs fa, SceneView gsv, PathBuf in, PathBuf out, ShadowBuf sh,
                                                   float4* L, KernelCounters kc, int tail_threshold) {
-    __shared__ int stack_mem[STACK * BLOCK + 2 * (BLOCK / 64) + 2];
+    __shared__ int stack_mem[LDS_STACK * BLOCK + 2 * (BLOCK / 64) + 2];
     extern __shared__ float4 lds_scene[];
-    int* stk = stack_mem + threadIdx.x;
-    int* scan = stack_mem + STACK * BLOCK;
+    const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
+    int* scan = stack_mem + LDS_STACK * BLOCK;
     const int n = uniform_load(kc.cnt_in);
     if (n <= tail_threshold) return; // k_finish takes the remaining paths
     const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
@@ -419,7 +421,7 @@ __global__ void __launch_bounds__(BLOCK, (STACK <= 32 ? EXTEND_WAVES : 1)) k_ext
             if (ps.depth > 0) {
                 f3 Lacc;
                 bool has_l;
-                alive = extend_step<STATS>(fa, sv, stk, ps, Lacc, has_l, has_shadow, sr, st);
+                alive = extend_step<STATS, V>(fa, sv, ts, ps, Lacc, has_l, has_shadow, sr, st);
                 if (has_l) add_radiance(L, ps.slot, Lacc);
             }
         }
@@ -441,12 +443,12 @@ __global__ void __launch_bounds__(BLOCK, (STACK <= 32 ? EXTEND_WAVES : 1)) k_ext
 // for high occupancy (the latency of the dependent node loads is what bounds
 // it); each lane writes its own hit record, no block synchronisation.
 // ---------------------------------------------------------------------------
-template <int STACK, bool STATS, int WAVES, bool LDS>
+template <int V, bool STATS, int WAVES, bool LDS>
 __global__ void __launch_bounds__(BLOCK, WAVES) k_trace(FrameArgs fa, SceneView gsv, PathBuf in, HitBuf hits,
                                                       const int* cnt, int tail_threshold, unsigned long long* stats) {
-    __shared__ int stack_mem[STACK * BLOCK];
+    __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
-    int* stk = stack_mem + threadIdx.x;
+    const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
     const int n = uniform_load(cnt);
     if (n <= tail_threshold) return; // k_finish takes the remaining paths
     const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
@@ -461,7 +463,7 @@ __global__ void __launch_bounds__(BLOCK, WAVES) k_trace(FrameArgs fa, SceneView 
             float tmin;
             uint32_t rflags;
             ray_extent(fa, sv, depth, sd & 0xFFFFFF, tmin, tmax, rflags);
-            trace_ray<false, STATS>(sv, f3of(p0), f3of(p1), tmin, tmax, rflags, stk, BLOCK, hit_ent, hit_prim, hu, hv, st);
+            trace_ray<false, STATS, V>(sv, f3of(p0), f3of(p1), tmin, tmax, rflags, ts, hit_ent, hit_prim, hu, hv, st);
             if (STATS && hit_ent >= 0) st.hits++;
         }
         hits.h[i] = make_float4(tmax, hu, hv, __int_as_float(hit_ent));
@@ -514,13 +516,13 @@ __global__ void __launch_bounds__(BLOCK) k_shade(FrameArgs fa, SceneView sv, Pat
 // empty per-bounce launches.  Same per-path arithmetic and the same radiance
 // accumulation order as the wavefront kernels.
 // ---------------------------------------------------------------------------
-template <int STACK, bool STATS, bool LDS>
+template <int V, bool STATS, bool LDS>
 __global__ void __launch_bounds__(BLOCK) k_finish(FrameArgs fa, SceneView gsv, PathBuf in, float4* L, const int* cnt,
                                                   int tail_threshold, unsigned long long* stats,
                                                   unsigned long long* tail_counts) {
-    __shared__ int stack_mem[STACK * BLOCK];
+    __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
-    int* stk = stack_mem + threadIdx.x;
+    const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
     const int n = uniform_load(cnt);
     if (n > tail_threshold || n == 0) return; // the wavefront kernels own this bounce
     const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
@@ -534,14 +536,14 @@ __global__ void __launch_bounds__(BLOCK) k_finish(FrameArgs fa, SceneView gsv, P
             f3 Lacc;
             bool has_l, has_shadow;
             ShadowRec sr;
-            bool alive = extend_step<STATS>(fa, sv, stk, ps, Lacc, has_l, has_shadow, sr, st);
+            bool alive = extend_step<STATS, V>(fa, sv, ts, ps, Lacc, has_l, has_shadow, sr, st);
             if (has_l) add_radiance(L, ps.slot, Lacc);
             if (has_shadow) {
                 ++shadows;
                 float tm = sr.tmax;
                 int e, p;
                 float u, v;
-                if (!trace_ray<true, STATS>(sv, sr.o, sr.d, 0.001f, tm, RAY_SHADOW, stk, BLOCK, e, p, u, v, sst))
+                if (!trace_ray<true, STATS, V>(sv, sr.o, sr.d, 0.001f, tm, RAY_SHADOW, ts, e, p, u, v, sst))
                     add_radiance(L, ps.slot, sr.color);
             }
             if (!alive) break;
@@ -567,12 +569,12 @@ __global__ void __launch_bounds__(BLOCK) k_finish(FrameArgs fa, SceneView gsv, P
 // shadow: any-hit traversal; on miss add the NEE contribution
 // (gpu_traverse_secondary, mapping_gpu.art:70-112; on_shadow_miss, pathtracer.art:202-209)
 // ---------------------------------------------------------------------------
-template <int STACK, bool STATS, bool LDS>
+template <int V, bool STATS, bool LDS>
 __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, float4* L, const int* cnt,
                                                   unsigned long long* stats) {
-    __shared__ int stack_mem[STACK * BLOCK];
+    __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
-    int* stk = stack_mem + threadIdx.x;
+    const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
     const int n = uniform_load(cnt);
     if (n == 0) return;
     const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
@@ -582,7 +584,7 @@ __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, f
         float tmax = s1.w;
         int e, p;
         float u, v;
-        if (!trace_ray<true, STATS>(sv, f3of(s0), f3of(s1), 0.001f, tmax, RAY_SHADOW, stk, BLOCK, e, p, u, v, st))
+        if (!trace_ray<true, STATS, V>(sv, f3of(s0), f3of(s1), 0.001f, tmax, RAY_SHADOW, ts, e, p, u, v, st))
             add_radiance(L, __float_as_int(s0.w), f3of(sh.s2[i]));
     }
     if (STATS) flush_stats<STATS>(st, stats, 4, false);
@@ -618,28 +620,28 @@ __global__ void k_pack_tiles(FrameArgs fa, const float* fb, float* dst, int num_
 }
 
 // hit-level test kernels (one ray per lane)
-template <int STACK>
+template <int V>
 __global__ void __launch_bounds__(BLOCK) k_trace_hits(SceneView sv, const float* rays, int n, uint32_t flags, int* ent_prim,
                                                       float* tuv, int any) {
-    __shared__ int stack_mem[STACK * BLOCK];
-    int* stk = stack_mem + threadIdx.x;
-    int i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n) return;
-    const float* r = rays + 8 * i;
-    float tmax = r[7];
-    int e, p;
-    float u = 0, v = 0;
+    __shared__ int stack_mem[LDS_STACK * BLOCK];
+    const TStack ts = make_tstack(stack_mem, LDS_STACK, sv.spill);
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
-    if (any) {
-        bool occ = trace_ray<true, false>(sv, mk(r[0], r[1], r[2]), mk(r[3], r[4], r[5]), r[6], tmax, flags, stk, BLOCK, e, p, u, v, st);
-        ent_prim[i] = occ ? 1 : 0;
-    } else {
-        trace_ray<false, false>(sv, mk(r[0], r[1], r[2]), mk(r[3], r[4], r[5]), r[6], tmax, flags, stk, BLOCK, e, p, u, v, st);
-        ent_prim[2 * i] = e;
-        ent_prim[2 * i + 1] = p;
-        tuv[3 * i] = e >= 0 ? tmax : r[7];
-        tuv[3 * i + 1] = u;
-        tuv[3 * i + 2] = v;
+    for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+        const float* r = rays + 8 * i;
+        float tmax = r[7];
+        int e, p;
+        float u = 0, v = 0;
+        if (any) {
+            bool occ = trace_ray<true, false, V>(sv, mk(r[0], r[1], r[2]), mk(r[3], r[4], r[5]), r[6], tmax, flags, ts, e, p, u, v, st);
+            ent_prim[i] = occ ? 1 : 0;
+        } else {
+            trace_ray<false, false, V>(sv, mk(r[0], r[1], r[2]), mk(r[3], r[4], r[5]), r[6], tmax, flags, ts, e, p, u, v, st);
+            ent_prim[2 * i] = e;
+            ent_prim[2 * i + 1] = p;
+            tuv[3 * i] = e >= 0 ? tmax : r[7];
+            tuv[3 * i + 1] = u;
+            tuv[3 * i + 2] = v;
+        }
     }
 }
 
@@ -697,7 +699,7 @@ struct igx_device {
     int64_t capacity_opt = 0;
     int64_t tail_opt = -1;   // paths at or below which k_finish takes over (-1 = auto)
     bool split = false;      // k_trace + k_shade per bounce (default: fused k_extend)
-    int trace_waves = 5;     // occupancy target of k_trace<16> (0 = compiler's choice; 5, 6, 8)
+    int trace_waves = 5;     // occupancy target of k_trace (5 waves per SIMD, anything else = compiler's choice)
     int64_t lds_scene_max = 48 * 1024; // stage traversal tables in LDS when they fit (0 = never)
     size_t lds_scene_bytes = 0;        // bytes staged per block for the current scene (0 = global tables)
     int leaf_size = 4;
@@ -706,8 +708,12 @@ struct igx_device {
     std::vector<void*> scene_allocs;
     SceneView sv{};
     igx_camera cam_desc{};
-    int stack_depth = 32;
-    int scene_depth = 0;
+    int variant = 0;       // traversal variant of the scene (device_scene.h: width, spill)
+    int bvh_width = 2;     // node width of the uploaded tables
+    int bvh_width_opt = 0; // option "bvh_width": 0 = auto, 2, 4 (applies at the next upload)
+    int scene_depth = 0;   // worst-case stack entries of the scene
+    int* spill_main = nullptr; // spill columns of the main and tail streams
+    int* spill_tail = nullptr;
     // streams
     Slot slots[2];
     int next_slot = 0;
@@ -753,7 +759,33 @@ igx_status upload(igx_device* dev, const std::vector<T>& v, const T** out) {
 void free_scene(igx_device* dev) {
     for (void* p : dev->scene_allocs) (void)hipFree(p);
     dev->scene_allocs.clear();
+    dev->spill_main = dev->spill_tail = nullptr;
     dev->has_scene = false;
+}
+
+// Traversal variant of the scene and the spill columns for the stack entries
+// beyond the LDS_STACK in LDS: one per grid thread of the largest grid, per
+// stream.
+igx_status configure_stack(igx_device* dev) {
+    const int need = dev->scene_depth;
+    const int extra = std::max(0, need - LDS_STACK);
+    dev->variant = (dev->bvh_width == 4 ? 2 : 0) | (extra > 0 ? 1 : 0);
+    const size_t threads = (size_t)dev->num_cus * MAX_BLOCKS_PER_CU * BLOCK;
+    for (int k = 0; k < 2; ++k) {
+        int*& old = k == 0 ? dev->spill_main : dev->spill_tail;
+        if (old) {
+            auto it = std::find(dev->scene_allocs.begin(), dev->scene_allocs.end(), (void*)old);
+            if (it != dev->scene_allocs.end()) dev->scene_allocs.erase(it);
+            (void)hipFree(old);
+            old = nullptr;
+        }
+        void* p = nullptr;
+        HIPCHK(hipMalloc(&p, std::max<size_t>(16, (size_t)extra * threads * sizeof(int))));
+        dev->scene_allocs.push_back(p);
+        (k == 0 ? dev->spill_main : dev->spill_tail) = static_cast<int*>(p);
+    }
+    dev->sv.spill = dev->spill_main;
+    return IGX_OK;
 }
 
 void free_slot_buffers(Slot& s) {
@@ -801,18 +833,19 @@ hipEvent_t slot_event(Slot& s) {
 
 int grid_for(igx_device* dev, long long items, int blocks_per_cu) {
     long long need = (items + BLOCK - 1) / BLOCK;
-    long long cap = (long long)dev->num_cus * blocks_per_cu;
+    long long cap = (long long)dev->num_cus * std::min(blocks_per_cu, MAX_BLOCKS_PER_CU);
     return (int)std::max<long long>(1, std::min(need, cap));
 }
 
-// Launch helpers dispatching on the traversal stack depth (LDS per block =
-// STACK * BLOCK * 4 bytes, so a shallow scene gets a small stack and more
-// resident blocks).
-#define IGX_DISPATCH_STACK(depth, MACRO)       \
-    do {                                       \
-        if ((depth) <= 16) { MACRO(16); }      \
-        else if ((depth) <= 32) { MACRO(32); } \
-        else { MACRO(64); }                    \
+// Launch helpers dispatching on the scene's traversal variant.
+#define IGX_DISPATCH_VARIANT(v, MACRO)        \
+    do {                                      \
+        switch (v) {                          \
+        case 0: MACRO(0); break;              \
+        case 1: MACRO(1); break;              \
+        case 2: MACRO(2); break;              \
+        default: MACRO(3); break;             \
+        }                                     \
     } while (0)
 
 template <bool STATS>
@@ -820,60 +853,58 @@ void launch_extend(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, cons
                    const KernelCounters& kc, int tail) {
     if (dev->lds_scene_bytes) {
 #define L_EXTL(S) hipLaunchKernelGGL((k_extend<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->stream, fa, dev->sv, in, out, s.sh, s.L, kc, tail)
-        IGX_DISPATCH_STACK(dev->stack_depth, L_EXTL);
+        IGX_DISPATCH_VARIANT(dev->variant, L_EXTL);
 #undef L_EXTL
         return;
     }
 #define L_EXT(S) hipLaunchKernelGGL((k_extend<S, STATS, false>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, out, s.sh, s.L, kc, tail)
-    IGX_DISPATCH_STACK(dev->stack_depth, L_EXT);
+    IGX_DISPATCH_VARIANT(dev->variant, L_EXT);
 #undef L_EXT
 }
-// k_trace variants: the 16-entry stack build comes with an occupancy target
-// (waves per SIMD, option "trace_waves"); deeper stacks are LDS-limited anyway.
-// With the traversal tables staged in LDS (small scenes) LDS sets occupancy.
+// k_trace variants: an occupancy target (waves per SIMD, option
+// "trace_waves"), unless the traversal tables are staged in LDS (small
+// scenes), where LDS sets occupancy.
 template <bool STATS, int W>
 void launch_trace_w(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const PathBuf& in, const int* cnt, int tail) {
-#define L_TR(S) hipLaunchKernelGGL((k_trace<S, STATS, (S == 16 ? W : 1), false>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, s.hb, cnt, tail, dev->dstats)
-    IGX_DISPATCH_STACK(dev->stack_depth, L_TR);
+#define L_TR(S) hipLaunchKernelGGL((k_trace<S, STATS, W, false>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, s.hb, cnt, tail, dev->dstats)
+    IGX_DISPATCH_VARIANT(dev->variant, L_TR);
 #undef L_TR
 }
 template <bool STATS>
 void launch_trace(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const PathBuf& in, const int* cnt, int tail) {
     if (dev->lds_scene_bytes) {
 #define L_TRL(S) hipLaunchKernelGGL((k_trace<S, STATS, 1, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->stream, fa, dev->sv, in, s.hb, cnt, tail, dev->dstats)
-        IGX_DISPATCH_STACK(dev->stack_depth, L_TRL);
+        IGX_DISPATCH_VARIANT(dev->variant, L_TRL);
 #undef L_TRL
         return;
     }
-    switch (dev->trace_waves) {
-    case 5: launch_trace_w<STATS, 5>(dev, s, grid, fa, in, cnt, tail); break;
-    case 6: launch_trace_w<STATS, 6>(dev, s, grid, fa, in, cnt, tail); break;
-    case 8: launch_trace_w<STATS, 8>(dev, s, grid, fa, in, cnt, tail); break;
-    default: launch_trace_w<STATS, 1>(dev, s, grid, fa, in, cnt, tail); break;
-    }
+    if (dev->trace_waves == 5) launch_trace_w<STATS, 5>(dev, s, grid, fa, in, cnt, tail);
+    else launch_trace_w<STATS, 1>(dev, s, grid, fa, in, cnt, tail);
 }
 template <bool STATS>
 void launch_shadow(igx_device* dev, Slot& s, int grid, const int* cnt) {
     if (dev->lds_scene_bytes) {
 #define L_SHL(S) hipLaunchKernelGGL((k_shadow<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->stream, dev->sv, s.sh, s.L, cnt, dev->dstats)
-        IGX_DISPATCH_STACK(dev->stack_depth, L_SHL);
+        IGX_DISPATCH_VARIANT(dev->variant, L_SHL);
 #undef L_SHL
         return;
     }
 #define L_SH(S) hipLaunchKernelGGL((k_shadow<S, STATS, false>), dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, s.sh, s.L, cnt, dev->dstats)
-    IGX_DISPATCH_STACK(dev->stack_depth, L_SH);
+    IGX_DISPATCH_VARIANT(dev->variant, L_SH);
 #undef L_SH
 }
 template <bool STATS>
 void launch_finish(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const PathBuf& in, const int* cnt, int tail) {
+    SceneView tsv = dev->sv;
+    tsv.spill = dev->spill_tail; // k_finish runs concurrently with the main stream's kernels
     if (dev->lds_scene_bytes) {
-#define L_FINL(S) hipLaunchKernelGGL((k_finish<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->tail_stream, fa, dev->sv, in, s.L, cnt, tail, dev->dstats, dev->tail_counts)
-        IGX_DISPATCH_STACK(dev->stack_depth, L_FINL);
+#define L_FINL(S) hipLaunchKernelGGL((k_finish<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->tail_stream, fa, tsv, in, s.L, cnt, tail, dev->dstats, dev->tail_counts)
+        IGX_DISPATCH_VARIANT(dev->variant, L_FINL);
 #undef L_FINL
         return;
     }
-#define L_FIN(S) hipLaunchKernelGGL((k_finish<S, STATS, false>), dim3(grid), dim3(BLOCK), 0, dev->tail_stream, fa, dev->sv, in, s.L, cnt, tail, dev->dstats, dev->tail_counts)
-    IGX_DISPATCH_STACK(dev->stack_depth, L_FIN);
+#define L_FIN(S) hipLaunchKernelGGL((k_finish<S, STATS, false>), dim3(grid), dim3(BLOCK), 0, dev->tail_stream, fa, tsv, in, s.L, cnt, tail, dev->dstats, dev->tail_counts)
+    IGX_DISPATCH_VARIANT(dev->variant, L_FIN);
 #undef L_FIN
 }
 
@@ -884,57 +915,28 @@ int resident_blocks(K kernel, size_t dyn_lds = 0) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, BLOCK, dyn_lds) != hipSuccess || nb < 1) nb = 1;
     return nb;
 }
+#define IGX_RESIDENT(K, ...)                                                                          \
+    do {                                                                                              \
+        switch (v) {                                                                                  \
+        case 0: return lds ? resident_blocks(K<0, __VA_ARGS__, true>, lds) : resident_blocks(K<0, __VA_ARGS__, false>); \
+        case 1: return lds ? resident_blocks(K<1, __VA_ARGS__, true>, lds) : resident_blocks(K<1, __VA_ARGS__, false>); \
+        case 2: return lds ? resident_blocks(K<2, __VA_ARGS__, true>, lds) : resident_blocks(K<2, __VA_ARGS__, false>); \
+        default: return lds ? resident_blocks(K<3, __VA_ARGS__, true>, lds) : resident_blocks(K<3, __VA_ARGS__, false>); \
+        }                                                                                             \
+    } while (0)
 template <bool STATS>
-int extend_blocks_per_cu(int depth, size_t lds) {
-    if (lds) {
-        if (depth <= 16) return resident_blocks(k_extend<16, STATS, true>, lds);
-        if (depth <= 32) return resident_blocks(k_extend<32, STATS, true>, lds);
-        return resident_blocks(k_extend<64, STATS, true>, lds);
-    }
-    if (depth <= 16) return resident_blocks(k_extend<16, STATS, false>);
-    if (depth <= 32) return resident_blocks(k_extend<32, STATS, false>);
-    return resident_blocks(k_extend<64, STATS, false>);
-}
+int extend_blocks_per_cu(int v, size_t lds) { IGX_RESIDENT(k_extend, STATS); }
 template <bool STATS>
-int trace_blocks_per_cu(int depth, int waves, size_t lds) {
-    if (lds) {
-        if (depth <= 16) return resident_blocks(k_trace<16, STATS, 1, true>, lds);
-        if (depth <= 32) return resident_blocks(k_trace<32, STATS, 1, true>, lds);
-        return resident_blocks(k_trace<64, STATS, 1, true>, lds);
-    }
-    if (depth <= 16) {
-        switch (waves) {
-        case 5: return resident_blocks(k_trace<16, STATS, 5, false>);
-        case 6: return resident_blocks(k_trace<16, STATS, 6, false>);
-        case 8: return resident_blocks(k_trace<16, STATS, 8, false>);
-        default: return resident_blocks(k_trace<16, STATS, 1, false>);
-        }
-    }
-    if (depth <= 32) return resident_blocks(k_trace<32, STATS, 1, false>);
-    return resident_blocks(k_trace<64, STATS, 1, false>);
-}
+int shadow_blocks_per_cu(int v, size_t lds) { IGX_RESIDENT(k_shadow, STATS); }
 template <bool STATS>
-int shadow_blocks_per_cu(int depth, size_t lds) {
-    if (lds) {
-        if (depth <= 16) return resident_blocks(k_shadow<16, STATS, true>, lds);
-        if (depth <= 32) return resident_blocks(k_shadow<32, STATS, true>, lds);
-        return resident_blocks(k_shadow<64, STATS, true>, lds);
-    }
-    if (depth <= 16) return resident_blocks(k_shadow<16, STATS, false>);
-    if (depth <= 32) return resident_blocks(k_shadow<32, STATS, false>);
-    return resident_blocks(k_shadow<64, STATS, false>);
-}
+int finish_blocks_per_cu(int v, size_t lds) { IGX_RESIDENT(k_finish, STATS); }
 template <bool STATS>
-int finish_blocks_per_cu(int depth, size_t lds) {
-    if (lds) {
-        if (depth <= 16) return resident_blocks(k_finish<16, STATS, true>, lds);
-        if (depth <= 32) return resident_blocks(k_finish<32, STATS, true>, lds);
-        return resident_blocks(k_finish<64, STATS, true>, lds);
-    }
-    if (depth <= 16) return resident_blocks(k_finish<16, STATS, false>);
-    if (depth <= 32) return resident_blocks(k_finish<32, STATS, false>);
-    return resident_blocks(k_finish<64, STATS, false>);
+int trace_blocks_per_cu(int v, int waves, size_t lds) {
+    if (lds) IGX_RESIDENT(k_trace, STATS, 1);
+    if (waves == 5) IGX_RESIDENT(k_trace, STATS, 5);
+    IGX_RESIDENT(k_trace, STATS, 1);
 }
+#undef IGX_RESIDENT
 
 // Wait for the chunk last run in `s` and fold its statistics in.
 igx_status harvest(igx_device* dev, Slot& s) {
@@ -1102,8 +1104,12 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     else if (k == "trace_waves") dev->trace_waves = (int)value;
     else if (k == "lds_scene_max") {
         dev->lds_scene_max = value;
-        size_t b = ((size_t)dev->sv.num_nodes * 4 + (size_t)dev->sv.num_inst * 4 + (size_t)dev->sv.num_tris * 3) * 16;
+        size_t b = ((size_t)dev->sv.num_nodes * dev->sv.node_f4 + (size_t)dev->sv.num_inst * 4 + (size_t)dev->sv.num_tris * 3) * 16;
         dev->lds_scene_bytes = dev->has_scene && (int64_t)b <= value ? b : 0;
+    }
+    else if (k == "bvh_width") {
+        if (value != 0 && value != 2 && value != 4) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "bvh_width must be 0 (auto), 2 or 4");
+        dev->bvh_width_opt = (int)value;
     }
     else if (k == "bvh_leaf_size") {
         if (value < 1 || value > 16) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "bvh_leaf_size must be in [1, 16]");
@@ -1125,20 +1131,12 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     if (dst != IGX_OK) return dst;
     free_scene(dev);
 
-    // ---- BLAS per trimesh shape, analytic spheres -------------------------
-    std::vector<igx::BvhNode> nodes;
-    std::vector<float4> tris, vtx, nrm, spheres;
-    std::vector<int4> idx;
-    struct ShapeDev { int type, root, vtx_off, idx_off_or_sphere; };
-    std::vector<ShapeDev> sdev(desc->num_shapes);
-    int blas_depth = 0;
+    // ---- phase 1: BVH2 of every trimesh shape and of the entity TLAS ------
+    std::vector<igx::BvhBuildResult> brs(desc->num_shapes);
+    int blas_depth2 = 0;
     for (uint32_t s = 0; s < desc->num_shapes; ++s) {
         const igx_shape& sh = desc->shapes[s];
-        if (sh.type == IGX_SHAPE_SPHERE) {
-            sdev[s] = {1, -1, 0, (int)spheres.size()};
-            spheres.push_back(make_float4(sh.sphere[0], sh.sphere[1], sh.sphere[2], sh.sphere[3]));
-            continue;
-        }
+        if (sh.type == IGX_SHAPE_SPHERE) continue;
         if (sh.mesh < 0 || (uint32_t)sh.mesh >= desc->num_meshes)
             return fail(dev, IGX_ERR_INVALID_ARGUMENT, "shape references an invalid mesh");
         const igx_mesh& m = desc->meshes[sh.mesh];
@@ -1161,28 +1159,97 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
                 bi.centroid[3 * f + a] = 0.5f * (lo + hi);
             }
         }
-        igx::BvhBuildResult br;
         try {
-            br = igx::build_bvh2(bi, dev->leaf_size);
+            brs[s] = igx::build_bvh2(bi, dev->leaf_size);
         } catch (const std::exception& ex) {
             return fail(dev, IGX_ERR_INVALID_ARGUMENT, ex.what());
         }
-        blas_depth = std::max(blas_depth, br.depth);
-        int node_off = (int)nodes.size();
-        int tri_off = (int)(tris.size() / 3);
-        for (auto nd : br.nodes) {
-            for (int k = 0; k < 2; ++k) {
-                if (nd.ref[k] >= 0) nd.ref[k] += node_off;
-                else if (nd.b[k * 6] <= nd.b[k * 6 + 1]) { // leaf (empty children keep ref -1)
-                    int code = ~nd.ref[k];
-                    int first = (code >> igx::kLeafCountBits) + tri_off;
-                    int count = (code & ((1 << igx::kLeafCountBits) - 1)) + 1;
-                    if (first >= (1 << 26)) return fail(dev, IGX_ERR_UNSUPPORTED, "too many triangles for the leaf encoding");
-                    nd.ref[k] = igx::encode_leaf(first, count);
-                }
+        blas_depth2 = std::max(blas_depth2, brs[s].depth);
+    }
+    igx::BvhBuildResult tlas_br;
+    if (desc->num_entities > 0) {
+        igx::BvhBuildInput bi;
+        for (uint32_t e = 0; e < desc->num_entities; ++e) {
+            const igx_entity& en = desc->entities[e];
+            if (en.shape < 0 || (uint32_t)en.shape >= desc->num_shapes)
+                return fail(dev, IGX_ERR_INVALID_ARGUMENT, "entity references an invalid shape");
+            if (en.material < 0 || (uint32_t)en.material >= desc->num_materials)
+                return fail(dev, IGX_ERR_INVALID_ARGUMENT, "entity references an invalid material");
+            for (int a = 0; a < 3; ++a) {
+                bi.bmin.push_back(en.bbox_min[a]);
+                bi.bmax.push_back(en.bbox_max[a]);
+                bi.centroid.push_back(0.5f * (en.bbox_min[a] + en.bbox_max[a]));
             }
-            nodes.push_back(nd);
         }
+        tlas_br = igx::build_bvh2(bi, 1);
+    }
+    // Node width: BVH2 while its whole stack fits the LDS column (fewer,
+    // cheaper node steps on small scenes), else 4-wide nodes (half the node
+    // iterations on deep trees; the deepest entries spill).  Option
+    // "bvh_width" forces either.
+    const int width = dev->bvh_width_opt == 2 || dev->bvh_width_opt == 4
+                          ? dev->bvh_width_opt
+                          : (tlas_br.depth + blas_depth2 + 3 <= LDS_STACK ? 2 : 4);
+    const int nf4 = node_f4(width);
+
+    // ---- phase 2: node, triangle and instance tables ----------------------
+    std::vector<float4> nodes; // nf4 float4s per node
+    std::vector<float4> tris, vtx, nrm, spheres;
+    std::vector<int4> idx;
+    // Append a built BVH2 (as Node2, or collapsed to 4-wide nodes) to the
+    // unified node array: inner refs move by the array offset, leaf codes by
+    // `leaf_off` slots.  Returns the node offset; `need` = stack entries the
+    // tree can occupy.
+    auto append_nodes = [&](const igx::BvhBuildResult& br, int leaf_off, int& need) -> int {
+        const int node_off = (int)(nodes.size() / nf4);
+        auto move_leaf = [&](int32_t ref) {
+            int code = ~ref;
+            return igx::encode_leaf((code >> igx::kLeafCountBits) + leaf_off, (code & ((1 << igx::kLeafCountBits) - 1)) + 1);
+        };
+        if (width == 2) {
+            for (auto nd : br.nodes) {
+                for (int k = 0; k < 2; ++k) {
+                    if (nd.ref[k] >= 0) nd.ref[k] += node_off;
+                    else if (nd.b[k * 6] <= nd.b[k * 6 + 1]) nd.ref[k] = move_leaf(nd.ref[k]); // empty children keep -1
+                }
+                float4 f[4];
+                std::memcpy(f, &nd, 64);
+                nodes.insert(nodes.end(), f, f + 4);
+            }
+            need = br.depth;
+        } else {
+            igx::Bvh4Result b4 = igx::collapse_bvh4(br);
+            for (auto nd : b4.nodes) {
+                for (int k = 0; k < 4; ++k) {
+                    if (nd.ref[k] >= 0) nd.ref[k] += node_off;
+                    else if (nd.ref[k] != igx::kEmptyRef) nd.ref[k] = move_leaf(nd.ref[k]);
+                }
+                float4 f[8];
+                std::memcpy(f, &nd, 128);
+                nodes.insert(nodes.end(), f, f + 8);
+            }
+            need = b4.stack_need;
+        }
+        return node_off;
+    };
+    struct ShapeDev { int type, root, vtx_off, idx_off_or_sphere; };
+    std::vector<ShapeDev> sdev(desc->num_shapes);
+    int blas_depth = 0;
+    for (uint32_t s = 0; s < desc->num_shapes; ++s) {
+        const igx_shape& sh = desc->shapes[s];
+        if (sh.type == IGX_SHAPE_SPHERE) {
+            sdev[s] = {1, -1, 0, (int)spheres.size()};
+            spheres.push_back(make_float4(sh.sphere[0], sh.sphere[1], sh.sphere[2], sh.sphere[3]));
+            continue;
+        }
+        const igx_mesh& m = desc->meshes[sh.mesh];
+        const igx::BvhBuildResult& br = brs[s];
+        int tri_off = (int)(tris.size() / 3);
+        if (tri_off + br.prim_order.size() >= (size_t)(1 << 26))
+            return fail(dev, IGX_ERR_UNSUPPORTED, "too many triangles for the leaf encoding");
+        int need = 0;
+        int node_off = append_nodes(br, tri_off, need);
+        blas_depth = std::max(blas_depth, need);
         for (uint32_t slot = 0; slot < br.prim_order.size(); ++slot) {
             uint32_t f = br.prim_order[slot];
             const uint32_t* ix = m.indices + 3 * f;
@@ -1210,6 +1277,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
         }
         for (uint32_t f = 0; f < m.num_faces; ++f)
             idx.push_back(make_int4((int)m.indices[3 * f], (int)m.indices[3 * f + 1], (int)m.indices[3 * f + 2], 0));
+        brs[s] = igx::BvhBuildResult{}; // release the host copy
     }
 
     // ---- TLAS over entities (leaf size 1), instance records ---------------
@@ -1217,27 +1285,8 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     int tlas_root = -1;
     int tlas_depth = 0;
     if (desc->num_entities > 0) {
-        igx::BvhBuildInput bi;
-        for (uint32_t e = 0; e < desc->num_entities; ++e) {
-            const igx_entity& en = desc->entities[e];
-            if (en.shape < 0 || (uint32_t)en.shape >= desc->num_shapes)
-                return fail(dev, IGX_ERR_INVALID_ARGUMENT, "entity references an invalid shape");
-            if (en.material < 0 || (uint32_t)en.material >= desc->num_materials)
-                return fail(dev, IGX_ERR_INVALID_ARGUMENT, "entity references an invalid material");
-            for (int a = 0; a < 3; ++a) {
-                bi.bmin.push_back(en.bbox_min[a]);
-                bi.bmax.push_back(en.bbox_max[a]);
-                bi.centroid.push_back(0.5f * (en.bbox_min[a] + en.bbox_max[a]));
-            }
-        }
-        igx::BvhBuildResult br = igx::build_bvh2(bi, 1);
-        tlas_depth = br.depth;
-        int node_off = (int)nodes.size();
-        for (auto nd : br.nodes) {
-            for (int k = 0; k < 2; ++k)
-                if (nd.ref[k] >= 0) nd.ref[k] += node_off;
-            nodes.push_back(nd);
-        }
+        const igx::BvhBuildResult& br = tlas_br;
+        int node_off = append_nodes(br, 0, tlas_depth);
         tlas_root = br.root_is_leaf ? br.root_leaf_ref : node_off; // single entity: start at its leaf
         for (uint32_t slot = 0; slot < br.prim_order.size(); ++slot) {
             uint32_t e = br.prim_order[slot];
@@ -1372,11 +1421,9 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     }
 
     // ---- upload ----------------------------------------------------------
-    std::vector<float4> node4(nodes.size() * 4);
-    if (!nodes.empty()) std::memcpy(node4.data(), nodes.data(), nodes.size() * 64);
     SceneView sv{};
     igx_status st;
-    if ((st = upload(dev, node4, &sv.nodes)) || (st = upload(dev, tris, &sv.tris)) || (st = upload(dev, inst, &sv.inst)) ||
+    if ((st = upload(dev, nodes, &sv.nodes)) || (st = upload(dev, tris, &sv.tris)) || (st = upload(dev, inst, &sv.inst)) ||
         (st = upload(dev, spheres, &sv.spheres)) || (st = upload(dev, ent, &sv.ent)) || (st = upload(dev, vtx, &sv.vtx)) ||
         (st = upload(dev, nrm, &sv.nrm)) || (st = upload(dev, idx, &sv.idx)) || (st = upload(dev, mats, &sv.mats)) ||
         (st = upload(dev, lights, &sv.lights))) {
@@ -1384,11 +1431,13 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
         return st;
     }
     sv.tlas_root = tlas_root;
-    sv.num_nodes = (int)nodes.size();
+    sv.num_nodes = (int)(nodes.size() / nf4);
+    sv.node_f4 = nf4;
+    dev->bvh_width = width;
     sv.num_inst = (int)(inst.size() / 4);
     sv.num_tris = (int)(tris.size() / 3);
     {
-        size_t b = ((size_t)sv.num_nodes * 4 + (size_t)sv.num_inst * 4 + (size_t)sv.num_tris * 3) * 16;
+        size_t b = ((size_t)sv.num_nodes * nf4 + (size_t)sv.num_inst * 4 + (size_t)sv.num_tris * 3) * 16;
         dev->lds_scene_bytes = (int64_t)b <= dev->lds_scene_max ? b : 0;
     }
     sv.num_lights = (int)lights.size();
@@ -1404,13 +1453,16 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     sv.clamp = desc->technique.clamp;
     dev->cam_desc = desc->camera;
     dev->sv = sv;
-    // stack: TLAS depth + BLAS depth + marker + resume entry + exit sentinel
+    // stack: TLAS pushes + BLAS pushes (the depth for BVH2) + marker + resume entry + exit sentinel
     dev->scene_depth = tlas_depth + blas_depth + 3;
-    if (dev->scene_depth > 64) {
+    if (dev->scene_depth > MAX_STACK) {
         free_scene(dev);
-        return fail(dev, IGX_ERR_UNSUPPORTED, "BVH too deep for the 64-entry LDS stack (depth " + std::to_string(dev->scene_depth) + ")");
+        return fail(dev, IGX_ERR_UNSUPPORTED, "BVH too deep for the traversal stack (" + std::to_string(dev->scene_depth) + " entries)");
     }
-    dev->stack_depth = dev->scene_depth <= 16 ? 16 : (dev->scene_depth <= 32 ? 32 : 64);
+    if ((st = configure_stack(dev)) != IGX_OK) {
+        free_scene(dev);
+        return st;
+    }
     dev->has_scene = true;
     return IGX_OK;
 }
@@ -1494,7 +1546,7 @@ extern "C" igx_status igx_render(igx_device* dev, const igx_render_params* p) {
 
     const int max_bounces = std::min(std::max(dev->sv.max_depth, 1), MAX_BOUNCES - 1);
     const bool inst = dev->instrument;
-    const int sd = dev->stack_depth;
+    const int sd = dev->variant;
     const size_t ldsb = dev->lds_scene_bytes;
     const int ext_bpc = inst ? extend_blocks_per_cu<true>(sd, ldsb) : extend_blocks_per_cu<false>(sd, ldsb);
     const int tr_bpc = inst ? trace_blocks_per_cu<true>(sd, dev->trace_waves, dev->lds_scene_bytes)
@@ -1684,7 +1736,7 @@ extern "C" igx_status igx_get_stats(igx_device* dev, igx_stats* out) {
     if (st != IGX_OK) return st;
     *out = dev->stats;
     out->bvh_depth = dev->scene_depth;
-    out->stack_entries = dev->stack_depth <= 16 ? 16 : (dev->stack_depth <= 32 ? 32 : 64);
+    out->stack_entries = LDS_STACK;
     unsigned long long h[16] = {0};
     HIPCHK(hipMemcpy(h, dev->dstats, sizeof(h), hipMemcpyDeviceToHost));
     out->node_visits = h[0];
@@ -1700,6 +1752,8 @@ extern "C" igx_status igx_get_stats(igx_device* dev, igx_stats* out) {
     out->wave_leaf_iters = h[10];
     out->shadow_wave_node_iters = h[11];
     out->shadow_wave_leaf_iters = h[12];
+    out->bvh_width = dev->bvh_width;
+    out->node_bytes = node_f4(dev->bvh_width) * 16;
     return IGX_OK;
 }
 
@@ -1726,9 +1780,9 @@ static igx_status trace_batch(igx_device* dev, const float* rays, int32_t n, uin
     HIPCHK(hipMalloc((void**)&d_ep, (size_t)n * 2 * sizeof(int)));
     HIPCHK(hipMalloc((void**)&d_tuv, (size_t)n * 3 * sizeof(float)));
     HIPCHK(hipMemcpy(d_rays, rays, (size_t)n * 8 * sizeof(float), hipMemcpyHostToDevice));
-    int grid = (n + BLOCK - 1) / BLOCK;
+    int grid = grid_for(dev, n, MAX_BLOCKS_PER_CU);
 #define L_TH(S) hipLaunchKernelGGL(k_trace_hits<S>, dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, d_rays, n, flags, d_ep, d_tuv, any)
-    IGX_DISPATCH_STACK(dev->stack_depth, L_TH);
+    IGX_DISPATCH_VARIANT(dev->variant, L_TH);
 #undef L_TH
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(dev->stream));

@@ -30,6 +30,8 @@ struct SceneView {
     int max_depth, min_depth, nee;
     float clamp;
     int num_nodes, num_inst, num_tris; // table sizes (for staging the traversal tables in LDS)
+    int* spill;            // traversal-stack overflow area of the launching stream (see TStack)
+    int node_f4;           // float4s per BVH node (4: BVH2, 8: 4-wide)
 };
 
 // Copy the traversal tables (nodes, instances, triangles) of a small scene
@@ -38,7 +40,7 @@ struct SceneView {
 // path, which the divergent node fetches otherwise keep busy.
 template <int BLOCK_>
 __device__ __forceinline__ SceneView stage_scene_lds(const SceneView& sv, float4* lds) {
-    const int n4 = sv.num_nodes * 4, i4 = sv.num_inst * 4, t3 = sv.num_tris * 3;
+    const int n4 = sv.num_nodes * sv.node_f4, i4 = sv.num_inst * 4, t3 = sv.num_tris * 3;
     for (int k = threadIdx.x; k < n4; k += BLOCK_) lds[k] = sv.nodes[k];
     for (int k = threadIdx.x; k < i4; k += BLOCK_) lds[n4 + k] = sv.inst[k];
     for (int k = threadIdx.x; k < t3; k += BLOCK_) lds[n4 + i4 + k] = sv.tris[k];
@@ -93,6 +95,35 @@ struct Trav {
 
 __device__ __forceinline__ bool is_leaf_ref(int r) { return r < 0 && r > REF_EXIT; }
 
+// Per-lane traversal stack: the first `cap` entries live in an LDS column
+// (entry e at lds[e * stride]); deeper entries, which only rays in the
+// deepest parts of a wide or deep BVH reach, spill to a global column
+// (entry e at spill[(e - cap) * sstride], one column per grid thread).  A
+// small LDS stack thus serves every scene: LDS per block, and so occupancy,
+// no longer scales with the worst-case stack depth.
+struct TStack {
+    int* lds;
+    int* spill;
+    int cap;
+    int stride;
+    int sstride;
+};
+template <bool SPILL>
+__device__ __forceinline__ void tpush(const TStack& s, int& sp, int v) {
+    if (!SPILL || sp < s.cap) s.lds[sp * s.stride] = v;
+    else s.spill[(sp - s.cap) * s.sstride] = v;
+    ++sp;
+}
+template <bool SPILL>
+__device__ __forceinline__ int tpop(const TStack& s, int& sp) {
+    --sp;
+    return (!SPILL || sp < s.cap) ? s.lds[sp * s.stride] : s.spill[(sp - s.cap) * s.sstride];
+}
+__device__ __forceinline__ TStack make_tstack(int* lds_base, int cap, int* spill) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    return TStack{lds_base + threadIdx.x, spill + g, cap, (int)blockDim.x, (int)(gridDim.x * blockDim.x)};
+}
+
 // Closest-hit acceptance with an order-independent tie rule: among hits at the
 // same distance the larger (entity, primitive) wins.  The reference keeps the
 // later-visited one (t <= tmax, intersection.art:97), which depends on BVH
@@ -103,7 +134,7 @@ __device__ __forceinline__ bool accept_hit(const Trav& t, float th, int ent, int
 }
 
 __device__ __forceinline__ void trav_init(const SceneView& sv, Trav& t, f3 o, f3 d, float tmin, float tmax, uint32_t rflags,
-                                          int* stk) {
+                                          const TStack& ts) {
     t.o = o;
     t.d = d;
     t.lo = o;
@@ -120,7 +151,7 @@ __device__ __forceinline__ void trav_init(const SceneView& sv, Trav& t, f3 o, f3
     t.hv = 0;
     t.in_blas = false;
     t.found = false;
-    stk[0] = REF_EXIT;
+    ts.lds[0] = REF_EXIT;
     t.sp = 1;
     t.node = sv.num_inst > 0 ? sv.tlas_root : REF_EXIT; // the root may be a leaf (one entity)
 }
@@ -128,8 +159,8 @@ __device__ __forceinline__ void trav_init(const SceneView& sv, Trav& t, f3 o, f3
 // Slab test of both children of BVH2 node `node` (intersect_ray_box,
 // intersection.art:170-181, with ray.tmin folded in).  Returns the next node
 // (nearer child first; the other is pushed) or the popped entry.
-template <bool STATS>
-__device__ __forceinline__ int node_step(const SceneView& sv, const Trav& t, int node, int* stk, int stride, int& sp,
+template <bool STATS, bool SPILL>
+__device__ __forceinline__ int node_step2(const SceneView& sv, const Trav& t, int node, const TStack& ts, int& sp,
                                          TraceStats& st) {
     if (STATS) {
         st.nodes++;
@@ -155,13 +186,78 @@ __device__ __forceinline__ int node_step(const SceneView& sv, const Trav& t, int
     bool h0 = en0 <= ex0, h1 = en1 <= ex1;
     if (h0 && h1) {
         bool first0 = en0 < en1;
-        stk[sp * stride] = first0 ? r.y : r.x;
-        ++sp;
+        tpush<SPILL>(ts, sp, first0 ? r.y : r.x);
         return first0 ? r.x : r.y;
     }
     if (h0) return r.x;
     if (h1) return r.y;
-    return stk[(--sp) * stride];
+    return tpop<SPILL>(ts, sp);
+}
+
+// Slab test of the four children of a 4-wide node (SoA bounds: one float4 per
+// bound, child k in component k).  Hit children are ordered by entry distance
+// with a 5-exchange sorting network; the nearest is returned and the others
+// pushed farthest-first, or the stack is popped when none is hit.  Absent
+// children have +inf bounds, which no slab test accepts.
+__device__ __forceinline__ void slab4(float lo, float hi, float idir, float iorg, float& tn, float& tf) {
+    float a = fmaf(lo, idir, iorg), b = fmaf(hi, idir, iorg);
+    tn = fminf(a, b);
+    tf = fmaxf(a, b);
+}
+__device__ __forceinline__ void cswap(float& da, int& ra, float& db, int& rb) {
+    bool sw = db < da;
+    float td = sw ? db : da;
+    int tr = sw ? rb : ra;
+    db = sw ? da : db;
+    rb = sw ? ra : rb;
+    da = td;
+    ra = tr;
+}
+template <bool STATS, bool SPILL>
+__device__ __forceinline__ int node_step4(const SceneView& sv, const Trav& t, int node, const TStack& ts, int& sp,
+                                          TraceStats& st) {
+    if (STATS) {
+        st.nodes++;
+        if (first_active_lane()) st.wnodes++;
+    }
+    const float4* np = sv.nodes + 8 * node;
+    const float4 lx = np[0], hx = np[1], ly = np[2], hy = np[3], lz = np[4], hz = np[5];
+    const int4 r = *reinterpret_cast<const int4*>(np + 6);
+    float d[4];
+    int ref[4] = {r.x, r.y, r.z, r.w};
+    const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, HX[4] = {hx.x, hx.y, hx.z, hx.w};
+    const float LY[4] = {ly.x, ly.y, ly.z, ly.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w};
+    const float LZ[4] = {lz.x, lz.y, lz.z, lz.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
+    int n = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        float nx, fx, ny, fy, nz, fz;
+        slab4(LX[k], HX[k], t.idir.x, t.iorg.x, nx, fx);
+        slab4(LY[k], HY[k], t.idir.y, t.iorg.y, ny, fy);
+        slab4(LZ[k], HZ[k], t.idir.z, t.iorg.z, nz, fz);
+        float en = fmaxf(fmaxf(nx, ny), fmaxf(nz, t.tmin));
+        float ex = fminf(fminf(fx, fy), fminf(fz, t.tmax));
+        bool h = en <= ex;
+        d[k] = h ? en : INFINITY;
+        n += h ? 1 : 0;
+    }
+    if (n == 0) return tpop<SPILL>(ts, sp);
+    cswap(d[0], ref[0], d[1], ref[1]);
+    cswap(d[2], ref[2], d[3], ref[3]);
+    cswap(d[0], ref[0], d[2], ref[2]);
+    cswap(d[1], ref[1], d[3], ref[3]);
+    cswap(d[1], ref[1], d[2], ref[2]);
+    if (n > 3) tpush<SPILL>(ts, sp, ref[3]);
+    if (n > 2) tpush<SPILL>(ts, sp, ref[2]);
+    if (n > 1) tpush<SPILL>(ts, sp, ref[1]);
+    return ref[0];
+}
+
+template <bool STATS, int V>
+__device__ __forceinline__ int node_step(const SceneView& sv, const Trav& t, int node, const TStack& ts, int& sp,
+                                         TraceStats& st) {
+    if constexpr (variant_width(V) == 4) return node_step4<STATS, variant_spill(V)>(sv, t, node, ts, sp, st);
+    else return node_step2<STATS, variant_spill(V)>(sv, t, node, ts, sp, st);
 }
 
 // Back from a BLAS: restore the world ray (recomputed: cheaper than keeping
@@ -263,11 +359,12 @@ __device__ __forceinline__ void tri_test(const SceneView& sv, Trav& t, int slot,
 // One traversal step (while-while): inner nodes down to a leaf, then that
 // leaf or the BLAS return marker.  Returns true once the ray is finished
 // (stack exhausted, or the first hit for ANY).
-template <bool ANY, bool STATS>
-__device__ __forceinline__ bool trav_step(const SceneView& sv, Trav& t, int* stk, int stride, TraceStats& st) {
+template <bool ANY, bool STATS, int V>
+__device__ __forceinline__ bool trav_step(const SceneView& sv, Trav& t, const TStack& ts, TraceStats& st) {
     int node = t.node;
     int sp = t.sp;
-    while (node >= 0) node = node_step<STATS>(sv, t, node, stk, stride, sp, st);
+    constexpr bool SPILL = variant_spill(V);
+    while (node >= 0) node = node_step<STATS, V>(sv, t, node, ts, sp, st);
     if (node == REF_EXIT) {
         t.node = node;
         t.sp = sp;
@@ -276,7 +373,7 @@ __device__ __forceinline__ bool trav_step(const SceneView& sv, Trav& t, int* stk
     if (STATS && first_active_lane()) st.wleaves++;
     if (node == REF_MARKER) {
         leave_blas(t);
-        t.node = stk[(--sp) * stride];
+        t.node = tpop<SPILL>(ts, sp);
         t.sp = sp;
         return false;
     }
@@ -297,11 +394,10 @@ __device__ __forceinline__ bool trav_step(const SceneView& sv, Trav& t, int* stk
             }
         }
         if (entered) {
-            stk[sp * stride] = REF_MARKER;
-            ++sp;
+            tpush<SPILL>(ts, sp, REF_MARKER);
             t.node = root;
         } else {
-            t.node = stk[(--sp) * stride];
+            t.node = tpop<SPILL>(ts, sp);
         }
     } else {
 #pragma unroll 1
@@ -313,20 +409,20 @@ __device__ __forceinline__ bool trav_step(const SceneView& sv, Trav& t, int* stk
                 return true;
             }
         }
-        t.node = stk[(--sp) * stride];
+        t.node = tpop<SPILL>(ts, sp);
     }
     t.sp = sp;
     return false;
 }
 
 // Whole-ray traversal (used by the tail kernel and the hit-level harness).
-template <bool ANY, bool STATS>
+template <bool ANY, bool STATS, int V>
 __device__ __forceinline__ bool trace_ray(const SceneView& sv, f3 o, f3 d, float tmin, float& tmax, uint32_t rflags,
-                                          int* stk, int stride, int& hit_ent, int& hit_prim, float& hu, float& hv,
+                                          const TStack& ts, int& hit_ent, int& hit_prim, float& hu, float& hv,
                                           TraceStats& st) {
     Trav t;
-    trav_init(sv, t, o, d, tmin, tmax, rflags, stk);
-    while (!trav_step<ANY, STATS>(sv, t, stk, stride, st)) {
+    trav_init(sv, t, o, d, tmin, tmax, rflags, ts);
+    while (!trav_step<ANY, STATS, V>(sv, t, ts, st)) {
     }
     tmax = t.tmax;
     hit_ent = t.hit_ent;

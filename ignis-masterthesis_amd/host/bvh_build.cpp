@@ -223,4 +223,104 @@ BvhBuildResult build_bvh2(const BvhBuildInput& in, int max_leaf, int bins) {
     return res;
 }
 
+namespace {
+
+struct Child2 {
+    float lo[3], hi[3];
+    int32_t ref; // BVH2 ref: >= 0 inner node index, < 0 leaf code
+};
+
+Child2 child_of(const BvhNode& n, int k) {
+    Child2 c;
+    const float* b = n.b + 6 * k;
+    c.lo[0] = b[0]; c.hi[0] = b[1];
+    c.lo[1] = b[2]; c.hi[1] = b[3];
+    c.lo[2] = b[4]; c.hi[2] = b[5];
+    c.ref = n.ref[k];
+    return c;
+}
+
+float half_area(const Child2& c) {
+    float dx = c.hi[0] - c.lo[0], dy = c.hi[1] - c.lo[1], dz = c.hi[2] - c.lo[2];
+    return dx * (dy + dz) + dy * dz;
+}
+
+} // namespace
+
+Bvh4Result collapse_bvh4(const BvhBuildResult& in) {
+    Bvh4Result res;
+    const float inf = std::numeric_limits<float>::infinity();
+    auto set = [&](Bvh4Node& n, int k, const Child2& c, int32_t ref) {
+        n.lo_x[k] = c.lo[0]; n.hi_x[k] = c.hi[0];
+        n.lo_y[k] = c.lo[1]; n.hi_y[k] = c.hi[1];
+        n.lo_z[k] = c.lo[2]; n.hi_z[k] = c.hi[2];
+        n.ref[k] = ref;
+    };
+    auto set_empty4 = [&](Bvh4Node& n, int k) {
+        n.lo_x[k] = n.hi_x[k] = n.lo_y[k] = n.hi_y[k] = n.lo_z[k] = n.hi_z[k] = inf;
+        n.ref[k] = kEmptyRef;
+    };
+    if (in.nodes.empty()) return res;
+    Bvh4Node root{};
+    for (int k = 0; k < 4; ++k) set_empty4(root, k);
+    res.nodes.push_back(root);
+    if (in.root_is_leaf || in.prim_order.empty()) {
+        if (in.root_is_leaf) set(res.nodes[0], 0, child_of(in.nodes[0], 0), in.root_leaf_ref);
+        res.depth = 1;
+        res.stack_need = 0;
+        return res;
+    }
+    // iterative DFS: (BVH2 inner node, output node, depth)
+    struct Item { int32_t src; int32_t out; int depth; };
+    std::vector<Item> stack{{0, 0, 1}};
+    std::vector<int> nchild(1, 0);
+    while (!stack.empty()) {
+        Item it = stack.back();
+        stack.pop_back();
+        res.depth = std::max(res.depth, it.depth);
+        Child2 kids[4];
+        int nk = 0;
+        kids[nk++] = child_of(in.nodes[it.src], 0);
+        kids[nk++] = child_of(in.nodes[it.src], 1);
+        while (nk < 4) {
+            int best = -1;
+            float best_area = -1;
+            for (int k = 0; k < nk; ++k)
+                if (kids[k].ref >= 0 && half_area(kids[k]) > best_area) { best = k; best_area = half_area(kids[k]); }
+            if (best < 0) break;
+            const BvhNode& e = in.nodes[kids[best].ref];
+            kids[best] = child_of(e, 0);
+            kids[nk++] = child_of(e, 1);
+        }
+        nchild[it.out] = nk;
+        // children in DFS order: inner children laid out after their parent
+        int32_t out_idx[4] = {-1, -1, -1, -1};
+        for (int k = 0; k < nk; ++k) {
+            if (kids[k].ref >= 0) {
+                out_idx[k] = (int32_t)res.nodes.size();
+                Bvh4Node nn{};
+                for (int j = 0; j < 4; ++j) set_empty4(nn, j);
+                res.nodes.push_back(nn);
+                nchild.push_back(0);
+                set(res.nodes[it.out], k, kids[k], out_idx[k]);
+            } else {
+                set(res.nodes[it.out], k, kids[k], kids[k].ref);
+            }
+        }
+        for (int k = nk - 1; k >= 0; --k)
+            if (out_idx[k] >= 0) stack.push_back({kids[k].ref, out_idx[k], it.depth + 1});
+    }
+    // stack need: pushes along a path = sum over its nodes of (children - 1);
+    // children come after their parent, so one reverse sweep computes it
+    std::vector<int> need(res.nodes.size(), 0);
+    for (size_t i = res.nodes.size(); i-- > 0;) {
+        int below = 0;
+        for (int k = 0; k < 4; ++k)
+            if (res.nodes[i].ref[k] >= 0) below = std::max(below, need[res.nodes[i].ref[k]]);
+        need[i] = (nchild[i] - 1) + below;
+    }
+    res.stack_need = need[0];
+    return res;
+}
+
 } // namespace igx

@@ -55,4 +55,30 @@ struct BvhBuildResult {
 // Build a BVH2 with binned SAH.  `max_leaf` caps primitives per leaf (<= 16).
 BvhBuildResult build_bvh2(const BvhBuildInput& in, int max_leaf, int bins = 32);
 
+// 4-wide node (128 B, two 64-B halves): child boxes as SoA so one float4
+// load gives one bound of all four children.
+//   float4 lo_x, hi_x, lo_y, hi_y, lo_z, hi_z   (child k in lane k)
+//   int32  ref[4]: >= 0 inner node index, < 0 leaf code (encode_leaf), or
+//                  kEmptyRef for an absent child, whose box is +inf on every
+//                  bound so the slab test can never accept it
+//   int32  pad[4]
+struct Bvh4Node {
+    float lo_x[4], hi_x[4], lo_y[4], hi_y[4], lo_z[4], hi_z[4];
+    int32_t ref[4];
+    int32_t pad[4];
+};
+static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node must be 128 bytes");
+constexpr int32_t kEmptyRef = (int32_t)0x80000002;
+
+struct Bvh4Result {
+    std::vector<Bvh4Node> nodes; // nodes[0] is the root
+    int stack_need = 0;          // worst-case traversal stack entries: max over paths of sum(children - 1)
+    int depth = 0;               // 4-wide levels
+};
+
+// Collapse a BVH2 into a BVH4: every 4-wide node absorbs the largest-area
+// inner grandchildren of its BVH2 node until it has four children (the
+// surface-area collapse of wide-BVH builders).  Leaf codes are kept.
+Bvh4Result collapse_bvh4(const BvhBuildResult& bvh2);
+
 } // namespace igx

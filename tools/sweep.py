@@ -13,6 +13,8 @@ p = ignis_amd.RenderParams(); p.width, p.height, p.spi = W, H, 8
 for o in opts:
     for k, v in o.items():
         dev.set_option(k, v)
+    if any(k in ("bvh_width", "bvh_leaf_size") for k in o):
+        dev.upload(scene)  # these take effect at upload
     for it in range(2):
         p.iteration = it; dev.render(p)
     dev.reset_stats(); dev.set_option("timing", 1)
@@ -27,4 +29,4 @@ for o in opts:
                       "tr": round(s["ms_trace"] / K, 3), "ext": round(s["ms_extend"] / K, 3), "sh": round(s["ms_shadow"] / K, 3), "fin": round(s["ms_finish"] / K, 3),
                       "gen": round(s["ms_generate"] / K, 3), "res": round(s["ms_resolve"] / K, 3),
                       "wf_bounces": s["launches_extend"] / K, "tail_rays": (s["tail_bounce_rays"] + s["tail_shadow_rays"]) / K,
-                      "depth": s["bvh_depth"], "stack": s["stack_entries"]}), flush=True)
+                      "depth": s["bvh_depth"], "width": s["bvh_width"]}), flush=True)
