@@ -40,12 +40,14 @@ constexpr int BLOCK = 256;
 constexpr int MAX_BLOCKS_PER_CU = 8;  // 2048 threads per CU; grids never exceed num_cus * this
 constexpr int MAX_STACK = 128;        // traversal stack entries (LDS + spill) per ray
 constexpr int MAX_BOUNCES = 256;
-// Occupancy target (waves per SIMD) of k_extend: 4 caps it at 128 VGPRs
-// without spills (the compiler's own choice is 142 -> 3 waves); measured
-// 9 % faster per diamond bounce.  k_finish keeps the compiler's choice (it
-// would spill).
+// Occupancy target (waves per SIMD) of k_extend, with global and with
+// LDS-staged traversal tables: 4 caps it at 128 VGPRs.  k_finish keeps the
+// compiler's choice (it would spill).
 #ifndef EXTEND_WAVES
 #define EXTEND_WAVES 4
+#endif
+#ifndef EXTEND_WAVES_LDS
+#define EXTEND_WAVES_LDS 4
 #endif
 
 // ---------------------------------------------------------------------------
@@ -400,7 +402,7 @@ __device__ __forceinline__ void block_append2(bool a, bool b, int* ca, int* cb, 
 // extend kernel: one bounce for every live path, compacted outputs
 // ---------------------------------------------------------------------------
 template <int V, bool STATS, bool LDS>
-__global__ void __launch_bounds__(BLOCK, EXTEND_WAVES) k_extend(FrameArgs fa, SceneView gsv, PathBuf in, PathBuf out, ShadowBuf sh,
+__global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : EXTEND_WAVES) k_extend(FrameArgs fa, SceneView gsv, PathBuf in, PathBuf out, ShadowBuf sh,
                                                   float4* L, KernelCounters kc, int tail_threshold) {
     __shared__ int stack_mem[LDS_STACK * BLOCK + 2 * (BLOCK / 64) + 2];
     extern __shared__ float4 lds_scene[];

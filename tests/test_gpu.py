@@ -122,6 +122,30 @@ def test_hit_parity_camera_and_random(device, root, name):
         assert_hit_parity(device.trace_hits(rays, flags), orc.trace_hits(rays, flags), rays, flags)
 
 
+@pytest.mark.parametrize("name", ["diamond_scene.json", "s_deep.json"])
+def test_bvh_width_invariance(device, root, name):
+    """BVH2 and the collapsed 4-wide BVH (each with and without stack spill:
+    diamond's BVH2 fits the LDS stack, S-deep's does not) return the same closest
+    hits and images bit for bit: the tie rule makes hits independent of topology
+    and traversal order."""
+    sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", name))
+    rays = np.concatenate([camera_rays(sc, 200, 200, jitter=0.41), random_rays(sc, 50000, seed=5)])
+    res, imgs = [], []
+    try:
+        for width in (2, 4):
+            device.set_option("bvh_width", width)
+            device.upload(sc)
+            assert device.stats()["bvh_width"] == width
+            res.append(device.trace_hits(rays, 0x1))
+            imgs.append(render_gpu(device, sc, 96, 96, 4))
+    finally:
+        device.set_option("bvh_width", 0)
+    (ep2, tuv2), (ep4, tuv4) = res
+    np.testing.assert_array_equal(ep2, ep4)
+    np.testing.assert_array_equal(tuv2, tuv4)
+    np.testing.assert_array_equal(imgs[0], imgs[1])
+
+
 @pytest.mark.parametrize("name", ["diamond_scene.json", "primitives.json", "s_deep.json", "s_soup_1m.json"])
 def test_occlusion_parity(device, root, name):
     sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", name))
