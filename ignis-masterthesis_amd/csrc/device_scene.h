@@ -16,13 +16,16 @@ constexpr int32_t REF_MARKER = (int32_t)0x80000000; // return from a BLAS to the
 constexpr int32_t REF_EXIT = (int32_t)0x80000001;   // bottom of the traversal stack
 constexpr int LEAF_COUNT_BITS = 4;
 
-// Traversal variant V (a kernel template parameter): bit 1 = 4-wide nodes
-// (128-B SoA node, host Bvh4Node) instead of BVH2 (64-B Node2, host BvhNode);
-// bit 0 = the scene's stack need exceeds the LDS stack, so pushes and pops
-// check for the spill area.  The upload picks the width per scene.
+// Kernel variant V (a template parameter): bit 1 = 4-wide nodes (128-B SoA
+// node, host Bvh4Node) instead of BVH2 (64-B Node2, host BvhNode); bit 0 =
+// the scene's stack need exceeds the LDS stack, so pushes and pops check for
+// the spill area; bit 2 = the scene uses materials or lights beyond the basic
+// set (igx_kernels.h, bsdf_eval), compiled into the shading kernels only then.
+// The upload picks the variant per scene.
 constexpr int LDS_STACK = 16; // LDS traversal-stack entries per lane
 __host__ __device__ constexpr int variant_width(int v) { return (v & 2) ? 4 : 2; }
 __host__ __device__ constexpr bool variant_spill(int v) { return (v & 1) != 0; }
+__host__ __device__ constexpr bool variant_full(int v) { return (v & 4) != 0; }
 __host__ __device__ constexpr int node_f4(int width) { return width == 4 ? 8 : 4; }
 
 // Instance record (one per TLAS leaf slot): 64 B

@@ -229,6 +229,7 @@ __device__ __forceinline__ void ray_extent(const FrameArgs& fa, const SceneView&
 // advances `ps` by one bounce.  Returns whether the path continues (ps then
 // holds the bounced ray); fills the radiance gathered at this vertex (Lacc,
 // has_l) and the NEE shadow ray (has_shadow, sr).
+template <bool FULL>
 __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView& sv, PathState& ps, int hit_ent,
                                            int hit_prim, float tmax, float hu, float hv, f3& Lacc, bool& has_l,
                                            bool& has_shadow, ShadowRec& sr) {
@@ -258,7 +259,7 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
         if (dt > FLT_EPS_) {
             const DevLight& Lt = sv.lights[m.light];
             f3 emit = mk(Lt.radiance[0], Lt.radiance[1], Lt.radiance[2]);
-            float pdf_s = light_pdf_direct_solid(sv, Lt, ps.o, dt, tmax * tmax, hu, hv);
+            float pdf_s = light_pdf_direct_solid<FULL>(sv, Lt, ps.o, dt, tmax * tmax, hu, hv);
             float mis = sv.nee ? 1 / (1 + ps.inv_pdf * (1.0f / (float)sv.num_lights) * pdf_s) : 1.0f;
             Lacc = add(Lacc, handle_color(sv, mulf(mul(ps.contrib, emit), mis)));
             has_l = true;
@@ -269,13 +270,13 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
     local_to_global(fa, fa.chunk_pixel0 + ps.slot / fa.spi, px, py);
     Rng rnd{create_random_seed(sample, fa.iter, fa.frame, px, py, fa.seed), ps.counter};
     f3 out_dir = neg(rd);
-    const bool specular = bsdf_is_specular(m);
+    const bool specular = bsdf_is_specular<FULL>(m);
     // on_shadow (pathtracer.art:52-112)
     if (sv.nee && !specular && sv.num_lights > 0 && ps.depth + 1 <= sv.max_depth) {
         int lid = sv.num_lights <= 1 ? 0 : rnd.next_i32(0, sv.num_lights - 1);
         float sel_pdf = 1.0f / (float)sv.num_lights;
         const DevLight& Lt = sv.lights[lid];
-        DirectSample ls = light_sample_direct(sv, Lt, rnd, s);
+        DirectSample ls = light_sample_direct<FULL>(sv, Lt, rnd, s);
         float pdf_l_s = pdf_as_solid(ls.pdf_value, ls.pdf_solid, ls.cos, ls.dist * ls.dist) * sel_pdf;
         if (pdf_l_s > FLT_EPS_ && ls.cos > FLT_EPS_) {
             f3 in_dir = ls.dir;
@@ -283,11 +284,11 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
             if (Lt.delta) {
                 mis = 1.0f;
             } else {
-                float pdf_e_s = bsdf_pdf(m, s, in_dir, out_dir); // pdf to sample the light by the bsdf
+                float pdf_e_s = bsdf_pdf<FULL>(m, s, in_dir, out_dir); // pdf to sample the light by the bsdf
                 mis = 1 / (1 + pdf_e_s / pdf_l_s);
             }
             float factor = ls.pdf_value / pdf_l_s;
-            f3 ev = bsdf_eval(m, s, in_dir, out_dir);
+            f3 ev = bsdf_eval<FULL>(m, s, in_dir, out_dir);
             sr.color = handle_color(sv, mulf(mul(ls.intensity, mul(ps.contrib, ev)), mis * factor));
             sr.o = s.point;
             if (Lt.infinite) {
@@ -302,7 +303,7 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
     }
     // on_bounce (pathtracer.art:165-200)
     if (!(ps.depth + 1 <= sv.max_depth)) return false;
-    BsdfSample bs = bsdf_sample(m, s, rnd, out_dir);
+    BsdfSample bs = bsdf_sample<FULL>(m, s, rnd, out_dir);
     if (!bs.valid) return false;
     f3 c2 = mul(ps.contrib, bs.color);
     float rr = 1.0f;
@@ -334,7 +335,7 @@ __device__ __forceinline__ bool extend_step(const FrameArgs& fa, const SceneView
     float hu = 0, hv = 0;
     trace_ray<false, STATS, V>(sv, ps.o, ps.d, tmin, tmax, rflags, ts, hit_ent, hit_prim, hu, hv, st);
     if (STATS && hit_ent >= 0) st.hits++;
-    return shade_step(fa, sv, ps, hit_ent, hit_prim, tmax, hu, hv, Lacc, has_l, has_shadow, sr);
+    return shade_step<variant_full(V)>(fa, sv, ps, hit_ent, hit_prim, tmax, hu, hv, Lacc, has_l, has_shadow, sr);
 }
 
 __device__ __forceinline__ void add_radiance(float4* L, int slot, f3 c) {
@@ -497,7 +498,7 @@ __global__ void __launch_bounds__(BLOCK) k_shade(FrameArgs fa, SceneView sv, Pat
                 int prim = hits.prim[i];
                 f3 Lacc;
                 bool has_l;
-                alive = shade_step(fa, sv, ps, __float_as_int(h.w), prim, h.x, h.y, h.z, Lacc, has_l, has_shadow, sr);
+                alive = shade_step<true>(fa, sv, ps, __float_as_int(h.w), prim, h.x, h.y, h.z, Lacc, has_l, has_shadow, sr);
                 if (has_l) add_radiance(L, ps.slot, Lacc);
             }
         }
@@ -713,6 +714,8 @@ struct igx_device {
     int variant = 0;       // traversal variant of the scene (device_scene.h: width, spill)
     int bvh_width = 2;     // node width of the uploaded tables
     int bvh_width_opt = 0; // option "bvh_width": 0 = auto, 2, 4 (applies at the next upload)
+    bool full_shading = false;     // the scene needs materials / lights beyond the basic set
+    bool full_shading_opt = false; // option "full_shading": 1 = always compile-in the whole set
     int scene_depth = 0;   // worst-case stack entries of the scene
     int* spill_main = nullptr; // spill columns of the main and tail streams
     int* spill_tail = nullptr;
@@ -771,7 +774,7 @@ void free_scene(igx_device* dev) {
 igx_status configure_stack(igx_device* dev) {
     const int need = dev->scene_depth;
     const int extra = std::max(0, need - LDS_STACK);
-    dev->variant = (dev->bvh_width == 4 ? 2 : 0) | (extra > 0 ? 1 : 0);
+    dev->variant = (dev->bvh_width == 4 ? 2 : 0) | (extra > 0 ? 1 : 0) | (dev->full_shading ? 4 : 0);
     const size_t threads = (size_t)dev->num_cus * MAX_BLOCKS_PER_CU * BLOCK;
     for (int k = 0; k < 2; ++k) {
         int*& old = k == 0 ? dev->spill_main : dev->spill_tail;
@@ -842,11 +845,25 @@ int grid_for(igx_device* dev, long long items, int blocks_per_cu) {
 // Launch helpers dispatching on the scene's traversal variant.
 #define IGX_DISPATCH_VARIANT(v, MACRO)        \
     do {                                      \
-        switch (v) {                          \
+        switch ((v) & 3) {                    \
         case 0: MACRO(0); break;              \
         case 1: MACRO(1); break;              \
         case 2: MACRO(2); break;              \
         default: MACRO(3); break;             \
+        }                                     \
+    } while (0)
+// shading kernels also dispatch on the material/light feature bit
+#define IGX_DISPATCH_VARIANT8(v, MACRO)       \
+    do {                                      \
+        switch (v) {                          \
+        case 0: MACRO(0); break;              \
+        case 1: MACRO(1); break;              \
+        case 2: MACRO(2); break;              \
+        case 3: MACRO(3); break;              \
+        case 4: MACRO(4); break;              \
+        case 5: MACRO(5); break;              \
+        case 6: MACRO(6); break;              \
+        default: MACRO(7); break;             \
         }                                     \
     } while (0)
 
@@ -855,12 +872,12 @@ void launch_extend(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, cons
                    const KernelCounters& kc, int tail) {
     if (dev->lds_scene_bytes) {
 #define L_EXTL(S) hipLaunchKernelGGL((k_extend<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->stream, fa, dev->sv, in, out, s.sh, s.L, kc, tail)
-        IGX_DISPATCH_VARIANT(dev->variant, L_EXTL);
+        IGX_DISPATCH_VARIANT8(dev->variant, L_EXTL);
 #undef L_EXTL
         return;
     }
 #define L_EXT(S) hipLaunchKernelGGL((k_extend<S, STATS, false>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, out, s.sh, s.L, kc, tail)
-    IGX_DISPATCH_VARIANT(dev->variant, L_EXT);
+    IGX_DISPATCH_VARIANT8(dev->variant, L_EXT);
 #undef L_EXT
 }
 // k_trace variants: an occupancy target (waves per SIMD, option
@@ -901,12 +918,12 @@ void launch_finish(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, cons
     tsv.spill = dev->spill_tail; // k_finish runs concurrently with the main stream's kernels
     if (dev->lds_scene_bytes) {
 #define L_FINL(S) hipLaunchKernelGGL((k_finish<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->tail_stream, fa, tsv, in, s.L, cnt, tail, dev->dstats, dev->tail_counts)
-        IGX_DISPATCH_VARIANT(dev->variant, L_FINL);
+        IGX_DISPATCH_VARIANT8(dev->variant, L_FINL);
 #undef L_FINL
         return;
     }
 #define L_FIN(S) hipLaunchKernelGGL((k_finish<S, STATS, false>), dim3(grid), dim3(BLOCK), 0, dev->tail_stream, fa, tsv, in, s.L, cnt, tail, dev->dstats, dev->tail_counts)
-    IGX_DISPATCH_VARIANT(dev->variant, L_FIN);
+    IGX_DISPATCH_VARIANT8(dev->variant, L_FIN);
 #undef L_FIN
 }
 
@@ -917,21 +934,35 @@ int resident_blocks(K kernel, size_t dyn_lds = 0) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, BLOCK, dyn_lds) != hipSuccess || nb < 1) nb = 1;
     return nb;
 }
-#define IGX_RESIDENT(K, ...)                                                                          \
-    do {                                                                                              \
-        switch (v) {                                                                                  \
-        case 0: return lds ? resident_blocks(K<0, __VA_ARGS__, true>, lds) : resident_blocks(K<0, __VA_ARGS__, false>); \
-        case 1: return lds ? resident_blocks(K<1, __VA_ARGS__, true>, lds) : resident_blocks(K<1, __VA_ARGS__, false>); \
-        case 2: return lds ? resident_blocks(K<2, __VA_ARGS__, true>, lds) : resident_blocks(K<2, __VA_ARGS__, false>); \
-        default: return lds ? resident_blocks(K<3, __VA_ARGS__, true>, lds) : resident_blocks(K<3, __VA_ARGS__, false>); \
-        }                                                                                             \
+#define IGX_RES1(K, V, ...) return lds ? resident_blocks(K<V, __VA_ARGS__, true>, lds) : resident_blocks(K<V, __VA_ARGS__, false>)
+#define IGX_RESIDENT(K, ...)                                         \
+    do {                                                             \
+        switch (v & 3) {                                             \
+        case 0: IGX_RES1(K, 0, __VA_ARGS__);                         \
+        case 1: IGX_RES1(K, 1, __VA_ARGS__);                         \
+        case 2: IGX_RES1(K, 2, __VA_ARGS__);                         \
+        default: IGX_RES1(K, 3, __VA_ARGS__);                        \
+        }                                                            \
+    } while (0)
+#define IGX_RESIDENT8(K, ...)                                        \
+    do {                                                             \
+        switch (v) {                                                 \
+        case 0: IGX_RES1(K, 0, __VA_ARGS__);                         \
+        case 1: IGX_RES1(K, 1, __VA_ARGS__);                         \
+        case 2: IGX_RES1(K, 2, __VA_ARGS__);                         \
+        case 3: IGX_RES1(K, 3, __VA_ARGS__);                         \
+        case 4: IGX_RES1(K, 4, __VA_ARGS__);                         \
+        case 5: IGX_RES1(K, 5, __VA_ARGS__);                         \
+        case 6: IGX_RES1(K, 6, __VA_ARGS__);                         \
+        default: IGX_RES1(K, 7, __VA_ARGS__);                        \
+        }                                                            \
     } while (0)
 template <bool STATS>
-int extend_blocks_per_cu(int v, size_t lds) { IGX_RESIDENT(k_extend, STATS); }
+int extend_blocks_per_cu(int v, size_t lds) { IGX_RESIDENT8(k_extend, STATS); }
 template <bool STATS>
 int shadow_blocks_per_cu(int v, size_t lds) { IGX_RESIDENT(k_shadow, STATS); }
 template <bool STATS>
-int finish_blocks_per_cu(int v, size_t lds) { IGX_RESIDENT(k_finish, STATS); }
+int finish_blocks_per_cu(int v, size_t lds) { IGX_RESIDENT8(k_finish, STATS); }
 template <bool STATS>
 int trace_blocks_per_cu(int v, int waves, size_t lds) {
     if (lds) IGX_RESIDENT(k_trace, STATS, 1);
@@ -939,6 +970,8 @@ int trace_blocks_per_cu(int v, int waves, size_t lds) {
     IGX_RESIDENT(k_trace, STATS, 1);
 }
 #undef IGX_RESIDENT
+#undef IGX_RESIDENT8
+#undef IGX_RES1
 
 // Wait for the chunk last run in `s` and fold its statistics in.
 igx_status harvest(igx_device* dev, Slot& s) {
@@ -1109,6 +1142,7 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
         size_t b = ((size_t)dev->sv.num_nodes * dev->sv.node_f4 + (size_t)dev->sv.num_inst * 4 + (size_t)dev->sv.num_tris * 3) * 16;
         dev->lds_scene_bytes = dev->has_scene && (int64_t)b <= value ? b : 0;
     }
+    else if (k == "full_shading") dev->full_shading_opt = value != 0;
     else if (k == "bvh_width") {
         if (value != 0 && value != 2 && value != 4) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "bvh_width must be 0 (auto), 2 or 4");
         dev->bvh_width_opt = (int)value;
@@ -1461,6 +1495,17 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
         free_scene(dev);
         return fail(dev, IGX_ERR_UNSUPPORTED, "BVH too deep for the traversal stack (" + std::to_string(dev->scene_depth) + " entries)");
     }
+    // shading feature set (variant bit 2): beyond Lambert + dielectric and the
+    // plane/env/point/spot/directional/sun lights
+    dev->full_shading = dev->full_shading_opt;
+    for (uint32_t i = 0; i < desc->num_materials; ++i) {
+        const igx_material& m = desc->materials[i];
+        if (m.bsdf_type == IGX_BSDF_CONDUCTOR || m.bsdf_type == IGX_BSDF_PLASTIC ||
+            (m.bsdf_type == IGX_BSDF_DIFFUSE && m.diffuse_alpha > 1.1920929e-7f))
+            dev->full_shading = true;
+    }
+    for (uint32_t l = 0; l < desc->num_lights; ++l)
+        if (desc->lights[l].type == IGX_LIGHT_SPHERE || desc->lights[l].type == IGX_LIGHT_MESH) dev->full_shading = true;
     if ((st = configure_stack(dev)) != IGX_OK) {
         free_scene(dev);
         return st;

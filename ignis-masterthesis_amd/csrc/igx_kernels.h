@@ -561,6 +561,7 @@ __device__ __forceinline__ float pdf_as_solid(float value, bool solid, float cos
 }
 
 // Light::sample_direct for the light types on the hot path
+template <bool FULL>
 __device__ __forceinline__ DirectSample light_sample_direct(const SceneView& sv, const DevLight& L, Rng& rnd,
                                                             const Surface& from) {
     DirectSample ds;
@@ -639,7 +640,7 @@ __device__ __forceinline__ DirectSample light_sample_direct(const SceneView& sv,
         ds.pdf_solid = true;
         ds.cos = z;
         ds.dist = INFINITY;
-    } else if (L.type == LIGHT_SPHERE || L.type == LIGHT_MESH) {
+    } else if (FULL && (L.type == LIGHT_SPHERE || L.type == LIGHT_MESH)) {
         // make_area_light.sample_direct (light/area.art:12-27) over the sphere emitter
         // (area.art:248-274) or the triangle-shape emitter (area.art:48-57)
         float ux = rnd.next_f32();
@@ -733,14 +734,15 @@ __device__ __forceinline__ DirectSample light_sample_direct(const SceneView& sv,
 // Light::pdf_direct for lights that can be hit (area: plane, sphere, mesh; env),
 // in solid-angle measure.  (hu, hv) are the hit's prim_coords, which the
 // shape emitter reuses as its sample coordinates (light/area.art:41, 59-67).
+template <bool FULL>
 __device__ __forceinline__ float light_pdf_direct_solid(const SceneView& sv, const DevLight& L, f3 ray_org, float cos,
                                                         float dist2, float hu, float hv) {
     if (L.type == LIGHT_PLANE) {
         SQ q = compute_sq(L, ray_org);
         return safe_div(1, q.s); // solid measure
     }
-    if (L.type == LIGHT_SPHERE) return pdf_as_solid(2 / L.spot[0], false, cos, dist2); // area.art:282-284
-    if (L.type == LIGHT_MESH) {
+    if (FULL && L.type == LIGHT_SPHERE) return pdf_as_solid(2 / L.spot[0], false, cos, dist2); // area.art:282-284
+    if (FULL && L.type == LIGHT_MESH) {
         const float4* ep = sv.ent + ENT_STRIDE * L.entity;
         float4 g0 = ep[0], g1 = ep[1], g2 = ep[2];
         int4 info = *reinterpret_cast<const int4*>(ep + 6);
@@ -998,11 +1000,12 @@ __device__ __forceinline__ BsdfSample specular_lobe_sample(const DevMaterial& m,
 __device__ __forceinline__ bool lobe_is_specular(const DevMaterial& m) { return m.dist == MF_DELTA; }
 
 // Diffuse: Lambert, or Oren-Nayar when roughness > eps (bsdf/diffuse.art:2-46)
+template <bool FULL = true>
 __device__ __forceinline__ f3 diffuse_eval(const DevMaterial& m, const Surface& s, f3 in, f3 out) {
     const f3 N = s.local.n;
     const f3 kd = mk(m.kd[0], m.kd[1], m.kd[2]);
     const float alpha = m.kd[3];
-    if (alpha <= FLT_EPS_) return mulf(kd, absolute_cos(in, N) * INV_PI_);
+    if (!FULL || alpha <= FLT_EPS_) return mulf(kd, absolute_cos(in, N) * INV_PI_);
     float a2 = alpha * alpha;
     float p1 = absolute_cos(in, N), p2 = absolute_cos(out, N);
     float sv = -p1 * p2 + positive_cos(out, in);
@@ -1012,13 +1015,14 @@ __device__ __forceinline__ f3 diffuse_eval(const DevMaterial& m, const Surface& 
     float C = 0.17f * a2 / (a2 + 0.13f);
     return mulf(add(mulf(kd, (A + (B * sv / t)) / PI_), mul(kd, mulf(kd, C / PI_))), p1);
 }
+template <bool FULL = true>
 __device__ __forceinline__ BsdfSample diffuse_sample(const DevMaterial& m, const Surface& s, Rng& rnd, f3 out) {
     float u = rnd.next_f32();
     float v = rnd.next_f32();
     float pdf;
     f3 ld = sample_cosine_hemisphere(u, v, &pdf);
     f3 dir = frame_to_world(s.local, ld);
-    if (m.kd[3] <= FLT_EPS_) return make_sample(dir, pdf, mk(m.kd[0], m.kd[1], m.kd[2]), 1);
+    if (!FULL || m.kd[3] <= FLT_EPS_) return make_sample(dir, pdf, mk(m.kd[0], m.kd[1], m.kd[2]), 1);
     return make_sample(dir, pdf, mulf(diffuse_eval(m, s, dir, out), 1 / pdf), 1);
 }
 __device__ __forceinline__ float diffuse_pdf(const Surface& s, f3 in) { return positive_cos(in, s.local.n) / PI_; }
@@ -1039,10 +1043,17 @@ __device__ __forceinline__ float plastic_mix(const DevMaterial& m, const Surface
     return fresnel_dielectric(m.ks[3] / m.kt[3], absolute_cos(out, s.local.n));
 }
 
+// FULL = false compiles only the materials and lights of the basic set
+// (Lambert diffuse, dielectric; plane/env/point/spot/directional/sun lights):
+// the upload picks that kernel variant when the scene needs nothing more, so
+// scenes like the diamond do not pay the wider shading code's registers.
+template <bool FULL>
 __device__ __forceinline__ bool bsdf_is_specular(const DevMaterial& m) {
-    return m.type == MAT_DIELECTRIC || (m.type == MAT_CONDUCTOR && m.dist == MF_DELTA);
+    return m.type == MAT_DIELECTRIC || (FULL && m.type == MAT_CONDUCTOR && m.dist == MF_DELTA);
 }
+template <bool FULL>
 __device__ __forceinline__ f3 bsdf_eval(const DevMaterial& m, const Surface& s, f3 in, f3 out) {
+    if (!FULL) return m.type == MAT_DIFFUSE ? diffuse_eval<false>(m, s, in, out) : mk(0, 0, 0);
     switch (m.type) {
     case MAT_DIFFUSE: return diffuse_eval(m, s, in, out);
     case MAT_CONDUCTOR: return m.dist == MF_DELTA ? mk(0, 0, 0) : rough_conductor_eval(m, s, in, out);
@@ -1054,7 +1065,9 @@ __device__ __forceinline__ f3 bsdf_eval(const DevMaterial& m, const Surface& s, 
     default: return mk(0, 0, 0);
     }
 }
+template <bool FULL>
 __device__ __forceinline__ float bsdf_pdf(const DevMaterial& m, const Surface& s, f3 in, f3 out) {
+    if (!FULL) return m.type == MAT_DIFFUSE ? diffuse_pdf(s, in) : 0.0f;
     switch (m.type) {
     case MAT_DIFFUSE: return diffuse_pdf(s, in);
     case MAT_CONDUCTOR: return m.dist == MF_DELTA ? 0.0f : rough_conductor_pdf(m, s, in, out);
@@ -1089,7 +1102,9 @@ __device__ __forceinline__ BsdfSample dielectric_sample(const DevMaterial& m, co
     return make_sample(reflect(out_dir, n), 1, mk(m.ks[0], m.ks[1], m.ks[2]), 1);
 }
 
+template <bool FULL>
 __device__ __forceinline__ BsdfSample bsdf_sample(const DevMaterial& m, const Surface& s, Rng& rnd, f3 out) {
+    if (!FULL) return m.type == MAT_DIELECTRIC ? dielectric_sample(m, s, rnd, out) : diffuse_sample<false>(m, s, rnd, out);
     switch (m.type) {
     case MAT_DIFFUSE: return diffuse_sample(m, s, rnd, out);
     case MAT_DIELECTRIC: return dielectric_sample(m, s, rnd, out);

@@ -146,6 +146,20 @@ def test_bvh_width_invariance(device, root, name):
     np.testing.assert_array_equal(imgs[0], imgs[1])
 
 
+def test_shading_variant_invariance(device, diamond_path):
+    """The basic-shading kernel variant (Lambert + dielectric only, chosen for the
+    diamond) and the full one render the diamond bit for bit alike."""
+    sc = ignis_amd.Scene.from_file(diamond_path)
+    imgs = []
+    try:
+        for full in (0, 1):
+            device.set_option("full_shading", full)
+            imgs.append(render_gpu(device, sc, 128, 128, 4))
+    finally:
+        device.set_option("full_shading", 0)
+    np.testing.assert_array_equal(imgs[0], imgs[1])
+
+
 @pytest.mark.parametrize("name", ["diamond_scene.json", "primitives.json", "s_deep.json", "s_soup_1m.json"])
 def test_occlusion_parity(device, root, name):
     sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", name))
