@@ -39,7 +39,7 @@ __host__ __device__ constexpr int node_f4(int width) { return width == 4 ? 8 : 4
 // info (shape, material, vtx_offset, idx_offset) -> 7 x 16 B.
 constexpr int ENT_STRIDE = 7;
 
-enum : int32_t { MAT_DIFFUSE = 0, MAT_DIELECTRIC = 1, MAT_CONDUCTOR = 2, MAT_PLASTIC = 3 };
+enum : int32_t { MAT_DIFFUSE = 0, MAT_DIELECTRIC = 1, MAT_CONDUCTOR = 2, MAT_PLASTIC = 3, MAT_PRINCIPLED = 4 };
 // microfacet distribution of conductor / plastic specular lobes
 // (BSDF::setupRoughness, src/runtime/bsdf/BSDF.cpp:53-99)
 enum : int32_t { MF_DELTA = 0, MF_VNDF_GGX = 1, MF_GGX = 2, MF_BECKMANN = 3 };

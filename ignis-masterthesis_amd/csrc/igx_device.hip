@@ -1429,6 +1429,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
         case IGX_BSDF_DIELECTRIC: d.type = MAT_DIELECTRIC; break;
         case IGX_BSDF_CONDUCTOR: d.type = MAT_CONDUCTOR; break;
         case IGX_BSDF_PLASTIC: d.type = MAT_PLASTIC; break;
+        case IGX_BSDF_PRINCIPLED: d.type = MAT_PRINCIPLED; break;
         default: return fail(dev, IGX_ERR_UNSUPPORTED, "unsupported bsdf type " + std::to_string(m.bsdf_type));
         }
         if (m.bsdf_type == IGX_BSDF_DIELECTRIC && m.thin) return fail(dev, IGX_ERR_UNSUPPORTED, "thin dielectric is not supported");
@@ -1453,6 +1454,29 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
         d.kt[3] = m.int_ior;
         d.eta[3] = m.alpha_u;
         d.kappa[3] = m.alpha_v;
+        if (m.bsdf_type == IGX_BSDF_PRINCIPLED) {
+            // packing of the principled closure (igx_kernels.h, principled_of)
+            DevMaterial q{};
+            q.type = MAT_PRINCIPLED;
+            q.light = d.light;
+            q.dist = MF_VNDF_GGX;
+            q.mirror = (m.thin ? 1 : 0) | (m.clearcoat_top_only ? 2 : 0);
+            for (int c = 0; c < 3; ++c) q.kd[c] = m.kd[c];
+            q.kd[3] = m.ior;
+            q.ks[0] = m.diffuse_transmission;
+            q.ks[1] = m.specular_transmission;
+            q.ks[2] = m.specular_tint;
+            q.ks[3] = m.alpha_u;
+            q.kt[0] = m.alpha_v;
+            q.kt[1] = m.flatness;
+            q.kt[2] = m.metallic;
+            q.kt[3] = m.sheen;
+            q.eta[0] = m.sheen_tint;
+            q.eta[1] = m.clearcoat;
+            q.eta[2] = m.clearcoat_gloss;
+            q.eta[3] = m.clearcoat_roughness;
+            d = q;
+        }
         mats[i] = d;
     }
 
@@ -1500,7 +1524,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     dev->full_shading = dev->full_shading_opt;
     for (uint32_t i = 0; i < desc->num_materials; ++i) {
         const igx_material& m = desc->materials[i];
-        if (m.bsdf_type == IGX_BSDF_CONDUCTOR || m.bsdf_type == IGX_BSDF_PLASTIC ||
+        if (m.bsdf_type == IGX_BSDF_CONDUCTOR || m.bsdf_type == IGX_BSDF_PLASTIC || m.bsdf_type == IGX_BSDF_PRINCIPLED ||
             (m.bsdf_type == IGX_BSDF_DIFFUSE && m.diffuse_alpha > 1.1920929e-7f))
             dev->full_shading = true;
     }

@@ -886,34 +886,37 @@ __device__ __forceinline__ float mf_pdf(const DevMaterial& m, const Frame& l, f3
     if (m.dist == MF_VNDF_GGX) return pdf_vndf_ggx(l, wo, h, m.eta[3], m.kappa[3]);
     return mf_D(m, l, h) * absolute_cos(l.n, h); // make_microfacet_distribution.pdf (:265)
 }
+// sample_vndf_ggx (:340-366) with sample_vndf_ggx_11 (:287-304) in frame l
+__device__ __forceinline__ f3 vndf_ggx_sample(const Frame& l, Rng& rnd, f3 wo, float au, float av) {
+    f3 vl = to_local(l, wo);
+    f3 sl = normalize(mk(au * vl.x, av * vl.y, vl.z));
+    float st = safe_sqrt(1 - sl.z * sl.z); // sin_cos_phi (core/shading.art:46-53)
+    float sin_phi = 0, cos_phi = 1;
+    if (fabsf(st) > FLT_EPS_) {
+        sin_phi = sl.y / st;
+        cos_phi = sl.x / st;
+    }
+    float ct = fabsf(sl.z);
+    float u0 = rnd.next_f32();
+    float u1 = rnd.next_f32();
+    float px, py;
+    concentric_disk(u0, u1, px, py);
+    float sv = 0.5f * (1 + ct);
+    float y = (1 - sv) * safe_sqrt(1 - px * px) + sv * py;
+    float z = safe_sqrt(1 - y * y - px * px);
+    float sin_t = safe_sqrt(1 - ct * ct);
+    float nrm = safe_div(1, sum_of_prod(sin_t, y, ct, z));
+    float slx = diff_of_prod(ct, y, sin_t, z) * nrm, sly = px * nrm;
+    float s2x = (cos_phi * slx - sin_phi * sly) * au;
+    float s2y = (sin_phi * slx + cos_phi * sly) * av;
+    f3 nh = isfinite(s2x) ? normalize(mk(-s2x, -s2y, 1)) : mk(0, 0, 0);
+    return frame_to_world(l, nh);
+}
 // Microfacet normal sample of the material's distribution for outgoing wo.
 __device__ __forceinline__ f3 mf_sample(const DevMaterial& m, const Frame& l, Rng& rnd, f3 wo, float& pdf) {
     const float au = m.eta[3], av = m.kappa[3];
     if (m.dist == MF_VNDF_GGX) {
-        // sample_vndf_ggx (:306-335) with sample_vndf_ggx_11 (:287-304)
-        f3 vl = to_local(l, wo);
-        f3 sl = normalize(mk(au * vl.x, av * vl.y, vl.z));
-        float st = safe_sqrt(1 - sl.z * sl.z); // sin_cos_phi (core/shading.art:46-53)
-        float sin_phi = 0, cos_phi = 1;
-        if (fabsf(st) > FLT_EPS_) {
-            sin_phi = sl.y / st;
-            cos_phi = sl.x / st;
-        }
-        float ct = fabsf(sl.z);
-        float u0 = rnd.next_f32();
-        float u1 = rnd.next_f32();
-        float px, py;
-        concentric_disk(u0, u1, px, py);
-        float sv = 0.5f * (1 + ct);
-        float y = (1 - sv) * safe_sqrt(1 - px * px) + sv * py;
-        float z = safe_sqrt(1 - y * y - px * px);
-        float sin_t = safe_sqrt(1 - ct * ct);
-        float nrm = safe_div(1, sum_of_prod(sin_t, y, ct, z));
-        float slx = diff_of_prod(ct, y, sin_t, z) * nrm, sly = px * nrm;
-        float s2x = (cos_phi * slx - sin_phi * sly) * au;
-        float s2y = (sin_phi * slx + cos_phi * sly) * av;
-        f3 nh = isfinite(s2x) ? normalize(mk(-s2x, -s2y, 1)) : mk(0, 0, 0);
-        f3 h = frame_to_world(l, nh);
+        f3 h = vndf_ggx_sample(l, rnd, wo, au, av);
         pdf = pdf_vndf_ggx(l, wo, h, au, av);
         return h;
     }
@@ -1043,6 +1046,263 @@ __device__ __forceinline__ float plastic_mix(const DevMaterial& m, const Surface
     return fresnel_dielectric(m.ks[3] / m.kt[3], absolute_cos(out, s.local.n));
 }
 
+// ---- principled BSDF (bsdf/principled.art) -----------------------------------
+// Works in the shading frame: wo / wi / h are local, the microfacet lobes use
+// the identity frame (make_vndf_ggx_distribution(face_normal, identity, ...)).
+// DevMaterial packing: kd = base colour, ior | ks = diffuse_transmission,
+// specular_transmission, specular_tint, roughness_u | kt = roughness_v,
+// flatness, metallic, sheen | eta = sheen_tint, clearcoat, clearcoat_gloss,
+// clearcoat_roughness | mirror bit 0 = thin, bit 1 = clearcoat_top_only.
+struct Principled {
+    f3 base;
+    float ior, dtrans, strans, stint, ru, rv, flat, metal, sheen, sheen_tint, cc, cc_gloss, cc_rough, eta;
+    bool thin, cc_top, entering;
+};
+__device__ __forceinline__ Principled principled_of(const DevMaterial& m, const Surface& s) {
+    Principled p;
+    p.base = mk(m.kd[0], m.kd[1], m.kd[2]);
+    p.ior = m.kd[3];
+    p.dtrans = m.ks[0];
+    p.strans = m.ks[1];
+    p.stint = m.ks[2];
+    p.ru = fmaxf(1e-3f, m.ks[3]);
+    p.rv = fmaxf(1e-3f, m.kt[0]);
+    p.flat = m.kt[1];
+    p.metal = m.kt[2];
+    p.sheen = m.kt[3];
+    p.sheen_tint = m.eta[0];
+    p.cc = m.eta[1];
+    p.cc_gloss = m.eta[2];
+    p.cc_rough = m.eta[3];
+    p.thin = (m.mirror & 1) != 0;
+    p.cc_top = (m.mirror & 2) != 0;
+    p.entering = s.entering;
+    p.eta = (s.entering || p.thin) ? 1 / p.ior : p.ior;
+    return p;
+}
+__device__ __forceinline__ Frame frame_identity() { return Frame{mk(1, 0, 0), mk(0, 1, 0), mk(0, 0, 1)}; }
+__device__ __forceinline__ float luminance(f3 c) { return c.x * 0.2126f + c.y * 0.7152f + c.z * 0.0722f; } // color.art:28
+__device__ __forceinline__ f3 tint_color(f3 c) {
+    float lum = luminance(c);
+    return lum <= FLT_EPS_ ? mk(1, 1, 1) : mk(c.x / lum, c.y / lum, c.z / lum);
+}
+__device__ __forceinline__ float schlick_approx(float f) { // fresnel.art:88-91
+    float s = clampf(1 - f, 0, 1);
+    return (s * s) * (s * s) * s;
+}
+__device__ __forceinline__ float schlick_r0(float eta) {
+    float f = clampf((eta - 1) / (eta + 1), -1, 1);
+    return f * f;
+}
+__device__ __forceinline__ bool same_hemi(f3 a, f3 b) { return (a.z >= 0) == (b.z >= 0); }
+__device__ __forceinline__ f3 make_same_hemi(f3 a, f3 b) { return same_hemi(a, b) ? b : neg(b); }
+__device__ __forceinline__ f3 make_positive_hemi(f3 v) { return v.z >= 0 ? v : neg(v); }
+__device__ __forceinline__ float refr_jacobian(float eta, float ci, float co) { // shading.art:71-74
+    float jd = ci + co * eta;
+    return safe_div(eta * eta * ci, jd * jd);
+}
+__device__ __forceinline__ f3 principled_reflection(const Principled& p, f3 wo, f3 wi, f3 h) {
+    const Frame I = frame_identity();
+    // evalDisneyFresnelTerm
+    float HdV = fabsf(dot(wo, h)), HdL = fabsf(dot(wi, h));
+    f3 F = mk(0, 0, 0);
+    if (!(HdV * HdL <= FLT_EPS_)) {
+        float f1 = fresnel_dielectric(p.eta, HdV);
+        f3 a = lerp3(mk(1, 1, 1), tint_color(p.base), p.stint);
+        f3 r0 = lerp3(mulf(a, schlick_r0(p.eta)), p.base, p.metal);
+        float sk = schlick_approx(HdL);
+        f3 f2 = add(r0, mulf(sub(mk(1, 1, 1), r0), sk));
+        F = lerp3(mk(f1, f1, f1), f2, p.metal);
+    }
+    float D = ndf_ggx(I, h, p.ru, p.rv);
+    float G = g1_smith(I, wi, p.ru, p.rv) * g1_smith(I, wo, p.ru, p.rv);
+    float jacob = safe_div(1, 4 * wo.z);
+    return mulf(F, fabsf(D * G * jacob));
+}
+__device__ __forceinline__ f3 principled_eval_local(const Principled& p, f3 wo, f3 wi) {
+    const Frame I = frame_identity();
+    const bool is_trans = !same_hemi(wi, wo);
+    f3 h = make_same_hemi(wo, is_trans ? normalize(add(wi, mulf(wo, p.eta))) : normalize(add(wi, wo)));
+    const bool in_front = p.entering == (wi.z >= 0), out_front = p.entering == (wo.z >= 0);
+    const float aNdL = fabsf(wi.z), aNdV = fabsf(wo.z);
+    if (aNdL <= 1e-5f) return mk(0, 0, 0);
+    f3 c = mk(0, 0, 0);
+    const float diffuse_weight = (p.thin ? 1.0f : 1 - clampf(p.metal, 0, 1)) * (1 - clampf(p.strans, 0, 1));
+    const float trans_weight = (1 - clampf(p.metal, 0, 1)) * clampf(p.strans, 0, 1);
+    const float lk = schlick_approx(aNdL), vk = schlick_approx(aNdV);
+    if (!is_trans) {
+        if (diffuse_weight > 0) { // evalDiffuseTerm
+            float diff = (1 - 0.5f * lk) * (1 - 0.5f * vk);
+            float VdotL = fabsf(dot(wi, wo));
+            float rr = (VdotL + 1) * (p.ru + p.rv) / 2;
+            float retro = rr * (lk + vk + lk * vk * (rr - 1));
+            float ss = 1;
+            if (p.thin) { // evalSubsurfaceTerm
+                float r2 = p.ru * p.rv;
+                float HdotL = dot(wi, h);
+                float fss90 = HdotL * HdotL * r2;
+                float fss = (1 - lk + fss90 * lk) * (1 - vk + fss90 * vk);
+                float sub_ = 1.25f * (fss * (1 / (aNdL + aNdV + 1e-5f) - 0.5f) + 0.5f);
+                ss = 1 - p.flat + sub_ * p.flat;
+            }
+            float d = INV_PI_ * (diff + retro) * ss * aNdL * diffuse_weight;
+            c = add(c, mulf(p.base, d));
+        }
+        if (p.sheen > 0) { // evalSheenTerm
+            f3 st = lerp3(mk(1, 1, 1), tint_color(p.base), p.sheen_tint);
+            c = add(c, mulf(mulf(st, p.sheen * lk * aNdL), diffuse_weight));
+        }
+        c = add(c, principled_reflection(p, wo, wi, h)); // spec_weight = 1
+        if ((!p.cc_top || (in_front && out_front)) && p.cc > 0) { // evalClearcoatTerm
+            const float F0 = 0.04f, R = 0.25f;
+            float R2 = fmaxf(0.001f, p.cc_rough * (1 - p.cc_gloss) + 0.01f * p.cc_gloss);
+            float aHdL = fabsf(dot(wi, h));
+            float d = ndf_ggx(I, h, R2, R2);
+            float f = F0 + (1 - F0) * schlick_approx(aHdL);
+            float g = g1_smith(I, wi, R, R) * g1_smith(I, wo, R, R);
+            float jacob = safe_div(1, 4 * wo.z);
+            float v = fabsf(R * d * f * g * jacob * wi.z);
+            c = add(c, mulf(mk(v, v, v), p.cc));
+        }
+    } else {
+        if (p.thin && p.dtrans > 0) { // evalTranslucentTerm
+            float diff = (1 - 0.5f * lk) * (1 - 0.5f * vk);
+            c = add(c, mulf(p.base, INV_PI_ * diff * aNdL * p.dtrans));
+        }
+        if (p.strans > 0) { // evalRefractionTerm
+            float term;
+            if (p.thin) {
+                float ft = fresnel_dielectric(p.eta, aNdV);
+                float F = ft + (1 - ft) * ft / (ft + 1);
+                term = 1 - F;
+            } else {
+                float HdI = dot(wi, h), HdO = dot(wo, h);
+                float F = fresnel_dielectric(p.eta, fabsf(HdO));
+                float D = ndf_ggx(I, h, p.ru, p.rv);
+                float G = g1_smith(I, wi, p.ru, p.rv) * g1_smith(I, wo, p.ru, p.rv);
+                float jacob = refr_jacobian(p.eta, HdI, HdO);
+                float norm = fabsf(safe_div(HdO * jacob, wo.z));
+                term = (1 - F) * D * G * norm;
+            }
+            f3 col = p.thin ? mk(sqrtf(p.base.x), sqrtf(p.base.y), sqrtf(p.base.z)) : p.base;
+            c = add(c, mulf(mulf(col, term), trans_weight));
+        }
+    }
+    return c;
+}
+struct Lobes { float diff_refl, diff_trans, spec_refl, spec_trans; };
+__device__ __forceinline__ Lobes principled_lobes(const Principled& p, f3 wo) { // calcLobeDistribution
+    float metal = clampf(p.metal, 0, 1), dt = clampf(p.dtrans, 0, 1), stn = clampf(p.strans, 0, 1);
+    float abs_gen = luminance(p.base);
+    float abs_spec = lerp1(1.0f, luminance(tint_color(p.base)), p.stint);
+    float diff_refl = clampf(abs_gen * (1 - metal) * (1 - stn), 0, 1);
+    float F = fresnel_dielectric(p.eta, fabsf(wo.z));
+    float spec_refl = clampf(abs_spec * (1 - F) + F, 0, 1);
+    if (!(dt > 0 || stn > 0)) {
+        float norm = diff_refl + spec_refl;
+        if (norm <= FLT_EPS_) return Lobes{1, 0, 0, 0};
+        return Lobes{diff_refl / norm, 0, spec_refl / norm, 0};
+    }
+    float diff_trans = clampf(abs_gen * dt * diff_refl, 0, 1);
+    float spec_trans = clampf((1 - F) * abs_gen * (1 - metal) * stn, 0, 1);
+    float norm = diff_refl + spec_refl + diff_trans + spec_trans;
+    if (norm <= FLT_EPS_) return Lobes{1, 0, 0, 0};
+    return Lobes{diff_refl / norm, diff_trans / norm, spec_refl / norm, spec_trans / norm};
+}
+__device__ __forceinline__ float bound_spec_pdf(float v) { return v <= 1e-5f ? 0.0f : v; }
+__device__ __forceinline__ float principled_spec_refl_pdf(const Principled& p, f3 wo, f3 wi) {
+    f3 pwo = make_positive_hemi(wo), pwi = make_positive_hemi(wi);
+    f3 H = normalize(add(pwo, pwi));
+    float cho = dot(pwo, H);
+    return fabsf(bound_spec_pdf(pdf_vndf_ggx(frame_identity(), pwo, H, p.ru, p.rv)) * safe_div(1, 4 * cho));
+}
+__device__ __forceinline__ float principled_spec_trans_pdf(const Principled& p, f3 wo, f3 wi) {
+    f3 pwo = make_positive_hemi(wo), pwi = neg(make_positive_hemi(wi));
+    f3 H = normalize(add(pwi, mulf(pwo, p.eta)));
+    float chi = dot(pwi, H), cho = dot(pwo, H);
+    return fabsf(bound_spec_pdf(pdf_vndf_ggx(frame_identity(), pwo, H, p.ru, p.rv)) * refr_jacobian(p.eta, chi, cho));
+}
+__device__ __forceinline__ float principled_pdf_local(const Principled& p, f3 wo, f3 wi) {
+    if (fabsf(wo.z) <= 1e-5f || fabsf(wi.z) <= 1e-5f) return 0;
+    Lobes l = principled_lobes(p, wo);
+    float dp = fabsf(wi.z) / PI_;
+    if (same_hemi(wo, wi)) return l.diff_refl * dp + l.spec_refl * principled_spec_refl_pdf(p, wo, wi);
+    if (p.thin) return l.diff_trans * dp + l.spec_trans;
+    return l.diff_trans * dp + l.spec_trans * principled_spec_trans_pdf(p, wo, wi);
+}
+__device__ __forceinline__ f3 principled_eval(const DevMaterial& m, const Surface& s, f3 in, f3 out) {
+    Principled p = principled_of(m, s);
+    return principled_eval_local(p, to_local(s.local, out), to_local(s.local, in));
+}
+__device__ __forceinline__ float principled_pdf(const DevMaterial& m, const Surface& s, f3 in, f3 out) {
+    Principled p = principled_of(m, s);
+    return principled_pdf_local(p, to_local(s.local, out), to_local(s.local, in));
+}
+__device__ __forceinline__ BsdfSample principled_sample(const DevMaterial& m, const Surface& s, Rng& rnd, f3 out) {
+    const Principled p = principled_of(m, s);
+    const Frame I = frame_identity();
+    const f3 wo = to_local(s.local, out);
+    if (fabsf(wo.z) <= 1e-5f) return reject_sample();
+    const Lobes l = principled_lobes(p, wo);
+    const float pick = rnd.next_f32();
+    f3 wi;
+    float pdf;
+    if (pick < l.diff_refl) {
+        float u = rnd.next_f32(), v = rnd.next_f32(), cp;
+        wi = make_same_hemi(wo, sample_cosine_hemisphere(u, v, &cp));
+        pdf = cp * l.diff_refl + principled_spec_refl_pdf(p, wo, wi) * l.spec_refl;
+    } else if (pick < l.diff_refl + l.diff_trans) {
+        float u = rnd.next_f32(), v = rnd.next_f32(), cp;
+        wi = neg(make_same_hemi(wo, sample_cosine_hemisphere(u, v, &cp)));
+        pdf = cp * l.diff_trans + principled_spec_trans_pdf(p, wo, wi) * l.spec_trans;
+    } else if (pick < l.diff_refl + l.diff_trans + l.spec_trans) {
+        if (p.thin) {
+            wi = neg(wo);
+            pdf = l.spec_trans;
+        } else {
+            f3 pwo = make_positive_hemi(wo);
+            f3 sn = vndf_ggx_sample(I, rnd, pwo, p.ru, p.rv);
+            float spdf = pdf_vndf_ggx(I, pwo, sn, p.ru, p.rv);
+            if (spdf <= 1e-5f || dot(sn, sn) <= FLT_EPS_) return reject_sample();
+            f3 oH = normalize(sn);
+            f3 H = signbit(dot(oH, pwo)) ? neg(oH) : oH;
+            float cho = dot(pwo, H);
+            // fresnel(eta, cos_h_o) (core/fresnel.art:15-26)
+            float eta2 = cho < 0 ? 1 / p.eta : p.eta;
+            float cos2_t = 1 - (1 - cho * cho) * eta2 * eta2;
+            if (!(cos2_t <= 0.0f)) {
+                float ct = sqrtf(cos2_t);
+                float cos_t = cho < 0 ? -ct : ct;
+                f3 pwi = normalize(refract(pwo, H, p.eta, cho, cos_t));
+                if (!(!same_hemi(pwo, pwi) && cho > FLT_EPS_ && -pwi.z > 1e-5f)) return reject_sample();
+                wi = neg(make_same_hemi(wo, pwi));
+                pdf = fabsf(spdf * refr_jacobian(p.eta, dot(pwi, H), cho)) * l.spec_trans + fabsf(wi.z) / PI_ * l.diff_trans;
+            } else { // total reflection
+                f3 pwi = normalize(reflect(pwo, H));
+                if (!(same_hemi(pwo, pwi) && cho > FLT_EPS_ && pwi.z > 1e-5f)) return reject_sample();
+                wi = make_same_hemi(wo, pwi);
+                pdf = spdf * safe_div(1, 4 * cho) * l.spec_trans + fabsf(wi.z) / PI_ * l.diff_trans;
+            }
+        }
+    } else {
+        f3 pwo = make_positive_hemi(wo);
+        f3 sn = vndf_ggx_sample(I, rnd, pwo, p.ru, p.rv);
+        float spdf = pdf_vndf_ggx(I, pwo, sn, p.ru, p.rv);
+        if (spdf <= 1e-5f || dot(sn, sn) <= FLT_EPS_) return reject_sample();
+        f3 oH = normalize(sn);
+        f3 H = signbit(dot(oH, pwo)) ? neg(oH) : oH;
+        float cho = dot(pwo, H);
+        f3 pwi = normalize(reflect(pwo, H));
+        if (!(same_hemi(pwo, pwi) && cho > FLT_EPS_ && pwi.z > 1e-5f)) return reject_sample();
+        wi = make_same_hemi(wo, pwi);
+        pdf = fabsf(spdf * safe_div(1, 4 * cho)) * l.spec_refl + fabsf(wi.z) / PI_ * l.diff_refl;
+    }
+    if (pdf <= FLT_EPS_) return reject_sample();
+    const float s_eta = (p.thin || same_hemi(wo, wi)) ? 1.0f : p.eta;
+    const f3 in_dir = frame_to_world(s.local, wi);
+    return make_sample(in_dir, pdf, mulf(principled_eval(m, s, in_dir, out), 1 / pdf), s_eta);
+}
+
 // FULL = false compiles only the materials and lights of the basic set
 // (Lambert diffuse, dielectric; plane/env/point/spot/directional/sun lights):
 // the upload picks that kernel variant when the scene needs nothing more, so
@@ -1056,6 +1316,7 @@ __device__ __forceinline__ f3 bsdf_eval(const DevMaterial& m, const Surface& s, 
     if (!FULL) return m.type == MAT_DIFFUSE ? diffuse_eval<false>(m, s, in, out) : mk(0, 0, 0);
     switch (m.type) {
     case MAT_DIFFUSE: return diffuse_eval(m, s, in, out);
+    case MAT_PRINCIPLED: return principled_eval(m, s, in, out);
     case MAT_CONDUCTOR: return m.dist == MF_DELTA ? mk(0, 0, 0) : rough_conductor_eval(m, s, in, out);
     case MAT_PLASTIC: {
         float k = plastic_mix(m, s, out);
@@ -1070,6 +1331,7 @@ __device__ __forceinline__ float bsdf_pdf(const DevMaterial& m, const Surface& s
     if (!FULL) return m.type == MAT_DIFFUSE ? diffuse_pdf(s, in) : 0.0f;
     switch (m.type) {
     case MAT_DIFFUSE: return diffuse_pdf(s, in);
+    case MAT_PRINCIPLED: return principled_pdf(m, s, in, out);
     case MAT_CONDUCTOR: return m.dist == MF_DELTA ? 0.0f : rough_conductor_pdf(m, s, in, out);
     case MAT_PLASTIC: {
         float k = plastic_mix(m, s, out);
@@ -1109,6 +1371,7 @@ __device__ __forceinline__ BsdfSample bsdf_sample(const DevMaterial& m, const Su
     case MAT_DIFFUSE: return diffuse_sample(m, s, rnd, out);
     case MAT_DIELECTRIC: return dielectric_sample(m, s, rnd, out);
     case MAT_CONDUCTOR: return specular_lobe_sample(m, s, rnd, out);
+    case MAT_PRINCIPLED: return principled_sample(m, s, rnd, out);
     default: break;
     }
     // plastic: make_variadic_mix_bsdf(diffuse_extra, specular, mix_f).sample (bsdf/mix.art:29-62)

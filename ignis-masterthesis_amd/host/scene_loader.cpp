@@ -472,6 +472,36 @@ static void build_scene(SceneStore& S, const Value& doc, const std::string& base
                 m.int_ior = bp.number("int_ior", dielectric_ior(bp.string("int_ior_material", "polypropylene"), name));
                 for (int c = 0; c < 3; ++c) { m.eta[c] = 0; m.kappa[c] = 1; }
                 setup_roughness(bp, m);
+            } else if (type == "principled") {
+                // PrincipledBSDF::serialize (PrincipledBSDF.cpp:11-60)
+                m.bsdf_type = IGX_BSDF_PRINCIPLED;
+                V3 base = bp.color("base_color", V3(0.8f, 0.8f, 0.8f));
+                m.kd[0] = base.x; m.kd[1] = base.y; m.kd[2] = base.z;
+                const std::string ior_mat = bp.string("ior_material", "");
+                m.ior = bp.number("ior", dielectric_ior(ior_mat.empty() ? "bk7" : ior_mat, name));
+                m.diffuse_transmission = bp.number("diffuse_transmission", 0.0f);
+                m.specular_transmission = bp.number("specular_transmission", 0.0f);
+                m.specular_tint = bp.number("specular_tint", 0.0f);
+                if (bp.has("roughness_u") || bp.has("roughness_v")) {
+                    m.alpha_u = bp.number("roughness_u", 0.5f);
+                    m.alpha_v = bp.number("roughness_v", 0.5f);
+                } else {
+                    // principled::compute_roughness (bsdf/principled.art:57-62)
+                    float r = bp.number("roughness", 0.5f), an = bp.number("anisotropic", 0.0f);
+                    float aspect = an == 0.0f ? 1.0f : std::sqrt(1 - std::min(std::max(an, 0.0f), 1.0f) * 0.9f);
+                    m.alpha_u = r * r / aspect;
+                    m.alpha_v = r * r * aspect;
+                }
+                m.distribution = IGX_MICROFACET_VNDF_GGX;
+                m.flatness = bp.number("flatness", 0.0f);
+                m.metallic = bp.number("metallic", 0.0f);
+                m.sheen = bp.number("sheen", 0.0f);
+                m.sheen_tint = bp.number("sheen_tint", 0.0f);
+                m.clearcoat = bp.number("clearcoat", 0.0f);
+                m.clearcoat_gloss = bp.number("clearcoat_gloss", 0.0f);
+                m.clearcoat_roughness = bp.number("clearcoat_roughness", 0.1f);
+                m.thin = bp.boolean("thin", false) ? 1 : 0;
+                m.clearcoat_top_only = bp.boolean("clearcoat_top_only", true) ? 1 : 0;
             } else {
                 fail("bsdf '" + name + "': unsupported bsdf type '" + type + "'");
             }

@@ -37,7 +37,11 @@ class Material(C.Structure):
     _fields_ = [("bsdf_type", C.c_int32), ("light", C.c_int32), ("thin", C.c_int32), ("distribution", C.c_int32),
                 ("kd", C.c_float * 3), ("ks", C.c_float * 3), ("kt", C.c_float * 3),
                 ("ext_ior", C.c_float), ("int_ior", C.c_float), ("eta", C.c_float * 3), ("kappa", C.c_float * 3),
-                ("alpha_u", C.c_float), ("alpha_v", C.c_float), ("diffuse_alpha", C.c_float), ("pad", C.c_float)]
+                ("alpha_u", C.c_float), ("alpha_v", C.c_float), ("diffuse_alpha", C.c_float), ("pad", C.c_float),
+                ("ior", C.c_float), ("diffuse_transmission", C.c_float), ("specular_transmission", C.c_float),
+                ("specular_tint", C.c_float), ("flatness", C.c_float), ("metallic", C.c_float), ("sheen", C.c_float),
+                ("sheen_tint", C.c_float), ("clearcoat", C.c_float), ("clearcoat_gloss", C.c_float),
+                ("clearcoat_roughness", C.c_float), ("clearcoat_top_only", C.c_int32)]
 
 
 # igx_light.type (include/igx_scene.h)

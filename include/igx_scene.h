@@ -70,7 +70,8 @@ enum {
     IGX_BSDF_DIFFUSE    = 0, /* Lambert / Oren-Nayar (bsdf/diffuse.art) */
     IGX_BSDF_DIELECTRIC = 1, /* pure (smooth) dielectric (bsdf/dielectric.art) */
     IGX_BSDF_CONDUCTOR  = 2, /* mirror / pure / rough conductor (bsdf/conductor.art) */
-    IGX_BSDF_PLASTIC    = 3  /* Fresnel mix of diffuse and a conductor lobe (bsdf/plastic.art) */
+    IGX_BSDF_PLASTIC    = 3, /* Fresnel mix of diffuse and a conductor lobe (bsdf/plastic.art) */
+    IGX_BSDF_PRINCIPLED = 4  /* Disney BSDF (bsdf/principled.art) */
 };
 /* microfacet distribution of conductor / plastic lobes (BSDF::setupRoughness, BSDF.cpp:53-99) */
 enum { IGX_MICROFACET_DELTA = 0, IGX_MICROFACET_VNDF_GGX = 1, IGX_MICROFACET_GGX = 2, IGX_MICROFACET_BECKMANN = 3 };
@@ -89,6 +90,11 @@ typedef struct igx_material {
     float alpha_u, alpha_v;/* microfacet roughness (compute_explicit, core/microfacet.art:395-402) */
     float diffuse_alpha;   /* Oren-Nayar roughness, 0 = Lambert */
     float pad;
+    /* principled (PrincipledBSDF.cpp:11-60): kd = base_color, alpha_u / alpha_v =
+     * roughness_u / roughness_v (already through compute_roughness), thin */
+    float ior, diffuse_transmission, specular_transmission, specular_tint, flatness, metallic;
+    float sheen, sheen_tint, clearcoat, clearcoat_gloss, clearcoat_roughness;
+    int32_t clearcoat_top_only;
 } igx_material;
 
 /* ---- lights ------------------------------------------------------------ */

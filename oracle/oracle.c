@@ -941,6 +941,8 @@ typedef struct {
     v3 kd, ks, kt, eta, kap;
     float n1, n2;
     const osurf* surf;
+    int principled;    /* make_principled_bsdf (bsdf/principled.art:238-481) */
+    const igx_material* mat;
 } obsdf;
 
 typedef struct { v3 dir; float pdf; v3 color; float eta; int ok; } osample;
@@ -1091,6 +1093,10 @@ static obsdf obsdf_make(const igx_material* m, const osurf* surf) {
             b.lobe = mirror ? LOBE_MIRROR : LOBE_PURE_CONDUCTOR;
         }
         break;
+    case IGX_BSDF_PRINCIPLED:
+        b.principled = 1;
+        b.mat = m;
+        break;
     case IGX_BSDF_PLASTIC:
         b.plastic = 1;
         b.lobe = LOBE_LAMBERT;
@@ -1103,7 +1109,7 @@ static obsdf obsdf_make(const igx_material* m, const osurf* surf) {
     return b;
 }
 static int obsdf_specular(const obsdf* b) {
-    return !b->plastic && (b->lobe == LOBE_DIELECTRIC || b->lobe == LOBE_MIRROR || b->lobe == LOBE_PURE_CONDUCTOR);
+    return !b->plastic && !b->principled && (b->lobe == LOBE_DIELECTRIC || b->lobe == LOBE_MIRROR || b->lobe == LOBE_PURE_CONDUCTOR);
 }
 static int lobe_specular(int lobe) { return lobe == LOBE_DIELECTRIC || lobe == LOBE_MIRROR || lobe == LOBE_PURE_CONDUCTOR; }
 
@@ -1197,13 +1203,273 @@ static osample lobe_sample(const obsdf* b, int lobe, rng_t* r, v3 out) {
     }
     }
 }
+
+/* ---- principled BSDF (bsdf/principled.art), restated in the local shading
+ * frame: w.z is the cosine to the shading normal, microfacet lobes use the
+ * identity frame. -------------------------------------------------------- */
+typedef struct {
+    v3 base;
+    float eta, ru, rv, dtr, str, stint, flat, metal, sheen, sheen_tint, cc, ccg, ccr;
+    int thin, cc_top, entering;
+} oprin;
+
+static const frame_t PRIN_IDENTITY = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+
+static oprin oprin_make(const igx_material* m, const osurf* sf) {
+    oprin p;
+    p.base = V(m->kd[0], m->kd[1], m->kd[2]);
+    p.ru = fmaxf(1e-3f, m->alpha_u);
+    p.rv = fmaxf(1e-3f, m->alpha_v);
+    p.dtr = m->diffuse_transmission;
+    p.str = m->specular_transmission;
+    p.stint = m->specular_tint;
+    p.flat = m->flatness;
+    p.metal = m->metallic;
+    p.sheen = m->sheen;
+    p.sheen_tint = m->sheen_tint;
+    p.cc = m->clearcoat;
+    p.ccg = m->clearcoat_gloss;
+    p.ccr = m->clearcoat_roughness;
+    p.thin = m->thin != 0;
+    p.cc_top = m->clearcoat_top_only != 0;
+    p.entering = sf->entering;
+    p.eta = (sf->entering || p.thin) ? 1 / m->ior : m->ior;
+    return p;
+}
+static float lum_of(v3 c) { return c.x * 0.2126f + c.y * 0.7152f + c.z * 0.0722f; }
+static v3 tint_of(v3 c) {
+    float l = lum_of(c);
+    if (l <= FLT_EPS_) return V(1, 1, 1);
+    return V(c.x / l, c.y / l, c.z / l);
+}
+static float schlick_w(float f) {
+    float s = clampf_(1 - f, 0, 1);
+    return (s * s) * (s * s) * s;
+}
+static int hemi_same(v3 a, v3 b) { return (a.z >= 0) == (b.z >= 0); }
+static v3 hemi_like(v3 a, v3 b) { return hemi_same(a, b) ? b : vneg(b); }
+static v3 hemi_pos(v3 v) { return v.z >= 0 ? v : vneg(v); }
+static float jac_refr(float eta, float ci, float co) {
+    float d = ci + co * eta;
+    return safe_div(eta * eta * ci, d * d);
+}
+static float prin_g(const oprin* p, v3 wi, v3 wo) {
+    return g1_smith_f(&PRIN_IDENTITY, wi, p->ru, p->rv) * g1_smith_f(&PRIN_IDENTITY, wo, p->ru, p->rv);
+}
+static v3 prin_eval_local(const oprin* p, v3 wo, v3 wi) {
+    int trans = !hemi_same(wi, wo);
+    v3 h = hemi_like(wo, trans ? vnormalize(vadd(wi, vmulf(wo, p->eta))) : vnormalize(vadd(wi, wo)));
+    int in_front = p->entering == (wi.z >= 0), out_front = p->entering == (wo.z >= 0);
+    float cl = fabsf(wi.z), cv = fabsf(wo.z);
+    if (cl <= 1e-5f) return V(0, 0, 0);
+    v3 c = V(0, 0, 0);
+    float m01 = clampf_(p->metal, 0, 1), s01 = clampf_(p->str, 0, 1);
+    float w_diff = (p->thin ? 1.0f : 1 - m01) * (1 - s01);
+    float w_trans = (1 - m01) * s01;
+    float lk = schlick_w(cl), vk = schlick_w(cv);
+    if (!trans) {
+        if (w_diff > 0) {
+            float base_d = (1 - 0.5f * lk) * (1 - 0.5f * vk);
+            float rr = (fabsf(vdot(wi, wo)) + 1) * (p->ru + p->rv) / 2;
+            float retro = rr * (lk + vk + lk * vk * (rr - 1));
+            float ss = 1;
+            if (p->thin) {
+                float hl = vdot(wi, h);
+                float f90 = hl * hl * (p->ru * p->rv);
+                float fss = (1 - lk + f90 * lk) * (1 - vk + f90 * vk);
+                float subs = 1.25f * (fss * (1 / (cl + cv + 1e-5f) - 0.5f) + 0.5f);
+                ss = 1 - p->flat + subs * p->flat;
+            }
+            c = vadd(c, vmulf(p->base, INV_PI_ * (base_d + retro) * ss * cl * w_diff));
+        }
+        if (p->sheen > 0) {
+            v3 tint = clerp(V(1, 1, 1), tint_of(p->base), p->sheen_tint);
+            c = vadd(c, vmulf(vmulf(tint, p->sheen * lk * cl), w_diff));
+        }
+        {   /* specular reflection with the Disney Fresnel term */
+            float hv = fabsf(vdot(wo, h)), hl = fabsf(vdot(wi, h));
+            v3 F = V(0, 0, 0);
+            if (!(hv * hl <= FLT_EPS_)) {
+                float f1 = fresnel_dielectric_f(p->eta, hv);
+                v3 a = clerp(V(1, 1, 1), tint_of(p->base), p->stint);
+                float r0f = clampf_((p->eta - 1) / (p->eta + 1), -1, 1);
+                v3 r0 = clerp(vmulf(a, r0f * r0f), p->base, p->metal);
+                float sw = schlick_w(hl);
+                v3 f2 = vadd(r0, vmulf(vsub(V(1, 1, 1), r0), sw));
+                F = clerp(V(f1, f1, f1), f2, p->metal);
+            }
+            float D = d_ggx(&PRIN_IDENTITY, h, p->ru, p->rv);
+            float G = prin_g(p, wi, wo);
+            c = vadd(c, vmulf(F, fabsf(D * G * safe_div(1, 4 * wo.z))));
+        }
+        if ((!p->cc_top || (in_front && out_front)) && p->cc > 0) {
+            const float R = 0.25f;
+            float r2 = fmaxf(0.001f, p->ccr * (1 - p->ccg) + 0.01f * p->ccg);
+            float d = d_ggx(&PRIN_IDENTITY, h, r2, r2);
+            float f = 0.04f + (1 - 0.04f) * schlick_w(fabsf(vdot(wi, h)));
+            float g = g1_smith_f(&PRIN_IDENTITY, wi, R, R) * g1_smith_f(&PRIN_IDENTITY, wo, R, R);
+            float v = fabsf(R * d * f * g * safe_div(1, 4 * wo.z) * wi.z);
+            c = vadd(c, vmulf(V(v, v, v), p->cc));
+        }
+    } else {
+        if (p->thin && p->dtr > 0) {
+            float base_d = (1 - 0.5f * lk) * (1 - 0.5f * vk);
+            c = vadd(c, vmulf(p->base, INV_PI_ * base_d * cl * p->dtr));
+        }
+        if (p->str > 0) {
+            float t;
+            if (p->thin) {
+                float ft = fresnel_dielectric_f(p->eta, cv);
+                t = 1 - (ft + (1 - ft) * ft / (ft + 1));
+            } else {
+                float hi = vdot(wi, h), ho = vdot(wo, h);
+                float F = fresnel_dielectric_f(p->eta, fabsf(ho));
+                float D = d_ggx(&PRIN_IDENTITY, h, p->ru, p->rv);
+                float G = prin_g(p, wi, wo);
+                float nrm = fabsf(safe_div(ho * jac_refr(p->eta, hi, ho), wo.z));
+                t = (1 - F) * D * G * nrm;
+            }
+            v3 col = p->thin ? V(sqrtf(p->base.x), sqrtf(p->base.y), sqrtf(p->base.z)) : p->base;
+            c = vadd(c, vmulf(vmulf(col, t), w_trans));
+        }
+    }
+    return c;
+}
+static void prin_lobes(const oprin* p, v3 wo, float* dr, float* dt, float* sr, float* st) {
+    float m01 = clampf_(p->metal, 0, 1), d01 = clampf_(p->dtr, 0, 1), s01 = clampf_(p->str, 0, 1);
+    float gen = lum_of(p->base);
+    float spec = lerp1(1.0f, lum_of(tint_of(p->base)), p->stint);
+    float a = clampf_(gen * (1 - m01) * (1 - s01), 0, 1);
+    float F = fresnel_dielectric_f(p->eta, fabsf(wo.z));
+    float b = clampf_(spec * (1 - F) + F, 0, 1);
+    float c = 0, d = 0;
+    if (d01 > 0 || s01 > 0) {
+        c = clampf_(gen * d01 * a, 0, 1);
+        d = clampf_((1 - F) * gen * (1 - m01) * s01, 0, 1);
+    }
+    float n = a + b + c + d;
+    if (n <= FLT_EPS_) { *dr = 1; *dt = 0; *sr = 0; *st = 0; return; }
+    *dr = a / n; *dt = c / n; *sr = b / n; *st = d / n;
+}
+static float prin_bound(float v) { return v <= 1e-5f ? 0.0f : v; }
+static float prin_refl_pdf(const oprin* p, v3 wo, v3 wi) {
+    v3 a = hemi_pos(wo), b = hemi_pos(wi);
+    v3 H = vnormalize(vadd(a, b));
+    return fabsf(prin_bound(vndf_pdf(&PRIN_IDENTITY, a, H, p->ru, p->rv)) * safe_div(1, 4 * vdot(a, H)));
+}
+static float prin_trans_pdf(const oprin* p, v3 wo, v3 wi) {
+    v3 a = hemi_pos(wo), b = vneg(hemi_pos(wi));
+    v3 H = vnormalize(vadd(b, vmulf(a, p->eta)));
+    return fabsf(prin_bound(vndf_pdf(&PRIN_IDENTITY, a, H, p->ru, p->rv)) * jac_refr(p->eta, vdot(b, H), vdot(a, H)));
+}
+static float prin_pdf_local(const oprin* p, v3 wo, v3 wi) {
+    if (fabsf(wo.z) <= 1e-5f || fabsf(wi.z) <= 1e-5f) return 0;
+    float dr, dt, sr, st;
+    prin_lobes(p, wo, &dr, &dt, &sr, &st);
+    float cp = fabsf(wi.z) / PI_;
+    if (hemi_same(wo, wi)) return dr * cp + sr * prin_refl_pdf(p, wo, wi);
+    if (p->thin) return dt * cp + st;
+    return dt * cp + st * prin_trans_pdf(p, wo, wi);
+}
+static v3 local_of(const frame_t* f, v3 v) { return V(vdot(f->t, v), vdot(f->b, v), vdot(f->n, v)); }
+static v3 prin_eval(const obsdf* b, v3 in, v3 out) {
+    oprin p = oprin_make(b->mat, b->surf);
+    return prin_eval_local(&p, local_of(&b->surf->local, out), local_of(&b->surf->local, in));
+}
+static float prin_pdf(const obsdf* b, v3 in, v3 out) {
+    oprin p = oprin_make(b->mat, b->surf);
+    return prin_pdf_local(&p, local_of(&b->surf->local, out), local_of(&b->surf->local, in));
+}
+/* VNDF GGX normal for local pwo (sample_vndf_ggx with the identity frame) */
+static v3 prin_vndf(const oprin* p, rng_t* r, v3 pwo, float* pdf) {
+    obsdf tmp;
+    osurf sf;
+    memset(&tmp, 0, sizeof(tmp));
+    memset(&sf, 0, sizeof(sf));
+    sf.local = PRIN_IDENTITY;
+    tmp.surf = &sf;
+    tmp.model = IGX_MICROFACET_VNDF_GGX;
+    tmp.au = p->ru;
+    tmp.av = p->rv;
+    return mf_sample(&tmp, r, pwo, pdf);
+}
+static osample prin_sample(const obsdf* b, rng_t* r, v3 out) {
+    const oprin p = oprin_make(b->mat, b->surf);
+    const frame_t* L = &b->surf->local;
+    v3 wo = local_of(L, out);
+    if (fabsf(wo.z) <= 1e-5f) return osample_reject();
+    float dr, dt, sr, st;
+    prin_lobes(&p, wo, &dr, &dt, &sr, &st);
+    float pick = rng_f32(r);
+    v3 wi;
+    float pdf;
+    if (pick < dr || pick < dr + dt) {
+        int refl = pick < dr;
+        float u = rng_f32(r), v = rng_f32(r);
+        float c = safe_sqrt(v), sn = safe_sqrt(1 - v), phi = 2 * PI_ * u;
+        v3 d = hemi_like(wo, V(sn * cosf(phi), sn * sinf(phi), c));
+        if (refl) {
+            wi = d;
+            pdf = (c / PI_) * dr + prin_refl_pdf(&p, wo, wi) * sr;
+        } else {
+            wi = vneg(d);
+            pdf = (c / PI_) * dt + prin_trans_pdf(&p, wo, wi) * st;
+        }
+    } else if (pick < dr + dt + st) {
+        if (p.thin) {
+            wi = vneg(wo);
+            pdf = st;
+        } else {
+            v3 a = hemi_pos(wo);
+            float mp;
+            v3 m = prin_vndf(&p, r, a, &mp);
+            if (mp <= 1e-5f || vdot(m, m) <= FLT_EPS_) return osample_reject();
+            v3 om = vnormalize(m);
+            v3 H = signbit(vdot(om, a)) ? vneg(om) : om;
+            float ch = vdot(a, H);
+            float e2 = ch < 0 ? 1 / p.eta : p.eta;
+            float c2 = 1 - (1 - ch * ch) * e2 * e2;
+            if (c2 <= 0.0f) { /* total internal reflection */
+                v3 bw = vnormalize(vreflect(a, H));
+                if (!(hemi_same(a, bw) && ch > FLT_EPS_ && bw.z > 1e-5f)) return osample_reject();
+                wi = hemi_like(wo, bw);
+                pdf = mp * safe_div(1, 4 * ch) * st + fabsf(wi.z) / PI_ * dt;
+            } else {
+                float ct = sqrtf(c2);
+                if (ch < 0) ct = -ct;
+                v3 bw = vnormalize(vsub(vmulf(H, p.eta * ch - ct), vmulf(a, p.eta)));
+                if (!(!hemi_same(a, bw) && ch > FLT_EPS_ && -bw.z > 1e-5f)) return osample_reject();
+                wi = vneg(hemi_like(wo, bw));
+                pdf = fabsf(mp * jac_refr(p.eta, vdot(bw, H), ch)) * st + fabsf(wi.z) / PI_ * dt;
+            }
+        }
+    } else {
+        v3 a = hemi_pos(wo);
+        float mp;
+        v3 m = prin_vndf(&p, r, a, &mp);
+        if (mp <= 1e-5f || vdot(m, m) <= FLT_EPS_) return osample_reject();
+        v3 om = vnormalize(m);
+        v3 H = signbit(vdot(om, a)) ? vneg(om) : om;
+        float ch = vdot(a, H);
+        v3 bw = vnormalize(vreflect(a, H));
+        if (!(hemi_same(a, bw) && ch > FLT_EPS_ && bw.z > 1e-5f)) return osample_reject();
+        wi = hemi_like(wo, bw);
+        pdf = fabsf(mp * safe_div(1, 4 * ch)) * sr + fabsf(wi.z) / PI_ * dr;
+    }
+    if (pdf <= FLT_EPS_) return osample_reject();
+    float se = (p.thin || hemi_same(wo, wi)) ? 1.0f : p.eta;
+    v3 in = frame_to_world(L, wi);
+    return osample_make(in, pdf, vmulf(prin_eval(b, in, out), 1 / pdf), se);
+}
 /* make_variadic_mix_bsdf (bsdf/mix.art) with k = Fresnel(out) for plastic */
 static float plastic_k(const obsdf* b, v3 out) { return fresnel_dielectric_f(b->n1 / b->n2, abs_cos(out, b->surf->local.n)); }
 static v3 obsdf_eval(const obsdf* b, v3 in, v3 out) {
+    if (b->principled) return prin_eval(b, in, out);
     if (!b->plastic) return lobe_eval(b, b->lobe, in, out);
     return clerp(lobe_eval(b, LOBE_LAMBERT, in, out), lobe_eval(b, b->spec, in, out), plastic_k(b, out));
 }
 static float obsdf_pdf(const obsdf* b, v3 in, v3 out) {
+    if (b->principled) return prin_pdf(b, in, out);
     if (!b->plastic) return lobe_pdf(b, b->lobe, in, out);
     return lerp1(lobe_pdf(b, LOBE_LAMBERT, in, out), lobe_pdf(b, b->spec, in, out), plastic_k(b, out));
 }
@@ -1217,6 +1483,7 @@ static osample mix_sample_first(const obsdf* b, int first, int second, rng_t* r,
     return s1;
 }
 static osample obsdf_sample(const obsdf* b, rng_t* r, v3 out) {
+    if (b->principled) return prin_sample(b, r, out);
     if (!b->plastic) return lobe_sample(b, b->lobe, r, out);
     float k = plastic_k(b, out);
     if (k <= 0) return lobe_sample(b, LOBE_LAMBERT, r, out);

@@ -443,6 +443,20 @@ def test_image_parity_area_emitters(device):
     assert close.mean() >= 0.99, close.mean()
 
 
+def test_image_parity_principled(device, root):
+    """§8f principled BSDF (bsdf/principled.art): nine lobe configurations, GPU vs oracle."""
+    sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", "principled.json"))
+    g = render_gpu(device, sc, 192, 192, 8)
+    o, _ = O.OracleScene(sc).render(192, 192, 8)
+    assert np.isfinite(g).all()
+    close = np.abs(g - o) <= 1e-2 * np.maximum(np.abs(o), 1e-2)
+    assert close.mean() >= 0.99, close.mean()
+    # fireflies of the thin / transmissive spheres dominate a plain mean: compare clamped
+    gc, oc = np.minimum(g, 10), np.minimum(o, 10)
+    assert abs(gc.mean() - oc.mean()) / oc.mean() < 0.01
+    assert rel_mse(g, o) <= 5e-3
+
+
 def test_gpu_furnace_mirror_exact(device):
     """make_mirror_bsdf (ks 1) in a white environment renders exactly 1 on the device too."""
     scene = {

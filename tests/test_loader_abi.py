@@ -229,3 +229,28 @@ def test_area_light_power():
                                                   transform=[{"scale": [2, 1, 1]}]))
     assert sc.desc.lights[0].type == _native.LIGHT_MESH
     assert sc.desc.lights[0].radiance[2] == pytest.approx(10 / (np.pi * 10), rel=1e-4)
+
+
+def test_principled_parameters():
+    """PrincipledBSDF::serialize (PrincipledBSDF.cpp:11-60): defaults, ior table, and
+    principled::compute_roughness (roughness^2, anisotropic aspect sqrt(1 - 0.9 a))."""
+    doc = {"bsdfs": [{"type": "principled", "name": "a"},
+                     {"type": "principled", "name": "b", "roughness": 0.6, "anisotropic": 0.5, "metallic": 0.3,
+                      "ior_material": "water", "thin": True, "clearcoat_top_only": False, "sheen": 0.25},
+                     {"type": "principled", "name": "c", "roughness_u": 0.2, "roughness_v": 0.05, "ior": 1.33}],
+           "shapes": [{"type": "rectangle", "name": "r"}],
+           "entities": [{"name": "e%d" % i, "shape": "r", "bsdf": n} for i, n in enumerate("abc")]}
+    sc = ignis_amd.Scene.from_string(doc)
+    d = sc.desc
+    mats = [d.materials[d.entities[i].material] for i in range(3)]
+    a, b, c = mats
+    assert a.bsdf_type == 4
+    np.testing.assert_allclose(a.kd[:], [0.8, 0.8, 0.8])
+    assert a.ior == pytest.approx(1.5046)
+    assert (a.alpha_u, a.alpha_v) == (pytest.approx(0.25), pytest.approx(0.25))
+    assert a.clearcoat_roughness == pytest.approx(0.1) and a.clearcoat_top_only == 1 and a.thin == 0
+    aspect = np.sqrt(1 - 0.5 * 0.9)
+    assert b.alpha_u == pytest.approx(0.36 / aspect, rel=1e-6) and b.alpha_v == pytest.approx(0.36 * aspect, rel=1e-6)
+    assert b.ior == pytest.approx(1.333) and b.metallic == pytest.approx(0.3) and b.sheen == pytest.approx(0.25)
+    assert b.thin == 1 and b.clearcoat_top_only == 0
+    assert (c.alpha_u, c.alpha_v, c.ior) == (pytest.approx(0.2), pytest.approx(0.05), pytest.approx(1.33))

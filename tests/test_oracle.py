@@ -202,6 +202,12 @@ def test_oracle_furnace_pure_conductor_is_fresnel():
     # white rough-plastic sphere traps and amplifies paths: checked at one bounce
     ({"type": "plastic", "diffuse_reflectance": [1, 1, 1], "roughness": 0.2}, 0.8, 1.1, 2),
     ({"type": "diffuse", "reflectance": [1, 1, 1], "roughness": 0.5}, 0.8, 1.02, 64),
+    # principled (bsdf/principled.art): metallic white = F 1 VNDF-GGX lobe; the Disney diffuse
+    # retro-reflection term and the specular lobe on top of it add a few percent; rough
+    # specular transmission (eta 1/1.5046) with total internal reflection
+    ({"type": "principled", "base_color": [1, 1, 1], "metallic": 1, "roughness": 0.3}, 0.93, 1.02, 64),
+    ({"type": "principled", "base_color": [1, 1, 1], "roughness": 0.5}, 0.95, 1.1, 64),
+    ({"type": "principled", "base_color": [1, 1, 1], "specular_transmission": 1, "roughness": 0.3}, 0.9, 1.05, 64),
 ])
 def test_oracle_furnace_energy(bsdf, lo, hi, depth):
     """White-albedo microfacet / plastic / Oren-Nayar spheres in a white environment lose at
