@@ -138,11 +138,11 @@ def suite_line(ignis_amd, dev_index, path, spi, iters):
     dev.reset_stats()
     dev.set_option("timing", 1)
     t0 = time.perf_counter()
-    for it in range(iters):
-        p.iteration = 1 + it
-        dev.render(p)
+    p.iteration = 1
+    dev.render_iterations(p, iters)
     dev.synchronize()
     dt = time.perf_counter() - t0
+    p.iteration = 0
     st = dev.stats()
     dev.set_option("timing", 0)
     rays = st["camera_rays"] + st["bounce_rays"] + st["shadow_rays"]
@@ -202,8 +202,9 @@ def main():
 
     def render_frame():
         dev.clear()
-        for it in range(iters):
-            dev.render(params(it))
+        # all iterations of the frame in one call: iterations whose paths fit the
+        # capacity are traced as one wavefront (a tile shard is small at N > 1)
+        dev.render_iterations(params(0), iters)
         if n_gpus > 1:
             # pack owned tiles, RCCL all_gather over xGMI, assemble on every rank
             torch.cuda.synchronize()

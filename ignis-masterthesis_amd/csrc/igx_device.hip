@@ -76,8 +76,21 @@ struct FrameArgs {
     const float* rays;   // device copy of the ray list (ray-list mode)
     int chunk_pixel0;    // first local pixel of this chunk
     int chunk_pixels;    // local pixels in this chunk
+    int chunk_iters;     // consecutive iterations (iter, iter + 1, ...) the chunk covers
     float inv_spi;
 };
+
+// path slot -> (local pixel, sample, iteration): slots run over the chunk's
+// pixels x spi samples, one such block per iteration of the chunk
+__device__ __forceinline__ void slot_coords(const FrameArgs& fa, int slot, int& lp, int& sample, int& iter) {
+    const int per_iter = fa.chunk_pixels * fa.spi;
+    const int it = slot / per_iter;
+    const int r = slot - it * per_iter;
+    const int q = r / fa.spi;
+    lp = fa.chunk_pixel0 + q;
+    sample = r - q * fa.spi;
+    iter = fa.iter + it;
+}
 
 // local pixel -> global (x, y); false if the slot lies outside the film
 __device__ __forceinline__ bool local_to_global(const FrameArgs& fa, int lp, int& x, int& y) {
@@ -109,19 +122,19 @@ __device__ __forceinline__ T uniform_load(const T* p) {
 // written as dead paths with depth 0), so no atomics.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(BLOCK) k_generate(FrameArgs fa, SceneView sv, PathBuf out, float4* L, int* cnt0) {
-    const int n = fa.chunk_pixels * fa.spi;
+    const int n = fa.chunk_pixels * fa.spi * fa.chunk_iters;
     if (blockIdx.x == 0 && threadIdx.x == 0) *cnt0 = n;
     for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
         L[i] = make_float4(0, 0, 0, 0);
-        int lp = fa.chunk_pixel0 + i / fa.spi;
-        int sample = i - (i / fa.spi) * fa.spi;
+        int lp, sample, iter;
+        slot_coords(fa, i, lp, sample, iter);
         int x, y;
         f3 o = mk(0, 0, 0), d = mk(0, 0, 1);
         uint32_t counter = 1;
         int depth = 0; // dead
         if (local_to_global(fa, lp, x, y)) {
             depth = 1;
-            Rng rnd{create_random_seed(sample, fa.iter, fa.frame, x, y, fa.seed), 1};
+            Rng rnd{create_random_seed(sample, iter, fa.frame, x, y, fa.seed), 1};
             if (fa.num_rays > 0) {
                 // make_list_emitter (driver/emitter.art:18-30): no random draws
                 const float* r = fa.rays + 8 * x;
@@ -209,7 +222,8 @@ __device__ __forceinline__ void ray_extent(const FrameArgs& fa, const SceneView&
                                            float& tmax, uint32_t& rflags) {
     if (depth == 1) {
         if (fa.num_rays > 0) {
-            int lp = fa.chunk_pixel0 + slot / fa.spi;
+            int lp, sample, iter;
+            slot_coords(fa, slot, lp, sample, iter);
             tmin = fa.rays[8 * lp + 6];
             tmax = fa.rays[8 * lp + 7];
             rflags = 0;
@@ -265,10 +279,11 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
             has_l = true;
         }
     }
-    int sample = ps.slot - (ps.slot / fa.spi) * fa.spi;
+    int lp, sample, iter;
+    slot_coords(fa, ps.slot, lp, sample, iter);
     int px, py;
-    local_to_global(fa, fa.chunk_pixel0 + ps.slot / fa.spi, px, py);
-    Rng rnd{create_random_seed(sample, fa.iter, fa.frame, px, py, fa.seed), ps.counter};
+    local_to_global(fa, lp, px, py);
+    Rng rnd{create_random_seed(sample, iter, fa.frame, px, py, fa.seed), ps.counter};
     f3 out_dir = neg(rd);
     const bool specular = bsdf_is_specular<FULL>(m);
     // on_shadow (pathtracer.art:52-112)
@@ -599,17 +614,24 @@ __global__ void __launch_bounds__(BLOCK) k_resolve(FrameArgs fa, const float4* L
     if (p >= fa.chunk_pixels) return;
     int x, y;
     if (!local_to_global(fa, fa.chunk_pixel0 + p, x, y)) return;
-    float r = 0, g = 0, b = 0;
-    for (int s = 0; s < fa.spi; ++s) {
-        float4 l = L[p * fa.spi + s];
-        r += l.x * fa.inv_spi;
-        g += l.y * fa.inv_spi;
-        b += l.z * fa.inv_spi;
-    }
     size_t o = 3 * ((size_t)y * fb_width + x);
-    fb[o + 0] += r;
-    fb[o + 1] += g;
-    fb[o + 2] += b;
+    float fr = fb[o + 0], fg = fb[o + 1], fbb = fb[o + 2];
+    for (int it = 0; it < fa.chunk_iters; ++it) { // one accumulation per iteration, in order
+        const float4* Li = L + ((size_t)it * fa.chunk_pixels + p) * fa.spi;
+        float r = 0, g = 0, b = 0;
+        for (int s = 0; s < fa.spi; ++s) {
+            float4 l = Li[s];
+            r += l.x * fa.inv_spi;
+            g += l.y * fa.inv_spi;
+            b += l.z * fa.inv_spi;
+        }
+        fr += r;
+        fg += g;
+        fbb += b;
+    }
+    fb[o + 0] = fr;
+    fb[o + 1] = fg;
+    fb[o + 2] = fbb;
 }
 
 __global__ void k_pack_tiles(FrameArgs fa, const float* fb, float* dst, int num_tiles) {
@@ -1538,8 +1560,13 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     return IGX_OK;
 }
 
-extern "C" igx_status igx_render(igx_device* dev, const igx_render_params* p) {
-    if (!dev || !p) return IGX_ERR_INVALID_ARGUMENT;
+// Render `count` consecutive iterations (p->iteration, p->iteration + 1, ...).
+// Small iterations are batched: one chunk then holds several iterations'
+// paths (up to the path capacity), so a shard with few pixels (multi-GPU
+// tiles) still fills the device; the film is bit-identical to `count`
+// single-iteration calls.
+static igx_status render_impl(igx_device* dev, const igx_render_params* p, int count) {
+    if (!dev || !p || count < 1) return IGX_ERR_INVALID_ARGUMENT;
     if (!dev->has_scene) return fail(dev, IGX_ERR_NO_SCENE, "no scene uploaded");
     if (p->spi < 1) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "spi must be >= 1");
     auto t_start = std::chrono::steady_clock::now();
@@ -1606,14 +1633,16 @@ extern "C" igx_status igx_render(igx_device* dev, const igx_render_params* p) {
     // capacity: whole iteration resident when it fits (<= 16M paths), pixel aligned
     long long total_paths = local_pixels * p->spi;
     if (total_paths == 0) {
-        dev->iteration_count++;
+        dev->iteration_count += count;
         return IGX_OK;
     }
-    long long cap = dev->capacity_opt > 0 ? dev->capacity_opt : std::min<long long>(total_paths, 1ll << 24);
+    long long cap = dev->capacity_opt > 0 ? dev->capacity_opt
+                                          : (count > 1 ? (1ll << 24) : std::min<long long>(total_paths, 1ll << 24));
     cap = std::min<long long>(cap, (1ll << 24) - 1);
     cap = std::max<long long>(p->spi, (cap / p->spi) * p->spi);
     const long long chunk_pixels_max = std::min<long long>(cap, total_paths) / p->spi;
-    const size_t slot_cap = (size_t)(chunk_pixels_max * p->spi);
+    const int iters_per_chunk = total_paths <= cap ? (int)std::min<long long>(count, cap / total_paths) : 1;
+    const size_t slot_cap = (size_t)(chunk_pixels_max * p->spi * iters_per_chunk);
 
     const int max_bounces = std::min(std::max(dev->sv.max_depth, 1), MAX_BOUNCES - 1);
     const bool inst = dev->instrument;
@@ -1628,7 +1657,10 @@ extern "C" igx_status igx_render(igx_device* dev, const igx_render_params* p) {
     const int sh_bpc = inst ? shadow_blocks_per_cu<true>(sd, dev->lds_scene_bytes) : shadow_blocks_per_cu<false>(sd, dev->lds_scene_bytes);
     const int fin_bpc = inst ? finish_blocks_per_cu<true>(sd, ldsb) : finish_blocks_per_cu<false>(sd, ldsb);
 
+    for (int it0 = 0; it0 < count; it0 += iters_per_chunk)
     for (long long px0 = 0; px0 < local_pixels; px0 += chunk_pixels_max) {
+        fa.iter = p->iteration + it0;
+        fa.chunk_iters = std::min(iters_per_chunk, count - it0);
         Slot& S = dev->slots[dev->next_slot];
         dev->next_slot ^= 1;
         igx_status st = harvest(dev, S); // waits for the chunk that used this slot two chunks ago
@@ -1649,10 +1681,10 @@ extern "C" igx_status igx_render(igx_device* dev, const igx_render_params* p) {
         int chunk_pixels = (int)std::min<long long>(chunk_pixels_max, local_pixels - px0);
         fa.chunk_pixel0 = (int)px0;
         fa.chunk_pixels = chunk_pixels;
-        long long n = (long long)chunk_pixels * p->spi;
+        long long n = (long long)chunk_pixels * p->spi * fa.chunk_iters;
         int tail = dev->tail_opt >= 0 ? (int)std::min<int64_t>(dev->tail_opt, 1 << 30) : (int)std::max<long long>(32768, n / 64);
         S.tail = tail;
-        S.camera = valid_pixels_in_chunk(fa) * p->spi;
+        S.camera = valid_pixels_in_chunk(fa) * p->spi * fa.chunk_iters;
         int* cnt = S.ctr; // cnt[2b]: paths entering bounce b, cnt[2b+1]: shadow rays of bounce b
         HIPCHK(hipMemsetAsync(S.ctr, 0, CTR_INTS * sizeof(int), dev->stream));
         begin_timed(2, -1, dev->stream);
@@ -1736,10 +1768,17 @@ extern "C" igx_status igx_render(igx_device* dev, const igx_render_params* p) {
         HIPCHK(hipEventRecord(S.done, dev->tail_stream));
         S.pending = true;
     }
-    dev->iteration_count++;
-    dev->stats.iterations++;
+    dev->iteration_count += count;
+    dev->stats.iterations += count;
     dev->stats.ms_render += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     return IGX_OK;
+}
+
+extern "C" igx_status igx_render(igx_device* dev, const igx_render_params* p) { return render_impl(dev, p, 1); }
+
+extern "C" igx_status igx_render_iterations(igx_device* dev, const igx_render_params* p, int32_t count) {
+    if (count < 1) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "iteration count must be >= 1");
+    return render_impl(dev, p, count);
 }
 
 extern "C" igx_status igx_get_framebuffer(igx_device* dev, float* host_rgb, size_t count, uint64_t* iteration_count) {

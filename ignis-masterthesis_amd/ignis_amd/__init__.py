@@ -145,6 +145,10 @@ class Device:
     def render(self, params):
         self._check(self._lib.igx_render(self._h, C.byref(params)))
 
+    def render_iterations(self, params, count):
+        """`count` consecutive iterations from params.iteration (igx_render_iterations)."""
+        self._check(self._lib.igx_render_iterations(self._h, C.byref(params), int(count)))
+
     def framebuffer(self, count):
         out = np.zeros(count, dtype=np.float32)
         it = C.c_uint64()

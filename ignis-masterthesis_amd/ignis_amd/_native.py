@@ -110,6 +110,7 @@ EXPORTED_SYMBOLS = [
     "igx_create", "igx_destroy", "igx_last_error", "igx_version", "igx_set_option", "igx_upload_scene",
     "igx_render", "igx_get_framebuffer", "igx_framebuffer_device_ptr", "igx_pack_tiles", "igx_clear",
     "igx_get_stats", "igx_reset_stats", "igx_trace_hits", "igx_trace_occlusion", "igx_synchronize",
+    "igx_render_iterations",
 ]
 
 _lib = None
@@ -143,6 +144,7 @@ def lib():
     L.igx_set_option.argtypes = [vp, C.c_char_p, C.c_int64]
     L.igx_upload_scene.argtypes = [vp, vp]
     L.igx_render.argtypes = [vp, C.POINTER(RenderParams)]
+    L.igx_render_iterations.argtypes = [vp, C.POINTER(RenderParams), C.c_int32]
     L.igx_get_framebuffer.argtypes = [vp, C.POINTER(C.c_float), C.c_size_t, C.POINTER(C.c_uint64)]
     L.igx_framebuffer_device_ptr.argtypes = [vp, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
     L.igx_pack_tiles.argtypes = [vp, C.POINTER(RenderParams), C.c_void_p, C.c_size_t]
@@ -153,7 +155,7 @@ def lib():
     L.igx_trace_hits.argtypes = [vp, C.POINTER(C.c_float), C.c_int32, C.c_uint32, C.POINTER(C.c_int32),
                                  C.POINTER(C.c_float)]
     L.igx_trace_occlusion.argtypes = [vp, C.POINTER(C.c_float), C.c_int32, C.c_uint32, C.POINTER(C.c_int32)]
-    for name in ["igx_create", "igx_destroy", "igx_set_option", "igx_upload_scene", "igx_render",
+    for name in ["igx_create", "igx_destroy", "igx_set_option", "igx_upload_scene", "igx_render", "igx_render_iterations",
                  "igx_get_framebuffer", "igx_framebuffer_device_ptr", "igx_pack_tiles", "igx_clear",
                  "igx_synchronize", "igx_get_stats", "igx_reset_stats", "igx_trace_hits", "igx_trace_occlusion"]:
         getattr(L, name).restype = C.c_int

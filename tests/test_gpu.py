@@ -146,6 +146,42 @@ def test_bvh_width_invariance(device, root, name):
     np.testing.assert_array_equal(imgs[0], imgs[1])
 
 
+@pytest.mark.parametrize("tile,capacity", [(None, 0), ((64, 1, 3), 0), (None, 20000)])
+def test_render_iterations_equals_single_calls(device, diamond_path, tile, capacity):
+    """igx_render_iterations (iterations batched into one wavefront when they fit the
+    capacity; pixel chunks otherwise) == the same iterations one igx_render call each,
+    bit for bit, with and without tile sharding."""
+    sc = ignis_amd.Scene.from_file(diamond_path)
+    w, h, spi, n = 160, 120, 2, 5
+    p = ignis_amd.RenderParams()
+    p.width, p.height, p.spi, p.iteration = w, h, spi, 3
+    if tile:
+        p.tile_size, p.tile_offset, p.tile_stride = tile
+    device.upload(sc)
+    device.set_option("capacity", capacity)
+    try:
+        device.clear()
+        device.reset_stats()
+        for it in range(n):
+            p.iteration = 3 + it
+            device.render(p)
+        a, ia = device.framebuffer(w * h * 3)
+        sa = device.stats()
+        device.clear()
+        device.reset_stats()
+        p.iteration = 3
+        device.render_iterations(p, n)
+        b, ib = device.framebuffer(w * h * 3)
+        sb = device.stats()
+    finally:
+        device.set_option("capacity", 0)
+    assert ia == ib == n
+    np.testing.assert_array_equal(a, b)
+    assert a.sum() > 0
+    for k in ("camera_rays", "bounce_rays", "shadow_rays", "iterations"):
+        assert sa[k] == sb[k], (k, sa[k], sb[k])
+
+
 def test_shading_variant_invariance(device, diamond_path):
     """The basic-shading kernel variant (Lambert + dielectric only, chosen for the
     diamond) and the full one render the diamond bit for bit alike."""

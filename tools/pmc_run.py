@@ -1,6 +1,7 @@
 """Workload for rocprofv3 counter passes: the bench's iterations of a scene
-(default diamond 1000x1000, spi 8) without timing or instrumentation, so every
-k_extend dispatch is the same kernel the bench times.
+(default diamond 1000x1000, spi 8), batched by igx_render_iterations like the
+bench, without timing or instrumentation, so every k_extend dispatch is the
+same kernel with the same path count the bench times.
 Usage: pmc_run.py [iterations] [scene file under scenes/]"""
 import os
 import sys
@@ -16,9 +17,8 @@ dev = ignis_amd.Device(0)
 dev.upload(scene)
 p = ignis_amd.RenderParams()
 p.width, p.height, p.spi = W, H, 8
-for it in range(iters):
-    p.iteration = it
-    dev.render(p)
+p.iteration = 0
+dev.render_iterations(p, iters)  # batched like the bench's frame
 dev.synchronize()
 st = dev.stats()
 print({k: st[k] for k in ("camera_rays", "bounce_rays", "shadow_rays", "launches_extend", "extend_rays")}, flush=True)
