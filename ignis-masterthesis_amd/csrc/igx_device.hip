@@ -39,7 +39,8 @@ namespace {
 constexpr int BLOCK = 256;
 constexpr int MAX_BLOCKS_PER_CU = 8;  // 2048 threads per CU; grids never exceed num_cus * this
 constexpr int MAX_STACK = 128;        // traversal stack entries (LDS + spill) per ray
-constexpr int MAX_BOUNCES = 256;
+constexpr int MAX_BOUNCES = 256;          // path depth is stored in 8 bits (p1.w, above the 24-bit RNG counter)
+constexpr long long MAX_CHUNK_PATHS = 1ll << 25; // paths per chunk (one wavefront), ~6 GB of stream buffers per slot
 // Occupancy target (waves per SIMD) of k_extend, with global and with
 // LDS-staged traversal tables: 4 caps it at 128 VGPRs.  k_finish keeps the
 // compiler's choice (it would spill).
@@ -54,7 +55,7 @@ constexpr int MAX_BOUNCES = 256;
 // Streams (SoA of 16-byte records)
 // ---------------------------------------------------------------------------
 struct PathBuf {
-    float4* p0; // org.xyz, (slot | depth << 24) as int bits
+    float4* p0; // org.xyz, slot (int bits)
     float4* p1; // dir.xyz, rnd counter
     float4* p2; // contrib.rgb, inv_pdf
     float* p3;  // eta
@@ -155,8 +156,8 @@ __global__ void __launch_bounds__(BLOCK) k_generate(FrameArgs fa, SceneView sv, 
             }
             counter = rnd.counter;
         }
-        out.p0[i] = make_float4(o.x, o.y, o.z, __int_as_float(i | (depth << 24)));
-        out.p1[i] = make_float4(d.x, d.y, d.z, __uint_as_float(counter));
+        out.p0[i] = make_float4(o.x, o.y, o.z, __int_as_float(i));
+        out.p1[i] = make_float4(d.x, d.y, d.z, __uint_as_float(counter | ((uint32_t)depth << 24)));
         out.p2[i] = make_float4(1, 1, 1, 0); // init_pt_raypayload (technique/pathtracer.art:33-38)
         out.p3[i] = 1.0f;
     }
@@ -193,10 +194,10 @@ __device__ __forceinline__ PathState load_path(const PathBuf& in, int i) {
     PathState s;
     s.o = f3of(p0);
     s.d = f3of(p1);
-    int sd = __float_as_int(p0.w);
-    s.slot = sd & 0xFFFFFF;
-    s.depth = sd >> 24;
-    s.counter = __float_as_uint(p1.w);
+    s.slot = __float_as_int(p0.w);
+    const uint32_t cd = __float_as_uint(p1.w);
+    s.depth = (int)(cd >> 24);
+    s.counter = cd & 0xFFFFFFu;
     s.contrib = f3of(p2);
     s.inv_pdf = p2.w;
     s.eta = in.p3[i];
@@ -204,8 +205,8 @@ __device__ __forceinline__ PathState load_path(const PathBuf& in, int i) {
 }
 
 __device__ __forceinline__ void store_path(const PathBuf& out, int i, const PathState& s) {
-    out.p0[i] = make_float4(s.o.x, s.o.y, s.o.z, __int_as_float(s.slot | (s.depth << 24)));
-    out.p1[i] = make_float4(s.d.x, s.d.y, s.d.z, __uint_as_float(s.counter));
+    out.p0[i] = make_float4(s.o.x, s.o.y, s.o.z, __int_as_float(s.slot));
+    out.p1[i] = make_float4(s.d.x, s.d.y, s.d.z, __uint_as_float(s.counter | ((uint32_t)s.depth << 24)));
     out.p2[i] = make_float4(s.contrib.x, s.contrib.y, s.contrib.z, s.inv_pdf);
     out.p3[i] = s.eta;
 }
@@ -473,14 +474,13 @@ __global__ void __launch_bounds__(BLOCK, WAVES) k_trace(FrameArgs fa, SceneView 
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
     for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
         float4 p0 = in.p0[i], p1 = in.p1[i];
-        int sd = __float_as_int(p0.w);
-        int depth = sd >> 24;
+        int depth = (int)(__float_as_uint(p1.w) >> 24);
         int hit_ent = -1, hit_prim = -1;
         float hu = 0, hv = 0, tmax = 0;
         if (depth > 0) {
             float tmin;
             uint32_t rflags;
-            ray_extent(fa, sv, depth, sd & 0xFFFFFF, tmin, tmax, rflags);
+            ray_extent(fa, sv, depth, __float_as_int(p0.w), tmin, tmax, rflags);
             trace_ray<false, STATS, V>(sv, f3of(p0), f3of(p1), tmin, tmax, rflags, ts, hit_ent, hit_prim, hu, hv, st);
             if (STATS && hit_ent >= 0) st.hits++;
         }
@@ -1529,6 +1529,10 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     float dy = desc->scene_bbox_max[1] - desc->scene_bbox_min[1];
     float dz = desc->scene_bbox_max[2] - desc->scene_bbox_min[2];
     sv.scene_radius = std::sqrt(dx * dx + dy * dy + dz * dz) / 2 * 1.01f;
+    if (desc->technique.max_depth > 255) {
+        free_scene(dev);
+        return fail(dev, IGX_ERR_UNSUPPORTED, "max_depth above 255 is not supported (8-bit path depth)");
+    }
     sv.max_depth = desc->technique.max_depth;
     sv.min_depth = desc->technique.min_depth;
     sv.nee = desc->technique.nee;
@@ -1637,8 +1641,8 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
         return IGX_OK;
     }
     long long cap = dev->capacity_opt > 0 ? dev->capacity_opt
-                                          : (count > 1 ? (1ll << 24) : std::min<long long>(total_paths, 1ll << 24));
-    cap = std::min<long long>(cap, (1ll << 24) - 1);
+                                          : (count > 1 ? MAX_CHUNK_PATHS : std::min<long long>(total_paths, 1ll << 24));
+    cap = std::min<long long>(cap, MAX_CHUNK_PATHS);
     cap = std::max<long long>(p->spi, (cap / p->spi) * p->spi);
     const long long chunk_pixels_max = std::min<long long>(cap, total_paths) / p->spi;
     const int iters_per_chunk = total_paths <= cap ? (int)std::min<long long>(count, cap / total_paths) : 1;
