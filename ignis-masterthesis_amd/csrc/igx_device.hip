@@ -54,16 +54,29 @@ constexpr long long MAX_CHUNK_PATHS = 1ll << 25; // paths per chunk (one wavefro
 // ---------------------------------------------------------------------------
 // Streams (SoA of 16-byte records)
 // ---------------------------------------------------------------------------
+// Every compacted stream is cut into NSH shards of `shard_cap` records
+// (record (s, pos) at index s * shard_cap + pos), each with its own counter:
+// a wave appends to the shard of its global wave index, so the append is one
+// returning atomic per wave on a word shared by 1/NSH of the waves, and no
+// block barrier holds a wave behind the slowest of its block.
+constexpr int NSH = 64;             // shards per stream (one per lane of the counting wave)
+constexpr int CSTRIDE = 16;         // ints between two shard counters: one 64-B atomic line each
+constexpr int CROW = NSH * CSTRIDE; // ints per counter row (one row per stream and bounce)
+constexpr int WAVES_PER_BLOCK = BLOCK / 64;
+constexpr int GRID_QUANTUM = NSH / WAVES_PER_BLOCK; // grids are multiples of this: every shard gets the same waves
+
 struct PathBuf {
     float4* p0; // org.xyz, slot (int bits)
     float4* p1; // dir.xyz, rnd counter
     float4* p2; // contrib.rgb, inv_pdf
     float* p3;  // eta
+    int shard_cap;
 };
 struct ShadowBuf {
     float4* s0; // org.xyz, slot
     float4* s1; // dir.xyz, tmax
     float4* s2; // colour.rgb, -
+    int shard_cap;
 };
 struct HitBuf {
     float4* h;  // t, u, v, entity (int bits; -1 = miss)
@@ -116,6 +129,54 @@ __device__ __forceinline__ T uniform_load(const T* p) {
 }
 
 // ---------------------------------------------------------------------------
+// Sharded streams (see PathBuf)
+// ---------------------------------------------------------------------------
+static_assert(NSH == 64 && BLOCK % 64 == 0 && NSH % WAVES_PER_BLOCK == 0, "one shard counter per lane of a wave");
+
+// Records of all shards of a counter row: lane l reads shard l; wave-uniform.
+__device__ __forceinline__ int row_total(const int* row) {
+    int v = row[lane_id() * CSTRIDE];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
+// Wave g of the grid's G waves serves shard s = g % NSH, as the k-th of the
+// K = G / NSH waves of that shard (grids are multiples of GRID_QUANTUM blocks).
+struct WaveWork {
+    int s, k, K;
+};
+__device__ __forceinline__ WaveWork wave_work() {
+    const int g = __builtin_amdgcn_readfirstlane((int)blockIdx.x * WAVES_PER_BLOCK + (int)(threadIdx.x >> 6));
+    return WaveWork{g % NSH, g / NSH, (int)gridDim.x * WAVES_PER_BLOCK / NSH};
+}
+
+// Storage index of path i of a freshly generated chunk: consecutive groups of
+// 64 paths go round-robin to the shards, so every wave of the first bounce
+// reads 64 neighbouring paths (8 pixels x spi 8).
+__device__ __forceinline__ int gen_index(int i, int shard_cap) {
+    return ((i >> 6) & (NSH - 1)) * shard_cap + ((i >> 12) << 6) + (i & 63);
+}
+// Shard counts of a generated chunk of n paths (written by lanes 0..NSH-1).
+__device__ __forceinline__ int gen_shard_count(int n, int s) {
+    const int rem = (n & (64 * NSH - 1)) - s * 64;
+    return (n >> 12) * 64 + (rem < 0 ? 0 : (rem > 64 ? 64 : rem));
+}
+
+// Wave-level compaction into two sharded streams: one returning atomic per
+// wave and stream (lanes 0 and 1 issue both in one instruction), positions
+// inside the wave by ballot prefix.  Needs every lane of the wave active.
+__device__ __forceinline__ void wave_append2(bool a, bool b, int* ca, int* cb, int& ia, int& ib) {
+    const int lane = lane_id();
+    const uint64_t ma = __ballot(a), mb = __ballot(b);
+    const uint64_t below = (1ull << lane) - 1ull;
+    const int want = lane == 0 ? __popcll(ma) : __popcll(mb);
+    int r = 0;
+    if (lane < 2 && want > 0) r = atomicAdd(lane == 0 ? ca : cb, want);
+    ia = __shfl(r, 0) + __popcll(ma & below);
+    ib = __shfl(r, 1) + __popcll(mb & below);
+}
+
+// ---------------------------------------------------------------------------
 // generate: camera rays (gpu_generate_rays, mapping_gpu.art:618-667;
 // make_camera_emitter, driver/emitter.art:6-16; perspective camera,
 // camera/perspective.art:29-42; uniform pixel sampler, sampler/pixel_sampler.art:4-10).
@@ -124,7 +185,7 @@ __device__ __forceinline__ T uniform_load(const T* p) {
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(BLOCK) k_generate(FrameArgs fa, SceneView sv, PathBuf out, float4* L, int* cnt0) {
     const int n = fa.chunk_pixels * fa.spi * fa.chunk_iters;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *cnt0 = n;
+    if (blockIdx.x == 0 && threadIdx.x < NSH) cnt0[threadIdx.x * CSTRIDE] = gen_shard_count(n, threadIdx.x);
     for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
         L[i] = make_float4(0, 0, 0, 0);
         int lp, sample, iter;
@@ -156,10 +217,11 @@ __global__ void __launch_bounds__(BLOCK) k_generate(FrameArgs fa, SceneView sv, 
             }
             counter = rnd.counter;
         }
-        out.p0[i] = make_float4(o.x, o.y, o.z, __int_as_float(i));
-        out.p1[i] = make_float4(d.x, d.y, d.z, __uint_as_float(counter | ((uint32_t)depth << 24)));
-        out.p2[i] = make_float4(1, 1, 1, 0); // init_pt_raypayload (technique/pathtracer.art:33-38)
-        out.p3[i] = 1.0f;
+        const int e = gen_index(i, out.shard_cap);
+        out.p0[e] = make_float4(o.x, o.y, o.z, __int_as_float(i));
+        out.p1[e] = make_float4(d.x, d.y, d.z, __uint_as_float(counter | ((uint32_t)depth << 24)));
+        out.p2[e] = make_float4(1, 1, 1, 0); // init_pt_raypayload (technique/pathtracer.art:33-38)
+        out.p3[e] = 1.0f;
     }
 }
 
@@ -383,60 +445,33 @@ __device__ __forceinline__ void flush_stats(const TraceStats& st, unsigned long 
     }
 }
 
-// Block-wide stream compaction: one atomic per block and stream per
-// iteration (the per-wave form is bound by a single word's atomic rate,
-// MI355X_MICROARCH.md "dequeue": ~88 atomics/us).  Order inside a block is
-// preserved.  `sh` holds 2 * (BLOCK/64) + 2 ints of LDS.
-__device__ __forceinline__ void block_append2(bool a, bool b, int* ca, int* cb, int* sh, int& ia, int& ib) {
-    const int wave = threadIdx.x / 64;
-    const int lane = lane_id();
-    uint64_t ma = __ballot(a), mb = __ballot(b);
-    uint64_t below = (1ull << lane) - 1ull;
-    if (lane == 0) {
-        sh[wave] = __popcll(ma);
-        sh[BLOCK / 64 + wave] = __popcll(mb);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int ta = 0, tb = 0;
-        for (int w = 0; w < BLOCK / 64; ++w) {
-            int x = sh[w], y = sh[BLOCK / 64 + w];
-            sh[w] = ta;
-            sh[BLOCK / 64 + w] = tb;
-            ta += x;
-            tb += y;
-        }
-        sh[2 * (BLOCK / 64)] = ta ? atomicAdd(ca, ta) : 0;
-        sh[2 * (BLOCK / 64) + 1] = tb ? atomicAdd(cb, tb) : 0;
-    }
-    __syncthreads();
-    ia = sh[2 * (BLOCK / 64)] + sh[wave] + __popcll(ma & below);
-    ib = sh[2 * (BLOCK / 64) + 1] + sh[BLOCK / 64 + wave] + __popcll(mb & below);
-    __syncthreads(); // sh is reused by the next iteration
-}
-
 // ---------------------------------------------------------------------------
-// extend kernel: one bounce for every live path, compacted outputs
+// extend kernel: one bounce for every live path, compacted outputs.  Each
+// wave walks its shard of the input stream and appends survivors and shadow
+// rays to the same shard of the output streams (wave_append2): no block
+// barrier, so a wave whose rays finish early moves on to its next 64 paths.
 // ---------------------------------------------------------------------------
 template <int V, bool STATS, bool LDS>
 __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : EXTEND_WAVES) k_extend(FrameArgs fa, SceneView gsv, PathBuf in, PathBuf out, ShadowBuf sh,
                                                   float4* L, KernelCounters kc, int tail_threshold) {
-    __shared__ int stack_mem[LDS_STACK * BLOCK + 2 * (BLOCK / 64) + 2];
+    __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
-    int* scan = stack_mem + LDS_STACK * BLOCK;
-    const int n = uniform_load(kc.cnt_in);
-    if (n <= tail_threshold) return; // k_finish takes the remaining paths
+    if (row_total(kc.cnt_in) <= tail_threshold) return; // k_finish takes the remaining paths (block-uniform)
     const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
-    for (int base = blockIdx.x * BLOCK; base < n; base += gridDim.x * BLOCK) {
-        int i = base + threadIdx.x;
+    const WaveWork w = wave_work();
+    const int ns = uniform_load(kc.cnt_in + w.s * CSTRIDE);
+    int* const c_out = kc.cnt_out + w.s * CSTRIDE;
+    int* const c_sh = kc.cnt_shadow + w.s * CSTRIDE;
+    for (int p0 = w.k * 64; p0 < ns; p0 += w.K * 64) {
+        const int pos = p0 + lane_id();
         bool alive = false, has_shadow = false;
         PathState ps;
         ShadowRec sr;
         ps.depth = 0;
-        if (i < n) {
-            ps = load_path(in, i);
+        if (pos < ns) {
+            ps = load_path(in, w.s * in.shard_cap + pos);
             if (ps.depth > 0) {
                 f3 Lacc;
                 bool has_l;
@@ -445,12 +480,13 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : EXTEND_WAVES) 
             }
         }
         int dst, sdst;
-        block_append2(alive, has_shadow, kc.cnt_out, kc.cnt_shadow, scan, dst, sdst);
-        if (alive) store_path(out, dst, ps);
+        wave_append2(alive, has_shadow, c_out, c_sh, dst, sdst);
+        if (alive) store_path(out, w.s * out.shard_cap + dst, ps);
         if (has_shadow) {
-            sh.s0[sdst] = make_float4(sr.o.x, sr.o.y, sr.o.z, __int_as_float(ps.slot));
-            sh.s1[sdst] = make_float4(sr.d.x, sr.d.y, sr.d.z, sr.tmax);
-            sh.s2[sdst] = make_float4(sr.color.x, sr.color.y, sr.color.z, 0);
+            const int e = w.s * sh.shard_cap + sdst;
+            sh.s0[e] = make_float4(sr.o.x, sr.o.y, sr.o.z, __int_as_float(ps.slot));
+            sh.s1[e] = make_float4(sr.d.x, sr.d.y, sr.d.z, sr.tmax);
+            sh.s2[e] = make_float4(sr.color.x, sr.color.y, sr.color.z, 0);
         }
     }
     if (STATS) flush_stats<STATS>(st, kc.stats, 0, true);
@@ -460,7 +496,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : EXTEND_WAVES) 
 // trace: closest hit of every live path's current ray (gpu_traverse_primary,
 // mapping_gpu.art:45-68).  Traversal only, so the kernel stays small enough
 // for high occupancy (the latency of the dependent node loads is what bounds
-// it); each lane writes its own hit record, no block synchronisation.
+// it); each lane writes its own hit record (same index as its path).
 // ---------------------------------------------------------------------------
 template <int V, bool STATS, int WAVES, bool LDS>
 __global__ void __launch_bounds__(BLOCK, WAVES) k_trace(FrameArgs fa, SceneView gsv, PathBuf in, HitBuf hits,
@@ -468,11 +504,13 @@ __global__ void __launch_bounds__(BLOCK, WAVES) k_trace(FrameArgs fa, SceneView 
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
-    const int n = uniform_load(cnt);
-    if (n <= tail_threshold) return; // k_finish takes the remaining paths
+    if (row_total(cnt) <= tail_threshold) return; // k_finish takes the remaining paths
     const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
-    for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+    const WaveWork w = wave_work();
+    const int ns = uniform_load(cnt + w.s * CSTRIDE);
+    for (int pos = w.k * 64 + lane_id(); pos < ns; pos += w.K * 64) {
+        const int i = w.s * in.shard_cap + pos;
         float4 p0 = in.p0[i], p1 = in.p1[i];
         int depth = (int)(__float_as_uint(p1.w) >> 24);
         int hit_ent = -1, hit_prim = -1;
@@ -493,20 +531,23 @@ __global__ void __launch_bounds__(BLOCK, WAVES) k_trace(FrameArgs fa, SceneView 
 // ---------------------------------------------------------------------------
 // shade: the path-tracer step at every hit / miss (gpu_hit_shade +
 // gpu_miss_shade, mapping_gpu.art:114-266) for all materials at once, with
-// block-aggregated compaction of surviving paths and shadow rays.
+// wave-level compaction of surviving paths and shadow rays.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(BLOCK) k_shade(FrameArgs fa, SceneView sv, PathBuf in, HitBuf hits, PathBuf out,
                                                  ShadowBuf sh, float4* L, KernelCounters kc, int tail_threshold) {
-    __shared__ int scan[2 * (BLOCK / 64) + 2];
-    const int n = uniform_load(kc.cnt_in);
-    if (n <= tail_threshold) return;
-    for (int base = blockIdx.x * BLOCK; base < n; base += gridDim.x * BLOCK) {
-        int i = base + threadIdx.x;
+    if (row_total(kc.cnt_in) <= tail_threshold) return;
+    const WaveWork w = wave_work();
+    const int ns = uniform_load(kc.cnt_in + w.s * CSTRIDE);
+    int* const c_out = kc.cnt_out + w.s * CSTRIDE;
+    int* const c_sh = kc.cnt_shadow + w.s * CSTRIDE;
+    for (int p0 = w.k * 64; p0 < ns; p0 += w.K * 64) {
+        const int pos = p0 + lane_id();
+        const int i = w.s * in.shard_cap + pos;
         bool alive = false, has_shadow = false;
         PathState ps;
         ShadowRec sr;
         ps.depth = 0;
-        if (i < n) {
+        if (pos < ns) {
             ps = load_path(in, i);
             if (ps.depth > 0) {
                 float4 h = hits.h[i];
@@ -518,12 +559,13 @@ __global__ void __launch_bounds__(BLOCK) k_shade(FrameArgs fa, SceneView sv, Pat
             }
         }
         int dst, sdst;
-        block_append2(alive, has_shadow, kc.cnt_out, kc.cnt_shadow, scan, dst, sdst);
-        if (alive) store_path(out, dst, ps);
+        wave_append2(alive, has_shadow, c_out, c_sh, dst, sdst);
+        if (alive) store_path(out, w.s * out.shard_cap + dst, ps);
         if (has_shadow) {
-            sh.s0[sdst] = make_float4(sr.o.x, sr.o.y, sr.o.z, __int_as_float(ps.slot));
-            sh.s1[sdst] = make_float4(sr.d.x, sr.d.y, sr.d.z, sr.tmax);
-            sh.s2[sdst] = make_float4(sr.color.x, sr.color.y, sr.color.z, 0);
+            const int e = w.s * sh.shard_cap + sdst;
+            sh.s0[e] = make_float4(sr.o.x, sr.o.y, sr.o.z, __int_as_float(ps.slot));
+            sh.s1[e] = make_float4(sr.d.x, sr.d.y, sr.d.z, sr.tmax);
+            sh.s2[e] = make_float4(sr.color.x, sr.color.y, sr.color.z, 0);
         }
     }
 }
@@ -541,14 +583,16 @@ __global__ void __launch_bounds__(BLOCK) k_finish(FrameArgs fa, SceneView gsv, P
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
-    const int n = uniform_load(cnt);
+    const int n = row_total(cnt);
     if (n > tail_threshold || n == 0) return; // the wavefront kernels own this bounce
     const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
     TraceStats sst{0, 0, 0, 0, 0, 0, 0};
     unsigned long long bounces = 0, shadows = 0;
-    for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
-        PathState ps = load_path(in, i);
+    const WaveWork w = wave_work();
+    const int ns = uniform_load(cnt + w.s * CSTRIDE);
+    for (int pos = w.k * 64 + lane_id(); pos < ns; pos += w.K * 64) {
+        PathState ps = load_path(in, w.s * in.shard_cap + pos);
         if (ps.depth <= 0) continue;
         for (;;) {
             f3 Lacc;
@@ -593,11 +637,13 @@ __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, f
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
-    const int n = uniform_load(cnt);
-    if (n == 0) return;
+    if (row_total(cnt) == 0) return;
     const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
-    for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+    const WaveWork w = wave_work();
+    const int ns = uniform_load(cnt + w.s * CSTRIDE);
+    for (int pos = w.k * 64 + lane_id(); pos < ns; pos += w.K * 64) {
+        const int i = w.s * sh.shard_cap + pos;
         float4 s0 = sh.s0[i], s1 = sh.s1[i];
         float tmax = s1.w;
         int e, p;
@@ -687,13 +733,15 @@ struct TimedLaunch {
 };
 
 struct Slot {
-    size_t cap = 0;
+    size_t cap = 0;            // paths per chunk
+    int shard_cap = 0;         // records per stream shard (NSH * shard_cap >= cap)
     PathBuf pa{}, pb{};
     ShadowBuf sh{};
     HitBuf hb{};
     float4* L = nullptr;
-    int* ctr = nullptr;        // device counters: ctr[2b] = paths entering bounce b, ctr[2b+1] = shadow rays of bounce b
+    int* ctr = nullptr;        // device shard counters: row 2b = paths entering bounce b, row 2b+1 = shadow rays of bounce b (CROW ints per row)
     int* pinned = nullptr;     // host mirror
+    long long n0 = 0;          // paths generated for the chunk (row 0)
     hipEvent_t done = nullptr; // recorded on the tail stream after the resolve
     std::vector<hipEvent_t> bounce_ev;
     std::vector<hipEvent_t> ev_pool;
@@ -708,7 +756,17 @@ struct Slot {
     long long camera = 0;
 };
 
-constexpr int CTR_INTS = 2 * MAX_BOUNCES + 4;
+constexpr int CTR_ROWS = 2 * MAX_BOUNCES + 4;
+constexpr size_t CTR_INTS = (size_t)CTR_ROWS * CROW;
+
+// records in counter row `row` of the slot's host mirror (row 0: generated paths)
+long long row_total(const Slot& s, int row) {
+    if (row == 0) return s.n0;
+    long long t = 0;
+    const int* r = s.pinned + (size_t)row * CROW;
+    for (int k = 0; k < NSH; ++k) t += r[k * CSTRIDE];
+    return t;
+}
 
 } // namespace
 
@@ -790,6 +848,11 @@ void free_scene(igx_device* dev) {
     dev->has_scene = false;
 }
 
+// Largest grid any stream kernel is launched with (grid_for).
+int max_grid(const igx_device* dev) {
+    return std::max(GRID_QUANTUM, dev->num_cus * MAX_BLOCKS_PER_CU / GRID_QUANTUM * GRID_QUANTUM);
+}
+
 // Traversal variant of the scene and the spill columns for the stack entries
 // beyond the LDS_STACK in LDS: one per grid thread of the largest grid, per
 // stream.
@@ -797,7 +860,7 @@ igx_status configure_stack(igx_device* dev) {
     const int need = dev->scene_depth;
     const int extra = std::max(0, need - LDS_STACK);
     dev->variant = (dev->bvh_width == 4 ? 2 : 0) | (extra > 0 ? 1 : 0) | (dev->full_shading ? 4 : 0);
-    const size_t threads = (size_t)dev->num_cus * MAX_BLOCKS_PER_CU * BLOCK;
+    const size_t threads = (size_t)max_grid(dev) * BLOCK;
     for (int k = 0; k < 2; ++k) {
         int*& old = k == 0 ? dev->spill_main : dev->spill_tail;
         if (old) {
@@ -825,6 +888,7 @@ void free_slot_buffers(Slot& s) {
     s.hb = HitBuf{};
     s.L = nullptr;
     s.cap = 0;
+    s.shard_cap = 0;
 }
 
 igx_status ensure_slot(igx_device* dev, Slot& s, size_t cap) {
@@ -836,16 +900,23 @@ igx_status ensure_slot(igx_device* dev, Slot& s, size_t cap) {
     }
     if (s.cap >= cap) return IGX_OK;
     free_slot_buffers(s);
-    auto alloc4 = [&](float4** p) -> igx_status { HIPCHK(hipMalloc((void**)p, cap * sizeof(float4))); return IGX_OK; };
+    // shard capacity: a generated chunk puts at most ceil(cap / (64 NSH)) groups
+    // of 64 paths in one shard, and a shard's outputs never exceed its inputs
+    const int shard_cap = (int)((cap + 64 * NSH - 1) / (64 * NSH)) * 64;
+    const size_t recs = (size_t)shard_cap * NSH;
+    auto alloc4 = [&](float4** p, size_t k) -> igx_status { HIPCHK(hipMalloc((void**)p, k * sizeof(float4))); return IGX_OK; };
     igx_status st;
-    if ((st = alloc4(&s.pa.p0)) || (st = alloc4(&s.pa.p1)) || (st = alloc4(&s.pa.p2))) return st;
-    HIPCHK(hipMalloc((void**)&s.pa.p3, cap * sizeof(float)));
-    if ((st = alloc4(&s.pb.p0)) || (st = alloc4(&s.pb.p1)) || (st = alloc4(&s.pb.p2))) return st;
-    HIPCHK(hipMalloc((void**)&s.pb.p3, cap * sizeof(float)));
-    if ((st = alloc4(&s.sh.s0)) || (st = alloc4(&s.sh.s1)) || (st = alloc4(&s.sh.s2)) || (st = alloc4(&s.L))) return st;
-    if ((st = alloc4(&s.hb.h))) return st;
-    HIPCHK(hipMalloc((void**)&s.hb.prim, cap * sizeof(int)));
+    if ((st = alloc4(&s.pa.p0, recs)) || (st = alloc4(&s.pa.p1, recs)) || (st = alloc4(&s.pa.p2, recs))) return st;
+    HIPCHK(hipMalloc((void**)&s.pa.p3, recs * sizeof(float)));
+    if ((st = alloc4(&s.pb.p0, recs)) || (st = alloc4(&s.pb.p1, recs)) || (st = alloc4(&s.pb.p2, recs))) return st;
+    HIPCHK(hipMalloc((void**)&s.pb.p3, recs * sizeof(float)));
+    if ((st = alloc4(&s.sh.s0, recs)) || (st = alloc4(&s.sh.s1, recs)) || (st = alloc4(&s.sh.s2, recs))) return st;
+    if ((st = alloc4(&s.L, cap))) return st; // radiance is indexed by path slot, not sharded
+    if ((st = alloc4(&s.hb.h, recs))) return st;
+    HIPCHK(hipMalloc((void**)&s.hb.prim, recs * sizeof(int)));
+    s.pa.shard_cap = s.pb.shard_cap = s.sh.shard_cap = shard_cap;
     s.cap = cap;
+    s.shard_cap = shard_cap;
     return IGX_OK;
 }
 
@@ -858,10 +929,14 @@ hipEvent_t slot_event(Slot& s) {
     return s.ev_pool[s.ev_next++];
 }
 
+// Grid of a stream kernel: enough blocks for `items`, at most the resident
+// blocks, always a multiple of GRID_QUANTUM (every shard gets the same waves).
 int grid_for(igx_device* dev, long long items, int blocks_per_cu) {
+    const long long q = GRID_QUANTUM;
     long long need = (items + BLOCK - 1) / BLOCK;
     long long cap = (long long)dev->num_cus * std::min(blocks_per_cu, MAX_BLOCKS_PER_CU);
-    return (int)std::max<long long>(1, std::min(need, cap));
+    long long g = std::min((need + q - 1) / q * q, std::max(q, cap / q * q));
+    return (int)std::max(q, g);
 }
 
 // Launch helpers dispatching on the scene's traversal variant.
@@ -999,18 +1074,18 @@ int trace_blocks_per_cu(int v, int waves, size_t lds) {
 igx_status harvest(igx_device* dev, Slot& s) {
     if (!s.pending) return IGX_OK;
     HIPCHK(hipEventSynchronize(s.done));
-    const int* c = s.pinned;
+    auto c = [&](int r) { return (uint64_t)row_total(s, r); };
     dev->stats.camera_rays += (uint64_t)s.camera;
-    for (int b = 1; b <= s.switch_bounce; ++b) dev->stats.bounce_rays += (uint64_t)c[2 * b];
-    for (int b = 0; b < s.switch_bounce; ++b) dev->stats.shadow_rays += (uint64_t)c[2 * b + 1];
-    for (int b = 0; b < s.switch_bounce; ++b) dev->stats.extend_rays += (uint64_t)c[2 * b];
-    for (int b = 1; b <= s.switch_bounce; ++b) dev->stats.extend_paths_out += (uint64_t)c[2 * b];
+    for (int b = 1; b <= s.switch_bounce; ++b) dev->stats.bounce_rays += c(2 * b);
+    for (int b = 0; b < s.switch_bounce; ++b) dev->stats.shadow_rays += c(2 * b + 1);
+    for (int b = 0; b < s.switch_bounce; ++b) dev->stats.extend_rays += c(2 * b);
+    for (int b = 1; b <= s.switch_bounce; ++b) dev->stats.extend_paths_out += c(2 * b);
     // every queued launch counts (as rocprofv3 sees them), including one that
     // found the live count at or below the tail threshold and exited at once
     dev->stats.launches_extend += (uint64_t)s.launched;
     dev->stats.launches_shadow += (uint64_t)s.launched;
     if (s.split) dev->stats.launches_trace += (uint64_t)s.launched;
-    bool finished = s.switch_bounce < MAX_BOUNCES && c[2 * s.switch_bounce] > 0;
+    bool finished = s.switch_bounce < MAX_BOUNCES && c(2 * s.switch_bounce) > 0;
     dev->stats.launches_finish += finished ? 1 : 0;
     if (dev->timing) {
         for (auto& t : s.timed) {
@@ -1689,13 +1764,14 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
         int tail = dev->tail_opt >= 0 ? (int)std::min<int64_t>(dev->tail_opt, 1 << 30) : (int)std::max<long long>(32768, n / 64);
         S.tail = tail;
         S.camera = valid_pixels_in_chunk(fa) * p->spi * fa.chunk_iters;
-        int* cnt = S.ctr; // cnt[2b]: paths entering bounce b, cnt[2b+1]: shadow rays of bounce b
-        HIPCHK(hipMemsetAsync(S.ctr, 0, CTR_INTS * sizeof(int), dev->stream));
+        int* cnt = S.ctr; // row 2b: paths entering bounce b, row 2b+1: shadow rays of bounce b
+        auto row = [&](int r) { return cnt + (size_t)r * CROW; };
+        HIPCHK(hipMemsetAsync(S.ctr, 0, (size_t)(2 * max_bounces + 4) * CROW * sizeof(int), dev->stream));
         begin_timed(2, -1, dev->stream);
         hipLaunchKernelGGL(k_generate, dim3(grid_for(dev, n, 8)), dim3(BLOCK), 0, dev->stream, fa, dev->sv, S.pa, S.L, cnt);
         end_timed(dev->stream);
         HIPCHK(hipGetLastError());
-        S.pinned[0] = (int)n;
+        S.n0 = n;
         const int ext_grid = grid_for(dev, n, ext_bpc);
         const int tr_grid = grid_for(dev, n, tr_bpc);
         const int shade_grid = grid_for(dev, n, shade_bpc);
@@ -1713,17 +1789,17 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
         for (int b = 0; switch_b < 0 && b < max_bounces; ++b) {
             if (b >= 2) {
                 HIPCHK(hipEventSynchronize(S.bounce_ev[b - 2]));
-                if (S.pinned[2 * (b - 1)] <= tail) {
+                if (row_total(S, 2 * (b - 1)) <= tail) {
                     switch_b = b - 1;
                     break;
                 }
             }
             PathBuf in = (b & 1) ? S.pb : S.pa, out = (b & 1) ? S.pa : S.pb;
-            KernelCounters kc{cnt + 2 * b, cnt + 2 * (b + 1), cnt + 2 * b + 1, dev->dstats};
+            KernelCounters kc{row(2 * b), row(2 * (b + 1)), row(2 * b + 1), dev->dstats};
             if (split) {
                 begin_timed(5, b, dev->stream);
-                if (inst) launch_trace<true>(dev, S, tr_grid, fa, in, cnt + 2 * b, tail);
-                else launch_trace<false>(dev, S, tr_grid, fa, in, cnt + 2 * b, tail);
+                if (inst) launch_trace<true>(dev, S, tr_grid, fa, in, row(2 * b), tail);
+                else launch_trace<false>(dev, S, tr_grid, fa, in, row(2 * b), tail);
                 end_timed(dev->stream);
                 begin_timed(0, b, dev->stream);
                 hipLaunchKernelGGL(k_shade, dim3(shade_grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, S.hb, out, S.sh, S.L, kc, tail);
@@ -1735,12 +1811,12 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
                 end_timed(dev->stream);
             }
             begin_timed(1, b, dev->stream);
-            if (inst) launch_shadow<true>(dev, S, sh_grid, cnt + 2 * b + 1);
-            else launch_shadow<false>(dev, S, sh_grid, cnt + 2 * b + 1);
+            if (inst) launch_shadow<true>(dev, S, sh_grid, row(2 * b + 1));
+            else launch_shadow<false>(dev, S, sh_grid, row(2 * b + 1));
             end_timed(dev->stream);
             HIPCHK(hipGetLastError());
-            // shadow count of bounce b and path count entering bounce b+1 (adjacent ints)
-            HIPCHK(hipMemcpyAsync(S.pinned + 2 * b + 1, cnt + 2 * b + 1, 2 * sizeof(int), hipMemcpyDeviceToHost, dev->stream));
+            // shadow counts of bounce b and path counts entering bounce b+1 (adjacent rows)
+            HIPCHK(hipMemcpyAsync(S.pinned + (size_t)(2 * b + 1) * CROW, row(2 * b + 1), 2 * CROW * sizeof(int), hipMemcpyDeviceToHost, dev->stream));
             hipEvent_t e = slot_event(S);
             (void)hipEventRecord(e, dev->stream);
             S.bounce_ev.push_back(e);
@@ -1751,7 +1827,7 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
             HIPCHK(hipStreamSynchronize(dev->stream));
             switch_b = max_bounces;
             for (int b = 1; b <= max_bounces; ++b)
-                if (S.pinned[2 * b] <= tail) { switch_b = b; break; }
+                if (row_total(S, 2 * b) <= tail) { switch_b = b; break; }
         }
         S.switch_bounce = switch_b;
         // tail + resolve on the tail stream, after the main stream reached this point
@@ -1761,8 +1837,8 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
         if (switch_b < MAX_BOUNCES) {
             PathBuf in = (switch_b & 1) ? S.pb : S.pa;
             begin_timed(4, switch_b, dev->tail_stream);
-            if (inst) launch_finish<true>(dev, S, fin_grid, fa, in, cnt + 2 * switch_b, tail);
-            else launch_finish<false>(dev, S, fin_grid, fa, in, cnt + 2 * switch_b, tail);
+            if (inst) launch_finish<true>(dev, S, fin_grid, fa, in, row(2 * switch_b), tail);
+            else launch_finish<false>(dev, S, fin_grid, fa, in, row(2 * switch_b), tail);
             end_timed(dev->tail_stream);
         }
         begin_timed(3, -1, dev->tail_stream);
