@@ -71,10 +71,11 @@ def algorithmic_bytes(stats_inst, st):
     return st["extend_rays"] * per_ray + st["extend_paths_out"] * 52 + shadow_wf * 48, per_ray
 
 
-def load_pmc(n_gpus, scene="diamond_scene"):
-    """Per-launch HBM traffic of the dominant kernel (k_extend) from the committed
-    rocprofv3 PMC summary of the same workload (profiles/pmc_extend*.json)."""
-    name = "pmc_extend.json" if scene == "diamond_scene" else f"pmc_extend_{scene}.json"
+def load_pmc(n_gpus, scene="diamond_scene", kernel="extend"):
+    """Per-launch HBM traffic of the dominant kernel (k_extend, or k_trace on
+    split scenes) from the committed rocprofv3 PMC summary of the same workload
+    (profiles/pmc_<kernel>[_<scene>].json, tools/profile_summary.py)."""
+    name = f"pmc_{kernel}.json" if scene == "diamond_scene" else f"pmc_{kernel}_{scene}.json"
     path = os.path.join(ROOT, "profiles", name)
     if n_gpus != 1 or not os.path.exists(path):
         return None
@@ -109,7 +110,7 @@ def roofline(dev, st, render_one, n_gpus, scene_key):
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
-        "traffic": load_pmc(n_gpus, scene_key),
+        "traffic": load_pmc(n_gpus, scene_key, "trace" if split else "extend"),
         "algorithmic_bytes_per_launch": round(alg_bytes / launches, 1),
         "bytes_per_ray": round(bytes_per_ray, 1),
         "visits_per_ray": {"nodes": round(inst["node_visits"] / max(1, inst["_rays_ext"]), 2),

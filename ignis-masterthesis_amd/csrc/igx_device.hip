@@ -533,6 +533,7 @@ __global__ void __launch_bounds__(BLOCK, WAVES) k_trace(FrameArgs fa, SceneView 
 // gpu_miss_shade, mapping_gpu.art:114-266) for all materials at once, with
 // wave-level compaction of surviving paths and shadow rays.
 // ---------------------------------------------------------------------------
+template <bool FULL>
 __global__ void __launch_bounds__(BLOCK) k_shade(FrameArgs fa, SceneView sv, PathBuf in, HitBuf hits, PathBuf out,
                                                  ShadowBuf sh, float4* L, KernelCounters kc, int tail_threshold) {
     if (row_total(kc.cnt_in) <= tail_threshold) return;
@@ -554,7 +555,7 @@ __global__ void __launch_bounds__(BLOCK) k_shade(FrameArgs fa, SceneView sv, Pat
                 int prim = hits.prim[i];
                 f3 Lacc;
                 bool has_l;
-                alive = shade_step<true>(fa, sv, ps, __float_as_int(h.w), prim, h.x, h.y, h.z, Lacc, has_l, has_shadow, sr);
+                alive = shade_step<FULL>(fa, sv, ps, __float_as_int(h.w), prim, h.x, h.y, h.z, Lacc, has_l, has_shadow, sr);
                 if (has_l) add_radiance(L, ps.slot, Lacc);
             }
         }
@@ -651,6 +652,96 @@ __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, f
         if (!trace_ray<true, STATS, V>(sv, f3of(s0), f3of(s1), 0.001f, tmax, RAY_SHADOW, ts, e, p, u, v, st))
             add_radiance(L, __float_as_int(s0.w), f3of(sh.s2[i]));
     }
+    if (STATS) flush_stats<STATS>(st, stats, 4, false);
+}
+
+// ---------------------------------------------------------------------------
+// Persistent-lane variants of trace and shadow (refill_loop) for scenes whose
+// traversal tables stay in global memory: there a node step waits on an
+// Infinity-Cache / HBM round trip, and refilling idle lanes cuts the number
+// of wave-level steps.  Each wave walks the positions k, k + K, ... (in
+// groups of 64) of its shard, like the grid-stride kernels.
+// ---------------------------------------------------------------------------
+#ifndef REFILL_WAVES
+#define REFILL_WAVES 5
+#endif
+struct ShardSeq {
+    int C; // positions in this wave's sequence (a multiple of 64)
+    int k, K;
+    __device__ __forceinline__ int operator()(int c) const { return (k + (c >> 6) * K) * 64 + (c & 63); }
+};
+__device__ __forceinline__ ShardSeq shard_seq(const WaveWork& w, int ns) {
+    const int groups = (ns + 63) >> 6;
+    const int mine = w.k < groups ? (groups - w.k + w.K - 1) / w.K : 0;
+    return ShardSeq{mine * 64, w.k, w.K};
+}
+
+template <int V, bool STATS>
+__global__ void __launch_bounds__(BLOCK, REFILL_WAVES) k_trace_refill(FrameArgs fa, SceneView sv, PathBuf in, HitBuf hits,
+                                                                     const int* cnt, int tail_threshold,
+                                                                     unsigned long long* stats, int refill_min) {
+    __shared__ int stack_mem[LDS_STACK * BLOCK];
+    const TStack ts = make_tstack(stack_mem, LDS_STACK, sv.spill);
+    if (row_total(cnt) <= tail_threshold) return; // k_finish takes the remaining paths
+    TraceStats st{0, 0, 0, 0, 0, 0, 0};
+    const WaveWork w = wave_work();
+    const int ns = uniform_load(cnt + w.s * CSTRIDE);
+    const int base = w.s * in.shard_cap;
+    const ShardSeq seq = shard_seq(w, ns);
+    refill_loop<false, STATS, V>(
+        sv, ts, seq.C, refill_min, [&](int c) { return seq(c); },
+        [&](int pos, Trav& t) -> bool {
+            if (pos >= ns) return false;
+            const int i = base + pos;
+            const float4 p0 = in.p0[i], p1 = in.p1[i];
+            const int depth = (int)(__float_as_uint(p1.w) >> 24);
+            if (depth == 0) {
+                hits.h[i] = make_float4(0, 0, 0, __int_as_float(-1));
+                hits.prim[i] = -1;
+                return false;
+            }
+            float tmin, tmax;
+            uint32_t rflags;
+            ray_extent(fa, sv, depth, __float_as_int(p0.w), tmin, tmax, rflags);
+            trav_init(sv, t, f3of(p0), f3of(p1), tmin, tmax, rflags, ts);
+            return true;
+        },
+        [&](int pos, const Trav& t) {
+            const int i = base + pos;
+            if (STATS && t.hit_ent >= 0) st.hits++;
+            hits.h[i] = make_float4(t.tmax, t.hu, t.hv, __int_as_float(t.hit_ent));
+            hits.prim[i] = t.hit_prim;
+        },
+        st);
+    if (STATS) flush_stats<STATS>(st, stats, 0, true);
+}
+
+template <int V, bool STATS>
+__global__ void __launch_bounds__(BLOCK, REFILL_WAVES) k_shadow_refill(SceneView sv, ShadowBuf sh, float4* L, const int* cnt,
+                                                                      unsigned long long* stats, int refill_min) {
+    __shared__ int stack_mem[LDS_STACK * BLOCK];
+    const TStack ts = make_tstack(stack_mem, LDS_STACK, sv.spill);
+    if (row_total(cnt) == 0) return;
+    TraceStats st{0, 0, 0, 0, 0, 0, 0};
+    const WaveWork w = wave_work();
+    const int ns = uniform_load(cnt + w.s * CSTRIDE);
+    const int base = w.s * sh.shard_cap;
+    const ShardSeq seq = shard_seq(w, ns);
+    refill_loop<true, STATS, V>(
+        sv, ts, seq.C, refill_min, [&](int c) { return seq(c); },
+        [&](int pos, Trav& t) -> bool {
+            if (pos >= ns) return false;
+            const int i = base + pos;
+            const float4 s0 = sh.s0[i], s1 = sh.s1[i];
+            trav_init(sv, t, f3of(s0), f3of(s1), 0.001f, s1.w, RAY_SHADOW, ts);
+            return true;
+        },
+        [&](int pos, const Trav& t) {
+            if (t.found) return;
+            const int i = base + pos;
+            add_radiance(L, __float_as_int(sh.s0[i].w), f3of(sh.s2[i]));
+        },
+        st);
     if (STATS) flush_stats<STATS>(st, stats, 4, false);
 }
 
@@ -781,10 +872,12 @@ struct igx_device {
     bool instrument = false;
     int64_t capacity_opt = 0;
     int64_t tail_opt = -1;   // paths at or below which k_finish takes over (-1 = auto)
-    bool split = false;      // k_trace + k_shade per bounce (default: fused k_extend)
+    int split_opt = -1;      // k_trace + k_shade per bounce instead of the fused k_extend (-1: auto = global-table scenes)
     int trace_waves = 5;     // occupancy target of k_trace (5 waves per SIMD, anything else = compiler's choice)
+    int refill_opt = -1;     // persistent-lane trace / shadow, refilled once this many lanes idle (0: off, -1: auto = 16)
     int64_t lds_scene_max = 48 * 1024; // stage traversal tables in LDS when they fit (0 = never)
     size_t lds_scene_bytes = 0;        // bytes staged per block for the current scene (0 = global tables)
+    size_t table_bytes = 0;            // traversal tables (nodes, instances, triangles) of the current scene
     int leaf_size = 4;
     // scene
     bool has_scene = false;
@@ -939,6 +1032,22 @@ int grid_for(igx_device* dev, long long items, int blocks_per_cu) {
     return (int)std::max(q, g);
 }
 
+// Kernel schedule per scene (measured per scene):
+//  * traversal tables in LDS (<= 48 KB): fused k_extend, grid-stride k_shadow;
+//  * tables in global memory: shadow rays with persistent lanes (k_shadow_refill,
+//    a refill once refill_min lanes idle);
+//  * tables beyond one XCD's L2 (4 MiB): also split the bounce into k_trace
+//    (persistent lanes) + k_shade -- there every node step waits on an
+//    Infinity-Cache / HBM round trip, and a traversal-only kernel keeps more
+//    waves resident and lets lanes refill.  On cache-resident scenes the
+//    fused kernel is faster (no hit records, rays already coherent).
+constexpr size_t SPLIT_TABLE_BYTES = 4u << 20;
+int refill_min(const igx_device* dev) { return dev->refill_opt >= 0 ? dev->refill_opt : 16; }
+bool use_refill(const igx_device* dev) { return refill_min(dev) > 0 && dev->lds_scene_bytes == 0; }
+bool use_split(const igx_device* dev) {
+    return dev->split_opt >= 0 ? dev->split_opt != 0 : (dev->lds_scene_bytes == 0 && dev->table_bytes > SPLIT_TABLE_BYTES);
+}
+
 // Launch helpers dispatching on the scene's traversal variant.
 #define IGX_DISPATCH_VARIANT(v, MACRO)        \
     do {                                      \
@@ -988,6 +1097,12 @@ void launch_trace_w(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, con
 }
 template <bool STATS>
 void launch_trace(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const PathBuf& in, const int* cnt, int tail) {
+    if (use_refill(dev)) {
+#define L_TRR(S) hipLaunchKernelGGL((k_trace_refill<S, STATS>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, s.hb, cnt, tail, dev->dstats, refill_min(dev))
+        IGX_DISPATCH_VARIANT(dev->variant, L_TRR);
+#undef L_TRR
+        return;
+    }
     if (dev->lds_scene_bytes) {
 #define L_TRL(S) hipLaunchKernelGGL((k_trace<S, STATS, 1, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->stream, fa, dev->sv, in, s.hb, cnt, tail, dev->dstats)
         IGX_DISPATCH_VARIANT(dev->variant, L_TRL);
@@ -999,6 +1114,12 @@ void launch_trace(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const
 }
 template <bool STATS>
 void launch_shadow(igx_device* dev, Slot& s, int grid, const int* cnt) {
+    if (use_refill(dev)) {
+#define L_SHR(S) hipLaunchKernelGGL((k_shadow_refill<S, STATS>), dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, s.sh, s.L, cnt, dev->dstats, refill_min(dev))
+        IGX_DISPATCH_VARIANT(dev->variant, L_SHR);
+#undef L_SHR
+        return;
+    }
     if (dev->lds_scene_bytes) {
 #define L_SHL(S) hipLaunchKernelGGL((k_shadow<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->stream, dev->sv, s.sh, s.L, cnt, dev->dstats)
         IGX_DISPATCH_VARIANT(dev->variant, L_SHL);
@@ -1054,20 +1175,34 @@ int resident_blocks(K kernel, size_t dyn_lds = 0) {
         default: IGX_RES1(K, 7, __VA_ARGS__);                        \
         }                                                            \
     } while (0)
+#define IGX_RESIDENT_G(K)                                            \
+    do {                                                             \
+        switch (v & 3) {                                             \
+        case 0: return resident_blocks(K<0, STATS>);                 \
+        case 1: return resident_blocks(K<1, STATS>);                 \
+        case 2: return resident_blocks(K<2, STATS>);                 \
+        default: return resident_blocks(K<3, STATS>);                \
+        }                                                            \
+    } while (0)
 template <bool STATS>
 int extend_blocks_per_cu(int v, size_t lds) { IGX_RESIDENT8(k_extend, STATS); }
 template <bool STATS>
-int shadow_blocks_per_cu(int v, size_t lds) { IGX_RESIDENT(k_shadow, STATS); }
+int shadow_blocks_per_cu(int v, size_t lds, bool refill) {
+    if (refill) IGX_RESIDENT_G(k_shadow_refill);
+    IGX_RESIDENT(k_shadow, STATS);
+}
 template <bool STATS>
 int finish_blocks_per_cu(int v, size_t lds) { IGX_RESIDENT8(k_finish, STATS); }
 template <bool STATS>
-int trace_blocks_per_cu(int v, int waves, size_t lds) {
+int trace_blocks_per_cu(int v, int waves, size_t lds, bool refill) {
+    if (refill) IGX_RESIDENT_G(k_trace_refill);
     if (lds) IGX_RESIDENT(k_trace, STATS, 1);
     if (waves == 5) IGX_RESIDENT(k_trace, STATS, 5);
     IGX_RESIDENT(k_trace, STATS, 1);
 }
 #undef IGX_RESIDENT
 #undef IGX_RESIDENT8
+#undef IGX_RESIDENT_G
 #undef IGX_RES1
 
 // Wait for the chunk last run in `s` and fold its statistics in.
@@ -1232,8 +1367,15 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     else if (k == "instrument") dev->instrument = value != 0;
     else if (k == "capacity") dev->capacity_opt = value;
     else if (k == "tail_threshold") dev->tail_opt = value;
-    else if (k == "split") dev->split = value != 0;
+    else if (k == "split") {
+        if (value < -1 || value > 1) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "split must be -1 (auto), 0 or 1");
+        dev->split_opt = (int)value;
+    }
     else if (k == "trace_waves") dev->trace_waves = (int)value;
+    else if (k == "refill") {
+        if (value < -1 || value > 64) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "refill must be -1 (auto) or in [0, 64]");
+        dev->refill_opt = (int)value;
+    }
     else if (k == "lds_scene_max") {
         dev->lds_scene_max = value;
         size_t b = ((size_t)dev->sv.num_nodes * dev->sv.node_f4 + (size_t)dev->sv.num_inst * 4 + (size_t)dev->sv.num_tris * 3) * 16;
@@ -1596,6 +1738,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     {
         size_t b = ((size_t)sv.num_nodes * nf4 + (size_t)sv.num_inst * 4 + (size_t)sv.num_tris * 3) * 16;
         dev->lds_scene_bytes = (int64_t)b <= dev->lds_scene_max ? b : 0;
+        dev->table_bytes = b;
     }
     sv.num_lights = (int)lights.size();
     sv.num_infinite = num_infinite;
@@ -1728,12 +1871,17 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
     const int sd = dev->variant;
     const size_t ldsb = dev->lds_scene_bytes;
     const int ext_bpc = inst ? extend_blocks_per_cu<true>(sd, ldsb) : extend_blocks_per_cu<false>(sd, ldsb);
-    const int tr_bpc = inst ? trace_blocks_per_cu<true>(sd, dev->trace_waves, dev->lds_scene_bytes)
-                            : trace_blocks_per_cu<false>(sd, dev->trace_waves, dev->lds_scene_bytes);
+    const bool refill = use_refill(dev);
+    const int tr_bpc = inst ? trace_blocks_per_cu<true>(sd, dev->trace_waves, dev->lds_scene_bytes, refill)
+                            : trace_blocks_per_cu<false>(sd, dev->trace_waves, dev->lds_scene_bytes, refill);
     int shade_bpc = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&shade_bpc, k_shade, BLOCK, 0) != hipSuccess || shade_bpc < 1) shade_bpc = 1;
-    const bool split = dev->split;
-    const int sh_bpc = inst ? shadow_blocks_per_cu<true>(sd, dev->lds_scene_bytes) : shadow_blocks_per_cu<false>(sd, dev->lds_scene_bytes);
+    const bool full = variant_full(sd);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&shade_bpc, full ? k_shade<true> : k_shade<false>, BLOCK, 0) != hipSuccess ||
+        shade_bpc < 1)
+        shade_bpc = 1;
+    const bool split = use_split(dev);
+    const int sh_bpc = inst ? shadow_blocks_per_cu<true>(sd, dev->lds_scene_bytes, refill)
+                            : shadow_blocks_per_cu<false>(sd, dev->lds_scene_bytes, refill);
     const int fin_bpc = inst ? finish_blocks_per_cu<true>(sd, ldsb) : finish_blocks_per_cu<false>(sd, ldsb);
 
     for (int it0 = 0; it0 < count; it0 += iters_per_chunk)
@@ -1802,7 +1950,7 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
                 else launch_trace<false>(dev, S, tr_grid, fa, in, row(2 * b), tail);
                 end_timed(dev->stream);
                 begin_timed(0, b, dev->stream);
-                hipLaunchKernelGGL(k_shade, dim3(shade_grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, S.hb, out, S.sh, S.L, kc, tail);
+                hipLaunchKernelGGL(full ? k_shade<true> : k_shade<false>, dim3(shade_grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, S.hb, out, S.sh, S.L, kc, tail);
                 end_timed(dev->stream);
             } else {
                 begin_timed(0, b, dev->stream);

@@ -432,6 +432,45 @@ __device__ __forceinline__ bool trace_ray(const SceneView& sv, f3 o, f3 d, float
     return t.found;
 }
 
+// Persistent lanes with ray refill (Aila & Laine, "Understanding the
+// efficiency of ray traversal on GPUs", 2009): a wave walks a sequence of C
+// ray positions; a lane whose ray is finished goes idle, and once at least
+// `refill_min` lanes are idle (or all are) the idle lanes take the next rays
+// of the sequence, so waves stop running long stretches with a handful of
+// active lanes.  No atomics: the sequence is fixed per wave (pos_of).
+// fetch(c, t) -> bool loads ray c into t (false: nothing to trace);
+// finish(c, t) consumes a finished ray.
+template <bool ANY, bool STATS, int V, typename PosOf, typename Fetch, typename Finish>
+__device__ __forceinline__ void refill_loop(const SceneView& sv, const TStack& ts, int C, int refill_min, PosOf pos_of,
+                                            Fetch fetch, Finish finish, TraceStats& st) {
+    const int lane = (int)__lane_id();
+    const uint64_t below = (1ull << lane) - 1ull;
+    int cursor = 0; // wave-uniform
+    bool busy = false;
+    int pos = 0;
+    Trav t;
+    for (;;) {
+        const uint64_t idle = __ballot(!busy);
+        const int nidle = __popcll(idle);
+        if (cursor < C && (nidle >= refill_min || nidle == 64)) {
+            if (!busy) {
+                const int c = cursor + __popcll(idle & below);
+                if (c < C) {
+                    pos = pos_of(c);
+                    busy = fetch(pos, t);
+                }
+            }
+            cursor += nidle;
+        } else if (nidle == 64) {
+            break; // sequence exhausted, nothing in flight
+        }
+        if (busy && trav_step<ANY, STATS, V>(sv, t, ts, st)) {
+            finish(pos, t);
+            busy = false;
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Surface element (shapes/trimesh.art:14-39, shapes/sphere.art:50-64)
 // ---------------------------------------------------------------------------

@@ -196,6 +196,33 @@ def test_shading_variant_invariance(device, diamond_path):
     np.testing.assert_array_equal(imgs[0], imgs[1])
 
 
+@pytest.mark.parametrize("name", ["diamond_scene.json", "s_deep.json"])
+def test_split_and_refill_invariance(device, root, name):
+    """Fused k_extend, split k_trace + k_shade, and the persistent-lane (refill)
+    trace and shadow kernels render the same image bit for bit, with the same ray
+    counts (diamond forced onto global traversal tables, where refill applies)."""
+    sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", name))
+    imgs, counts = [], []
+    try:
+        device.upload(sc)
+        device.set_option("lds_scene_max", 0)
+        for split, refill in ((0, 0), (1, 0), (1, 16), (0, 8), (-1, -1)):
+            device.set_option("split", split)
+            device.set_option("refill", refill)
+            device.reset_stats()
+            imgs.append(render_gpu(device, sc, 112, 80, 4))
+            st = device.stats()
+            counts.append((st["camera_rays"], st["bounce_rays"], st["shadow_rays"]))
+    finally:
+        device.set_option("split", -1)
+        device.set_option("refill", -1)
+        device.set_option("lds_scene_max", 48 * 1024)
+    for im, c in zip(imgs[1:], counts[1:]):
+        np.testing.assert_array_equal(imgs[0], im)
+        assert c == counts[0]
+    assert imgs[0].sum() > 0
+
+
 @pytest.mark.parametrize("name", ["diamond_scene.json", "primitives.json", "s_deep.json", "s_soup_1m.json"])
 def test_occlusion_parity(device, root, name):
     sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", name))

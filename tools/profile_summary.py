@@ -46,6 +46,12 @@ def kernel_stats(src_dir, tag):
     print("\n".join(lines[:14]))
 
 
+def pmc_file(kernel, scene):
+    """profiles/pmc_<kernel>[_<scene>].json (bench.py's load_pmc reads the same name)."""
+    k = kernel[2:] if kernel.startswith("k_") else kernel
+    return f"pmc_{k}.json" if scene == "diamond_scene" else f"pmc_{k}_{scene}.json"
+
+
 def pmc(fetch_dir, write_dir, kernel="k_extend", scene="diamond_scene"):
     def per_dispatch(d, counter):
         f = find(d, "*counter_collection.csv")
@@ -73,7 +79,7 @@ def pmc(fetch_dir, write_dir, kernel="k_extend", scene="diamond_scene"):
         "hbm_bytes_per_launch": round((2 * fetch + write) * 1024, 1),
         "correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE reports half of wide reads; MI355X_MICROARCH.md HBM section); Infinity-Cache hits are included in the counters",
     }
-    name = "pmc_extend.json" if scene == "diamond_scene" else f"pmc_extend_{scene}.json"
+    name = pmc_file(kernel, scene)
     json.dump(res, open(os.path.join(ROOT, "profiles", name), "w"), indent=1)
     print(json.dumps(res, indent=1))
 
@@ -84,4 +90,5 @@ if __name__ == "__main__":
     kernel_stats(os.path.join(out, "prof"), tag)
     pmc(os.path.join(out, "pmc_fetch"), os.path.join(out, "pmc_write"))
     if os.path.isdir(os.path.join(out, "pmc_fetch_soup")):
-        pmc(os.path.join(out, "pmc_fetch_soup"), os.path.join(out, "pmc_write_soup"), scene="s_soup_16m")
+        # global-table scenes run split: k_trace (persistent-lane k_trace_refill) is the dominant kernel
+        pmc(os.path.join(out, "pmc_fetch_soup"), os.path.join(out, "pmc_write_soup"), kernel="k_trace", scene="s_soup_16m")
