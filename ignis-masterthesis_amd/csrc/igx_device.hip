@@ -34,7 +34,18 @@
 
 using namespace igxd;
 
-namespace {
+// The file is compiled once per part (Makefile: -DIGX_PART=n) so the many
+// kernel instantiations build in parallel:
+//   0 = host driver, C-ABI and the small kernels; 1 = k_extend variants;
+//   2 = k_finish variants; 3 = k_trace / k_trace_refill / k_shade / k_shadow /
+//   k_shadow_refill variants.  Types and device functions are shared; each
+//   part instantiates only its own launch helpers (explicit instantiation),
+//   the others see them as extern templates.
+#ifndef IGX_PART
+#define IGX_PART 0
+#endif
+
+namespace igxh {
 
 constexpr int BLOCK = 256;
 constexpr int MAX_BLOCKS_PER_CU = 8;  // 2048 threads per CU; grids never exceed num_cus * this
@@ -183,6 +194,7 @@ __device__ __forceinline__ void wave_append2(bool a, bool b, int* ca, int* cb, i
 // Slot i of the chunk holds path i; no compaction (tile padding slots are
 // written as dead paths with depth 0), so no atomics.
 // ---------------------------------------------------------------------------
+#if IGX_PART == 0
 __global__ void __launch_bounds__(BLOCK) k_generate(FrameArgs fa, SceneView sv, PathBuf out, float4* L, int* cnt0) {
     const int n = fa.chunk_pixels * fa.spi * fa.chunk_iters;
     if (blockIdx.x == 0 && threadIdx.x < NSH) cnt0[threadIdx.x * CSTRIDE] = gen_shard_count(n, threadIdx.x);
@@ -224,6 +236,8 @@ __global__ void __launch_bounds__(BLOCK) k_generate(FrameArgs fa, SceneView sv, 
         out.p3[e] = 1.0f;
     }
 }
+
+#endif
 
 // ---------------------------------------------------------------------------
 // One bounce of one path: closest hit + technique (gpu_traverse_primary +
@@ -745,6 +759,7 @@ __global__ void __launch_bounds__(BLOCK, REFILL_WAVES) k_shadow_refill(SceneView
     if (STATS) flush_stats<STATS>(st, stats, 4, false);
 }
 
+#if IGX_PART == 0
 // resolve: fb += sum_s L_s / spi (driver/accumulator.art:13-19, make_standard_accumulator)
 __global__ void __launch_bounds__(BLOCK) k_resolve(FrameArgs fa, const float4* L, float* fb, int fb_width) {
     int p = blockIdx.x * BLOCK + threadIdx.x;
@@ -780,6 +795,8 @@ __global__ void k_pack_tiles(FrameArgs fa, const float* fb, float* dst, int num_
         for (int c = 0; c < 3; ++c) dst[3 * i + c] = in ? fb[3 * ((size_t)y * fa.width + x) + c] : 0.0f;
     }
 }
+
+#endif
 
 // hit-level test kernels (one ray per lane)
 template <int V>
@@ -851,7 +868,7 @@ constexpr int CTR_ROWS = 2 * MAX_BOUNCES + 4;
 constexpr size_t CTR_INTS = (size_t)CTR_ROWS * CROW;
 
 // records in counter row `row` of the slot's host mirror (row 0: generated paths)
-long long row_total(const Slot& s, int row) {
+inline long long row_total(const Slot& s, int row) {
     if (row == 0) return s.n0;
     long long t = 0;
     const int* r = s.pinned + (size_t)row * CROW;
@@ -859,7 +876,9 @@ long long row_total(const Slot& s, int row) {
     return t;
 }
 
-} // namespace
+} // namespace igxh
+
+using namespace igxh;
 
 struct igx_device {
     int hip_device = 0;
@@ -908,8 +927,9 @@ struct igx_device {
     igx_stats stats{};
 };
 
-namespace {
+namespace igxh {
 
+#if IGX_PART == 0
 igx_status fail(igx_device* d, igx_status s, const std::string& msg) {
     if (d) d->last_error = msg;
     return s;
@@ -1032,6 +1052,8 @@ int grid_for(igx_device* dev, long long items, int blocks_per_cu) {
     return (int)std::max(q, g);
 }
 
+#endif // IGX_PART == 0
+
 // Kernel schedule per scene (measured per scene):
 //  * traversal tables in LDS (<= 48 KB): fused k_extend, grid-stride k_shadow;
 //  * tables in global memory: shadow rays with persistent lanes (k_shadow_refill,
@@ -1042,9 +1064,9 @@ int grid_for(igx_device* dev, long long items, int blocks_per_cu) {
 //    waves resident and lets lanes refill.  On cache-resident scenes the
 //    fused kernel is faster (no hit records, rays already coherent).
 constexpr size_t SPLIT_TABLE_BYTES = 4u << 20;
-int refill_min(const igx_device* dev) { return dev->refill_opt >= 0 ? dev->refill_opt : 16; }
-bool use_refill(const igx_device* dev) { return refill_min(dev) > 0 && dev->lds_scene_bytes == 0; }
-bool use_split(const igx_device* dev) {
+inline int refill_min(const igx_device* dev) { return dev->refill_opt >= 0 ? dev->refill_opt : 16; }
+inline bool use_refill(const igx_device* dev) { return refill_min(dev) > 0 && dev->lds_scene_bytes == 0; }
+inline bool use_split(const igx_device* dev) {
     return dev->split_opt >= 0 ? dev->split_opt != 0 : (dev->lds_scene_bytes == 0 && dev->table_bytes > SPLIT_TABLE_BYTES);
 }
 
@@ -1203,8 +1225,56 @@ int trace_blocks_per_cu(int v, int waves, size_t lds, bool refill) {
 #undef IGX_RESIDENT
 #undef IGX_RESIDENT8
 #undef IGX_RESIDENT_G
+
+void launch_shade(igx_device* dev, bool full, int grid, const FrameArgs& fa, const PathBuf& in, const HitBuf& hb,
+                  const PathBuf& out, const ShadowBuf& sh, float4* L, const KernelCounters& kc, int tail);
+int shade_blocks_per_cu(bool full);
+#if IGX_PART == 3
+void launch_shade(igx_device* dev, bool full, int grid, const FrameArgs& fa, const PathBuf& in, const HitBuf& hb,
+                  const PathBuf& out, const ShadowBuf& sh, float4* L, const KernelCounters& kc, int tail) {
+    if (full) hipLaunchKernelGGL(k_shade<true>, dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, hb, out, sh, L, kc, tail);
+    else hipLaunchKernelGGL(k_shade<false>, dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, hb, out, sh, L, kc, tail);
+}
+int shade_blocks_per_cu(bool full) { return full ? resident_blocks(k_shade<true>) : resident_blocks(k_shade<false>); }
+#endif
+
+// Launch helpers: defined (explicitly instantiated) in their part, extern elsewhere.
+#define IGX_EXTEND_HELPERS(X, S)                                                                                     \
+    X void launch_extend<S>(igx_device*, Slot&, int, const FrameArgs&, const PathBuf&, const PathBuf&,               \
+                            const KernelCounters&, int);                                                             \
+    X int extend_blocks_per_cu<S>(int, size_t);
+#define IGX_FINISH_HELPERS(X, S)                                                                                     \
+    X void launch_finish<S>(igx_device*, Slot&, int, const FrameArgs&, const PathBuf&, const int*, int);             \
+    X int finish_blocks_per_cu<S>(int, size_t);
+#define IGX_TRACE_HELPERS(X, S)                                                                                      \
+    X void launch_trace<S>(igx_device*, Slot&, int, const FrameArgs&, const PathBuf&, const int*, int);              \
+    X void launch_shadow<S>(igx_device*, Slot&, int, const int*);                                                    \
+    X int trace_blocks_per_cu<S>(int, int, size_t, bool);                                                            \
+    X int shadow_blocks_per_cu<S>(int, size_t, bool);
+#if IGX_PART == 1
+IGX_EXTEND_HELPERS(template, true)
+IGX_EXTEND_HELPERS(template, false)
+#else
+IGX_EXTEND_HELPERS(extern template, true)
+IGX_EXTEND_HELPERS(extern template, false)
+#endif
+#if IGX_PART == 2
+IGX_FINISH_HELPERS(template, true)
+IGX_FINISH_HELPERS(template, false)
+#else
+IGX_FINISH_HELPERS(extern template, true)
+IGX_FINISH_HELPERS(extern template, false)
+#endif
+#if IGX_PART == 3
+IGX_TRACE_HELPERS(template, true)
+IGX_TRACE_HELPERS(template, false)
+#else
+IGX_TRACE_HELPERS(extern template, true)
+IGX_TRACE_HELPERS(extern template, false)
+#endif
 #undef IGX_RES1
 
+#if IGX_PART == 0
 // Wait for the chunk last run in `s` and fold its statistics in.
 igx_status harvest(igx_device* dev, Slot& s) {
     if (!s.pending) return IGX_OK;
@@ -1300,8 +1370,11 @@ void setup_camera(igx_device* dev, int width, int height) {
     k.tmax = c.far_clip;
 }
 
+#endif // IGX_PART == 0
+
 } // namespace
 
+#if IGX_PART == 0
 // ===========================================================================
 // C-ABI
 // ===========================================================================
@@ -1874,11 +1947,8 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
     const bool refill = use_refill(dev);
     const int tr_bpc = inst ? trace_blocks_per_cu<true>(sd, dev->trace_waves, dev->lds_scene_bytes, refill)
                             : trace_blocks_per_cu<false>(sd, dev->trace_waves, dev->lds_scene_bytes, refill);
-    int shade_bpc = 0;
     const bool full = variant_full(sd);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&shade_bpc, full ? k_shade<true> : k_shade<false>, BLOCK, 0) != hipSuccess ||
-        shade_bpc < 1)
-        shade_bpc = 1;
+    const int shade_bpc = shade_blocks_per_cu(full);
     const bool split = use_split(dev);
     const int sh_bpc = inst ? shadow_blocks_per_cu<true>(sd, dev->lds_scene_bytes, refill)
                             : shadow_blocks_per_cu<false>(sd, dev->lds_scene_bytes, refill);
@@ -1909,7 +1979,14 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
         fa.chunk_pixel0 = (int)px0;
         fa.chunk_pixels = chunk_pixels;
         long long n = (long long)chunk_pixels * p->spi * fa.chunk_iters;
-        int tail = dev->tail_opt >= 0 ? (int)std::min<int64_t>(dev->tail_opt, 1 << 30) : (int)std::max<long long>(32768, n / 64);
+        // tail threshold (auto): n / 64, but at most what one pass of k_finish
+        // holds (one path per resident lane): beyond that the tail kernel's
+        // lanes loop over several long paths each and it outlasts the
+        // overlapping chunk (diamond 32M-path chunks: 500K -> 196K tail paths,
+        // 204.6 -> 195.0 ms per frame, tools/sweep_frame.py)
+        const long long fin_lanes = (long long)fin_bpc * dev->num_cus * BLOCK;
+        int tail = dev->tail_opt >= 0 ? (int)std::min<int64_t>(dev->tail_opt, 1 << 30)
+                                      : (int)std::max<long long>(32768, std::min(n / 64, fin_lanes));
         S.tail = tail;
         S.camera = valid_pixels_in_chunk(fa) * p->spi * fa.chunk_iters;
         int* cnt = S.ctr; // row 2b: paths entering bounce b, row 2b+1: shadow rays of bounce b
@@ -1950,7 +2027,7 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
                 else launch_trace<false>(dev, S, tr_grid, fa, in, row(2 * b), tail);
                 end_timed(dev->stream);
                 begin_timed(0, b, dev->stream);
-                hipLaunchKernelGGL(full ? k_shade<true> : k_shade<false>, dim3(shade_grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, S.hb, out, S.sh, S.L, kc, tail);
+                launch_shade(dev, full, shade_grid, fa, in, S.hb, out, S.sh, S.L, kc, tail);
                 end_timed(dev->stream);
             } else {
                 begin_timed(0, b, dev->stream);
@@ -2139,3 +2216,5 @@ extern "C" igx_status igx_trace_hits(igx_device* dev, const float* rays, int32_t
 extern "C" igx_status igx_trace_occlusion(igx_device* dev, const float* rays, int32_t n, uint32_t flags, int32_t* occluded) {
     return trace_batch(dev, rays, n, flags, occluded, nullptr, 1);
 }
+
+#endif // IGX_PART == 0

@@ -1,16 +1,20 @@
 """Dev tool: per-kernel VGPR / spill / LDS usage of the gfx950 code object in
-build/igx_device.o (reads the AMDGPU metadata notes)."""
+build/igx_device_p*.o (reads the AMDGPU metadata notes).
+usage: kernel_resources.py [name filter] [objects...]"""
+import glob
 import re
 import subprocess
 import sys
 
 LLVM = "/opt/rocm/llvm/bin"
-obj = sys.argv[1] if len(sys.argv) > 1 else "ignis-masterthesis_amd/build/igx_device.o"
-pat = sys.argv[2] if len(sys.argv) > 2 else "k_"
-subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin=/tmp/_fat.bin", obj, "/tmp/_host.o"], check=True)
-subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", "--input=/tmp/_fat.bin",
-                "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--output=/tmp/_dev.co"], check=True)
-notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", "/tmp/_dev.co"], capture_output=True, text=True).stdout
+pat = sys.argv[1] if len(sys.argv) > 1 else "k_"
+objs = sys.argv[2:] or sorted(glob.glob("ignis-masterthesis_amd/build/igx_device_p*.o"))
+notes = ""
+for obj in objs:
+    subprocess.run([f"{LLVM}/llvm-objcopy", "--dump-section=.hip_fatbin=/tmp/_fat.bin", obj, "/tmp/_host.o"], check=True)
+    subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", "--input=/tmp/_fat.bin",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--output=/tmp/_dev.co"], check=True)
+    notes += subprocess.run([f"{LLVM}/llvm-readelf", "--notes", "/tmp/_dev.co"], capture_output=True, text=True).stdout
 for b in notes.split(".name:")[1:]:
     name = b.split("\n")[0].strip()
     if pat not in name:
