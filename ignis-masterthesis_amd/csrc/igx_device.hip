@@ -865,6 +865,9 @@ struct Slot {
 };
 
 constexpr int CTR_ROWS = 2 * MAX_BOUNCES + 4;
+// BLAS with more triangles build without spatial splits (load time; their
+// triangles are small next to the scene in the suite's soups)
+constexpr uint32_t SPATIAL_SPLIT_MAX_FACES = 1u << 21;
 constexpr size_t CTR_INTS = (size_t)CTR_ROWS * CROW;
 
 // records in counter row `row` of the slot's host mirror (row 0: generated paths)
@@ -898,6 +901,10 @@ struct igx_device {
     size_t lds_scene_bytes = 0;        // bytes staged per block for the current scene (0 = global tables)
     size_t table_bytes = 0;            // traversal tables (nodes, instances, triangles) of the current scene
     int leaf_size = 4;
+    // SBVH for BLAS up to SPATIAL_SPLIT_MAX_FACES triangles (option "spatial_splits"):
+    // off by default -- measured slower on the diamond (196 -> 230 ms per frame)
+    // and neutral on primitives, S-deep and soup-1M
+    bool spatial_splits = false;
     // scene
     bool has_scene = false;
     std::vector<void*> scene_allocs;
@@ -1459,6 +1466,7 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
         if (value != 0 && value != 2 && value != 4) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "bvh_width must be 0 (auto), 2 or 4");
         dev->bvh_width_opt = (int)value;
     }
+    else if (k == "spatial_splits") dev->spatial_splits = value != 0;
     else if (k == "bvh_leaf_size") {
         if (value < 1 || value > 16) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "bvh_leaf_size must be in [1, 16]");
         dev->leaf_size = (int)value;
@@ -1508,7 +1516,15 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
             }
         }
         try {
-            brs[s] = igx::build_bvh2(bi, dev->leaf_size);
+            if (dev->spatial_splits && m.num_faces <= SPATIAL_SPLIT_MAX_FACES) {
+                std::vector<float> tv(9 * (size_t)m.num_faces);
+                for (uint32_t f = 0; f < m.num_faces; ++f)
+                    for (int k = 0; k < 3; ++k)
+                        for (int a = 0; a < 3; ++a) tv[9 * (size_t)f + 3 * k + a] = m.vertices[3 * m.indices[3 * f + k] + a];
+                brs[s] = igx::build_sbvh2(bi, tv, dev->leaf_size);
+            } else {
+                brs[s] = igx::build_bvh2(bi, dev->leaf_size);
+            }
         } catch (const std::exception& ex) {
             return fail(dev, IGX_ERR_INVALID_ARGUMENT, ex.what());
         }

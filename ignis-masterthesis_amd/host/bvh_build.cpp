@@ -156,6 +156,49 @@ void set_empty(BvhNode& n, int k) {
     set_child(n, k, e, -1);
 }
 
+// Flatten a tmp-node tree into BvhNodes in DFS pre-order; each inner tmp node
+// becomes one BvhNode (leaves become leaf codes in their parent).
+void flatten(const std::vector<TmpNode>& tn, int32_t root, BvhBuildResult& res) {
+    auto leaf_ref = [&](const TmpNode& t) { return encode_leaf((int32_t)t.first, (int32_t)t.count); };
+    struct Item { int32_t tmp; int32_t out; int depth; };
+    std::vector<Item> stack;
+    res.nodes.emplace_back();
+    if (tn[root].left < 0) {
+        // root itself is a leaf: both children reference it (an empty child
+        // box would pass the min/max slab test; a duplicate leaf is harmless
+        // for closest and any hit)
+        set_child(res.nodes[0], 0, tn[root].box, leaf_ref(tn[root]));
+        set_child(res.nodes[0], 1, tn[root].box, leaf_ref(tn[root]));
+        res.depth = 1;
+        res.root_is_leaf = true;
+        res.root_leaf_ref = leaf_ref(tn[root]);
+        return;
+    }
+    stack.push_back({root, 0, 1});
+    while (!stack.empty()) {
+        Item it = stack.back();
+        stack.pop_back();
+        res.depth = std::max(res.depth, it.depth);
+        const TmpNode& t = tn[it.tmp];
+        int32_t kids[2] = {t.left, t.right};
+        // push right first so the left subtree is laid out right after its parent
+        int32_t out_idx[2] = {-1, -1};
+        for (int k = 0; k < 2; ++k) {
+            const TmpNode& c = tn[kids[k]];
+            if (c.left < 0) {
+                set_child(res.nodes[it.out], k, c.box, leaf_ref(c));
+            } else {
+                out_idx[k] = (int32_t)res.nodes.size();
+                res.nodes.emplace_back();
+                set_child(res.nodes[it.out], k, c.box, out_idx[k]);
+            }
+            res.nodes[it.out].pad[k] = 0;
+        }
+        for (int k = 1; k >= 0; --k)
+            if (out_idx[k] >= 0) stack.push_back({kids[k], out_idx[k], it.depth + 1});
+    }
+}
+
 } // namespace
 
 BvhBuildResult build_bvh2(const BvhBuildInput& in, int max_leaf, int bins) {
@@ -181,45 +224,263 @@ BvhBuildResult build_bvh2(const BvhBuildInput& in, int max_leaf, int bins) {
     int32_t root = b.build(0, (uint32_t)n, 0);
     res.prim_order = std::move(idx);
 
-    // Flatten: BvhNodes in DFS pre-order; each inner tmp node becomes one BvhNode.
-    auto leaf_ref = [&](const TmpNode& t) { return encode_leaf((int32_t)t.first, (int32_t)t.count); };
-    struct Item { int32_t tmp; int32_t out; int depth; };
-    std::vector<Item> stack;
-    res.nodes.emplace_back();
-    if (b.nodes[root].left < 0) {
-        // root itself is a leaf: both children reference it (an empty child
-        // box would pass the min/max slab test; a duplicate leaf is harmless
-        // for closest and any hit)
-        set_child(res.nodes[0], 0, b.nodes[root].box, leaf_ref(b.nodes[root]));
-        set_child(res.nodes[0], 1, b.nodes[root].box, leaf_ref(b.nodes[root]));
-        res.depth = 1;
-        res.root_is_leaf = true;
-        res.root_leaf_ref = leaf_ref(b.nodes[root]);
-        return res;
+    flatten(b.nodes, root, res);
+    return res;
+}
+
+// ---------------------------------------------------------------------------
+// Split BVH (Stich, Friedrich and Dietrich, "Spatial Splits in Bounding Volume
+// Hierarchies", HPG 2009).  At every node the binned object split competes
+// with a binned spatial split whose bins hold the bounds of the triangles'
+// parts clipped to the bin slabs; a triangle the chosen plane cuts is then
+// referenced from both sides, each with the bounds of its part.  Spatial
+// splits are tried only where the object split's children overlap by more
+// than alpha of the root area, and the added references are capped.
+// ---------------------------------------------------------------------------
+namespace {
+
+struct Ref {
+    uint32_t prim;
+    Box box;
+};
+
+bool nonempty(const Box& b) { return b.lo[0] <= b.hi[0] && b.lo[1] <= b.hi[1] && b.lo[2] <= b.hi[2]; }
+
+Box overlap(const Box& a, const Box& b) {
+    Box r;
+    for (int k = 0; k < 3; ++k) {
+        r.lo[k] = std::max(a.lo[k], b.lo[k]);
+        r.hi[k] = std::min(a.hi[k], b.hi[k]);
     }
-    stack.push_back({root, 0, 1});
-    while (!stack.empty()) {
-        Item it = stack.back();
-        stack.pop_back();
-        res.depth = std::max(res.depth, it.depth);
-        const TmpNode& t = b.nodes[it.tmp];
-        int32_t kids[2] = {t.left, t.right};
-        // push right first so the left subtree is laid out right after its parent
-        int32_t out_idx[2] = {-1, -1};
-        for (int k = 0; k < 2; ++k) {
-            const TmpNode& c = b.nodes[kids[k]];
-            if (c.left < 0) {
-                set_child(res.nodes[it.out], k, c.box, leaf_ref(c));
-            } else {
-                out_idx[k] = (int32_t)res.nodes.size();
-                res.nodes.emplace_back();
-                set_child(res.nodes[it.out], k, c.box, out_idx[k]);
+    return r;
+}
+
+// Bounds of the part of triangle v (9 floats) with lo <= x[axis] <= hi,
+// widened by a few ulps of the triangle's extent (so rounding of the
+// edge-plane points never shrinks it below the true part) and intersected
+// with the reference's current bounds `cur`.  Empty box if nothing is left.
+Box clip_part(const float* v, int axis, float lo, float hi, const Box& cur) {
+    Box b;
+    for (int i = 0; i < 3; ++i) {
+        const float* a = v + 3 * i;
+        const float* c = v + 3 * ((i + 1) % 3);
+        const float pa = a[axis], pc = c[axis];
+        if (pa >= lo && pa <= hi) b.grow_point(a);
+        const float planes[2] = {lo, hi};
+        for (float pl : planes) {
+            if ((pa < pl && pc > pl) || (pa > pl && pc < pl)) {
+                const double t = ((double)pl - pa) / ((double)pc - pa);
+                float q[3];
+                for (int k = 0; k < 3; ++k) q[k] = (float)((double)a[k] + t * ((double)c[k] - a[k]));
+                q[axis] = pl;
+                b.grow_point(q);
             }
-            res.nodes[it.out].pad[k] = 0;
         }
-        for (int k = 1; k >= 0; --k)
-            if (out_idx[k] >= 0) stack.push_back({kids[k], out_idx[k], it.depth + 1});
     }
+    if (!nonempty(b)) return Box();
+    for (int k = 0; k < 3; ++k) {
+        const float tmin = std::min({v[k], v[3 + k], v[6 + k]}), tmax = std::max({v[k], v[3 + k], v[6 + k]});
+        const float scale = std::max({std::fabs(tmin), std::fabs(tmax), tmax - tmin});
+        const float e = 8 * std::numeric_limits<float>::epsilon() * scale;
+        b.lo[k] -= e;
+        b.hi[k] += e;
+    }
+    Box r = overlap(b, cur);
+    return nonempty(r) ? r : Box();
+}
+
+struct SplitBuilder {
+    const float* V; // 9 floats per primitive
+    int max_leaf, bins;
+    float min_overlap; // alpha * root half-area
+    long long budget;  // references spatial splits may still add
+    std::vector<TmpNode> nodes;
+    std::vector<uint32_t> order;
+
+    int32_t make_leaf(const std::vector<Ref>& refs, const Box& box) {
+        int32_t me = (int32_t)nodes.size();
+        nodes.emplace_back();
+        nodes[me].box = box;
+        nodes[me].first = (uint32_t)order.size();
+        nodes[me].count = (uint32_t)refs.size();
+        for (const Ref& r : refs) order.push_back(r.prim);
+        return me;
+    }
+
+    static void center(const Box& b, float* c) {
+        for (int k = 0; k < 3; ++k) c[k] = 0.5f * (b.lo[k] + b.hi[k]);
+    }
+
+    int32_t build(std::vector<Ref>& refs) {
+        const uint32_t n = (uint32_t)refs.size();
+        Box box, cbox;
+        for (const Ref& r : refs) {
+            box.grow(r.box);
+            float c[3];
+            center(r.box, c);
+            cbox.grow_point(c);
+        }
+        if (n == 1) return make_leaf(refs, box);
+        const float parent_area = std::max(box.half_area(), 1e-30f);
+        const float inf = std::numeric_limits<float>::max();
+
+        // object split: binned SAH over reference centroids
+        float best_o = inf;
+        int ax_o = -1, bin_o = -1;
+        Box lb_o, rb_o;
+        std::vector<Box> bb(bins), rbox(bins);
+        std::vector<uint32_t> cnt(bins), rcnt(bins);
+        for (int axis = 0; axis < 3; ++axis) {
+            const float ext = cbox.hi[axis] - cbox.lo[axis];
+            if (!(ext > 0)) continue;
+            const float scale = bins / ext;
+            for (int b = 0; b < bins; ++b) { bb[b] = Box(); cnt[b] = 0; }
+            for (const Ref& r : refs) {
+                float c[3];
+                center(r.box, c);
+                int b = std::min(bins - 1, (int)((c[axis] - cbox.lo[axis]) * scale));
+                bb[b].grow(r.box);
+                cnt[b]++;
+            }
+            Box acc;
+            uint32_t c = 0;
+            for (int b = bins - 1; b > 0; --b) {
+                acc.grow(bb[b]);
+                c += cnt[b];
+                rbox[b] = acc;
+                rcnt[b] = c;
+            }
+            acc = Box();
+            c = 0;
+            for (int b = 0; b < bins - 1; ++b) {
+                acc.grow(bb[b]);
+                c += cnt[b];
+                if (c == 0 || rcnt[b + 1] == 0) continue;
+                float cost = acc.half_area() * c + rbox[b + 1].half_area() * rcnt[b + 1];
+                if (cost < best_o) { best_o = cost; ax_o = axis; bin_o = b; lb_o = acc; rb_o = rbox[b + 1]; }
+            }
+        }
+
+        // spatial split: binned over the node box, triangles clipped to the bins
+        float best_s = inf;
+        int ax_s = -1;
+        float pos_s = 0;
+        bool try_spatial = budget > 0;
+        if (ax_o >= 0) {
+            Box ov = overlap(lb_o, rb_o);
+            try_spatial = try_spatial && nonempty(ov) && ov.half_area() > min_overlap;
+        }
+        if (try_spatial) {
+            std::vector<uint32_t> enter(bins), leave(bins);
+            for (int axis = 0; axis < 3; ++axis) {
+                const float lo0 = box.lo[axis], ext = box.hi[axis] - lo0;
+                if (!(ext > 0)) continue;
+                const float w = ext / bins;
+                auto plane = [&](int b) { return b >= bins ? box.hi[axis] : lo0 + w * b; };
+                for (int b = 0; b < bins; ++b) { bb[b] = Box(); enter[b] = leave[b] = 0; }
+                for (const Ref& r : refs) {
+                    int b0 = std::min(bins - 1, std::max(0, (int)((r.box.lo[axis] - lo0) / w)));
+                    int b1 = std::min(bins - 1, std::max(b0, (int)((r.box.hi[axis] - lo0) / w)));
+                    enter[b0]++;
+                    leave[b1]++;
+                    if (b0 == b1) {
+                        bb[b0].grow(r.box);
+                        continue;
+                    }
+                    for (int b = b0; b <= b1; ++b) {
+                        Box part = clip_part(V + 9 * (size_t)r.prim, axis, plane(b), plane(b + 1), r.box);
+                        if (nonempty(part)) bb[b].grow(part);
+                    }
+                }
+                Box acc;
+                uint32_t c = 0;
+                for (int b = bins - 1; b > 0; --b) {
+                    acc.grow(bb[b]);
+                    c += leave[b];
+                    rbox[b] = acc;
+                    rcnt[b] = c;
+                }
+                acc = Box();
+                c = 0;
+                for (int b = 0; b < bins - 1; ++b) {
+                    acc.grow(bb[b]);
+                    c += enter[b];
+                    if (c == 0 || rcnt[b + 1] == 0 || !nonempty(acc) || !nonempty(rbox[b + 1])) continue;
+                    float cost = acc.half_area() * c + rbox[b + 1].half_area() * rcnt[b + 1];
+                    if (cost < best_s) { best_s = cost; ax_s = axis; pos_s = plane(b + 1); }
+                }
+            }
+        }
+
+        const float best = std::min(best_o, best_s);
+        const float split_cost = best < inf ? 1.0f + best / parent_area : inf;
+        if ((int)n <= max_leaf && (float)n <= split_cost) return make_leaf(refs, box);
+
+        std::vector<Ref> L, R;
+        if (best_s < best_o) {
+            for (const Ref& r : refs) {
+                if (r.box.hi[ax_s] <= pos_s) { L.push_back(r); continue; }
+                if (r.box.lo[ax_s] >= pos_s) { R.push_back(r); continue; }
+                Box lbx = clip_part(V + 9 * (size_t)r.prim, ax_s, -inf, pos_s, r.box);
+                Box rbx = clip_part(V + 9 * (size_t)r.prim, ax_s, pos_s, inf, r.box);
+                if (nonempty(lbx) && nonempty(rbx)) {
+                    L.push_back({r.prim, lbx});
+                    R.push_back({r.prim, rbx});
+                    --budget;
+                } else if (nonempty(rbx)) {
+                    R.push_back(r);
+                } else {
+                    L.push_back(r);
+                }
+            }
+        } else if (ax_o >= 0) {
+            const float scale = bins / (cbox.hi[ax_o] - cbox.lo[ax_o]);
+            for (const Ref& r : refs) {
+                float c[3];
+                center(r.box, c);
+                int b = std::min(bins - 1, (int)((c[ax_o] - cbox.lo[ax_o]) * scale));
+                (b <= bin_o ? L : R).push_back(r);
+            }
+        }
+        if (L.empty() || R.empty()) {
+            // no useful plane (coincident centroids): halve the list
+            L.assign(refs.begin(), refs.begin() + n / 2);
+            R.assign(refs.begin() + n / 2, refs.end());
+        }
+        std::vector<Ref>().swap(refs);
+        const int32_t me = (int32_t)nodes.size();
+        nodes.emplace_back();
+        nodes[me].box = box;
+        const int32_t l = build(L);
+        const int32_t r = build(R);
+        nodes[me].left = l;
+        nodes[me].right = r;
+        return me;
+    }
+};
+
+} // namespace
+
+BvhBuildResult build_sbvh2(const BvhBuildInput& in, const std::vector<float>& tri9, int max_leaf, float ref_budget,
+                           int bins) {
+    const size_t n = in.count();
+    if (n == 0 || tri9.size() != 9 * n) return build_bvh2(in, max_leaf, bins);
+    if (max_leaf < 1 || max_leaf > (1 << kLeafCountBits)) throw std::invalid_argument("max_leaf out of range");
+    std::vector<Ref> refs(n);
+    Box root;
+    for (size_t i = 0; i < n; ++i) {
+        refs[i].prim = (uint32_t)i;
+        refs[i].box.grow(&in.bmin[3 * i], &in.bmax[3 * i]);
+        root.grow(refs[i].box);
+    }
+    SplitBuilder sb{tri9.data(), max_leaf, bins, 1e-5f * root.half_area(), (long long)(ref_budget * (double)n), {}, {}};
+    sb.nodes.reserve(2 * n / std::max(1, max_leaf) + 4);
+    const int32_t r = sb.build(refs);
+    if (sb.order.size() >= (size_t)kMaxLeafFirst) throw std::invalid_argument("too many references for the leaf encoding");
+    BvhBuildResult res;
+    res.max_leaf = max_leaf;
+    res.prim_order = std::move(sb.order);
+    flatten(sb.nodes, r, res);
     return res;
 }
 

@@ -55,6 +55,14 @@ struct BvhBuildResult {
 // Build a BVH2 with binned SAH.  `max_leaf` caps primitives per leaf (<= 16).
 BvhBuildResult build_bvh2(const BvhBuildInput& in, int max_leaf, int bins = 32);
 
+// Binned SAH with spatial splits (SBVH) over triangles: `tri9` holds the
+// three vertices of primitive i at [9 i, 9 i + 9).  A triangle may be
+// referenced by several leaves (prim_order then repeats it); at most
+// ref_budget * count references are added.  Closest hits are unchanged:
+// every reference box bounds its part of the triangle.
+BvhBuildResult build_sbvh2(const BvhBuildInput& in, const std::vector<float>& tri9, int max_leaf,
+                           float ref_budget = 0.3f, int bins = 32);
+
 // 4-wide node (128 B, two 64-B halves): child boxes as SoA so one float4
 // load gives one bound of all four children.
 //   float4 lo_x, hi_x, lo_y, hi_y, lo_z, hi_z   (child k in lane k)

@@ -1,0 +1,192 @@
+// Host check of the BVH builders (compiled and run by tests/test_bvh_host.py
+// with g++ against ignis-masterthesis_amd/host/bvh_build.cpp; no GPU): the
+// closest hit found through the built BVH2 -- binned SAH (build_bvh2) and
+// with spatial splits (build_sbvh2) -- equals brute force on random rays, for
+// scenes of long thin triangles (where spatial splits engage), large
+// overlapping triangles and a small-triangle soup.  Prints one line per case.
+#include "bvh_build.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <random>
+#include <vector>
+
+using namespace igx;
+
+namespace {
+
+// Moeller-Trumbore in the device's Tri1 form (e1 = v0 - v1, e2 = v2 - v0,
+// n = cross(e1, e2); igx_kernels.h tri_test)
+bool tri_hit(const float* v, const float* o, const float* d, float tmax, float& t) {
+    float e1[3], e2[3], n[3], c[3], r[3];
+    for (int k = 0; k < 3; ++k) {
+        e1[k] = v[k] - v[3 + k];
+        e2[k] = v[6 + k] - v[k];
+        c[k] = v[k] - o[k];
+    }
+    auto cross = [](const float* a, const float* b, float* out) {
+        out[0] = a[1] * b[2] - a[2] * b[1];
+        out[1] = a[2] * b[0] - a[0] * b[2];
+        out[2] = a[0] * b[1] - a[1] * b[0];
+    };
+    auto dot = [](const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; };
+    cross(e1, e2, n);
+    cross(d, c, r);
+    const float det = dot(n, d);
+    const float inv = 1.0f / det;
+    const float u = dot(r, e2) * inv, w = dot(r, e1) * inv;
+    const float eps = 1.1920929e-7f;
+    if (!(u >= -eps && w >= -eps && 1 - u - w >= -eps)) return false;
+    t = dot(c, n) * inv;
+    return t >= 0 && t <= tmax;
+}
+
+struct Hit {
+    int prim = -1;
+    float t = INFINITY;
+    void accept(int p, float th) {
+        if (th < t || (th == t && p > prim)) { t = th; prim = p; }
+    }
+};
+
+bool box_hit(const float* b, const float* o, const double* id, float tmax) {
+    double tn = 0, tf = tmax;
+    for (int k = 0; k < 3; ++k) {
+        double t0 = ((double)b[2 * k] - o[k]) * id[k], t1 = ((double)b[2 * k + 1] - o[k]) * id[k];
+        if (t0 > t1) std::swap(t0, t1);
+        tn = std::max(tn, t0);
+        tf = std::min(tf, t1);
+    }
+    return tn <= tf;
+}
+
+Hit trace(const BvhBuildResult& br, const std::vector<float>& V, const float* o, const float* d) {
+    Hit h;
+    const double id[3] = {1.0 / d[0], 1.0 / d[1], 1.0 / d[2]};
+    auto leaf = [&](int32_t ref) {
+        const int code = ~ref, first = code >> kLeafCountBits, count = (code & ((1 << kLeafCountBits) - 1)) + 1;
+        for (int i = first; i < first + count; ++i) {
+            const int p = (int)br.prim_order[i];
+            float t;
+            if (tri_hit(&V[9 * (size_t)p], o, d, h.t, t)) h.accept(p, t);
+        }
+    };
+    if (br.root_is_leaf) {
+        leaf(br.root_leaf_ref);
+        return h;
+    }
+    std::vector<int32_t> st{0};
+    while (!st.empty()) {
+        const BvhNode& nd = br.nodes[st.back()];
+        st.pop_back();
+        for (int k = 0; k < 2; ++k) {
+            const float* b = nd.b + 6 * k;
+            if (!(b[0] <= b[1]) || !box_hit(b, o, id, h.t)) continue;
+            if (nd.ref[k] >= 0) st.push_back(nd.ref[k]);
+            else leaf(nd.ref[k]);
+        }
+    }
+    return h;
+}
+
+Hit brute(const std::vector<float>& V, const float* o, const float* d) {
+    Hit h;
+    for (size_t p = 0; p < V.size() / 9; ++p) {
+        float t;
+        if (tri_hit(&V[9 * p], o, d, INFINITY, t)) h.accept((int)p, t);
+    }
+    return h;
+}
+
+BvhBuildInput bounds(const std::vector<float>& V) {
+    BvhBuildInput in;
+    const size_t n = V.size() / 9;
+    in.bmin.resize(3 * n);
+    in.bmax.resize(3 * n);
+    in.centroid.resize(3 * n);
+    for (size_t p = 0; p < n; ++p)
+        for (int a = 0; a < 3; ++a) {
+            float lo = std::min({V[9 * p + a], V[9 * p + 3 + a], V[9 * p + 6 + a]});
+            float hi = std::max({V[9 * p + a], V[9 * p + 3 + a], V[9 * p + 6 + a]});
+            in.bmin[3 * p + a] = lo;
+            in.bmax[3 * p + a] = hi;
+            in.centroid[3 * p + a] = 0.5f * (lo + hi);
+        }
+    return in;
+}
+
+// SAH cost of a BVH2 (node traversal 1, triangle test 1, relative to the root area)
+double sah(const BvhBuildResult& br) {
+    double cost = 0, root = 0;
+    for (size_t i = 0; i < br.nodes.size(); ++i)
+        for (int k = 0; k < 2; ++k) {
+            const float* b = br.nodes[i].b + 6 * k;
+            if (!(b[0] <= b[1])) continue;
+            double dx = b[1] - b[0], dy = b[3] - b[2], dz = b[5] - b[4];
+            double a = dx * (dy + dz) + dy * dz;
+            if (i == 0) root += a;
+            int32_t r = br.nodes[i].ref[k];
+            cost += a * (r >= 0 ? 1.0 : (double)(((~r) & ((1 << kLeafCountBits) - 1)) + 1));
+        }
+    return root > 0 ? 1.0 + cost / root : 0.0;
+}
+
+}  // namespace
+
+int main() {
+    std::mt19937 rng(42);
+    std::uniform_real_distribution<float> U(-1, 1);
+    struct Case { const char* name; std::vector<float> V; };
+    std::vector<Case> cases;
+    {  // long thin triangles from a ring to a common apex region (a pavilion, like Diamond.ply)
+        std::vector<float> V;
+        for (int i = 0; i < 600; ++i) {
+            float a0 = 6.2831853f * i / 600, a1 = 6.2831853f * (i + 1) / 600;
+            float ax[3] = {0.02f * U(rng), 0.02f * U(rng), -1.0f + 0.05f * U(rng)};
+            float p[9] = {ax[0], ax[1], ax[2], std::cos(a0), std::sin(a0), 0.3f * U(rng), std::cos(a1), std::sin(a1), 0.3f * U(rng)};
+            V.insert(V.end(), p, p + 9);
+        }
+        cases.push_back({"slivers", V});
+    }
+    {  // large overlapping triangles
+        std::vector<float> V;
+        for (int i = 0; i < 1500 * 9; ++i) V.push_back(U(rng));
+        cases.push_back({"large", V});
+    }
+    {  // small-triangle soup
+        std::vector<float> V;
+        for (int i = 0; i < 4000; ++i) {
+            float c[3] = {U(rng), U(rng), U(rng)};
+            for (int k = 0; k < 9; ++k) V.push_back(c[k % 3] + 0.03f * U(rng));
+        }
+        cases.push_back({"soup", V});
+    }
+    int bad_total = 0;
+    for (const Case& cs : cases) {
+        const size_t n = cs.V.size() / 9;
+        BvhBuildInput in = bounds(cs.V);
+        for (int split = 0; split < 2; ++split) {
+            BvhBuildResult br = split ? build_sbvh2(in, cs.V, 4) : build_bvh2(in, 4);
+            std::vector<char> seen(n, 0);
+            for (uint32_t p : br.prim_order) seen[p] = 1;
+            int missing = (int)std::count(seen.begin(), seen.end(), 0);
+            int bad = 0, hits = 0;
+            std::mt19937 rr(7);
+            std::uniform_real_distribution<float> R(-2, 2);
+            for (int i = 0; i < 20000; ++i) {
+                float o[3] = {R(rr), R(rr), R(rr)}, d[3] = {R(rr), R(rr), R(rr)};
+                float l = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+                for (float& x : d) x /= l;
+                Hit a = trace(br, cs.V, o, d), b = brute(cs.V, o, d);
+                hits += b.prim >= 0;
+                if (a.prim != b.prim || !(a.t == b.t || (a.prim < 0 && b.prim < 0))) ++bad;
+            }
+            std::printf("%s %s refs %zu/%zu nodes %zu sah %.2f hits %d mismatches %d missing %d\n", cs.name,
+                        split ? "sbvh" : "bvh2", br.prim_order.size(), n, br.nodes.size(), sah(br), hits, bad, missing);
+            bad_total += bad + missing;
+        }
+    }
+    std::printf(bad_total ? "FAIL\n" : "ok\n");
+    return bad_total ? 1 : 0;
+}

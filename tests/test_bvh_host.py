@@ -1,0 +1,23 @@
+"""Host BVH builders (CPU only): closest hits through the binned-SAH BVH2 and
+the spatial-split BVH equal brute force on random rays (tests/native/bvh_check.cpp,
+compiled here with g++ against host/bvh_build.cpp)."""
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HOST = os.path.join(ROOT, "ignis-masterthesis_amd", "host")
+
+
+def test_bvh_builders_match_brute_force(tmp_path):
+    exe = str(tmp_path / "bvh_check")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", "-I", HOST, os.path.join(ROOT, "tests", "native", "bvh_check.cpp"),
+                    os.path.join(HOST, "bvh_build.cpp"), "-o", exe], check=True)
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    print(out.stdout)
+    assert out.returncode == 0, out.stdout + out.stderr
+    lines = [l.split() for l in out.stdout.splitlines() if " refs " in l]
+    assert len(lines) == 6
+    # spatial splits engage on the thin triangles and lower their SAH cost
+    sl = {l[1]: l for l in lines if l[0] == "slivers"}
+    assert int(sl["sbvh"][3].split("/")[0]) > int(sl["bvh2"][3].split("/")[0])
+    assert float(sl["sbvh"][7]) < float(sl["bvh2"][7])

@@ -146,6 +146,26 @@ def test_bvh_width_invariance(device, root, name):
     np.testing.assert_array_equal(imgs[0], imgs[1])
 
 
+@pytest.mark.parametrize("name", ["diamond_scene.json", "s_deep.json"])
+def test_spatial_split_invariance(device, root, name):
+    """BLAS built with spatial splits (SBVH: triangles referenced from several
+    leaves) and without return the same closest hits and images bit for bit."""
+    sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", name))
+    rays = np.concatenate([camera_rays(sc, 200, 200, jitter=0.29), random_rays(sc, 50000, seed=11)])
+    res, imgs = [], []
+    try:
+        for split in (0, 1):
+            device.set_option("spatial_splits", split)
+            device.upload(sc)
+            res.append(device.trace_hits(rays, 0x1))
+            imgs.append(render_gpu(device, sc, 96, 96, 4))
+    finally:
+        device.set_option("spatial_splits", 0)
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    np.testing.assert_array_equal(res[0][1], res[1][1])
+    np.testing.assert_array_equal(imgs[0], imgs[1])
+
+
 @pytest.mark.parametrize("tile,capacity", [(None, 0), ((64, 1, 3), 0), (None, 20000)])
 def test_render_iterations_equals_single_calls(device, diamond_path, tile, capacity):
     """igx_render_iterations (iterations batched into one wavefront when they fit the
