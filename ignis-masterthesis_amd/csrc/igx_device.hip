@@ -690,13 +690,15 @@ __device__ __forceinline__ ShardSeq shard_seq(const WaveWork& w, int ns) {
     return ShardSeq{mine * 64, w.k, w.K};
 }
 
-template <int V, bool STATS>
-__global__ void __launch_bounds__(BLOCK, REFILL_WAVES) k_trace_refill(FrameArgs fa, SceneView sv, PathBuf in, HitBuf hits,
+template <int V, bool STATS, bool LDS>
+__global__ void __launch_bounds__(BLOCK, REFILL_WAVES) k_trace_refill(FrameArgs fa, SceneView gsv, PathBuf in, HitBuf hits,
                                                                      const int* cnt, int tail_threshold,
                                                                      unsigned long long* stats, int refill_min) {
     __shared__ int stack_mem[LDS_STACK * BLOCK];
-    const TStack ts = make_tstack(stack_mem, LDS_STACK, sv.spill);
+    extern __shared__ float4 lds_scene[];
+    const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
     if (row_total(cnt) <= tail_threshold) return; // k_finish takes the remaining paths
+    const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
     const WaveWork w = wave_work();
     const int ns = uniform_load(cnt + w.s * CSTRIDE);
@@ -730,12 +732,14 @@ __global__ void __launch_bounds__(BLOCK, REFILL_WAVES) k_trace_refill(FrameArgs 
     if (STATS) flush_stats<STATS>(st, stats, 0, true);
 }
 
-template <int V, bool STATS>
-__global__ void __launch_bounds__(BLOCK, REFILL_WAVES) k_shadow_refill(SceneView sv, ShadowBuf sh, float4* L, const int* cnt,
+template <int V, bool STATS, bool LDS>
+__global__ void __launch_bounds__(BLOCK, REFILL_WAVES) k_shadow_refill(SceneView gsv, ShadowBuf sh, float4* L, const int* cnt,
                                                                       unsigned long long* stats, int refill_min) {
     __shared__ int stack_mem[LDS_STACK * BLOCK];
-    const TStack ts = make_tstack(stack_mem, LDS_STACK, sv.spill);
+    extern __shared__ float4 lds_scene[];
+    const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
     if (row_total(cnt) == 0) return;
+    const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
     const WaveWork w = wave_work();
     const int ns = uniform_load(cnt + w.s * CSTRIDE);
@@ -1072,7 +1076,10 @@ int grid_for(igx_device* dev, long long items, int blocks_per_cu) {
 //    fused kernel is faster (no hit records, rays already coherent).
 constexpr size_t SPLIT_TABLE_BYTES = 4u << 20;
 inline int refill_min(const igx_device* dev) { return dev->refill_opt >= 0 ? dev->refill_opt : 16; }
-inline bool use_refill(const igx_device* dev) { return refill_min(dev) > 0 && dev->lds_scene_bytes == 0; }
+// auto: global-table scenes only; an explicit "refill" applies to LDS-staged scenes too
+inline bool use_refill(const igx_device* dev) {
+    return refill_min(dev) > 0 && (dev->lds_scene_bytes == 0 || dev->refill_opt > 0);
+}
 inline bool use_split(const igx_device* dev) {
     return dev->split_opt >= 0 ? dev->split_opt != 0 : (dev->lds_scene_bytes == 0 && dev->table_bytes > SPLIT_TABLE_BYTES);
 }
@@ -1127,7 +1134,13 @@ void launch_trace_w(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, con
 template <bool STATS>
 void launch_trace(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const PathBuf& in, const int* cnt, int tail) {
     if (use_refill(dev)) {
-#define L_TRR(S) hipLaunchKernelGGL((k_trace_refill<S, STATS>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, s.hb, cnt, tail, dev->dstats, refill_min(dev))
+#define L_TRR(S)                                                                                                        \
+    if (dev->lds_scene_bytes)                                                                                            \
+        hipLaunchKernelGGL((k_trace_refill<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->stream, fa, \
+                           dev->sv, in, s.hb, cnt, tail, dev->dstats, refill_min(dev));                                  \
+    else                                                                                                                 \
+        hipLaunchKernelGGL((k_trace_refill<S, STATS, false>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, s.hb, \
+                           cnt, tail, dev->dstats, refill_min(dev))
         IGX_DISPATCH_VARIANT(dev->variant, L_TRR);
 #undef L_TRR
         return;
@@ -1144,7 +1157,13 @@ void launch_trace(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const
 template <bool STATS>
 void launch_shadow(igx_device* dev, Slot& s, int grid, const int* cnt) {
     if (use_refill(dev)) {
-#define L_SHR(S) hipLaunchKernelGGL((k_shadow_refill<S, STATS>), dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, s.sh, s.L, cnt, dev->dstats, refill_min(dev))
+#define L_SHR(S)                                                                                                        \
+    if (dev->lds_scene_bytes)                                                                                            \
+        hipLaunchKernelGGL((k_shadow_refill<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->stream,   \
+                           dev->sv, s.sh, s.L, cnt, dev->dstats, refill_min(dev));                                       \
+    else                                                                                                                 \
+        hipLaunchKernelGGL((k_shadow_refill<S, STATS, false>), dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, s.sh, s.L, \
+                           cnt, dev->dstats, refill_min(dev))
         IGX_DISPATCH_VARIANT(dev->variant, L_SHR);
 #undef L_SHR
         return;
@@ -1204,15 +1223,7 @@ int resident_blocks(K kernel, size_t dyn_lds = 0) {
         default: IGX_RES1(K, 7, __VA_ARGS__);                        \
         }                                                            \
     } while (0)
-#define IGX_RESIDENT_G(K)                                            \
-    do {                                                             \
-        switch (v & 3) {                                             \
-        case 0: return resident_blocks(K<0, STATS>);                 \
-        case 1: return resident_blocks(K<1, STATS>);                 \
-        case 2: return resident_blocks(K<2, STATS>);                 \
-        default: return resident_blocks(K<3, STATS>);                \
-        }                                                            \
-    } while (0)
+#define IGX_RESIDENT_G(K) IGX_RESIDENT(K, STATS)
 template <bool STATS>
 int extend_blocks_per_cu(int v, size_t lds) { IGX_RESIDENT8(k_extend, STATS); }
 template <bool STATS>

@@ -220,13 +220,15 @@ def test_shading_variant_invariance(device, diamond_path):
 def test_split_and_refill_invariance(device, root, name):
     """Fused k_extend, split k_trace + k_shade, and the persistent-lane (refill)
     trace and shadow kernels render the same image bit for bit, with the same ray
-    counts (diamond forced onto global traversal tables, where refill applies)."""
+    counts, with global and (diamond) LDS-staged traversal tables."""
     sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", name))
     imgs, counts = [], []
     try:
         device.upload(sc)
-        device.set_option("lds_scene_max", 0)
-        for split, refill in ((0, 0), (1, 0), (1, 16), (0, 8), (-1, -1)):
+        # global tables, then (diamond) LDS-staged tables with explicit split / refill
+        runs = [(0, 0, 0), (0, 1, 0), (0, 1, 16), (0, 0, 8), (0, -1, -1), (48 * 1024, 1, 16), (48 * 1024, 0, 32)]
+        for lds, split, refill in runs:
+            device.set_option("lds_scene_max", lds)
             device.set_option("split", split)
             device.set_option("refill", refill)
             device.reset_stats()
