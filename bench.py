@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample length")
     ap.add_argument("--suite", type=int, default=1, help="also measure the other §8d scenes (N=1 only)")
+    ap.add_argument("--check-frame", action="store_true",
+                    help="N>1: rank 0 also renders the whole frame alone and checks the gathered frame equals it bit for bit")
     return ap.parse_args()
 
 
@@ -165,13 +167,17 @@ def main():
     n_gpus = max(world, 1)
 
     import torch
+    # IGX_BENCH_REHEARSAL=1: every rank on GPU 0, gloo with host staging -- a
+    # one-GPU dry run of the multi-GPU path (tile sharding, pack, gather,
+    # assembly, max-over-ranks timing); the real run uses RCCL, one GPU per rank
+    rehearsal = os.environ.get("IGX_BENCH_REHEARSAL") == "1"
+    gpu = 0 if (rehearsal or world == 1) else local_rank
+    comm = "cpu" if rehearsal else "cuda"
     dist = None
+    torch.cuda.set_device(gpu)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", init_method="env://")
-    else:
-        torch.cuda.set_device(0)
+        dist.init_process_group("gloo" if rehearsal else "nccl", init_method="env://")
 
     import ignis_amd
 
@@ -179,7 +185,7 @@ def main():
     W, H = scene.film_size
     spi = args.spi
     iters = max(1, math.ceil(args.spp / spi))
-    dev = ignis_amd.Device(local_rank if world > 1 else 0)
+    dev = ignis_amd.Device(gpu)
     dev.upload(scene)
 
     from ignis_amd import shard
@@ -195,7 +201,7 @@ def main():
     if n_gpus > 1:
         max_tiles = shard.max_tiles_per_rank(W, H, TILE, n_gpus)
         pack = torch.zeros(max_tiles * TILE * TILE * 3, dtype=torch.float32, device="cuda")
-        gather_bufs = [torch.zeros_like(pack) for _ in range(n_gpus)]
+        gather_bufs = [torch.zeros(pack.numel(), dtype=torch.float32, device=comm) for _ in range(n_gpus)]
         frame = torch.zeros((W * H, 3), dtype=torch.float32, device="cuda")
         dst = torch.from_numpy(shard.packed_destinations(W, H, TILE, n_gpus)).cuda()
         valid = dst >= 0
@@ -210,8 +216,8 @@ def main():
             # pack owned tiles, RCCL all_gather over xGMI, assemble on every rank
             torch.cuda.synchronize()
             dev.pack_tiles(params(0), pack.data_ptr(), pack.numel())
-            dist.all_gather(gather_bufs, pack)
-            allpix = torch.cat(gather_bufs).view(-1, 3)
+            dist.all_gather(gather_bufs, pack if comm == "cuda" else pack.cpu())
+            allpix = torch.cat(gather_bufs).to("cuda").view(-1, 3)
             frame[dst_valid] = allpix[valid]
 
     for _ in range(args.warmup):
@@ -236,12 +242,30 @@ def main():
     rays_local = rays_ext + st["shadow_rays"]
     totals = np.array([rays_local, st["camera_rays"], st["bounce_rays"], st["shadow_rays"]], dtype=np.float64)
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=comm)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        tt = torch.tensor(totals, dtype=torch.float64, device="cuda")
+        tt = torch.tensor(totals, dtype=torch.float64, device=comm)
         dist.all_reduce(tt, op=dist.ReduceOp.SUM)
         totals = tt.cpu().numpy()
+
+    frame_check = None
+    if n_gpus > 1 and args.check_frame:
+        # the gathered frame of the last timed step against the whole frame
+        # rendered by one device (tile sharding is exact: DESIGN.md §6)
+        gathered = frame.cpu().numpy()
+        ok = torch.tensor([0.0], dtype=torch.float64, device=comm)
+        if rank == 0:
+            ref = ignis_amd.Device(gpu)
+            ref.upload(scene)
+            p = ignis_amd.RenderParams()
+            p.width, p.height, p.spi = W, H, spi
+            ref.render_iterations(p, iters)
+            full, _ = ref.framebuffer(W * H * 3)
+            ref.close()
+            ok[0] = float(np.array_equal(full.reshape(-1, 3), gathered))
+        dist.broadcast(ok, 0)
+        frame_check = bool(ok.item())
 
     # ---- roofline of the dominant kernel, live HIP-event timing ----
     roof = roofline(dev, st, lambda: dev.render(params(0)), n_gpus, os.path.splitext(os.path.basename(args.scene))[0])
@@ -295,6 +319,8 @@ def main():
             "parity": parity,
             "suite": suite,
         }
+        if frame_check is not None:
+            result["frame_equals_single_gpu"] = frame_check
         print(json.dumps(result), flush=True)
     if dist:
         dist.barrier()

@@ -143,6 +143,7 @@ __device__ __forceinline__ T uniform_load(const T* p) {
 // Sharded streams (see PathBuf)
 // ---------------------------------------------------------------------------
 static_assert(NSH == 64 && BLOCK % 64 == 0 && NSH % WAVES_PER_BLOCK == 0, "one shard counter per lane of a wave");
+static_assert(BLOCK == TSTACK_STRIDE, "traversal stacks are laid out for BLOCK threads");
 
 // Records of all shards of a counter row: lane l reads shard l; wave-uniform.
 __device__ __forceinline__ int row_total(const int* row) {

@@ -101,27 +101,29 @@ __device__ __forceinline__ bool is_leaf_ref(int r) { return r < 0 && r > REF_EXI
 // (entry e at spill[(e - cap) * sstride], one column per grid thread).  A
 // small LDS stack thus serves every scene: LDS per block, and so occupancy,
 // no longer scales with the worst-case stack depth.
+// The LDS column stride is the block size, a compile-time constant: a push or
+// pop is then one shift-add, not a quarter-rate v_mul_lo_u32.
+constexpr int TSTACK_STRIDE = 256; // threads per block of every traversal kernel
 struct TStack {
     int* lds;
     int* spill;
     int cap;
-    int stride;
     int sstride;
 };
 template <bool SPILL>
 __device__ __forceinline__ void tpush(const TStack& s, int& sp, int v) {
-    if (!SPILL || sp < s.cap) s.lds[sp * s.stride] = v;
+    if (!SPILL || sp < s.cap) s.lds[sp * TSTACK_STRIDE] = v;
     else s.spill[(sp - s.cap) * s.sstride] = v;
     ++sp;
 }
 template <bool SPILL>
 __device__ __forceinline__ int tpop(const TStack& s, int& sp) {
     --sp;
-    return (!SPILL || sp < s.cap) ? s.lds[sp * s.stride] : s.spill[(sp - s.cap) * s.sstride];
+    return (!SPILL || sp < s.cap) ? s.lds[sp * TSTACK_STRIDE] : s.spill[(sp - s.cap) * s.sstride];
 }
 __device__ __forceinline__ TStack make_tstack(int* lds_base, int cap, int* spill) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    return TStack{lds_base + threadIdx.x, spill + g, cap, (int)blockDim.x, (int)(gridDim.x * blockDim.x)};
+    const int g = blockIdx.x * TSTACK_STRIDE + threadIdx.x;
+    return TStack{lds_base + threadIdx.x, spill + g, cap, (int)(gridDim.x * TSTACK_STRIDE)};
 }
 
 // Closest-hit acceptance with an order-independent tie rule: among hits at the
