@@ -8,8 +8,9 @@ seed 0.  One "step" = one full 256-spp frame.  Rays = camera rays + bounce rays
 (closest-hit traversals) + valid shadow rays (any-hit traversals), counted on
 the device.
 
-Multi-GPU (torchrun, one rank per GPU): the film is cut into 64x64 tiles dealt
-round-robin to the ranks (tile t -> rank t % N); every rank renders all 32
+Multi-GPU (torchrun, one rank per GPU): the film is cut into square tiles
+(40 px for 1000-px films: a tile column count coprime with N, shard.balanced_tile)
+dealt round-robin to the ranks (tile t -> rank t % N); every rank renders all 32
 iterations of its tiles, packs them, and an RCCL all_gather over xGMI assembles
 the frame.  Total work is fixed, so scaling is "strong".
 
@@ -30,7 +31,6 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
-TILE = 64
 
 
 def parse():
@@ -189,21 +189,22 @@ def main():
     dev.upload(scene)
 
     from ignis_amd import shard
+    tile = shard.balanced_tile(W, n_gpus)
 
     def params(it):
         p = ignis_amd.RenderParams()
         p.width, p.height, p.spi, p.iteration, p.frame, p.seed = W, H, spi, it, 0, 0
         if n_gpus > 1:
-            p.tile_size, p.tile_offset, p.tile_stride = TILE, rank, n_gpus
+            p.tile_size, p.tile_offset, p.tile_stride = tile, rank, n_gpus
         return p
 
     gather_bufs = None
     if n_gpus > 1:
-        max_tiles = shard.max_tiles_per_rank(W, H, TILE, n_gpus)
-        pack = torch.zeros(max_tiles * TILE * TILE * 3, dtype=torch.float32, device="cuda")
+        max_tiles = shard.max_tiles_per_rank(W, H, tile, n_gpus)
+        pack = torch.zeros(max_tiles * tile * tile * 3, dtype=torch.float32, device="cuda")
         gather_bufs = [torch.zeros(pack.numel(), dtype=torch.float32, device=comm) for _ in range(n_gpus)]
         frame = torch.zeros((W * H, 3), dtype=torch.float32, device="cuda")
-        dst = torch.from_numpy(shard.packed_destinations(W, H, TILE, n_gpus)).cuda()
+        dst = torch.from_numpy(shard.packed_destinations(W, H, tile, n_gpus)).cuda()
         valid = dst >= 0
         dst_valid = dst[valid]
 
@@ -307,7 +308,7 @@ def main():
                 "workload": f"diamond_scene.json {W}x{H}, {iters * spi} spp = {iters} iterations x spi {spi}, path tracer max_depth 64, seed 0",
                 "scene": os.path.basename(args.scene),
                 "width": W, "height": H, "spp": iters * spi, "spi": spi,
-                "parallelism": f"tile-shard x{n_gpus} (64x64 tiles round-robin) + RCCL all_gather" if n_gpus > 1 else "single GPU",
+                "parallelism": f"tile-shard x{n_gpus} ({tile}x{tile} tiles round-robin) + RCCL all_gather" if n_gpus > 1 else "single GPU",
             },
             "msamples_per_s": round(samples / elapsed / 1e6, 2),
             "rays": {"camera": int(totals[1]), "bounce": int(totals[2]), "shadow": int(totals[3])},

@@ -7,7 +7,22 @@ packs them as [tile k of this rank][row][col][rgb], padded to T×T.  After an
 all_gather of equal-size packed buffers every rank assembles the frame with
 one scatter through the destination table built here.
 """
+import math
+
 import numpy as np
+
+
+def balanced_tile(width, n_ranks, lo=32, hi=64, prefer=40):
+    """Tile size for n_ranks: the one nearest `prefer` in [lo, hi] whose tile
+    column count is coprime with n_ranks, so round-robin ownership (t % N)
+    staggers from row to row instead of giving each rank whole tile columns.
+    Whole columns load ranks unevenly when the image content is uneven
+    (diamond, 8 ranks, 64-px tiles: slowest rank 28.3 ms, fastest 22.6 ms;
+    40-px tiles, 25 columns: 25.0 / 24.5 ms; tools/shard_sim.py)."""
+    for t in sorted(range(lo, hi + 1), key=lambda t: (abs(t - prefer), t)):
+        if math.gcd((width + t - 1) // t, max(1, n_ranks)) == 1:
+            return t
+    return prefer
 
 
 def tile_grid(width, height, tile):

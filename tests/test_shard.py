@@ -43,6 +43,18 @@ def test_pack_assemble_roundtrip(w, h, T, N):
     np.testing.assert_array_equal(out, frame)
 
 
+@pytest.mark.parametrize("w,N", [(1000, 2), (1000, 4), (1000, 8), (4096, 8), (1000, 5), (1000, 3)])
+def test_balanced_tile_staggers_ownership(w, N):
+    """Tile column count coprime with N: along a tile row, consecutive rows start
+    the round-robin at different ranks, so no rank owns whole tile columns."""
+    import math
+    T = shard.balanced_tile(w, N)
+    tx, _ = shard.tile_grid(w, w, T)
+    assert 32 <= T <= 64 and math.gcd(tx, N) == 1
+    owners_col0 = {(r * tx) % N for r in range(N)}
+    assert owners_col0 == set(range(N))
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

@@ -1,37 +1,42 @@
-"""Dev tool: per-rank frame time of the N-GPU tile-sharded bench, simulated on
-one GPU by rendering only rank 0's tiles (tile_offset 0, tile_stride N) --
-the strong-scaling efficiency the driver's multi-GPU runs can reach."""
+"""Dev tool: strong-scaling efficiency of the N-GPU tile-sharded bench,
+simulated on one GPU: every rank's tile set (tile_offset = rank, tile_stride
+= N) is rendered in turn as a full 256-spp frame; the job time at N is the
+slowest rank's.  usage: shard_sim.py [scene] [tile sizes, comma-separated]"""
 import json, os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "ignis-masterthesis_amd"))
 import ignis_amd
 
 scene = ignis_amd.Scene.from_file(os.path.join(ROOT, sys.argv[1] if len(sys.argv) > 1 else "scenes/diamond_scene.json"))
+tiles = [int(t) for t in (sys.argv[2] if len(sys.argv) > 2 else "64").split(",")]
 W, H = scene.film_size
 dev = ignis_amd.Device(0)
 dev.upload(scene)
-opts = json.loads(sys.argv[2]) if len(sys.argv) > 2 else {}
-batched = opts.pop("batched", 1)
-for k, v in opts.items():
-    dev.set_option(k, v)
-base = None
-for n in (1, 2, 4, 8):
-    def frame():
+
+
+def frame(n, rank, tile):
+    dev.clear()
+    p = ignis_amd.RenderParams()
+    p.width, p.height, p.spi, p.iteration = W, H, 8, 0
+    if n > 1:
+        p.tile_size, p.tile_offset, p.tile_stride = tile, rank, n
+    dev.render_iterations(p, 32)
+    dev.synchronize()
+    best = None
+    for _ in range(2):
         dev.clear()
-        p = ignis_amd.RenderParams()
-        p.width, p.height, p.spi, p.iteration = W, H, 8, 0
-        if n > 1:
-            p.tile_size, p.tile_offset, p.tile_stride = 64, 0, n
-        if batched:
-            dev.render_iterations(p, 32)
-        else:
-            for it in range(32):
-                p.iteration = it
-                dev.render(p)
+        t = time.perf_counter()
+        dev.render_iterations(p, 32)
         dev.synchronize()
-    frame()
-    t = time.perf_counter()
-    frame()
-    dt = time.perf_counter() - t
-    base = base or dt
-    print(json.dumps({"batched": batched, "n": n, "ms_frame_rank0": round(dt * 1e3, 2), "efficiency": round(base / (n * dt), 3)}), flush=True)
+        dt = time.perf_counter() - t
+        best = dt if best is None else min(best, dt)
+    return best
+
+
+t1 = frame(1, 0, 0)
+print(json.dumps({"n": 1, "ms_frame": round(t1 * 1e3, 2)}), flush=True)
+for tile in tiles:
+    for n in (2, 4, 8):
+        ts = [frame(n, r, tile) for r in range(n)]
+        print(json.dumps({"tile": tile, "n": n, "ms_max_rank": round(max(ts) * 1e3, 2), "ms_min_rank": round(min(ts) * 1e3, 2),
+                          "efficiency": round(t1 / (n * max(ts)), 3)}), flush=True)
