@@ -899,6 +899,7 @@ struct igx_device {
     bool instrument = false;
     int64_t capacity_opt = 0;
     int64_t tail_opt = -1;   // paths at or below which k_finish takes over (-1 = auto)
+    int64_t tail_last_opt = -1; // the same for the last chunk of a render call, whose tail overlaps nothing (-1 = tail_opt)
     int split_opt = -1;      // k_trace + k_shade per bounce instead of the fused k_extend (-1: auto = global-table scenes)
     int trace_waves = 5;     // occupancy target of k_trace (5 waves per SIMD, anything else = compiler's choice)
     int refill_opt = -1;     // persistent-lane trace / shadow, refilled once this many lanes idle (0: off, -1: auto = 16)
@@ -1459,6 +1460,7 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     else if (k == "instrument") dev->instrument = value != 0;
     else if (k == "capacity") dev->capacity_opt = value;
     else if (k == "tail_threshold") dev->tail_opt = value;
+    else if (k == "tail_threshold_last") dev->tail_last_opt = value;
     else if (k == "split") {
         if (value < -1 || value > 1) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "split must be -1 (auto), 0 or 1");
         dev->split_opt = (int)value;
@@ -2013,7 +2015,9 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
         // overlapping chunk (diamond 32M-path chunks: 500K -> 196K tail paths,
         // 204.6 -> 195.0 ms per frame, tools/sweep_frame.py)
         const long long fin_lanes = (long long)fin_bpc * dev->num_cus * BLOCK;
-        int tail = dev->tail_opt >= 0 ? (int)std::min<int64_t>(dev->tail_opt, 1 << 30)
+        const bool last_chunk = it0 + iters_per_chunk >= count && px0 + chunk_pixels_max >= local_pixels;
+        const int64_t topt = last_chunk && dev->tail_last_opt >= 0 ? dev->tail_last_opt : dev->tail_opt;
+        int tail = topt >= 0 ? (int)std::min<int64_t>(topt, 1 << 30)
                                       : (int)std::max<long long>(32768, std::min(n / 64, fin_lanes));
         S.tail = tail;
         S.camera = valid_pixels_in_chunk(fa) * p->spi * fa.chunk_iters;
