@@ -677,8 +677,11 @@ __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, f
 // of wave-level steps.  Each wave walks the positions k, k + K, ... (in
 // groups of 64) of its shard, like the grid-stride kernels.
 // ---------------------------------------------------------------------------
+// occupancy target of the persistent-lane kernels (waves per SIMD): 6 caps
+// them at 80 VGPRs (trace 4.8 -> 4.5 ms per S-deep iteration, soup-16M
+// 45.6 -> 43.3); 7 and 8 spill and run slower
 #ifndef REFILL_WAVES
-#define REFILL_WAVES 5
+#define REFILL_WAVES 6
 #endif
 struct ShardSeq {
     int C; // positions in this wave's sequence (a multiple of 64)
