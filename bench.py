@@ -124,13 +124,14 @@ def roofline(dev, st, render_one, n_gpus, scene_key):
     }
 
 
-def suite_line(ignis_amd, dev_index, path, spi, iters):
+def suite_line(ignis_amd, dev_index, path, spi, iters, size=None):
     """Short single-GPU measurement of another scene of SURVEY.md §8d (load and
     BVH build excluded): Mrays/s over `iters` iterations after one warm-up,
-    plus the dominant kernel's roofline on that scene."""
+    plus the dominant kernel's roofline on that scene.  `size` overrides the
+    scene's film (the camera keeps its horizontal field of view)."""
     t_load = time.perf_counter()
     scene = ignis_amd.Scene.from_file(path)
-    W, H = scene.film_size
+    W, H = size or scene.film_size
     dev = ignis_amd.Device(dev_index)
     dev.upload(scene)
     t_load = time.perf_counter() - t_load
@@ -283,8 +284,11 @@ def main():
         suite = None
         if n_gpus == 1 and args.suite:
             # other scenes of SURVEY.md §8d, incl. the HBM roofline scene of record (S-soup-16M)
-            suite = [suite_line(ignis_amd, 0, os.path.join(ROOT, "scenes", f), spi, n)
-                     for f, n in (("primitives.json", 8), ("s_deep.json", 4), ("s_soup_1m.json", 2), ("s_soup_16m.json", 1))]
+            suite = [suite_line(ignis_amd, 0, os.path.join(ROOT, "scenes", f), spi, n, size)
+                     for f, n, size in (("primitives.json", 8, None), ("s_deep.json", 4, None), ("s_soup_1m.json", 2, None),
+                                        ("s_soup_16m.json", 1, None),
+                                        # config 5 stand-in: S-deep at 4096x4096, 64 spp
+                                        ("s_deep.json", 8, (4096, 4096)))]
             for line in suite:
                 line["roofline"]["note"] = (
                     "HBM roofline scene of record: 1.8 GB of BVH + triangles, far above the on-chip caches"

@@ -51,7 +51,8 @@ constexpr int BLOCK = 256;
 constexpr int MAX_BLOCKS_PER_CU = 8;  // 2048 threads per CU; grids never exceed num_cus * this
 constexpr int MAX_STACK = 128;        // traversal stack entries (LDS + spill) per ray
 constexpr int MAX_BOUNCES = 256;          // path depth is stored in 8 bits (p1.w, above the 24-bit RNG counter)
-constexpr long long MAX_CHUNK_PATHS = 1ll << 25; // paths per chunk (one wavefront), ~6 GB of stream buffers per slot
+constexpr long long MAX_CHUNK_PATHS = 1ll << 27; // paths per chunk (one wavefront), ~25 GB of stream buffers per slot
+constexpr long long PATH_SLOT_BYTES = 2 * 52 + 48 + 20 + 16; // two path buffers, shadow ray, hit record, radiance
 // Occupancy target (waves per SIMD) of k_extend, with global and with
 // LDS-staged traversal tables: 4 caps it at 128 VGPRs.  k_finish keeps the
 // compiler's choice (it would spill).
@@ -897,6 +898,7 @@ struct igx_device {
     hipStream_t tail_stream = nullptr;
     std::string last_error;
     int num_cus = 256;
+    size_t mem_total = 0;     // device memory (bytes)
     // options
     bool timing = false;
     bool instrument = false;
@@ -1414,7 +1416,10 @@ extern "C" igx_status igx_create(int hip_device, igx_device** out) {
         return IGX_ERR_HIP;
     }
     hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, hip_device) == hipSuccess) dev->num_cus = prop.multiProcessorCount;
+    if (hipGetDeviceProperties(&prop, hip_device) == hipSuccess) {
+        dev->num_cus = prop.multiProcessorCount;
+        dev->mem_total = prop.totalGlobalMem;
+    }
     if (hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&dev->tail_stream, hipStreamNonBlocking) != hipSuccess) {
         delete dev;
@@ -1964,8 +1969,16 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
         dev->iteration_count += count;
         return IGX_OK;
     }
+    // default chunk of a multi-iteration render: the largest power of two
+    // whose two stream slots take at most a quarter of the device memory
+    // (MI355X: 128 M paths, 2 x 25 GB).  Fewer, larger chunks leave fewer
+    // tails that overlap nothing: diamond frame 193 -> 179 ms, S-deep 4096^2
+    // 865 -> 823 ms from 32 M to 128 M paths (tools/sweep_frame.py)
+    long long auto_chunk_paths = 1ll << 24;
+    while (auto_chunk_paths < MAX_CHUNK_PATHS && 2 * (2 * auto_chunk_paths) * PATH_SLOT_BYTES <= (long long)(dev->mem_total / 4))
+        auto_chunk_paths *= 2;
     long long cap = dev->capacity_opt > 0 ? dev->capacity_opt
-                                          : (count > 1 ? MAX_CHUNK_PATHS : std::min<long long>(total_paths, 1ll << 24));
+                                          : (count > 1 ? auto_chunk_paths : std::min<long long>(total_paths, 1ll << 24));
     cap = std::min<long long>(cap, MAX_CHUNK_PATHS);
     cap = std::max<long long>(p->spi, (cap / p->spi) * p->spi);
     const long long chunk_pixels_max = std::min<long long>(cap, total_paths) / p->spi;

@@ -1,13 +1,13 @@
 """Dev tool: one bench frame (all iterations in one igx_render_iterations call,
 as bench.py renders them) of a scene under several device-option sets.
-usage: sweep_frame.py scene.json '<json list of option dicts>' [iterations]"""
+usage: sweep_frame.py scene.json '<json list of option dicts>' [iterations] [film WxH]"""
 import json, os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "ignis-masterthesis_amd"))
 import ignis_amd
 
 scene = ignis_amd.Scene.from_file(os.path.join(ROOT, sys.argv[1]))
-W, H = scene.film_size
+W, H = (int(v) for v in sys.argv[4].split("x")) if len(sys.argv) > 4 else scene.film_size
 opts = json.loads(sys.argv[2]) if len(sys.argv) > 2 else [{}]
 iters = int(sys.argv[3]) if len(sys.argv) > 3 else 32
 dev = ignis_amd.Device(0)
