@@ -9,8 +9,8 @@ timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_o
 timeout -k 10 600 python3 bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err && cat gpurun_out/bench.json && \
 rm -rf gpurun_out/prof gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_fetch_soup gpurun_out/pmc_write_soup && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --suite 0 > gpurun_out/prof_bench.json 2> gpurun_out/prof.err && \
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 tools/pmc_run.py 2 > gpurun_out/pmc_fetch.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 tools/pmc_run.py 2 > gpurun_out/pmc_write.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 tools/pmc_run.py 32 > gpurun_out/pmc_fetch.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 tools/pmc_run.py 32 > gpurun_out/pmc_write.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_soup -o run --output-format csv -- python3 tools/pmc_run.py 1 s_soup_16m.json > gpurun_out/pmc_fetch_soup.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_soup -o run --output-format csv -- python3 tools/pmc_run.py 1 s_soup_16m.json > gpurun_out/pmc_write_soup.log 2>&1
 rc=$?
