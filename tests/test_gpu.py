@@ -166,6 +166,28 @@ def test_spatial_split_invariance(device, root, name):
     np.testing.assert_array_equal(imgs[0], imgs[1])
 
 
+@pytest.mark.parametrize("name", ["diamond_scene.json", "s_deep.json"])
+def test_tail_threshold_invariance(device, root, name):
+    """Paths finished by the tail kernel and by the wavefront kernels are
+    bit-identical: no tail, the whole chunk in the tail from the first bounce,
+    and the automatic threshold render the same image with the same ray counts."""
+    sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", name))
+    imgs, counts = [], []
+    try:
+        for tail in (0, 1 << 30, 3000, -1):
+            device.set_option("tail_threshold", tail)
+            device.reset_stats()
+            imgs.append(render_gpu(device, sc, 120, 90, 4))
+            st = device.stats()
+            counts.append((st["camera_rays"], st["bounce_rays"], st["shadow_rays"]))
+    finally:
+        device.set_option("tail_threshold", -1)
+    for im, c in zip(imgs[1:], counts[1:]):
+        np.testing.assert_array_equal(imgs[0], im)
+        assert c == counts[0]
+    assert imgs[0].sum() > 0
+
+
 @pytest.mark.parametrize("tile,capacity", [(None, 0), ((64, 1, 3), 0), (None, 20000)])
 def test_render_iterations_equals_single_calls(device, diamond_path, tile, capacity):
     """igx_render_iterations (iterations batched into one wavefront when they fit the

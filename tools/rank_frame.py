@@ -23,8 +23,15 @@ for o in opts:
     ts = []
     for rep in range(4):
         dev.clear()
+        dev.reset_stats()
+        dev.set_option("timing", 1 if rep == 3 else 0)
         t = time.perf_counter()
         dev.render_iterations(p, 32)
         dev.synchronize()
         ts.append(time.perf_counter() - t)
-    print(json.dumps({"opt": o, "n": n, "ms_frame": round(min(ts[1:]) * 1e3, 2)}), flush=True)
+    st = dev.stats()
+    dev.set_option("timing", 0)
+    print(json.dumps({"opt": o, "n": n, "ms_frame": round(min(ts[1:3]) * 1e3, 2), "ms_timed": round(ts[3] * 1e3, 2),
+                      "ext": round(st["ms_extend"], 2), "tr": round(st["ms_trace"], 2), "sh": round(st["ms_shadow"], 2),
+                      "fin": round(st["ms_finish"], 2), "gen": round(st["ms_generate"], 2), "res": round(st["ms_resolve"], 2),
+                      "wf_bounces": st["launches_extend"], "tail_rays": st["tail_bounce_rays"] + st["tail_shadow_rays"]}), flush=True)
