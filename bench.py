@@ -209,36 +209,71 @@ def main():
         valid = dst >= 0
         dst_valid = dst[valid]
 
+    # N > 1: frames alternate between two device handles on the rank's GPU (own
+    # streams, framebuffer and path slots), so frame k+1's wavefront is queued
+    # before frame k is packed and gathered: the gather and frame k's tail
+    # kernel (its longest paths) overlap the next frame's
+    # bounces, as consecutive frames already overlap on one GPU (N = 1 has no
+    # per-frame synchronisation).  Every frame is fully rendered and gathered
+    # inside the timed region.
+    devs = [dev]
+    if n_gpus > 1:
+        devs.append(ignis_amd.Device(gpu))
+        devs[1].upload(scene)
+    pending = []
+    count = [0]
+
+    def gather(d):
+        # pack owned tiles, RCCL all_gather over xGMI, assemble on every rank
+        torch.cuda.current_stream().synchronize()  # the previous gather has read `pack`
+        d.pack_tiles(params(0), pack.data_ptr(), pack.numel())  # waits for d's frame
+        dist.all_gather(gather_bufs, pack if comm == "cuda" else pack.cpu())
+        allpix = torch.cat(gather_bufs).to("cuda").view(-1, 3)
+        frame[dst_valid] = allpix[valid]
+
     def render_frame():
-        dev.clear()
+        d = devs[count[0] % len(devs)]
+        count[0] += 1
+        d.clear()
         # all iterations of the frame in one call: iterations whose paths fit the
-        # capacity are traced as one wavefront (a tile shard is small at N > 1)
-        dev.render_iterations(params(0), iters)
+        # capacity are traced as one wavefront
+        d.render_iterations(params(0), iters)
         if n_gpus > 1:
-            # pack owned tiles, RCCL all_gather over xGMI, assemble on every rank
-            torch.cuda.synchronize()
-            dev.pack_tiles(params(0), pack.data_ptr(), pack.numel())
-            dist.all_gather(gather_bufs, pack if comm == "cuda" else pack.cpu())
-            allpix = torch.cat(gather_bufs).to("cuda").view(-1, 3)
-            frame[dst_valid] = allpix[valid]
+            if pending:
+                gather(pending.pop())
+            pending.append(d)
+
+    def drain_frames():
+        if pending:
+            gather(pending.pop())
+        torch.cuda.synchronize()
 
     for _ in range(args.warmup):
         render_frame()
+    drain_frames()
 
-    dev.reset_stats()
-    dev.set_option("timing", 1)
+    for d in devs:
+        d.reset_stats()
+        d.set_option("timing", 1)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         render_frame()
-    torch.cuda.synchronize()
+    drain_frames()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     st = dev.stats()
-    dev.set_option("timing", 0)
+    for d in devs[1:]:
+        s2 = d.stats()
+        for key in ("camera_rays", "bounce_rays", "shadow_rays", "ms_trace", "ms_extend", "ms_shadow", "ms_finish",
+                    "ms_generate", "ms_resolve", "launches_extend", "launches_trace", "extend_rays", "extend_paths_out",
+                    "tail_shadow_rays", "tail_bounce_rays"):
+            st[key] += s2[key]
+    for d in devs:
+        d.set_option("timing", 0)
 
     rays_ext = st["camera_rays"] + st["bounce_rays"]
     rays_local = rays_ext + st["shadow_rays"]
@@ -330,7 +365,8 @@ def main():
     if dist:
         dist.barrier()
         dist.destroy_process_group()
-    dev.close()
+    for d in devs:
+        d.close()
     return result
 
 

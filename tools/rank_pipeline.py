@@ -1,0 +1,45 @@
+"""Dev tool: average frame time of one rank's tile set (N-GPU bench shard,
+simulated on one GPU) over K back-to-back frames, with one device handle
+(each frame drained before the next, as the gather requires) and with two
+handles alternating (bench.py's N > 1 pipelining: frame k+1 queued before
+frame k is drained).  usage: rank_pipeline.py scene N [K]"""
+import json, os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ignis-masterthesis_amd"))
+import ignis_amd
+from ignis_amd import shard
+
+scene = ignis_amd.Scene.from_file(os.path.join(ROOT, sys.argv[1]))
+n = int(sys.argv[2])
+K = int(sys.argv[3]) if len(sys.argv) > 3 else 6
+W, H = scene.film_size
+devs = [ignis_amd.Device(0), ignis_amd.Device(0)]
+for d in devs:
+    d.upload(scene)
+p = ignis_amd.RenderParams()
+p.width, p.height, p.spi = W, H, 8
+if n > 1:
+    p.tile_size, p.tile_offset, p.tile_stride = shard.balanced_tile(W, n), 0, n
+
+
+def run(handles):
+    pending = None
+    t = time.perf_counter()
+    for k in range(K):
+        d = handles[k % len(handles)]
+        d.clear()
+        d.render_iterations(p, 32)
+        if pending is not None:
+            pending.synchronize()
+        pending = d
+        if len(handles) == 1:
+            d.synchronize()
+            pending = None
+    if pending is not None:
+        pending.synchronize()
+    return (time.perf_counter() - t) / K
+
+
+for handles in (devs[:1], devs, devs[:1], devs):
+    run(handles)
+    print(json.dumps({"n": n, "handles": len(handles), "ms_per_frame": round(run(handles) * 1e3, 2)}), flush=True)
