@@ -224,6 +224,36 @@ def test_render_iterations_equals_single_calls(device, diamond_path, tile, capac
         assert sa[k] == sb[k], (k, sa[k], sb[k])
 
 
+def test_bench_frame_equals_single_iterations(device, diamond_path):
+    """At the bench's full size (diamond 1000x1000, 32 iterations of spi 8 =
+    256 spp) the batched frame -- 128 M-path chunks, 16 iterations each -- is
+    bit for bit the frame of 32 single-iteration renders, with the same ray
+    counts: chunking, sharded streams and the tail are exact at scale."""
+    sc = ignis_amd.Scene.from_file(diamond_path)
+    w, h = sc.film_size
+    p = ignis_amd.RenderParams()
+    p.width, p.height, p.spi = w, h, 8
+    device.upload(sc)
+    device.clear()
+    device.reset_stats()
+    p.iteration = 0
+    device.render_iterations(p, 32)
+    a, ia = device.framebuffer(w * h * 3)
+    sa = device.stats()
+    device.clear()
+    device.reset_stats()
+    for it in range(32):
+        p.iteration = it
+        device.render(p)
+    b, ib = device.framebuffer(w * h * 3)
+    sb = device.stats()
+    assert ia == ib == 32
+    np.testing.assert_array_equal(a, b)
+    for k in ("camera_rays", "bounce_rays", "shadow_rays"):
+        assert sa[k] == sb[k], (k, sa[k], sb[k])
+    assert sa["camera_rays"] == w * h * 8 * 32
+
+
 def test_shading_variant_invariance(device, diamond_path):
     """The basic-shading kernel variant (Lambert + dielectric only, chosen for the
     diamond) and the full one render the diamond bit for bit alike."""
