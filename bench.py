@@ -385,17 +385,21 @@ def cpu_baseline(scene, dev, W, H, spi, target_s):
     fb, st = orc.render(W, H, spi, iteration=0, threads=threads, window=(0, y0, W, y0 + rows))
     fb0 = fb.copy()  # iteration 0 alone, for the parity check below
     seconds, rays = st["seconds"], st["camera_rays"] + st["bounce_rays"] + st["shadow_rays"]
+    per_iter = [rays / st["seconds"] / 1e6]  # Mrays/s of every timed iteration (min/med/max, scripts/benchmark.sh)
     iters = 1
     while seconds < 0.8 * target_s and iters < 256:
         fb, st = orc.render(W, H, spi, iteration=iters, threads=threads, window=(0, y0, W, y0 + rows), fb=fb)
+        r = st["camera_rays"] + st["bounce_rays"] + st["shadow_rays"]
+        per_iter.append(r / st["seconds"] / 1e6)
         seconds += st["seconds"]
-        rays += st["camera_rays"] + st["bounce_rays"] + st["shadow_rays"]
+        rays += r
         iters += 1
     cpu = {
         "value": round(rays / seconds / 1e6, 3),
         "unit": "Mrays/s",
         "cores": threads,
         "kind": "port",
+        "min_med_max": [round(min(per_iter), 3), round(float(np.median(per_iter)), 3), round(max(per_iter), 3)],
         "sample": f"oracle/oracle.c (restated reference CPU device), {threads} threads, rows {y0}-{y0 + rows} of the {W}x{H} diamond frame, {iters} iteration(s) x spi {spi} = {iters * spi} spp, {rays / 1e6:.0f} Mrays in {seconds:.1f} s",
     }
     # parity: GPU iteration 0 of the same frame vs the oracle band
