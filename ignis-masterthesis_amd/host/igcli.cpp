@@ -53,6 +53,7 @@ int main(int argc, char** argv) {
         sc.Database = desc;
         dev.assignScene(sc);
         std::vector<double> rates;
+        double total_s = 0; // wall time of the render loop (cli/main.cpp:127-135)
         for (int it = 0; it < iters; ++it) {
             IG::RenderSettings rs;
             rs.spi = spi;
@@ -65,13 +66,15 @@ int main(int argc, char** argv) {
             dev.synchronize(); // render() only queues the iteration
             double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
             rates.push_back((double)spi * desc->film_width * desc->film_height / s / 1e6);
+            total_s += s;
         }
         igx_stats st = dev.getStatistics();
         std::sort(rates.begin(), rates.end());
         double rays = (double)(st.camera_rays + st.bounce_rays + st.shadow_rays);
         std::printf("# %f %f %f Msamples/s\n", rates.front(), rates[rates.size() / 2], rates.back());
-        std::printf("# %.3f Mrays/s (camera %llu, bounce %llu, shadow %llu) over %.3f ms\n", rays / (st.ms_render * 1e3), (unsigned long long)st.camera_rays,
-                    (unsigned long long)st.bounce_rays, (unsigned long long)st.shadow_rays, st.ms_render);
+        std::printf("# %.3f Mrays/s (camera %llu, bounce %llu, shadow %llu) over %.3f ms\n", rays / total_s / 1e6,
+                    (unsigned long long)st.camera_rays, (unsigned long long)st.bounce_rays, (unsigned long long)st.shadow_rays,
+                    total_s * 1e3);
         if (!out_path.empty()) {
             IG::AOVAccessor acc = dev.getFramebufferForHost();
             float inv = acc.IterationCount ? 1.0f / acc.IterationCount : 0.0f;
