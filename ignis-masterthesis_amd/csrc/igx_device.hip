@@ -52,7 +52,7 @@ constexpr int MAX_BLOCKS_PER_CU = 8;  // 2048 threads per CU; grids never exceed
 constexpr int MAX_STACK = 128;        // traversal stack entries (LDS + spill) per ray
 constexpr int MAX_BOUNCES = 256;          // path depth is stored in 8 bits (p1.w, above the 24-bit RNG counter)
 constexpr long long MAX_CHUNK_PATHS = 1ll << 27; // paths per chunk (one wavefront), ~25 GB of stream buffers per slot
-constexpr long long PATH_SLOT_BYTES = 2 * 52 + 48 + 20 + 16; // two path buffers, shadow ray, hit record, radiance
+constexpr long long PATH_SLOT_BYTES = 2 * 56 + 48 + 20 + 16; // two path buffers, shadow ray, hit record, radiance
 // Occupancy target (waves per SIMD) of k_extend, with global and with
 // LDS-staged traversal tables: 4 caps it at 128 VGPRs.  k_finish keeps the
 // compiler's choice (it would spill).
@@ -81,7 +81,7 @@ struct PathBuf {
     float4* p0; // org.xyz, slot (int bits)
     float4* p1; // dir.xyz, rnd counter
     float4* p2; // contrib.rgb, inv_pdf
-    float* p3;  // eta
+    float2* p3; // eta, RNG seed (uint bits): hashed once by k_generate, not per bounce
     int shard_cap;
 };
 struct ShadowBuf {
@@ -206,11 +206,12 @@ __global__ void __launch_bounds__(BLOCK) k_generate(FrameArgs fa, SceneView sv, 
         slot_coords(fa, i, lp, sample, iter);
         int x, y;
         f3 o = mk(0, 0, 0), d = mk(0, 0, 1);
-        uint32_t counter = 1;
+        uint32_t counter = 1, seed = 0;
         int depth = 0; // dead
         if (local_to_global(fa, lp, x, y)) {
             depth = 1;
-            Rng rnd{create_random_seed(sample, iter, fa.frame, x, y, fa.seed), 1};
+            seed = create_random_seed(sample, iter, fa.frame, x, y, fa.seed);
+            Rng rnd{seed, 1};
             if (fa.num_rays > 0) {
                 // make_list_emitter (driver/emitter.art:18-30): no random draws
                 const float* r = fa.rays + 8 * x;
@@ -235,7 +236,7 @@ __global__ void __launch_bounds__(BLOCK) k_generate(FrameArgs fa, SceneView sv, 
         out.p0[e] = make_float4(o.x, o.y, o.z, __int_as_float(i));
         out.p1[e] = make_float4(d.x, d.y, d.z, __uint_as_float(counter | ((uint32_t)depth << 24)));
         out.p2[e] = make_float4(1, 1, 1, 0); // init_pt_raypayload (technique/pathtracer.art:33-38)
-        out.p3[e] = 1.0f;
+        out.p3[e] = make_float2(1.0f, __uint_as_float(seed));
     }
 }
 
@@ -256,7 +257,7 @@ struct KernelCounters {
 
 struct PathState {
     f3 o, d;
-    uint32_t counter;
+    uint32_t counter, seed;
     f3 contrib;
     float inv_pdf, eta;
     int slot, depth;
@@ -278,7 +279,9 @@ __device__ __forceinline__ PathState load_path(const PathBuf& in, int i) {
     s.counter = cd & 0xFFFFFFu;
     s.contrib = f3of(p2);
     s.inv_pdf = p2.w;
-    s.eta = in.p3[i];
+    const float2 p3 = in.p3[i];
+    s.eta = p3.x;
+    s.seed = __float_as_uint(p3.y);
     return s;
 }
 
@@ -286,7 +289,7 @@ __device__ __forceinline__ void store_path(const PathBuf& out, int i, const Path
     out.p0[i] = make_float4(s.o.x, s.o.y, s.o.z, __int_as_float(s.slot));
     out.p1[i] = make_float4(s.d.x, s.d.y, s.d.z, __uint_as_float(s.counter | ((uint32_t)s.depth << 24)));
     out.p2[i] = make_float4(s.contrib.x, s.contrib.y, s.contrib.z, s.inv_pdf);
-    out.p3[i] = s.eta;
+    out.p3[i] = make_float2(s.eta, __uint_as_float(s.seed));
 }
 
 __device__ __forceinline__ f3 handle_color(const SceneView& sv, f3 c) {
@@ -358,11 +361,9 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
             has_l = true;
         }
     }
-    int lp, sample, iter;
-    slot_coords(fa, ps.slot, lp, sample, iter);
-    int px, py;
-    local_to_global(fa, lp, px, py);
-    Rng rnd{create_random_seed(sample, iter, fa.frame, px, py, fa.seed), ps.counter};
+    // seed of the path's (sample, iteration, frame, pixel, user seed),
+    // create_random_seed (core/random.art:34-43), carried in the path state
+    Rng rnd{ps.seed, ps.counter};
     f3 out_dir = neg(rd);
     const bool specular = bsdf_is_specular<FULL>(m);
     // on_shadow (pathtracer.art:52-112)
@@ -1038,9 +1039,9 @@ igx_status ensure_slot(igx_device* dev, Slot& s, size_t cap) {
     auto alloc4 = [&](float4** p, size_t k) -> igx_status { HIPCHK(hipMalloc((void**)p, k * sizeof(float4))); return IGX_OK; };
     igx_status st;
     if ((st = alloc4(&s.pa.p0, recs)) || (st = alloc4(&s.pa.p1, recs)) || (st = alloc4(&s.pa.p2, recs))) return st;
-    HIPCHK(hipMalloc((void**)&s.pa.p3, recs * sizeof(float)));
+    HIPCHK(hipMalloc((void**)&s.pa.p3, recs * sizeof(float2)));
     if ((st = alloc4(&s.pb.p0, recs)) || (st = alloc4(&s.pb.p1, recs)) || (st = alloc4(&s.pb.p2, recs))) return st;
-    HIPCHK(hipMalloc((void**)&s.pb.p3, recs * sizeof(float)));
+    HIPCHK(hipMalloc((void**)&s.pb.p3, recs * sizeof(float2)));
     if ((st = alloc4(&s.sh.s0, recs)) || (st = alloc4(&s.sh.s1, recs)) || (st = alloc4(&s.sh.s2, recs))) return st;
     if ((st = alloc4(&s.L, cap))) return st; // radiance is indexed by path slot, not sharded
     if ((st = alloc4(&s.hb.h, recs))) return st;
