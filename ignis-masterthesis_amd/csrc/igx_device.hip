@@ -2,16 +2,22 @@
 //
 // Hot path = the reference's per-iteration loop gpu_trace
 // (src/artic/driver/mapping_gpu.art:728-870) re-designed for CDNA4:
-//   * all paths of an iteration are resident in HBM (capacity = spi*W*H up to
-//     16M paths) instead of refilling a 1M-ray stream (mapping_gpu.art:1125);
+//   * all paths of one or more iterations are resident in HBM as one wavefront
+//     ("chunk", up to 128 M paths) instead of refilling a 1M-ray stream
+//     (mapping_gpu.art:1125);
 //   * one fused "extend" kernel per bounce does closest-hit traversal AND
 //     shading (the reference launches traverse, 3 sort kernels with a host scan,
 //     one hit-shade kernel per material, miss shade, then compaction with a D2H
-//     sync: mapping_gpu.art:45-68, 403-498, 114-205, 229-266, 685-714);
+//     sync: mapping_gpu.art:45-68, 403-498, 114-205, 229-266, 685-714); scenes
+//     whose tables exceed one XCD's L2 split it into a persistent-lane trace
+//     kernel and a shade kernel;
 //   * surviving paths and shadow rays are compacted on the fly with a 64-lane
-//     ballot and one atomic per wave (no sort, no host round trip);
+//     ballot and one atomic per wave on one of 64 shard counters (no sort, no
+//     host round trip);
 //   * shadow rays are traced by a separate any-hit kernel over the compacted
 //     shadow stream (gpu_traverse_secondary, mapping_gpu.art:70-112);
+//   * the last paths of a chunk run to their end in a tail kernel on a second
+//     stream, overlapping the next chunk;
 //   * radiance is accumulated per path slot with plain read-modify-writes (each
 //     slot is owned by exactly one ray at a time), then a resolve kernel adds
 //     sum(L_s)/spi to the framebuffer -- deterministic, no float atomics
