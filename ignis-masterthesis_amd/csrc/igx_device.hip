@@ -777,29 +777,60 @@ __global__ void __launch_bounds__(BLOCK, REFILL_WAVES) k_shadow_refill(SceneView
 
 #if IGX_PART == 0
 // resolve: fb += sum_s L_s / spi (driver/accumulator.art:13-19, make_standard_accumulator)
-__global__ void __launch_bounds__(BLOCK) k_resolve(FrameArgs fa, const float4* L, float* fb, int fb_width) {
-    int p = blockIdx.x * BLOCK + threadIdx.x;
-    if (p >= fa.chunk_pixels) return;
-    int x, y;
-    if (!local_to_global(fa, fa.chunk_pixel0 + p, x, y)) return;
-    size_t o = 3 * ((size_t)y * fb_width + x);
-    float fr = fb[o + 0], fg = fb[o + 1], fbb = fb[o + 2];
-    for (int it = 0; it < fa.chunk_iters; ++it) { // one accumulation per iteration, in order
-        const float4* Li = L + ((size_t)it * fa.chunk_pixels + p) * fa.spi;
-        float r = 0, g = 0, b = 0;
-        for (int s = 0; s < fa.spi; ++s) {
-            float4 l = Li[s];
-            r += l.x * fa.inv_spi;
-            g += l.y * fa.inv_spi;
-            b += l.z * fa.inv_spi;
-        }
-        fr += r;
-        fg += g;
-        fbb += b;
+// A block owns 64 pixels; its RES_G waves sum one iteration each (lanes =
+// pixels, the sample loop in order) into LDS, and wave 0 adds the iterations
+// into the framebuffer in iteration order, so the float sums are those of one
+// accumulation per render call.  One pixel per lane with all iterations in one
+// lane was latency-bound (2.1 ms per 128M-path chunk); this form takes 1.4 ms.
+// Coalesced loads through a 55 KB LDS transpose tile measured slower (3.2 ms):
+// the kernel overlaps the next chunk's k_extend, whose LDS-resident BVH leaves
+// no room for blocks with a large LDS footprint.
+constexpr int RES_G = 8;
+__global__ void __launch_bounds__(64 * RES_G) k_resolve(FrameArgs fa, const float4* L, float* fb, int fb_width) {
+    __shared__ float part[RES_G][3][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int p = blockIdx.x * 64 + lane;
+    int x = 0, y = 0;
+    const bool in = p < fa.chunk_pixels && local_to_global(fa, fa.chunk_pixel0 + p, x, y);
+    const size_t o = 3 * ((size_t)y * fb_width + x);
+    float fr = 0, fg = 0, fbb = 0;
+    if (w == 0 && in) {
+        fr = fb[o + 0];
+        fg = fb[o + 1];
+        fbb = fb[o + 2];
     }
-    fb[o + 0] = fr;
-    fb[o + 1] = fg;
-    fb[o + 2] = fbb;
+    for (int it0 = 0; it0 < fa.chunk_iters; it0 += RES_G) { // block-uniform trip count
+        const int it = it0 + w;
+        if (in && it < fa.chunk_iters) {
+            const float4* Li = L + ((size_t)it * fa.chunk_pixels + p) * fa.spi;
+            float r = 0, g = 0, b = 0;
+#pragma unroll 8
+            for (int s = 0; s < fa.spi; ++s) {
+                float4 l = Li[s];
+                r += l.x * fa.inv_spi;
+                g += l.y * fa.inv_spi;
+                b += l.z * fa.inv_spi;
+            }
+            part[w][0][lane] = r;
+            part[w][1][lane] = g;
+            part[w][2][lane] = b;
+        }
+        __syncthreads();
+        if (w == 0 && in) {
+            const int m = min(RES_G, fa.chunk_iters - it0);
+            for (int k = 0; k < m; ++k) { // one accumulation per iteration, in order
+                fr += part[k][0][lane];
+                fg += part[k][1][lane];
+                fbb += part[k][2][lane];
+            }
+        }
+        __syncthreads();
+    }
+    if (w == 0 && in) {
+        fb[o + 0] = fr;
+        fb[o + 1] = fg;
+        fb[o + 2] = fbb;
+    }
 }
 
 __global__ void k_pack_tiles(FrameArgs fa, const float* fb, float* dst, int num_tiles) {
@@ -2122,7 +2153,7 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
             end_timed(dev->tail_stream);
         }
         begin_timed(3, -1, dev->tail_stream);
-        hipLaunchKernelGGL(k_resolve, dim3((chunk_pixels + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, dev->tail_stream, fa, S.L, dev->fb, width);
+        hipLaunchKernelGGL(k_resolve, dim3((chunk_pixels + 63) / 64), dim3(64 * RES_G), 0, dev->tail_stream, fa, S.L, dev->fb, width);
         end_timed(dev->tail_stream);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(S.done, dev->tail_stream));
