@@ -110,6 +110,7 @@ struct FrameArgs {
     int chunk_pixels;    // local pixels in this chunk
     int chunk_iters;     // consecutive iterations (iter, iter + 1, ...) the chunk covers
     float inv_spi;
+    int gen_n;           // > 0: this k_extend launch is bounce 0 and generates its n camera paths itself
 };
 
 // path slot -> (local pixel, sample, iteration): slots run over the chunk's
@@ -202,47 +203,57 @@ __device__ __forceinline__ void wave_append2(bool a, bool b, int* ca, int* cb, i
 // Slot i of the chunk holds path i; no compaction (tile padding slots are
 // written as dead paths with depth 0), so no atomics.
 // ---------------------------------------------------------------------------
+// Path i of the chunk at its camera vertex (k_generate, and k_extend's fused
+// bounce 0).  Path state layout: see PathState below.
+struct GenPath {
+    f3 o, d;
+    uint32_t counter, seed;
+    int depth;
+};
+__device__ __forceinline__ GenPath gen_path(const FrameArgs& fa, const SceneView& sv, int i) {
+    int lp, sample, iter;
+    slot_coords(fa, i, lp, sample, iter);
+    int x, y;
+    GenPath g{mk(0, 0, 0), mk(0, 0, 1), 1, 0, 0}; // depth 0: dead (tile padding)
+    if (local_to_global(fa, lp, x, y)) {
+        g.depth = 1;
+        g.seed = create_random_seed(sample, iter, fa.frame, x, y, fa.seed);
+        Rng rnd{g.seed, 1};
+        if (fa.num_rays > 0) {
+            // make_list_emitter (driver/emitter.art:18-30): no random draws
+            const float* r = fa.rays + 8 * x;
+            g.o = mk(r[0], r[1], r[2]);
+            g.d = mk(r[3], r[4], r[5]);
+        } else {
+            float rx = rnd.next_f32();
+            float ry = rnd.next_f32();
+            float nx = 2 * ((float)x + rx) / (float)fa.width - 1;
+            float ny = 1 - 2 * ((float)y + ry) / (float)fa.height;
+            const DevCamera& c = sv.cam;
+            f3 v = mk(c.scale_x * nx, c.scale_y * ny, 1);
+            f3 w = mk(c.right[0] * v.x + c.up[0] * v.y + c.dir[0] * v.z,
+                      c.right[1] * v.x + c.up[1] * v.y + c.dir[1] * v.z,
+                      c.right[2] * v.x + c.up[2] * v.y + c.dir[2] * v.z);
+            g.o = mk(c.eye[0], c.eye[1], c.eye[2]);
+            g.d = normalize(w);
+        }
+        g.counter = rnd.counter;
+    }
+    return g;
+}
+
 #if IGX_PART == 0
 __global__ void __launch_bounds__(BLOCK) k_generate(FrameArgs fa, SceneView sv, PathBuf out, float4* L, int* cnt0) {
     const int n = fa.chunk_pixels * fa.spi * fa.chunk_iters;
     if (blockIdx.x == 0 && threadIdx.x < NSH) cnt0[threadIdx.x * CSTRIDE] = gen_shard_count(n, threadIdx.x);
     for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
         L[i] = make_float4(0, 0, 0, 0);
-        int lp, sample, iter;
-        slot_coords(fa, i, lp, sample, iter);
-        int x, y;
-        f3 o = mk(0, 0, 0), d = mk(0, 0, 1);
-        uint32_t counter = 1, seed = 0;
-        int depth = 0; // dead
-        if (local_to_global(fa, lp, x, y)) {
-            depth = 1;
-            seed = create_random_seed(sample, iter, fa.frame, x, y, fa.seed);
-            Rng rnd{seed, 1};
-            if (fa.num_rays > 0) {
-                // make_list_emitter (driver/emitter.art:18-30): no random draws
-                const float* r = fa.rays + 8 * x;
-                o = mk(r[0], r[1], r[2]);
-                d = mk(r[3], r[4], r[5]);
-            } else {
-                float rx = rnd.next_f32();
-                float ry = rnd.next_f32();
-                float nx = 2 * ((float)x + rx) / (float)fa.width - 1;
-                float ny = 1 - 2 * ((float)y + ry) / (float)fa.height;
-                const DevCamera& c = sv.cam;
-                f3 v = mk(c.scale_x * nx, c.scale_y * ny, 1);
-                f3 w = mk(c.right[0] * v.x + c.up[0] * v.y + c.dir[0] * v.z,
-                          c.right[1] * v.x + c.up[1] * v.y + c.dir[1] * v.z,
-                          c.right[2] * v.x + c.up[2] * v.y + c.dir[2] * v.z);
-                o = mk(c.eye[0], c.eye[1], c.eye[2]);
-                d = normalize(w);
-            }
-            counter = rnd.counter;
-        }
+        const GenPath g = gen_path(fa, sv, i);
         const int e = gen_index(i, out.shard_cap);
-        out.p0[e] = make_float4(o.x, o.y, o.z, __int_as_float(i));
-        out.p1[e] = make_float4(d.x, d.y, d.z, __uint_as_float(counter | ((uint32_t)depth << 24)));
+        out.p0[e] = make_float4(g.o.x, g.o.y, g.o.z, __int_as_float(i));
+        out.p1[e] = make_float4(g.d.x, g.d.y, g.d.z, __uint_as_float(g.counter | ((uint32_t)g.depth << 24)));
         out.p2[e] = make_float4(1, 1, 1, 0); // init_pt_raypayload (technique/pathtracer.art:33-38)
-        out.p3[e] = make_float2(1.0f, __uint_as_float(seed));
+        out.p3[e] = make_float2(1.0f, __uint_as_float(g.seed));
     }
 }
 
@@ -480,11 +491,15 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : EXTEND_WAVES) 
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
-    if (row_total(kc.cnt_in) <= tail_threshold) return; // k_finish takes the remaining paths (block-uniform)
+    // gen_n > 0 (bounce 0 with generation fused; the host launches it only
+    // when n > tail): the paths are the chunk's camera paths in k_generate's
+    // shard order, built here instead of being read from the input stream.
+    const bool gen = fa.gen_n > 0;
+    if (!gen && row_total(kc.cnt_in) <= tail_threshold) return; // k_finish takes the remaining paths (block-uniform)
     const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
     const WaveWork w = wave_work();
-    const int ns = uniform_load(kc.cnt_in + w.s * CSTRIDE);
+    const int ns = gen ? gen_shard_count(fa.gen_n, w.s) : uniform_load(kc.cnt_in + w.s * CSTRIDE);
     int* const c_out = kc.cnt_out + w.s * CSTRIDE;
     int* const c_sh = kc.cnt_shadow + w.s * CSTRIDE;
     for (int p0 = w.k * 64; p0 < ns; p0 += w.K * 64) {
@@ -494,7 +509,22 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : EXTEND_WAVES) 
         ShadowRec sr;
         ps.depth = 0;
         if (pos < ns) {
-            ps = load_path(in, w.s * in.shard_cap + pos);
+            if (gen) { // inverse of gen_index
+                const int i = ((pos >> 6) << 12) | (w.s << 6) | (pos & 63);
+                const GenPath g = gen_path(fa, sv, i);
+                L[i] = make_float4(0, 0, 0, 0);
+                ps.o = g.o;
+                ps.d = g.d;
+                ps.counter = g.counter;
+                ps.seed = g.seed;
+                ps.depth = g.depth;
+                ps.slot = i;
+                ps.contrib = mk(1, 1, 1); // init_pt_raypayload (technique/pathtracer.art:33-38)
+                ps.inv_pdf = 0;
+                ps.eta = 1.0f;
+            } else {
+                ps = load_path(in, w.s * in.shard_cap + pos);
+            }
             if (ps.depth > 0) {
                 f3 Lacc;
                 bool has_l;
@@ -943,6 +973,7 @@ struct igx_device {
     int64_t capacity_opt = 0;
     int64_t tail_opt = -1;   // paths at or below which k_finish takes over (-1 = auto)
     int64_t tail_last_opt = -1; // the same for the last chunk of a render call, whose tail overlaps nothing (-1 = tail_opt)
+    bool fuse_generate = true; // bounce 0 of the fused k_extend builds its camera paths (no k_generate pass)
     int split_opt = -1;      // k_trace + k_shade per bounce instead of the fused k_extend (-1: auto = global-table scenes)
     int trace_waves = 5;     // occupancy target of k_trace (5 waves per SIMD, anything else = compiler's choice)
     int refill_opt = -1;     // persistent-lane trace / shadow, refilled once this many lanes idle (0: off, -1: auto = 16)
@@ -1507,6 +1538,7 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     else if (k == "capacity") dev->capacity_opt = value;
     else if (k == "tail_threshold") dev->tail_opt = value;
     else if (k == "tail_threshold_last") dev->tail_last_opt = value;
+    else if (k == "fuse_generate") dev->fuse_generate = value != 0;
     else if (k == "split") {
         if (value < -1 || value > 1) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "split must be -1 (auto), 0 or 1");
         dev->split_opt = (int)value;
@@ -2078,10 +2110,15 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
         int* cnt = S.ctr; // row 2b: paths entering bounce b, row 2b+1: shadow rays of bounce b
         auto row = [&](int r) { return cnt + (size_t)r * CROW; };
         HIPCHK(hipMemsetAsync(S.ctr, 0, (size_t)(2 * max_bounces + 4) * CROW * sizeof(int), dev->stream));
-        begin_timed(2, -1, dev->stream);
-        hipLaunchKernelGGL(k_generate, dim3(grid_for(dev, n, 8)), dim3(BLOCK), 0, dev->stream, fa, dev->sv, S.pa, S.L, cnt);
-        end_timed(dev->stream);
-        HIPCHK(hipGetLastError());
+        // camera paths: built by bounce 0 of the fused k_extend when the chunk
+        // runs through it (saves the 72 B/path round trip of k_generate)
+        const bool fuse_gen = dev->fuse_generate && !split && n > tail;
+        if (!fuse_gen) {
+            begin_timed(2, -1, dev->stream);
+            hipLaunchKernelGGL(k_generate, dim3(grid_for(dev, n, 8)), dim3(BLOCK), 0, dev->stream, fa, dev->sv, S.pa, S.L, cnt);
+            end_timed(dev->stream);
+            HIPCHK(hipGetLastError());
+        }
         S.n0 = n;
         const int ext_grid = grid_for(dev, n, ext_bpc);
         const int tr_grid = grid_for(dev, n, tr_bpc);
@@ -2117,8 +2154,10 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
                 end_timed(dev->stream);
             } else {
                 begin_timed(0, b, dev->stream);
-                if (inst) launch_extend<true>(dev, S, ext_grid, fa, in, out, kc, tail);
-                else launch_extend<false>(dev, S, ext_grid, fa, in, out, kc, tail);
+                FrameArgs fb = fa;
+                fb.gen_n = fuse_gen && b == 0 ? (int)n : 0;
+                if (inst) launch_extend<true>(dev, S, ext_grid, fb, in, out, kc, tail);
+                else launch_extend<false>(dev, S, ext_grid, fb, in, out, kc, tail);
                 end_timed(dev->stream);
             }
             begin_timed(1, b, dev->stream);
