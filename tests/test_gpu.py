@@ -188,6 +188,37 @@ def test_tail_threshold_invariance(device, root, name):
     assert imgs[0].sum() > 0
 
 
+@pytest.mark.parametrize("name", ["diamond_scene.json", "s_deep.json"])
+@pytest.mark.parametrize("tile", [None, (64, 1, 3)])
+def test_fused_generate_invariance(device, root, name, tile):
+    """Camera paths built by bounce 0 of k_extend (fuse_generate, default) and
+    by the separate k_generate pass give the same image and ray counts, bit
+    for bit, also with tile padding (dead slots) in the chunk."""
+    sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", name))
+    imgs, counts = [], []
+    try:
+        device.set_option("tail_threshold", 0)  # force the wavefront path, where the fusion applies
+        for fuse in (0, 1):
+            device.set_option("fuse_generate", fuse)
+            device.reset_stats()
+            device.clear()
+            device.upload(sc)
+            p = ignis_amd.RenderParams()
+            p.width, p.height, p.spi = 150, 100, 4
+            if tile:
+                p.tile_size, p.tile_offset, p.tile_stride = tile
+            device.render_iterations(p, 2)
+            imgs.append(device.framebuffer(150 * 100 * 3)[0])
+            st = device.stats()
+            counts.append((st["camera_rays"], st["bounce_rays"], st["shadow_rays"]))
+    finally:
+        device.set_option("fuse_generate", 1)
+        device.set_option("tail_threshold", -1)
+    np.testing.assert_array_equal(imgs[0], imgs[1])
+    assert counts[0] == counts[1]
+    assert imgs[0].sum() > 0
+
+
 @pytest.mark.parametrize("tile,capacity", [(None, 0), ((64, 1, 3), 0), (None, 20000)])
 def test_render_iterations_equals_single_calls(device, diamond_path, tile, capacity):
     """igx_render_iterations (iterations batched into one wavefront when they fit the
