@@ -60,7 +60,9 @@ def algorithmic_bytes(stats_inst, st):
       64 B per instance + 48 B per
       triangle + 288 B of shading fetches per hit (entity 112, face 16,
       3 vertices + 3 normals 96, material 64); plus 52 B per surviving path
-      and 48 B per shadow ray written;
+      and 48 B per shadow ray written; bounce 0 builds the camera paths
+      itself (fuse_generate), so a camera ray reads no path state but zeroes
+      its 16 B radiance slot (-36 B);
     * split k_trace: 32 B ray read + 20 B hit written + the same BVH terms.
     """
     n = max(stats_inst["_rays_ext"], 1)
@@ -70,7 +72,8 @@ def algorithmic_bytes(stats_inst, st):
         return st["extend_rays"] * per_ray, per_ray
     per_ray = 52 + 32 + bvh + 288.0 * stats_inst["_hits"] / n
     shadow_wf = st["shadow_rays"] - st["tail_shadow_rays"]
-    return st["extend_rays"] * per_ray + st["extend_paths_out"] * 52 + shadow_wf * 48, per_ray
+    total = st["extend_rays"] * per_ray + st["extend_paths_out"] * 52 + shadow_wf * 48 - st["camera_rays"] * 36
+    return total, per_ray
 
 
 def load_pmc(n_gpus, scene="diamond_scene", kernel="extend"):

@@ -198,6 +198,7 @@ def test_fused_generate_invariance(device, root, name, tile):
     imgs, counts = [], []
     try:
         device.set_option("tail_threshold", 0)  # force the wavefront path, where the fusion applies
+        device.set_option("split", 0)  # and the fused schedule (S-deep's tables are global)
         for fuse in (0, 1):
             device.set_option("fuse_generate", fuse)
             device.reset_stats()
@@ -213,6 +214,7 @@ def test_fused_generate_invariance(device, root, name, tile):
             counts.append((st["camera_rays"], st["bounce_rays"], st["shadow_rays"]))
     finally:
         device.set_option("fuse_generate", 1)
+        device.set_option("split", -1)
         device.set_option("tail_threshold", -1)
     np.testing.assert_array_equal(imgs[0], imgs[1])
     assert counts[0] == counts[1]
