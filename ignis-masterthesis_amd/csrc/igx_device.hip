@@ -2294,6 +2294,8 @@ extern "C" igx_status igx_get_stats(igx_device* dev, igx_stats* out) {
     out->shadow_wave_leaf_iters = h[12];
     out->bvh_width = dev->bvh_width;
     out->node_bytes = node_f4(dev->bvh_width) * 16;
+    out->lds_scene_bytes = (int32_t)dev->lds_scene_bytes;
+    out->shadow_blocks_per_cu = dev->has_scene ? shadow_blocks_per_cu<false>(dev->variant, dev->lds_scene_bytes, use_refill(dev)) : 0;
     return IGX_OK;
 }
 
