@@ -44,7 +44,8 @@ enum : int32_t { MAT_DIFFUSE = 0, MAT_DIELECTRIC = 1, MAT_CONDUCTOR = 2, MAT_PLA
 // (BSDF::setupRoughness, src/runtime/bsdf/BSDF.cpp:53-99)
 enum : int32_t { MF_DELTA = 0, MF_VNDF_GGX = 1, MF_GGX = 2, MF_BECKMANN = 3 };
 struct DevMaterial {   // 128 B
-    int32_t type, light, dist, mirror; // mirror: delta conductor with eta = 0, k = 1 (make_mirror_bsdf)
+    int32_t type, light, dist, mirror; // mirror: delta conductor with eta = 0, k = 1 (make_mirror_bsdf);
+                                       // dielectric: thin interface; principled: flag bits
     float kd[4];        // diffuse reflectance; w = Oren-Nayar roughness (0: Lambert)
     float ks[4];        // specular reflectance; w = n1 (ext ior)
     float kt[4];        // specular transmittance; w = n2 (int ior)

@@ -1852,7 +1852,6 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
         case IGX_BSDF_PRINCIPLED: d.type = MAT_PRINCIPLED; break;
         default: return fail(dev, IGX_ERR_UNSUPPORTED, "unsupported bsdf type " + std::to_string(m.bsdf_type));
         }
-        if (m.bsdf_type == IGX_BSDF_DIELECTRIC && m.thin) return fail(dev, IGX_ERR_UNSUPPORTED, "thin dielectric is not supported");
         if (m.distribution < IGX_MICROFACET_DELTA || m.distribution > IGX_MICROFACET_BECKMANN)
             return fail(dev, IGX_ERR_INVALID_ARGUMENT, "invalid microfacet distribution");
         d.light = m.light >= 0 && (uint32_t)m.light < desc->num_lights ? light_remap[m.light] : -1;
@@ -1869,6 +1868,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
             mirror = mirror && std::fabs(m.eta[c]) <= 1e-4f && std::fabs(m.kappa[c] - 1.0f) <= 1e-4f;
         }
         d.mirror = mirror ? 1 : 0;
+        if (m.bsdf_type == IGX_BSDF_DIELECTRIC) d.mirror = m.thin ? 1 : 0; // dielectric: thin flag
         d.kd[3] = m.bsdf_type == IGX_BSDF_DIFFUSE ? m.diffuse_alpha : 0.0f;
         d.ks[3] = m.ext_ior;
         d.kt[3] = m.int_ior;

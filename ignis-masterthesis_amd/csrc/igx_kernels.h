@@ -1386,6 +1386,14 @@ __device__ __forceinline__ float bsdf_pdf(const DevMaterial& m, const Surface& s
 // make_pure_dielectric_bsdf.sample, adjoint = false (bsdf/dielectric.art)
 __device__ __forceinline__ BsdfSample dielectric_sample(const DevMaterial& m, const Surface& s, Rng& rnd, f3 out_dir) {
     float n1 = m.ks[3], n2 = m.kt[3];
+    if (m.mirror) {
+        // thin interface (make_thin_dielectric_bsdf, bsdf/dielectric.art:26-47): always
+        // outside -> inside, F sums the slab's inter-reflections, straight transmission
+        float f = fresnel_dielectric(n1 / n2, absolute_cos(out_dir, s.local.n));
+        float F = f + (1 - f) * f / (f + 1);
+        if (rnd.next_f32() > F) return make_sample(mulf(out_dir, -1.0f), 1, mk(m.kt[0], m.kt[1], m.kt[2]), 1);
+        return make_sample(normalize(reflect(out_dir, s.local.n)), 1, mk(m.ks[0], m.ks[1], m.ks[2]), 1);
+    }
     float k = s.entering ? n1 / n2 : n2 / n1;
     f3 n = s.local.n;
     float cos_o = dot(out_dir, n);

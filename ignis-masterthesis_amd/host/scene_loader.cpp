@@ -217,38 +217,92 @@ M4 get_transform(const Props& p, const char* key = "transform") {
     return t;
 }
 
-// Merge externals into the main document (Parser.cpp:451-454)
-void merge_into(Value& dst, const Value& src) {
-    for (auto& kv : src.obj) {
-        Value* existing = nullptr;
-        for (auto& d : dst.obj)
-            if (d.first == kv.first) existing = &d.second;
-        if (!existing) {
-            dst.obj.push_back(kv);
-        } else if (existing->is_array() && kv.second.is_array()) {
-            existing->arr.insert(existing->arr.end(), kv.second.arr.begin(), kv.second.arr.end());
-        } else if (existing->is_object() && kv.second.is_object()) {
-            merge_into(*existing, kv.second);
+// Scene-level merge of externals, as the reference parser does it:
+// `InternalSceneParser::loadFromJSON` (Parser.cpp:450-459) loads every external
+// first, each into its own Scene that `Scene::addFrom` (Scene.cpp:5-23) copies
+// into the current one, replacing objects of the same name and taking the
+// external's technique / camera / film (even an absent one); only then are the
+// current file's own objects added (`handleNamedObject`, Parser.cpp:350-392),
+// again replacing by name, and its camera / technique / film set.  Named
+// objects keep the position of their first definition.  Each object remembers
+// the directory of the file that defined it (`SceneObject::baseDir`), so mesh
+// paths of an external resolve against the external's directory.
+const char* const kNamedCategories[] = {"shapes", "textures", "bsdfs", "lights", "media", "entities"};
+const char* const kAnonymous[] = {"camera", "technique", "film"};
+
+void put_named(Value& list, const Value& obj) {
+    const Value* nm = obj.find("name");
+    if (!nm || !nm->is_string()) fail("named scene object without a string 'name'");
+    for (auto& e : list.arr) {
+        const Value* en = e.find("name");
+        if (en && en->str == nm->str) {
+            e = obj;
+            return;
         }
     }
+    list.arr.push_back(obj);
+}
+
+Value& category(Value& doc, const std::string& key) {
+    for (auto& kv : doc.obj)
+        if (kv.first == key) return kv.second;
+    Value v;
+    v.type = Value::Array;
+    doc.obj.emplace_back(key, v);
+    return doc.obj.back().second;
+}
+
+void set_key(Value& doc, const std::string& key, const Value* v) {
+    for (auto it = doc.obj.begin(); it != doc.obj.end(); ++it)
+        if (it->first == key) {
+            doc.obj.erase(it);
+            break;
+        }
+    if (v) doc.obj.emplace_back(key, *v);
+}
+
+// Scene::addFrom(other)
+void add_from(Value& dst, const Value& src) {
+    for (const char* cat : kNamedCategories)
+        if (const Value* l = src.find(cat))
+            for (auto& o : l->arr) put_named(category(dst, cat), o);
+    for (const char* k : kAnonymous) set_key(dst, k, src.find(k));
 }
 
 Value load_document(const std::string& text, const std::string& base_dir, int depth = 0) {
     if (depth > 8) fail("externals nested too deep");
     Value doc = igx::json::parse(text);
     if (!doc.is_object()) fail("scene root must be an object");
+    Value scene;
+    scene.type = Value::Object;
     if (const Value* ext = doc.find("externals")) {
         if (!ext->is_array()) fail("externals must be an array");
-        std::vector<Value> extra;
         for (auto& e : ext->arr) {
             const Value* fn = e.find("filename");
             if (!fn || !fn->is_string()) fail("external without filename");
             std::string path = join_path(base_dir, fn->str);
-            extra.push_back(load_document(read_file(path), dir_of(path), depth + 1));
+            add_from(scene, load_document(read_file(path), dir_of(path), depth + 1));
         }
-        for (auto& x : extra) merge_into(doc, x);
     }
-    return doc;
+    for (const char* k : kAnonymous)
+        if (const Value* v = doc.find(k)) set_key(scene, k, v);
+    for (const char* cat : kNamedCategories) {
+        const Value* l = doc.find(cat);
+        if (!l) continue;
+        if (!l->is_array()) fail(std::string("'") + cat + "' must be an array");
+        for (auto& o : l->arr) {
+            if (!o.is_object()) fail(std::string("'") + cat + "' elements must be objects");
+            Value obj = o;
+            if (!obj.find("__base_dir")) {
+                Value bd;
+                bd.type = Value::String;
+                bd.str = base_dir;
+                obj.obj.emplace_back("__base_dir", bd);
+            }
+            put_named(category(scene, cat), obj);
+        }
+    }
+    return scene;
 }
 
 const Value* array_of(const Value& doc, const char* key) {
@@ -533,7 +587,8 @@ static void build_scene(SceneStore& S, const Value& doc, const std::string& base
                 b.inflate(1e-5f);
                 for (int i = 0; i < 3; ++i) { ls.shape.bbox_min[i] = b.min[i]; ls.shape.bbox_max[i] = b.max[i]; }
             } else {
-                ls.mesh = setup_trimesh(type, sp, base_dir, name);
+                const Value* obj_dir = s.find("__base_dir");
+                ls.mesh = setup_trimesh(type, sp, obj_dir && obj_dir->is_string() ? obj_dir->str : base_dir, name);
                 ls.is_mesh = true;
                 ls.shape.type = IGX_SHAPE_TRIMESH;
                 BBox b = ls.mesh.compute_bbox();

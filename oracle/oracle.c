@@ -930,7 +930,7 @@ static inline float fresnel_factor(float eta, float cos_i, float cos_t) {
 /* hit (bsdf/diffuse.art, dielectric.art, conductor.art, plastic.art, mix.art */
 /* and core/microfacet.art), restated as one record + lobe functions.        */
 /* ------------------------------------------------------------------------ */
-enum { LOBE_LAMBERT, LOBE_OREN_NAYAR, LOBE_DIELECTRIC, LOBE_MIRROR, LOBE_PURE_CONDUCTOR, LOBE_ROUGH_CONDUCTOR };
+enum { LOBE_LAMBERT, LOBE_OREN_NAYAR, LOBE_DIELECTRIC, LOBE_MIRROR, LOBE_PURE_CONDUCTOR, LOBE_ROUGH_CONDUCTOR, LOBE_THIN_DIELECTRIC };
 
 typedef struct {
     int lobe;          /* primary lobe; plastic = mix(LAMBERT+scatter, spec) */
@@ -1084,7 +1084,7 @@ static obsdf obsdf_make(const igx_material* m, const osurf* surf) {
     int rough = m->distribution != IGX_MICROFACET_DELTA && m->alpha_u > 1e-4f && m->alpha_v > 1e-4f;
     b.model = rough ? m->distribution : IGX_MICROFACET_DELTA;
     switch (m->bsdf_type) {
-    case IGX_BSDF_DIELECTRIC: b.lobe = LOBE_DIELECTRIC; break;
+    case IGX_BSDF_DIELECTRIC: b.lobe = m->thin ? LOBE_THIN_DIELECTRIC : LOBE_DIELECTRIC; break;
     case IGX_BSDF_CONDUCTOR:
         if (rough) b.lobe = LOBE_ROUGH_CONDUCTOR;
         else {
@@ -1109,9 +1109,11 @@ static obsdf obsdf_make(const igx_material* m, const osurf* surf) {
     return b;
 }
 static int obsdf_specular(const obsdf* b) {
-    return !b->plastic && !b->principled && (b->lobe == LOBE_DIELECTRIC || b->lobe == LOBE_MIRROR || b->lobe == LOBE_PURE_CONDUCTOR);
+    return !b->plastic && !b->principled && (b->lobe == LOBE_DIELECTRIC || b->lobe == LOBE_THIN_DIELECTRIC || b->lobe == LOBE_MIRROR || b->lobe == LOBE_PURE_CONDUCTOR);
 }
-static int lobe_specular(int lobe) { return lobe == LOBE_DIELECTRIC || lobe == LOBE_MIRROR || lobe == LOBE_PURE_CONDUCTOR; }
+static int lobe_specular(int lobe) {
+    return lobe == LOBE_DIELECTRIC || lobe == LOBE_THIN_DIELECTRIC || lobe == LOBE_MIRROR || lobe == LOBE_PURE_CONDUCTOR;
+}
 
 static v3 rough_eval(const obsdf* b, v3 in, v3 out) {
     v3 N = b->surf->local.n;
@@ -1182,6 +1184,16 @@ static osample lobe_sample(const obsdf* b, int lobe, rng_t* r, v3 out) {
         }
         if (rng_f32(r) > ft_factor) return osample_make(vsub(vmulf(N, k * co - ft_cos_t), vmulf(out, k)), 1, b->kt, k);
         return osample_make(vreflect(out, N), 1, b->ks, 1);
+    }
+    case LOBE_THIN_DIELECTRIC: {
+        /* make_thin_dielectric_bsdf (bsdf/dielectric.art:26-47): always outside -> inside,
+         * F = f + (1 - f) f / (f + 1) (the inter-reflection sum of a thin slab), straight
+         * transmission with eta 1 */
+        float k = b->n1 / b->n2;
+        float f = fresnel_dielectric_f(k, abs_cos(out, N));
+        float F = f + (1 - f) * f / (f + 1);
+        if (rng_f32(r) > F) return osample_make(vmulf(out, -1), 1, b->kt, 1);
+        return osample_make(vnormalize(vreflect(out, N)), 1, b->ks, 1);
     }
     case LOBE_MIRROR: return osample_make(vreflect(out, N), 1, b->ks, 1);
     case LOBE_PURE_CONDUCTOR: {
