@@ -11,8 +11,10 @@ the device.
 Multi-GPU (torchrun, one rank per GPU): the film is cut into square tiles
 (40 px for 1000-px films: a tile column count coprime with N, shard.balanced_tile)
 dealt round-robin to the ranks (tile t -> rank t % N); every rank renders all 32
-iterations of its tiles, packs them, and an RCCL all_gather over xGMI assembles
-the frame.  Total work is fixed, so scaling is "strong".
+iterations of its tiles, packs them, and an RCCL gather over xGMI brings the
+packed tiles to rank 0, which assembles the frame.  Total work is fixed, so
+scaling is "strong".  `--scene scenes/s_deep.json --size 4096 --spp 64` is the
+config-5 stand-in.
 
 Output: ONE JSON line on rank 0.
 """
@@ -41,6 +43,7 @@ def parse():
     ap.add_argument("--scene", default=os.path.join(ROOT, "scenes", "diamond_scene.json"))
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--spi", type=int, default=8)
+    ap.add_argument("--size", type=int, default=0, help="square film size overriding the scene's (config 5: 4096)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample length")
     ap.add_argument("--suite", type=int, default=1, help="also measure the other §8d scenes (N=1 only)")
@@ -49,31 +52,42 @@ def parse():
     return ap.parse_args()
 
 
-def algorithmic_bytes(stats_inst, st):
-    """Algorithmic bytes of the dominant wavefront kernel's launches, DESIGN.md §4.
+MALL_BYTES = 256 << 20  # Infinity Cache (MI355X_MICROARCH.md): tables below it stay on-chip between launches
 
-    Per-ray visit counts (BVH2 nodes, instance records, triangles, hits) come
-    from an instrumented pass; ray counts are those the wavefront kernels
-    handled in the timed run (the tail kernel's rays are excluded).
-    * fused k_extend (default): per closest-hit ray 52 B path state read +
-      32 B radiance read/write + 128 B per 4-wide node (64 B per BVH2 node) +
-      64 B per instance + 48 B per
-      triangle + 288 B of shading fetches per hit (entity 112, face 16,
-      3 vertices + 3 normals 96, material 64); plus 52 B per surviving path
-      and 48 B per shadow ray written; bounce 0 builds the camera paths
-      itself (fuse_generate), so a camera ray reads no path state but zeroes
-      its 16 B radiance slot (-36 B);
-    * split k_trace: 32 B ray read + 20 B hit written + the same BVH terms.
-    """
-    n = max(stats_inst["_rays_ext"], 1)
-    bvh = float(st.get("node_bytes", 64)) * stats_inst["node_visits"] / n + 64.0 * stats_inst["leaf_visits"] / n + 48.0 * stats_inst["tri_tests"] / n
+
+def algorithmic_bytes(inst, st):
+    """Algorithmic HBM bytes of the dominant kernel's launches.
+
+    Streams, on every scene:
+    * fused k_extend: per closest-hit ray 52 B path state read (camera rays:
+      none, bounce 0 builds them, fuse_generate) and its 16 B radiance slot
+      read + written (camera rays: written only); 52 B per surviving path and
+      48 B per shadow ray written;
+    * split k_trace: 32 B ray read + 20 B hit record written per ray.
+    Scene tables: when the traversal + shading tables fit the 256 MiB
+    Infinity Cache (diamond, primitives, S-deep, S-soup-1M) they are fetched
+    from HBM about once and every further node / triangle / vertex read is an
+    on-chip hit (LDS on the LDS-staged diamond), so they add nothing per ray.
+    Beyond it (S-soup-16M, 1.8 GB) every visit is a potential HBM read:
+    node_bytes per node + 64 B per instance + 48 B per triangle per ray, plus
+    (fused) 288 B of shading fetches per hit.
+    Returns (total bytes, per-ray bytes, memory-system bytes): the last counts
+    every table read the kernel issues whatever level serves it (the
+    round-1 'algorithmic' figure, a work rate, not an HBM figure)."""
+    n = max(inst["_rays_ext"], 1)
+    bvh = float(st.get("node_bytes", 64)) * inst["node_visits"] / n + 64.0 * inst["leaf_visits"] / n + 48.0 * inst["tri_tests"] / n
+    shade = 288.0 * inst["_hits"] / n
+    resident = st["table_bytes"] + st["shading_bytes"] <= MALL_BYTES
     if st["launches_trace"] > 0:
-        per_ray = 32 + 20 + bvh
-        return st["extend_rays"] * per_ray, per_ray
-    per_ray = 52 + 32 + bvh + 288.0 * stats_inst["_hits"] / n
+        stream = 32 + 20
+        per_ray = stream + (0 if resident else bvh)
+        return st["extend_rays"] * per_ray, per_ray, st["extend_rays"] * (stream + bvh)
     shadow_wf = st["shadow_rays"] - st["tail_shadow_rays"]
-    total = st["extend_rays"] * per_ray + st["extend_paths_out"] * 52 + shadow_wf * 48 - st["camera_rays"] * 36
-    return total, per_ray
+    cam = st["camera_rays"]
+    streams = (st["extend_rays"] - cam) * (52 + 32) + cam * 16 + st["extend_paths_out"] * 52 + shadow_wf * 48
+    tables = st["extend_rays"] * (bvh + shade)
+    total = streams + (0 if resident else tables)
+    return total, total / max(st["extend_rays"], 1), streams + tables
 
 
 def load_pmc(n_gpus, scene="diamond_scene", kernel="extend"):
@@ -86,15 +100,15 @@ def load_pmc(n_gpus, scene="diamond_scene", kernel="extend"):
         return None
     try:
         with open(path) as f:
-            d = json.load(f)
-        return float(d["hbm_bytes_per_launch"])
+            return json.load(f)
     except Exception:
         return None
 
 
 def roofline(dev, st, render_one, n_gpus, scene_key):
-    """Roofline object of the dominant kernel: algorithmic bytes (visit counts
-    from an instrumented, untimed pass) over its HIP-event launch time."""
+    """Roofline object of the dominant kernel: algorithmic HBM bytes (visit
+    counts from an instrumented, untimed pass) over its HIP-event launch time,
+    next to the PMC-measured HBM traffic of the same kernel."""
     dev.reset_stats()
     dev.set_option("instrument", 1)
     dev.clear()
@@ -103,13 +117,16 @@ def roofline(dev, st, render_one, n_gpus, scene_key):
     dev.set_option("instrument", 0)
     inst["_rays_ext"] = inst["camera_rays"] + inst["bounce_rays"]
     inst["_hits"] = inst["shaded_hits"]
-    alg_bytes, bytes_per_ray = algorithmic_bytes(inst, st)
+    alg_bytes, bytes_per_ray, mem_bytes = algorithmic_bytes(inst, st)
     split = st["launches_trace"] > 0
     launches = max(st["launches_trace"] if split else st["launches_extend"], 1)
     avg_launch_s = (st["ms_trace"] if split else st["ms_extend"]) / 1e3 / launches
     achieved = (alg_bytes / launches) / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
-    traffic = load_pmc(n_gpus, scene_key, "trace" if split else "extend")
-    return {
+    pmc = load_pmc(n_gpus, scene_key, "trace" if split else "extend")
+    traffic = float(pmc["hbm_bytes_per_launch"]) if pmc else None
+    simd = inst["node_visits"] / max(1, 64 * inst["wave_node_iters"])
+    resident = st["table_bytes"] + st["shading_bytes"] <= MALL_BYTES
+    out = {
         "bound": "hbm",
         "kernel": "k_trace (closest-hit traversal)" if split else "k_extend (closest-hit traversal + shading, fused)",
         "achieved": round(achieved, 1),
@@ -119,15 +136,26 @@ def roofline(dev, st, render_one, n_gpus, scene_key):
         "traffic": traffic,
         # measured HBM bandwidth of the same launches (PMC bytes / HIP-event time)
         "traffic_gbs": round(traffic / avg_launch_s / 1e9, 1) if traffic and avg_launch_s > 0 else None,
+        "frac_traffic": round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4) if traffic and avg_launch_s > 0 else None,
+        "traffic_raw": {k: pmc[k] for k in ("fetch_size_kib_per_launch", "write_size_kib_per_launch")} if pmc else None,
         "algorithmic_bytes_per_launch": round(alg_bytes / launches, 1),
         "bytes_per_ray": round(bytes_per_ray, 1),
+        "tables_on_chip": bool(resident),
+        "table_bytes": int(st["table_bytes"] + st["shading_bytes"]),
+        # every table read the kernel issues, whatever serves it (LDS, L2, Infinity Cache, HBM)
+        "memory_system_gbs": round((mem_bytes / launches) / avg_launch_s / 1e9, 1) if avg_launch_s > 0 else None,
         "visits_per_ray": {"nodes": round(inst["node_visits"] / max(1, inst["_rays_ext"]), 2),
                            "instances": round(inst["leaf_visits"] / max(1, inst["_rays_ext"]), 2),
                            "triangles": round(inst["tri_tests"] / max(1, inst["_rays_ext"]), 2)},
-        "simd_efficiency": round(inst["node_visits"] / max(1, 64 * inst["wave_node_iters"]), 3),
+        "simd_efficiency": round(simd, 3),
         "avg_launch_us": round(avg_launch_s * 1e6, 2),
         "launches": launches,
     }
+    out["limiter"] = (f"not HBM: tables on chip, node loop at {simd:.0%} SIMD efficiency (divergent per-lane "
+                      "traversal; VALU-issue bound, profiles/r01_pmc_diamond.md)" if resident else
+                      f"dependent node-fetch latency: {simd:.0%} SIMD efficiency, L2 hit rate ~44% "
+                      "(profiles/pmc_trace_s_soup_16m.json)")
+    return out
 
 
 def suite_line(ignis_amd, dev_index, path, spi, iters, size=None):
@@ -189,7 +217,7 @@ def main():
     import ignis_amd
 
     scene = ignis_amd.Scene.from_file(args.scene)
-    W, H = scene.film_size
+    W, H = (args.size, args.size) if args.size > 0 else scene.film_size
     spi = args.spi
     iters = max(1, math.ceil(args.spp / spi))
     dev = ignis_amd.Device(gpu)
@@ -209,7 +237,7 @@ def main():
     if n_gpus > 1:
         max_tiles = shard.max_tiles_per_rank(W, H, tile, n_gpus)
         pack = torch.zeros(max_tiles * tile * tile * 3, dtype=torch.float32, device="cuda")
-        gather_bufs = [torch.zeros(pack.numel(), dtype=torch.float32, device=comm) for _ in range(n_gpus)]
+        gather_bufs = [torch.zeros(pack.numel(), dtype=torch.float32, device=comm) for _ in range(n_gpus)] if rank == 0 else None
         frame = torch.zeros((W * H, 3), dtype=torch.float32, device="cuda")
         dst = torch.from_numpy(shard.packed_destinations(W, H, tile, n_gpus)).cuda()
         valid = dst >= 0
@@ -230,12 +258,13 @@ def main():
     count = [0]
 
     def gather(d):
-        # pack owned tiles, RCCL all_gather over xGMI, assemble on every rank
+        # pack owned tiles, RCCL gather over xGMI to rank 0, assemble there
         torch.cuda.current_stream().synchronize()  # the previous gather has read `pack`
         d.pack_tiles(params(0), pack.data_ptr(), pack.numel())  # waits for d's frame
-        dist.all_gather(gather_bufs, pack if comm == "cuda" else pack.cpu())
-        allpix = torch.cat(gather_bufs).to("cuda").view(-1, 3)
-        frame[dst_valid] = allpix[valid]
+        dist.gather(pack if comm == "cuda" else pack.cpu(), gather_bufs, dst=0)
+        if rank == 0:
+            allpix = torch.cat(gather_bufs).to("cuda").view(-1, 3)
+            frame[dst_valid] = allpix[valid]
 
     def render_frame():
         d = devs[count[0] % len(devs)]
@@ -254,7 +283,9 @@ def main():
             gather(pending.pop())
         torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
+    # every device handle renders (and gathers) at least once before timing:
+    # its framebuffer, path slots and events are allocated outside the timed region
+    for _ in range(max(args.warmup, len(devs))):
         render_frame()
     drain_frames()
 
@@ -312,11 +343,10 @@ def main():
 
     # ---- roofline of the dominant kernel, live HIP-event timing ----
     roof = roofline(dev, st, lambda: dev.render(params(0)), n_gpus, os.path.splitext(os.path.basename(args.scene))[0])
-    if dev.stats()["node_bytes"] and os.path.basename(args.scene) == "diamond_scene.json":
-        roof["note"] = ("the diamond's traversal tables (~24 KB) are staged in LDS per block: the algorithmic bytes "
-                        "count node / instance / triangle reads served from LDS, so frac measures work per second "
-                        "against the HBM roof, not HBM utilisation (traffic_gbs is that); the HBM scene of record "
-                        "is S-soup-16M (suite)")
+    roof["note"] = ("achieved counts the HBM bytes the kernel must move (path / radiance / shadow-ray streams; "
+                    "table reads too when the tables exceed the Infinity Cache); traffic is the rocprofv3 PMC "
+                    "measurement of the same kernel and workload; memory_system_gbs counts every table read "
+                    "including LDS / cache hits (a work rate)")
 
     result = None
     if rank == 0:
@@ -339,8 +369,7 @@ def main():
                 line["roofline"]["note"] = (
                     "HBM roofline scene of record: 1.8 GB of BVH + triangles, far above the on-chip caches"
                     if line["scene"] == "s_soup_16m.json" else
-                    "traversal tables fit the 256 MB Infinity Cache (SURVEY.md 8d): algorithmic bytes count "
-                    "cache hits too, so frac is not an HBM utilisation here")
+                    "tables fit the 256 MB Infinity Cache: achieved counts the ray streams only")
         result = {
             "metric": "Mrays/s (primary+secondary) at fixed spp; per-pixel L2 vs CPU ref",
             "value": round(value, 2),
@@ -353,12 +382,12 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic camera paths over the reference's diamond_scene.json (scene data from the reference checkout)",
+            "data": f"synthetic camera paths over {os.path.basename(args.scene)} (scene data from the reference checkout or the SURVEY.md §8d generators)",
             "config": {
-                "workload": f"diamond_scene.json {W}x{H}, {iters * spi} spp = {iters} iterations x spi {spi}, path tracer max_depth 64, seed 0",
+                "workload": f"{os.path.basename(args.scene)} {W}x{H}, {iters * spi} spp = {iters} iterations x spi {spi}, path tracer max_depth {scene.desc.technique.max_depth}, seed 0",
                 "scene": os.path.basename(args.scene),
                 "width": W, "height": H, "spp": iters * spi, "spi": spi,
-                "parallelism": f"tile-shard x{n_gpus} ({tile}x{tile} tiles round-robin) + RCCL all_gather" if n_gpus > 1 else "single GPU",
+                "parallelism": f"tile-shard x{n_gpus} ({tile}x{tile} tiles round-robin) + RCCL gather to rank 0" if n_gpus > 1 else "single GPU",
             },
             "msamples_per_s": round(samples / elapsed / 1e6, 2),
             "rays": {"camera": int(totals[1]), "bounce": int(totals[2]), "shadow": int(totals[3])},
@@ -421,7 +450,10 @@ def cpu_baseline(scene, dev, W, H, spi, target_s):
     g, _ = dev.framebuffer(W * H * 3)
     g = g.reshape(H, W, 3)[y0:y0 + rows]
     o = fb0.reshape(H, W, 3)[y0:y0 + rows]
-    e = (g - o) ** 2 / (o ** 2 + 1e-2)
+    # RunEvaluations' error_image (scripts/RunEvaluations.py:80-87): RelSE where the
+    # oracle pixel is non-zero, AbsSE where it is zero, clamped at the 99th percentile
+    nz = o != 0
+    e = np.where(nz, np.square((g - o) / np.where(nz, o, 1)), np.square(g))
     e = np.minimum(e, np.percentile(e, 99))
     parity = {
         "rows": [y0, y0 + rows],

@@ -980,6 +980,7 @@ struct igx_device {
     int64_t lds_scene_max = 48 * 1024; // stage traversal tables in LDS when they fit (0 = never)
     size_t lds_scene_bytes = 0;        // bytes staged per block for the current scene (0 = global tables)
     size_t table_bytes = 0;            // traversal tables (nodes, instances, triangles) of the current scene
+    size_t shading_bytes = 0;          // shading tables (entities, vertices, normals, faces, materials, lights)
     int leaf_size = 4;
     // SBVH for BLAS up to SPATIAL_SPLIT_MAX_FACES triangles (option "spatial_splits"):
     // off by default -- measured slower on the diamond (196 -> 230 ms per frame)
@@ -1920,6 +1921,8 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
         size_t b = ((size_t)sv.num_nodes * nf4 + (size_t)sv.num_inst * 4 + (size_t)sv.num_tris * 3) * 16;
         dev->lds_scene_bytes = (int64_t)b <= dev->lds_scene_max ? b : 0;
         dev->table_bytes = b;
+        dev->shading_bytes = ent.size() * sizeof(ent[0]) + vtx.size() * sizeof(vtx[0]) + nrm.size() * sizeof(nrm[0]) +
+                             idx.size() * sizeof(idx[0]) + mats.size() * sizeof(DevMaterial) + lights.size() * sizeof(lights[0]);
     }
     sv.num_lights = (int)lights.size();
     sv.num_infinite = num_infinite;
@@ -2237,6 +2240,11 @@ extern "C" igx_status igx_framebuffer_device_ptr(igx_device* dev, float** ptr, s
 extern "C" igx_status igx_pack_tiles(igx_device* dev, const igx_render_params* p, float* dst, size_t count) {
     if (!dev || !p || !dst || p->tile_size <= 0) return IGX_ERR_INVALID_ARGUMENT;
     if (!dev->fb) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "no framebuffer");
+    if (p->width != dev->fb_w || p->height != dev->fb_h || p->tile_stride <= 0 || p->tile_offset < 0)
+        return fail(dev, IGX_ERR_INVALID_ARGUMENT,
+                    "pack_tiles: film " + std::to_string(p->width) + "x" + std::to_string(p->height) +
+                        " does not match the framebuffer " + std::to_string(dev->fb_w) + "x" + std::to_string(dev->fb_h) +
+                        " (or invalid tile offset / stride)");
     FrameArgs fa{};
     fa.width = p->width;
     fa.height = p->height;
@@ -2296,6 +2304,8 @@ extern "C" igx_status igx_get_stats(igx_device* dev, igx_stats* out) {
     out->node_bytes = node_f4(dev->bvh_width) * 16;
     out->lds_scene_bytes = (int32_t)dev->lds_scene_bytes;
     out->shadow_blocks_per_cu = dev->has_scene ? shadow_blocks_per_cu<false>(dev->variant, dev->lds_scene_bytes, use_refill(dev)) : 0;
+    out->table_bytes = dev->table_bytes;
+    out->shading_bytes = dev->shading_bytes;
     return IGX_OK;
 }
 

@@ -32,11 +32,12 @@ def device():
     d.close()
 
 
-def rel_mse(img, ref, eps=1e-2):
-    """Mean of the 99th-percentile-clamped relative squared error (scripts/RunEvaluations.py:80-87)."""
-    e = (img - ref) ** 2 / (ref ** 2 + eps)
-    e = np.minimum(e, np.percentile(e, 99))
-    return float(e.mean())
+def rel_mse(img, ref):
+    """RunEvaluations' error_image (scripts/RunEvaluations.py:80-87, tests/evalref.py):
+    RelSE where ref != 0, AbsSE where ref == 0, mean clamped at the 99th percentile."""
+    import evalref
+
+    return evalref.error_image(np.asarray(img, np.float32), np.asarray(ref, np.float32))[0]
 
 
 def render_gpu(device, scene, w, h, spi, iteration=0, seed=0, tile=None, capacity=0):
@@ -640,3 +641,57 @@ def test_gpu_furnace_mirror_exact(device):
     }
     fb = render_gpu(device, ignis_amd.Scene.from_string(scene), 64, 64, 2)
     np.testing.assert_allclose(fb, 1.0, rtol=0, atol=1e-6)
+
+
+@pytest.mark.parametrize("n_shards", [8, 3])
+def test_config5_tile_shard_gather_equals_single_device(root, n_shards):
+    """BASELINE config 5 stand-in: S-deep at 4096x4096, 64 spp
+    (8 iterations of spi 8), tile-sharded over N shards exactly as bench.py
+    shards it (shard.balanced_tile, round-robin tiles, igx_pack_tiles, gather
+    of equal-size packed buffers, assembly on rank 0): the assembled frame
+    equals the single-device frame bit for bit."""
+    import torch
+    from ignis_amd import shard
+
+    sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", "s_deep.json"))
+    W = H = 4096
+    spi, iters = 8, 8
+    dev = ignis_amd.Device(0)
+    try:
+        dev.upload(sc)
+        p = ignis_amd.RenderParams()
+        p.width, p.height, p.spi = W, H, spi
+        dev.render_iterations(p, iters)
+        full, it = dev.framebuffer(W * H * 3)
+        assert it == iters and np.isfinite(full).all() and full.mean() > 0
+        T = shard.balanced_tile(W, n_shards)
+        per = shard.max_tiles_per_rank(W, H, T, n_shards) * T * T * 3
+        packs = []
+        for r in range(n_shards):
+            dev.clear()
+            q = ignis_amd.RenderParams()
+            q.width, q.height, q.spi = W, H, spi
+            q.tile_size, q.tile_offset, q.tile_stride = T, r, n_shards
+            dev.render_iterations(q, iters)
+            buf = torch.zeros(per, dtype=torch.float32, device="cuda")
+            dev.pack_tiles(q, buf.data_ptr(), buf.numel())
+            packs.append(buf.cpu().numpy())
+        dst = shard.packed_destinations(W, H, T, n_shards)
+        frame = shard.assemble(np.concatenate(packs).reshape(-1, 3), dst, np.zeros((W * H, 3), np.float32))
+        np.testing.assert_array_equal(frame.reshape(-1), full)
+    finally:
+        dev.close()
+
+
+def test_pack_tiles_rejects_a_film_that_is_not_the_framebuffer(device, diamond_path):
+    """igx_pack_tiles reads dev->fb through the tile table: a film larger than
+    the allocated framebuffer must be refused, not read out of bounds."""
+    import torch
+
+    sc = ignis_amd.Scene.from_file(diamond_path)
+    render_gpu(device, sc, 200, 150, 4, tile=(64, 0, 3))
+    buf = torch.zeros(64 * 64 * 3 * 64, dtype=torch.float32, device="cuda")
+    p = ignis_amd.RenderParams()
+    p.width, p.height, p.spi, p.tile_size, p.tile_offset, p.tile_stride = 400, 300, 4, 64, 0, 3
+    with pytest.raises(ignis_amd.IgxError, match="does not match the framebuffer"):
+        device.pack_tiles(p, buf.data_ptr(), buf.numel())

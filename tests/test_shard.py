@@ -68,11 +68,15 @@ def _worker(rank, world, port, w, h, T, q):
     frame = rng.random((w * h, 3), dtype=np.float32)   # same "render" on every rank
     # each rank keeps only its tiles, as the device does under tile sharding
     pack = torch.from_numpy(pack_host(frame, w, h, T, rank, world))
-    bufs = [torch.zeros_like(pack) for _ in range(world)]
-    dist.all_gather(bufs, pack)
-    dst = torch.from_numpy(shard.packed_destinations(w, h, T, world))
-    out = shard.assemble(torch.cat(bufs).view(-1, 3), dst, torch.zeros((w * h, 3)))
-    ok = bool(torch.equal(out, torch.from_numpy(frame)))
+    # gather to rank 0 only, as bench.py does it over RCCL
+    bufs = [torch.zeros_like(pack) for _ in range(world)] if rank == 0 else None
+    dist.gather(pack, bufs, dst=0)
+    if rank == 0:
+        dst = torch.from_numpy(shard.packed_destinations(w, h, T, world))
+        out = shard.assemble(torch.cat(bufs).view(-1, 3), dst, torch.zeros((w * h, 3)))
+        ok = bool(torch.equal(out, torch.from_numpy(frame)))
+    else:
+        ok = True
     # max-over-ranks timing reduction used by bench.py
     t = torch.tensor([float(rank + 1)], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -86,6 +90,7 @@ def test_gloo_world2_gather_assembles_frame():
     q = ctx.Queue()
     port = _free_port()
     w, h, T, world = 200, 150, 64, 2
+    # also exercised with world 3 below
     procs = [ctx.Process(target=_worker, args=(r, world, port, w, h, T, q)) for r in range(world)]
     for p in procs:
         p.start()
@@ -95,3 +100,19 @@ def test_gloo_world2_gather_assembles_frame():
         assert p.exitcode == 0
     assert all(ok for _, ok, _ in res), res
     assert all(t == float(world) for _, _, t in res)
+
+
+def test_gloo_world3_gather_assembles_frame():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    w, h, world = 4096 // 16, 4096 // 16, 3
+    T = shard.balanced_tile(w, world)
+    procs = [ctx.Process(target=_worker, args=(r, world, port, w, h, T, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok, _ in res), res
