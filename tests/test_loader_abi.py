@@ -1,5 +1,6 @@
 """Scene ingestion and the C-ABI surface (CPU only: no GPU calls)."""
 import ctypes as C
+import sys
 import os
 import re
 
@@ -254,3 +255,17 @@ def test_principled_parameters():
     assert b.ior == pytest.approx(1.333) and b.metallic == pytest.approx(0.3) and b.sheen == pytest.approx(0.25)
     assert b.thin == 1 and b.clearcoat_top_only == 0
     assert (c.alpha_u, c.alpha_v, c.ior) == (pytest.approx(0.2), pytest.approx(0.05), pytest.approx(1.33))
+
+
+def test_procedural_geometry_matches_frozen_fixture():
+    """Every procedural shape the scenes use, and the plane / sphere emitter
+    detection on the scene meshes, reproduce tests/golden/procedural_shapes.npz
+    bit for bit (tests/golden/make_shape_fixture.py)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import make_shape_fixture
+
+    ref = np.load(os.path.join(os.path.dirname(__file__), "golden", "procedural_shapes.npz"))
+    got = make_shape_fixture.generate()
+    assert sorted(got) == sorted(ref.files)
+    for k in ref.files:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
