@@ -52,7 +52,9 @@ def parse():
     return ap.parse_args()
 
 
-MALL_BYTES = 256 << 20  # Infinity Cache (MI355X_MICROARCH.md): tables below it stay on-chip between launches
+# Tables up to half the 256 MiB Infinity Cache count as on-chip: a table stays resident only while it and
+# everything streamed between two uses of a line fit the cache (MI355X_MICROARCH.md, Infinity Cache)
+MALL_BYTES = 128 << 20
 
 
 def algorithmic_bytes(inst, st):

@@ -84,10 +84,56 @@ def pmc(fetch_dir, write_dir, kernel="k_extend", scene="diamond_scene"):
     print(json.dumps(res, indent=1))
 
 
+def calibration(fetch_dir, write_dir, trace_dir, log, tag):
+    """FETCH_SIZE / WRITE_SIZE against known byte counts (tools/pmc_calibrate.hip):
+    counter bytes per useful byte for each access pattern of the hot path."""
+    def per_kernel(d, counter):
+        f = find(d, "*counter_collection.csv")
+        out = {}
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == counter:
+                k = short(r["Kernel_Name"])
+                out[k] = out.get(k, 0.0) + float(r["Counter_Value"]) * 1024
+        return out
+    fetch = per_kernel(fetch_dir, "FETCH_SIZE")
+    write = per_kernel(write_dir, "WRITE_SIZE")
+    dur = {short(r["Name"]): float(r["AverageNs"]) for r in csv.DictReader(open(find(trace_dir, "*kernel_stats.csv")))}
+    rows = []
+    for line in open(log):
+        line = line.strip()
+        if not line.startswith("{"):
+            continue
+        d = json.loads(line)
+        k = d["kernel"]
+        key = [n for n in fetch if n.endswith(k.split("<")[0]) and (("<" not in k) or k.split("<")[1].split(">")[0] in n)]
+        key = key[0] if key else k
+        useful = d.get("expected_unique_bytes", d.get("bytes"))
+        rec = {"kernel": k, "useful_bytes": useful, "fetch_size_bytes": fetch.get(key, 0.0),
+               "write_size_bytes": write.get(key, 0.0), "avg_ns": dur.get(key)}
+        if "record_bytes" in d:
+            rec["record_bytes"] = d["record_bytes"]
+            rec["lines_128B_per_record"] = round(rec["fetch_size_bytes"] / 64 / d["lanes"], 3)
+        rec["fetch_over_useful"] = round(rec["fetch_size_bytes"] / useful, 4) if "write" not in k else None
+        rec["write_over_useful"] = round(rec["write_size_bytes"] / useful, 4) if "write" in k else None
+        rows.append(rec)
+    res = {"what": "rocprofv3 FETCH_SIZE / WRITE_SIZE vs known bytes on gfx950 (tools/pmc_calibrate.hip)",
+           "finding": "FETCH_SIZE counts 64 B per 128-B line fetched from the memory side, for streaming and for "
+                      "scattered 16/48/64/128-B records alike: HBM line bytes = 2 x FETCH_SIZE; WRITE_SIZE is exact "
+                      "for streaming stores",
+           "kernels": rows}
+    json.dump(res, open(os.path.join(ROOT, "profiles", f"{tag}_pmc_calibration.json"), "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
 if __name__ == "__main__":
     tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
     out = os.path.join(ROOT, "gpurun_out")
     kernel_stats(os.path.join(out, "prof"), tag)
+    if os.path.isdir(os.path.join(out, "prof_soup")):
+        kernel_stats(os.path.join(out, "prof_soup"), tag + "_s_soup_16m")
+    if os.path.isdir(os.path.join(out, "cal_fetch")):
+        calibration(os.path.join(out, "cal_fetch"), os.path.join(out, "cal_write"), os.path.join(out, "cal_trace"),
+                    os.path.join(out, "cal_fetch.log"), tag)
     pmc(os.path.join(out, "pmc_fetch"), os.path.join(out, "pmc_write"))
     if os.path.isdir(os.path.join(out, "pmc_fetch_soup")):
         # global-table scenes run split: k_trace (persistent-lane k_trace_refill) is the dominant kernel
