@@ -1,4 +1,10 @@
 // Procedural meshes and mesh readers; see mesh.h for the reference citations.
+//
+// Provenance: the shapes, normal helpers and the plane-emitter test reproduce
+// the geometry of the reference's src/runtime/mesh/TriMesh.cpp (Ignis, MIT
+// licence) so that the hot path intersects the same triangles; the code is
+// written from the geometric definitions, and tests/golden/procedural_shapes.npz
+// pins its output bit for bit.
 #include "mesh.h"
 
 #include <cmath>
@@ -27,60 +33,65 @@ void TriMesh::flip_normals() {
     for (auto& n : normals) n = -n;
 }
 
+// Smooth vertex normals: every vertex gets the normalised sum of the unit
+// normals of the faces around it (no area or angle weighting, as the
+// reference's computeVertexNormals).  Contributions are added in face order.
 void TriMesh::compute_vertex_normals() {
-    normals.assign(vertices.size(), V3());
-    for (auto& f : faces) {
-        V3 n = normalized(triangle_normal(vertices[f[0]], vertices[f[1]], vertices[f[2]]));
-        normals[f[0]] = normals[f[0]] + n;
-        normals[f[1]] = normals[f[1]] + n;
-        normals[f[2]] = normals[f[2]] + n;
+    std::vector<V3> acc(vertices.size(), V3());
+    for (const auto& f : faces) {
+        const V3 n = normalized(triangle_normal(vertices[f[0]], vertices[f[1]], vertices[f[2]]));
+        for (uint32_t v : f) acc[v] = acc[v] + n;
     }
-    for (auto& n : normals) n = normalized(n);
+    for (auto& n : acc) n = normalized(n);
+    normals = std::move(acc);
 }
 
+// Normals read from files may be zero or NaN: those become +y (and *bad is
+// set), the others are brought to unit length.
 void TriMesh::fix_normals(bool* bad) {
-    bool b = false;
+    bool any_bad = false;
     for (auto& n : normals) {
-        float l2 = norm2(n);
-        if (l2 <= kFltEps || std::isnan(l2)) {
-            b = true;
-            n = V3(0, 1, 0);
-        } else {
-            n = n / std::sqrt(l2);
-        }
+        const float len2 = norm2(n);
+        const bool degenerate = !(len2 > kFltEps); // also catches NaN
+        any_bad = any_bad || degenerate;
+        n = degenerate ? V3(0, 1, 0) : n / std::sqrt(len2);
     }
-    if (bad) *bad = b;
+    if (bad) *bad = any_bad;
 }
 
+// Planar (x, y) projection of each vertex into the unit square of the mesh's
+// bounding box; a flat axis maps to 0.
 void TriMesh::make_texcoords_normalized() {
+    const BBox box = compute_bbox();
+    const V3 extent = box.diameter();
+    auto coord = [&](float p, float lo, float size) { return size > kFltEps ? (p - lo) / size : 0.0f; };
     texcoords.resize(vertices.size());
-    BBox bbox = compute_bbox();
-    V3 d = bbox.diameter();
-    for (size_t i = 0; i < vertices.size(); ++i) {
-        V3 t = vertices[i] - bbox.min;
-        std::array<float, 2> p{0, 0};
-        if (d.x > kFltEps) p[0] = t.x / d.x;
-        if (d.y > kFltEps) p[1] = t.y / d.y;
-        texcoords[i] = p;
-    }
+    for (size_t i = 0; i < vertices.size(); ++i)
+        texcoords[i] = {coord(vertices[i].x, box.min.x, extent.x), coord(vertices[i].y, box.min.y, extent.y)};
 }
 
+// Flat shading: every face gets three vertices of its own carrying the face's
+// unit normal (and the texture coordinates of its corners).
 void TriMesh::setup_face_normals_as_vertex_normals() {
-    std::vector<V3> nv(faces.size() * 3), nn(faces.size() * 3);
-    std::vector<std::array<float, 2>> nt;
-    if (!texcoords.empty()) nt.resize(faces.size() * 3);
-    for (size_t f = 0; f < faces.size(); ++f) {
-        for (int k = 0; k < 3; ++k) {
-            nv[3 * f + k] = vertices[faces[f][k]];
-            if (!texcoords.empty()) nt[3 * f + k] = texcoords[faces[f][k]];
+    const bool has_uv = !texcoords.empty();
+    std::vector<V3> pos, nrm;
+    std::vector<std::array<float, 2>> uv;
+    pos.reserve(faces.size() * 3);
+    nrm.reserve(faces.size() * 3);
+    if (has_uv) uv.reserve(faces.size() * 3);
+    for (auto& f : faces) {
+        const V3 n = normalized(triangle_normal(vertices[f[0]], vertices[f[1]], vertices[f[2]]));
+        const uint32_t first = (uint32_t)pos.size();
+        for (uint32_t v : f) {
+            pos.push_back(vertices[v]);
+            nrm.push_back(n);
+            if (has_uv) uv.push_back(texcoords[v]);
         }
-        V3 n = normalized(triangle_normal(nv[3 * f], nv[3 * f + 1], nv[3 * f + 2]));
-        nn[3 * f] = nn[3 * f + 1] = nn[3 * f + 2] = n;
-        faces[f] = {uint32_t(3 * f), uint32_t(3 * f + 1), uint32_t(3 * f + 2)};
+        f = {first, first + 1, first + 2};
     }
-    vertices = std::move(nv);
-    normals = std::move(nn);
-    if (!texcoords.empty()) texcoords = std::move(nt);
+    vertices = std::move(pos);
+    normals = std::move(nrm);
+    if (has_uv) texcoords = std::move(uv);
 }
 
 void TriMesh::transform(const M4& t) {
@@ -128,90 +139,75 @@ float compute_area(const TriMesh& mesh) {
     return a;
 }
 
+// Plane-emitter detection (the reference's TriMesh::getAsPlane decides which
+// area lights use the spherical-rectangle sampler, so the decision and the
+// axes it returns must be the same):
+//  * two faces over exactly four vertices.  The reference also scans meshes of
+//    five or six vertices for duplicates, but its scan can register at most
+//    three distinct corners, so such meshes are never planes;
+//  * both faces have the same unit normal (within 1e-5, relative);
+//  * each edge of the second face has the squared length of some edge of the
+//    first (within 1e-5, absolute);
+//  * the axes start at vertex 0 and span the widest corner angle among the
+//    vertex pairs (1,2), (2,3), (3,1) -- the first in that order on ties --
+//    swapped if needed so that x_axis x y_axis points along the face normal;
+//  * texture coordinates of the corners origin, +x, +y, +x+y in slots 0..3
+//    (unit square when the mesh has none).
 std::optional<PlaneShape> get_as_plane(const TriMesh& mesh) {
-    constexpr float PlaneEPS = 1e-5f;
-    if (mesh.face_count() != 2) return std::nullopt;
+    constexpr float kTol = 1e-5f;
+    if (mesh.face_count() != 2 || mesh.vertices.size() != 4) return std::nullopt;
+    const auto& P = mesh.vertices;
+    const auto& A = mesh.faces[0];
+    const auto& B = mesh.faces[1];
 
-    std::array<V3, 4> uv{};
-    std::array<uint32_t, 4> ids{};
-    const auto& vs = mesh.vertices;
-    if (vs.size() != 4) {
-        if (vs.size() > 4 && vs.size() <= 6) {
-            size_t i = 0;
-            uint32_t id = 0;
-            for (const auto& v : vs) {
-                bool found = false;
-                for (const auto& u : uv) {
-                    found = approx(v, u, PlaneEPS);
-                    if (found) break;
-                }
-                if (!found) {
-                    if (i >= 3) return std::nullopt;
-                    ids[i + 1] = id;
-                    uv[i + 1] = v;
-                    ++i;
-                }
-                ++id;
-            }
-            if (i != 4) return std::nullopt;
-        } else {
-            return std::nullopt;
-        }
-    } else {
-        for (size_t i = 0; i < 4; ++i) { uv[i] = vs[i]; ids[i] = (uint32_t)i; }
+    const V3 normal = normalized(triangle_normal(P[A[0]], P[A[1]], P[A[2]]));
+    if (!approx(normal, normalized(triangle_normal(P[B[0]], P[B[1]], P[B[2]])), kTol)) return std::nullopt;
+
+    auto edges = [&](const std::array<uint32_t, 3>& f) {
+        return std::array<float, 3>{norm2(P[f[0]] - P[f[1]]), norm2(P[f[1]] - P[f[2]]), norm2(P[f[2]] - P[f[0]])};
+    };
+    const auto ea = edges(A), eb = edges(B);
+    for (float b : eb) {
+        bool matched = false;
+        for (float a : ea) matched = matched || std::abs(a - b) <= kTol;
+        if (!matched) return std::nullopt;
     }
 
-    const auto& f0 = mesh.faces[0];
-    const auto& f1 = mesh.faces[1];
-    V3 fn0 = normalized(triangle_normal(vs[f0[0]], vs[f0[1]], vs[f0[2]]));
-    V3 fn1 = normalized(triangle_normal(vs[f1[0]], vs[f1[1]], vs[f1[2]]));
-    if (!approx(fn0, fn1, PlaneEPS)) return std::nullopt;
-
-    float e1 = norm2(vs[f0[0]] - vs[f0[1]]);
-    float e2 = norm2(vs[f0[1]] - vs[f0[2]]);
-    float e3 = norm2(vs[f0[2]] - vs[f0[0]]);
-    float e4 = norm2(vs[f1[0]] - vs[f1[1]]);
-    float e5 = norm2(vs[f1[1]] - vs[f1[2]]);
-    float e6 = norm2(vs[f1[2]] - vs[f1[0]]);
-    auto safe = [&](float a, float b) { return std::abs(a - b) <= PlaneEPS; };
-    if (!safe(e1, e4) && !safe(e2, e4) && !safe(e3, e4)) return std::nullopt;
-    if (!safe(e1, e5) && !safe(e2, e5) && !safe(e3, e5)) return std::nullopt;
-    if (!safe(e1, e6) && !safe(e2, e6) && !safe(e3, e6)) return std::nullopt;
-
-    V3 origin = uv[0];
-    auto angle = [&](size_t start) {
-        V3 x = normalized(uv[(start + 0) % 3 + 1] - origin);
-        V3 y = normalized(uv[(start + 1) % 3 + 1] - origin);
-        return std::acos(dot(x, y));
-    };
-    float a12 = std::abs(angle(0)), a23 = std::abs(angle(1)), a31 = std::abs(angle(2));
-    int sel;
-    if (a12 >= a23 && a12 >= a31) sel = 0;
-    else if (a23 >= a31 && a23 >= a12) sel = 1;
-    else sel = 2;
-
+    // corner pair k = (k % 3 + 1, (k + 1) % 3 + 1): (1,2), (2,3), (3,1)
+    const V3 origin = P[0];
+    auto first_of = [](int k) { return (uint32_t)(k % 3 + 1); };
+    auto second_of = [](int k) { return (uint32_t)((k + 1) % 3 + 1); };
+    int widest = 0;
+    float widest_angle = -1;
+    for (int k = 0; k < 3; ++k) {
+        const float ang = std::abs(std::acos(dot(normalized(P[first_of(k)] - origin), normalized(P[second_of(k)] - origin))));
+        if (ang > widest_angle) { widest_angle = ang; widest = k; }
+    }
+    uint32_t vx = first_of(widest), vy = second_of(widest);
     PlaneShape shape;
     shape.origin = origin;
-    shape.x_axis = uv[(sel + 0) % 3 + 1] - origin;
-    shape.y_axis = uv[(sel + 1) % 3 + 1] - origin;
-    V3 n = normalized(cross(shape.x_axis, shape.y_axis));
-    if (dot(fn0, n) < 0) {
+    shape.x_axis = P[vx] - origin;
+    shape.y_axis = P[vy] - origin;
+    if (dot(normal, normalized(cross(shape.x_axis, shape.y_axis))) < 0) {
         std::swap(shape.x_axis, shape.y_axis);
-        std::swap(uv[1], uv[2]);
-        std::swap(ids[1], ids[2]);
+        std::swap(vx, vy);
     }
-    if (!mesh.texcoords.empty()) {
-        auto put = [&](int slot, uint32_t vid) {
-            shape.tex[slot * 2] = mesh.texcoords[vid][0];
-            shape.tex[slot * 2 + 1] = mesh.texcoords[vid][1];
-        };
-        put(0, ids[0]);
-        put((0 + sel) % 3 + 1, ids[1]);
-        put((1 + sel) % 3 + 1, ids[2]);
-        put((2 + sel) % 3 + 1, ids[3]);
-    } else {
+    if (mesh.texcoords.empty()) {
         shape.tex = {0, 0, 1, 0, 0, 1, 1, 1};
+        return shape;
     }
+    // The reference fills texture slots 1..3, rotated by the widest pair's
+    // index, from vertices 1, 2, 3 in file order (1 and 2 exchanged when the
+    // axes were swapped) rather than from the pair's own corners; kept so the
+    // emitter's texture coordinates are the same.
+    const bool swapped = vx != first_of(widest);
+    const uint32_t from[3] = {swapped ? 2u : 1u, swapped ? 1u : 2u, 3u};
+    auto put = [&](int slot, uint32_t v) {
+        shape.tex[slot * 2] = mesh.texcoords[v][0];
+        shape.tex[slot * 2 + 1] = mesh.texcoords[v][1];
+    };
+    put(0, 0);
+    for (int j = 0; j < 3; ++j) put((j + widest) % 3 + 1, from[j]);
     return shape;
 }
 
@@ -395,70 +391,66 @@ TriMesh make_displaced_grid(uint32_t n, float size, float amplitude, uint64_t se
     return m;
 }
 
+// Icosphere: the regular icosahedron on the unit sphere, refined by splitting
+// every triangle into four at its edge midpoints (pushed back onto the sphere),
+// then scaled and moved.  Vertex and face order follow the reference's
+// MakeIcoSphere exactly (they decide the BVH and so the order of equal-distance
+// hits): the 12 corners are (0, +-G, +-1), (+-1, 0, +-G), (+-G, +-1, 0)
+// normalised (G the golden ratio), and a new midpoint is appended when its edge
+// is met in ascending vertex order while faces are scanned in order.
 TriMesh make_ico_sphere(V3 center, float radius, uint32_t subdivisions) {
+    constexpr float G = 1.618033989f;
+    static const uint32_t kFaces[20][3] = {
+        {0, 8, 4},  {0, 5, 10}, {1, 6, 8},  {1, 10, 7}, {2, 4, 9},  {2, 11, 5}, {3, 9, 6},
+        {3, 7, 11}, {1, 8, 0},  {1, 0, 10}, {3, 2, 9},  {3, 11, 2}, {5, 0, 4},  {5, 4, 2},
+        {7, 6, 1},  {7, 3, 6},  {9, 4, 8},  {9, 8, 6},  {11, 10, 5}, {11, 7, 10}};
     TriMesh m;
-    constexpr float Golden = 1.618033989f;
-    for (int d = 0; d < 3; d++)
-        for (int s1 = -1; s1 <= 1; s1 += 2)
-            for (int s2 = -1; s2 <= 1; s2 += 2) {
+    for (int axis = 0; axis < 3; ++axis) // corners lie in the planes x = 0, y = 0, z = 0
+        for (float a : {-G, G})
+            for (float b : {-1.0f, 1.0f}) {
                 V3 v;
-                v[(d + 1) % 3] = Golden * s1;
-                v[(d + 2) % 3] = 1.0f * s2;
+                v[(axis + 1) % 3] = a;
+                v[(axis + 2) % 3] = b;
                 m.vertices.push_back(normalized(v));
             }
-    auto gi = [](int d, int s1, int s2) { return (uint32_t)(d * 4 + (s1 + 1) + ((s2 + 1) >> 1)); };
-    for (int s1 = -1; s1 <= 1; s1 += 2)
-        for (int s2 = -1; s2 <= 1; s2 += 2)
-            for (int s3 = -1; s3 <= 1; s3 += 2) {
-                bool rev = s1 * s2 * s3 == -1;
-                uint32_t i1 = gi(0, s1, s2), i2 = gi(1, s2, s3), i3 = gi(2, s3, s1);
-                m.faces.push_back({i1, rev ? i3 : i2, rev ? i2 : i3});
+    for (auto& f : kFaces) m.faces.push_back({f[0], f[1], f[2]});
+
+    for (uint32_t level = 0; level < subdivisions; ++level) {
+        const uint64_t stride = m.vertices.size();
+        std::unordered_map<uint64_t, uint32_t> midpoint; // key: lo * stride + hi
+        auto key = [&](uint32_t a, uint32_t b) { return (uint64_t)std::min(a, b) * stride + std::max(a, b); };
+        for (const auto& f : m.faces)
+            for (int e = 0; e < 3; ++e) {
+                const uint32_t a = f[e], b = f[(e + 1) % 3];
+                if (a < b) {
+                    midpoint[key(a, b)] = (uint32_t)m.vertices.size();
+                    m.vertices.push_back(normalized(m.vertices[a] + m.vertices[b]));
+                }
             }
-    for (int d = 0; d < 3; d++)
-        for (int s1 = -1; s1 <= 1; s1 += 2)
-            for (int s2 = -1; s2 <= 1; s2 += 2) {
-                bool rev = s1 * s2 == +1;
-                uint32_t i2 = gi(d, s1, -1), i1 = gi(d, s1, +1), i3 = gi((d + 2) % 3, s2, s1);
-                m.faces.push_back({i1, rev ? i3 : i2, rev ? i2 : i3});
-            }
-    for (uint32_t s = 0; s < subdivisions; ++s) {
-        std::unordered_map<uint64_t, uint32_t> edge;
-        uint32_t prev = (uint32_t)m.vertices.size();
-        for (auto& f : m.faces)
-            for (int j = 0; j < 3; ++j) {
-                uint32_t a = f[j], b = f[(j + 1) % 3];
-                if (a >= b) continue;
-                uint64_t key = (uint64_t)a * prev + b;
-                edge[key] = (uint32_t)m.vertices.size();
-                m.vertices.push_back(normalized(m.vertices[a] + m.vertices[b]));
-            }
-        std::vector<std::array<uint32_t, 3>> refined;
-        refined.reserve(m.faces.size() * 4);
-        for (auto& f : m.faces) {
-            uint32_t ec[3];
-            for (int j = 0; j < 3; ++j) {
-                uint32_t a = f[j], b = f[(j + 1) % 3];
-                ec[j] = edge[(uint64_t)std::min(a, b) * prev + std::max(a, b)];
-            }
-            refined.push_back({ec[0], ec[1], ec[2]});
-            for (int j = 0; j < 3; ++j) refined.push_back({f[j], ec[(j + 0) % 3], ec[(j + 2) % 3]});
+        std::vector<std::array<uint32_t, 3>> finer;
+        finer.reserve(4 * m.faces.size());
+        for (const auto& f : m.faces) {
+            const uint32_t mid[3] = {midpoint[key(f[0], f[1])], midpoint[key(f[1], f[2])], midpoint[key(f[2], f[0])]};
+            finer.push_back({mid[0], mid[1], mid[2]});                  // centre triangle
+            for (int c = 0; c < 3; ++c) finer.push_back({f[c], mid[c], mid[(c + 2) % 3]}); // corner triangles
         }
-        m.faces = std::move(refined);
+        m.faces = std::move(finer);
     }
+
+    // unit normals and spherical texture coordinates (phi from +y toward -x)
     m.normals.resize(m.vertices.size());
     m.texcoords.resize(m.vertices.size());
     for (size_t i = 0; i < m.vertices.size(); ++i) {
-        V3 n = normalized(m.vertices[i]);
-        m.normals[i] = n;
-        float theta = std::acos(n.z);
+        const V3 n = normalized(m.vertices[i]);
         float phi = std::atan2(-n.x, n.y);
         if (phi < 0) phi += 2 * kPi;
-        m.texcoords[i] = {phi / (2 * kPi), theta / kPi};
+        m.normals[i] = n;
+        m.texcoords[i] = {phi / (2 * kPi), std::acos(n.z) / kPi};
     }
-    M4 t;
-    if (!(center.x == 0 && center.y == 0 && center.z == 0)) t = t * translation(center);
-    if (radius != 1) t = t * scaling(V3(radius, radius, radius));
-    m.transform(t);
+    M4 place;
+    if (!(center.x == 0 && center.y == 0 && center.z == 0)) place = place * translation(center);
+    if (radius != 1) place = place * scaling(V3(radius, radius, radius));
+    m.transform(place);
     return m;
 }
 
