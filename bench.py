@@ -412,37 +412,68 @@ def main():
     return result
 
 
+def cpu_threads():
+    """Threads of the CPU baseline: the reference CPU device uses
+    hardware_concurrency (Device.cpp:347).  Here that is the CPUs this process
+    may run on (affinity / cgroup cpuset), capped by OMP_NUM_THREADS, which the
+    GPU boxes set to the job's CPU share (the machine has many more)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(scene, dev, W, H, spi, target_s):
-    """Oracle (C restatement of the reference CPU device) on a bounded band of the
-    same frame, timed on this host; also the per-pixel parity of the GPU band."""
+    """Oracle (C restatement of the reference CPU device: binned-SAH BVH4 over
+    Tri4 leaves, per-path integration in 16x16 tiles) timed on this host with
+    scripts/benchmark.sh's protocol (lines 13-14, 58-91): 2 warm-up runs, then
+    10 timed runs, min / median / max.  One run renders one iteration (spi
+    samples) of a band of rows of the same frame, the band sized so that the
+    12 runs take about target_s; value = the median run.  Also the per-pixel
+    parity of the GPU band (iteration 0)."""
     from oracle import oracle_py as O
-    threads = min(16, os.cpu_count() or 1)
+    threads = cpu_threads()
     orc = O.OracleScene(scene)
-    # calibrate on 8 rows, then size the band (and, once the band is the whole
-    # frame, the number of iterations) for about target_s seconds of CPU work
+    # calibrate on 8 rows, then size the band for ~target_s / 12 per run
     y0 = H // 2
     _, st = orc.render(W, H, spi, iteration=0, threads=threads, window=(0, y0, W, y0 + 8))
-    rows = int(max(8, min(H, 8 * target_s / max(st["seconds"], 1e-3))))
+    rows = int(max(8, min(H, 8 * (target_s / 12) / max(st["seconds"], 1e-4))))
     y0 = max(0, H // 2 - rows // 2)
-    fb, st = orc.render(W, H, spi, iteration=0, threads=threads, window=(0, y0, W, y0 + rows))
-    fb0 = fb.copy()  # iteration 0 alone, for the parity check below
-    seconds, rays = st["seconds"], st["camera_rays"] + st["bounce_rays"] + st["shadow_rays"]
-    per_iter = [rays / st["seconds"] / 1e6]  # Mrays/s of every timed iteration (min/med/max, scripts/benchmark.sh)
-    iters = 1
-    while seconds < 0.8 * target_s and iters < 256:
-        fb, st = orc.render(W, H, spi, iteration=iters, threads=threads, window=(0, y0, W, y0 + rows), fb=fb)
-        r = st["camera_rays"] + st["bounce_rays"] + st["shadow_rays"]
-        per_iter.append(r / st["seconds"] / 1e6)
-        seconds += st["seconds"]
-        rays += r
-        iters += 1
+    win = (0, y0, W, y0 + rows)
+    fb0 = None
+    runs = []
+    for it in range(12):
+        fb, st = orc.render(W, H, spi, iteration=it, threads=threads, window=win)
+        if it == 0:
+            fb0 = fb.copy()  # iteration 0, for the parity check below
+        if it >= 2:  # 2 warm-up runs
+            runs.append(((st["camera_rays"] + st["bounce_rays"] + st["shadow_rays"]) / st["seconds"] / 1e6, st["seconds"]))
+    rates = sorted(r for r, _ in runs)
+    med = float(np.median(rates))
     cpu = {
-        "value": round(rays / seconds / 1e6, 3),
+        "value": round(med, 3),
         "unit": "Mrays/s",
         "cores": threads,
         "kind": "port",
-        "min_med_max": [round(min(per_iter), 3), round(float(np.median(per_iter)), 3), round(max(per_iter), 3)],
-        "sample": f"oracle/oracle.c (restated reference CPU device), {threads} threads, rows {y0}-{y0 + rows} of the {W}x{H} diamond frame, {iters} iteration(s) x spi {spi} = {iters * spi} spp, {rays / 1e6:.0f} Mrays in {seconds:.1f} s",
+        "min_med_max": [round(rates[0], 3), round(med, 3), round(rates[-1], 3)],
+        "cpu_model": cpu_model(),
+        "machine_logical_cpus": os.cpu_count(),
+        "sample": f"oracle/oracle.c (restated reference CPU device, SAH BVH4 + Tri4 leaves), {threads} threads "
+                  f"(the job's CPU share of a {os.cpu_count()}-CPU {cpu_model()} host), rows {y0}-{y0 + rows} of the "
+                  f"{W}x{H} frame, 2 warm-up + 10 timed runs of one iteration (spi {spi}) each, "
+                  f"{sum(t for _, t in runs):.1f} s timed",
     }
     # parity: GPU iteration 0 of the same frame vs the oracle band
     dev.clear()

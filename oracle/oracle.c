@@ -132,8 +132,16 @@ typedef struct {
 } ochild;
 typedef struct { ochild c[2]; } onode;
 
+/* 4-wide node of the CPU traversal (the reference CPU device's Node4,
+ * traversal/mapping_cpu.art:3-13: four child boxes SoA, child refs) */
 typedef struct {
-    onode* nodes;
+    float lo[3][4], hi[3][4];
+    int32_t ref[4]; /* >= 0 inner node, < 0 leaf: ~(first << 4 | (count-1)) */
+    int32_t n;      /* valid children */
+} onode4;
+
+typedef struct {
+    onode4* nodes;
     int num_nodes;
     int32_t* order; /* leaf slot -> primitive */
 } obvh;
@@ -170,7 +178,14 @@ struct oracle_scene {
     float scene_radius;
 };
 
-/* ---- simple object-median BVH2 builder (independent of the product's SAH builder) */
+/* ---- binned-SAH BVH2, collapsed to 4-wide nodes --------------------------
+ * The reference CPU device traverses BVH4 trees with Tri4 leaves built by
+ * madmann91/bvh's SAH builders (TriMeshProvider.cpp:551-559, TriBVHAdapter.h,
+ * BvhNAdapter.h).  This is an independent, simple equivalent: 16-bin SAH over
+ * the three axes (leaf when no split beats the leaf cost), then each 4-wide
+ * node absorbs the largest-area inner children of its binary subtree.
+ * Closest hits do not depend on the tree (the equal-distance rule below is
+ * order-independent), so the tree only sets the speed of the CPU baseline. */
 typedef struct {
     const float* bmin;
     const float* bmax;
@@ -178,61 +193,143 @@ typedef struct {
     onode* nodes;
     int num_nodes, cap;
     int max_leaf;
-    int axis;
 } obuild;
 
-static obuild* g_sort_ctx; /* qsort context (builders run single-threaded) */
-static int cmp_centroid(const void* a, const void* b) {
-    int32_t ia = *(const int32_t*)a, ib = *(const int32_t*)b;
-    int ax = g_sort_ctx->axis;
-    float ca = g_sort_ctx->bmin[3 * ia + ax] + g_sort_ctx->bmax[3 * ia + ax];
-    float cb = g_sort_ctx->bmin[3 * ib + ax] + g_sort_ctx->bmax[3 * ib + ax];
-    if (ca < cb) return -1;
-    if (ca > cb) return 1;
-    return ia < ib ? -1 : (ia > ib);
+#define SAH_BINS 16
+static float box_half_area(const float* lo, const float* hi) {
+    float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+    if (dx < 0 || dy < 0 || dz < 0) return 0;
+    return dx * dy + dy * dz + dz * dx;
+}
+static void box_empty(float* lo, float* hi) {
+    for (int k = 0; k < 3; ++k) { lo[k] = FLT_MAX_; hi[k] = -FLT_MAX_; }
+}
+static void box_grow(float* lo, float* hi, const float* plo, const float* phi) {
+    for (int k = 0; k < 3; ++k) {
+        if (plo[k] < lo[k]) lo[k] = plo[k];
+        if (phi[k] > hi[k]) hi[k] = phi[k];
+    }
 }
 static void range_box(obuild* b, int first, int count, float* lo, float* hi) {
-    for (int k = 0; k < 3; ++k) { lo[k] = FLT_MAX_; hi[k] = -FLT_MAX_; }
-    for (int i = first; i < first + count; ++i) {
-        int p = b->idx[i];
-        for (int k = 0; k < 3; ++k) {
-            if (b->bmin[3 * p + k] < lo[k]) lo[k] = b->bmin[3 * p + k];
-            if (b->bmax[3 * p + k] > hi[k]) hi[k] = b->bmax[3 * p + k];
-        }
-    }
+    box_empty(lo, hi);
+    for (int i = first; i < first + count; ++i) box_grow(lo, hi, b->bmin + 3 * b->idx[i], b->bmax + 3 * b->idx[i]);
 }
-/* returns child ref for range */
-static int32_t build_range(obuild* b, int first, int count) {
-    if (count <= b->max_leaf) return ~((first << 4) | (count - 1));
-    float lo[3], hi[3];
-    for (int k = 0; k < 3; ++k) { lo[k] = FLT_MAX_; hi[k] = -FLT_MAX_; }
-    for (int i = first; i < first + count; ++i) {
-        int p = b->idx[i];
-        for (int k = 0; k < 3; ++k) {
-            float c = 0.5f * (b->bmin[3 * p + k] + b->bmax[3 * p + k]);
-            if (c < lo[k]) lo[k] = c;
-            if (c > hi[k]) hi[k] = c;
-        }
-    }
-    int axis = 0;
-    if (hi[1] - lo[1] > hi[axis] - lo[axis]) axis = 1;
-    if (hi[2] - lo[2] > hi[axis] - lo[axis]) axis = 2;
-    b->axis = axis;
-    g_sort_ctx = b;
-    qsort(b->idx + first, (size_t)count, sizeof(int32_t), cmp_centroid);
-    int mid = count / 2;
+static int32_t new_node(obuild* b) {
     if (b->num_nodes == b->cap) {
         b->cap = b->cap * 2 + 16;
         b->nodes = (onode*)realloc(b->nodes, sizeof(onode) * (size_t)b->cap);
     }
-    int me = b->num_nodes++;
+    return b->num_nodes++;
+}
+/* returns the child ref of the range [first, first + count) */
+static int32_t build_range(obuild* b, int first, int count) {
+    float clo[3], chi[3];
+    box_empty(clo, chi);
+    for (int i = first; i < first + count; ++i) {
+        int p = b->idx[i];
+        float c[3];
+        for (int k = 0; k < 3; ++k) c[k] = 0.5f * (b->bmin[3 * p + k] + b->bmax[3 * p + k]);
+        box_grow(clo, chi, c, c);
+    }
+    float plo[3], phi[3];
+    range_box(b, first, count, plo, phi);
+    const float leaf_cost = (float)count * box_half_area(plo, phi); /* intersection cost 1, traversal 1 */
+    float best_cost = FLT_MAX_;
+    int best_axis = -1, best_bin = 0;
+    for (int ax = 0; ax < 3; ++ax) {
+        float ext = chi[ax] - clo[ax];
+        if (!(ext > 0)) continue;
+        int cnt[SAH_BINS] = {0};
+        float blo[SAH_BINS][3], bhi[SAH_BINS][3];
+        for (int i = 0; i < SAH_BINS; ++i) box_empty(blo[i], bhi[i]);
+        for (int i = first; i < first + count; ++i) {
+            int p = b->idx[i];
+            float c = 0.5f * (b->bmin[3 * p + ax] + b->bmax[3 * p + ax]);
+            int bin = (int)((c - clo[ax]) / ext * SAH_BINS);
+            bin = bin < 0 ? 0 : (bin >= SAH_BINS ? SAH_BINS - 1 : bin);
+            cnt[bin]++;
+            box_grow(blo[bin], bhi[bin], b->bmin + 3 * p, b->bmax + 3 * p);
+        }
+        float rarea[SAH_BINS];
+        int rcnt[SAH_BINS];
+        float lo[3], hi[3];
+        box_empty(lo, hi);
+        int n = 0;
+        for (int i = SAH_BINS - 1; i > 0; --i) {
+            box_grow(lo, hi, blo[i], bhi[i]);
+            n += cnt[i];
+            rarea[i] = box_half_area(lo, hi);
+            rcnt[i] = n;
+        }
+        box_empty(lo, hi);
+        n = 0;
+        for (int i = 0; i < SAH_BINS - 1; ++i) {
+            box_grow(lo, hi, blo[i], bhi[i]);
+            n += cnt[i];
+            if (n == 0 || rcnt[i + 1] == 0) continue;
+            float cost = box_half_area(plo, phi) + (float)n * box_half_area(lo, hi) + (float)rcnt[i + 1] * rarea[i + 1];
+            if (cost < best_cost) { best_cost = cost; best_axis = ax; best_bin = i; }
+        }
+    }
+    if (count <= b->max_leaf && (best_axis < 0 || leaf_cost <= best_cost)) return ~((first << 4) | (count - 1));
+    int mid;
+    if (best_axis >= 0) {
+        float ext = chi[best_axis] - clo[best_axis];
+        int i = first, j = first + count - 1;
+        while (i <= j) { /* partition by bin */
+            int p = b->idx[i];
+            float c = 0.5f * (b->bmin[3 * p + best_axis] + b->bmax[3 * p + best_axis]);
+            int bin = (int)((c - clo[best_axis]) / ext * SAH_BINS);
+            bin = bin < 0 ? 0 : (bin >= SAH_BINS ? SAH_BINS - 1 : bin);
+            if (bin <= best_bin) ++i;
+            else { int t = b->idx[i]; b->idx[i] = b->idx[j]; b->idx[j] = t; --j; }
+        }
+        mid = i - first;
+    } else {
+        mid = count / 2; /* all centroids equal: halve */
+    }
+    int32_t me = new_node(b);
     int32_t l = build_range(b, first, mid);
     int32_t r = build_range(b, first + mid, count - mid);
-    onode* n = &b->nodes[me];
-    range_box(b, first, mid, n->c[0].lo, n->c[0].hi);
-    range_box(b, first + mid, count - mid, n->c[1].lo, n->c[1].hi);
-    n->c[0].ref = l;
-    n->c[1].ref = r;
+    onode* nd = &b->nodes[me];
+    range_box(b, first, mid, nd->c[0].lo, nd->c[0].hi);
+    range_box(b, first + mid, count - mid, nd->c[1].lo, nd->c[1].hi);
+    nd->c[0].ref = l;
+    nd->c[1].ref = r;
+    return me;
+}
+/* collapse the binary subtree under node2 `i` into 4-wide nodes; returns the new node index */
+static int32_t collapse(const obuild* b, int32_t i, onode4** out, int* n_out, int* cap) {
+    ochild kids[4];
+    int nk = 2;
+    kids[0] = b->nodes[i].c[0];
+    kids[1] = b->nodes[i].c[1];
+    while (nk < 4) {
+        int pick = -1;
+        float area = -1;
+        for (int k = 0; k < nk; ++k)
+            if (kids[k].ref >= 0 && box_half_area(kids[k].lo, kids[k].hi) > area) {
+                area = box_half_area(kids[k].lo, kids[k].hi);
+                pick = k;
+            }
+        if (pick < 0) break;
+        const onode* g = &b->nodes[kids[pick].ref];
+        kids[pick] = g->c[0];
+        kids[nk++] = g->c[1];
+    }
+    if (*n_out == *cap) {
+        *cap = *cap * 2 + 16;
+        *out = (onode4*)realloc(*out, sizeof(onode4) * (size_t)*cap);
+    }
+    int32_t me = (*n_out)++;
+    onode4 nd;
+    memset(&nd, 0, sizeof(nd));
+    nd.n = nk;
+    for (int k = 0; k < nk; ++k) {
+        for (int a = 0; a < 3; ++a) { nd.lo[a][k] = kids[k].lo[a]; nd.hi[a][k] = kids[k].hi[a]; }
+        nd.ref[k] = kids[k].ref >= 0 ? collapse(b, kids[k].ref, out, n_out, cap) : kids[k].ref;
+    }
+    (*out)[me] = nd;
     return me;
 }
 static obvh build_bvh(const float* bmin, const float* bmax, int n, int max_leaf) {
@@ -244,18 +341,23 @@ static obvh build_bvh(const float* bmin, const float* bmax, int n, int max_leaf)
     b.idx = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
     for (int i = 0; i < n; ++i) b.idx[i] = i;
     obvh out;
-    int32_t root = n > max_leaf ? build_range(&b, 0, n) : -1;
-    if (root < 0) {
-        /* a single leaf: root node with the leaf duplicated in both children */
-        b.nodes = (onode*)malloc(sizeof(onode));
-        b.num_nodes = 1;
-        for (int k = 0; k < 2; ++k) {
-            range_box(&b, 0, n, b.nodes[0].c[k].lo, b.nodes[0].c[k].hi);
-            b.nodes[0].c[k].ref = ~((0 << 4) | (n - 1));
-        }
+    out.nodes = NULL;
+    out.num_nodes = 0;
+    int cap = 0;
+    int32_t root = n > 0 ? build_range(&b, 0, n) : -1;
+    if (root >= 0) {
+        collapse(&b, root, &out.nodes, &out.num_nodes, &cap);
+    } else {
+        /* a single leaf: a root node holding just that leaf */
+        out.nodes = (onode4*)calloc(1, sizeof(onode4));
+        out.num_nodes = 1;
+        out.nodes[0].n = n > 0 ? 1 : 0;
+        out.nodes[0].ref[0] = root;
+        float lo[3], hi[3];
+        range_box(&b, 0, n, lo, hi);
+        for (int a = 0; a < 3; ++a) { out.nodes[0].lo[a][0] = lo[a]; out.nodes[0].hi[a][0] = hi[a]; }
     }
-    out.nodes = b.nodes;
-    out.num_nodes = b.num_nodes;
+    free(b.nodes);
     out.order = b.idx;
     return out;
 }
@@ -481,8 +583,27 @@ static int sphere_test(const oray* r, const float* sph, float* tt) {
     return 0;
 }
 
-#define OSTACK 128
+#define OSTACK 256
 typedef struct { int32_t ref; float tmin; } sentry;
+
+/* One 4-wide node: slab-test the valid children and push the hit ones, the
+ * nearest on top (cpu_traverse_helper, traversal/mapping_cpu.art:398-495). */
+static inline void push_children(const onode4* n, const oray* r, sentry* stack, int* sp) {
+    float en[4];
+    int32_t ref[4];
+    int m = 0;
+    for (int k = 0; k < n->n; ++k) {
+        float e, x;
+        float lo[3] = {n->lo[0][k], n->lo[1][k], n->lo[2][k]}, hi[3] = {n->hi[0][k], n->hi[1][k], n->hi[2][k]};
+        ray_box(r, lo, hi, &e, &x);
+        if (x < e) continue;
+        int j = m++; /* insertion by entry distance, farthest first */
+        while (j > 0 && en[j - 1] < e) { en[j] = en[j - 1]; ref[j] = ref[j - 1]; --j; }
+        en[j] = e;
+        ref[j] = n->ref[k];
+    }
+    for (int j = 0; j < m; ++j) stack[(*sp)++] = (sentry){ref[j], en[j]};
+}
 
 /* BLAS traversal in entity space (cpu_traverse_helper_prim) */
 static int traverse_blas(const oshape* sh, oray* r, int any, ohit* h, otstats* st) {
@@ -495,23 +616,7 @@ static int traverse_blas(const oshape* sh, oray* r, int any, ohit* h, otstats* s
         if (e.tmin > r->tmax) continue; /* cull */
         if (e.ref >= 0) {
             st->nodes++;
-            const onode* n = &sh->bvh.nodes[e.ref];
-            float en[2], ex[2];
-            int hitc[2];
-            for (int k = 0; k < 2; ++k) {
-                ray_box(r, n->c[k].lo, n->c[k].hi, &en[k], &ex[k]);
-                hitc[k] = !(ex[k] < en[k]);
-            }
-            /* nearer child on top */
-            if (hitc[0] && hitc[1]) {
-                int first = en[0] <= en[1] ? 0 : 1;
-                stack[sp++] = (sentry){n->c[1 - first].ref, en[1 - first]};
-                stack[sp++] = (sentry){n->c[first].ref, en[first]};
-            } else if (hitc[0]) {
-                stack[sp++] = (sentry){n->c[0].ref, en[0]};
-            } else if (hitc[1]) {
-                stack[sp++] = (sentry){n->c[1].ref, en[1]};
-            }
+            push_children(&sh->bvh.nodes[e.ref], r, stack, &sp);
         } else {
             int code = ~e.ref;
             int first = code >> 4, count = (code & 15) + 1;
@@ -552,22 +657,7 @@ static int trace_scene(const oracle_scene* s, const oray* ray_in, int any, ohit*
         if (e.tmin > ray.tmax) continue;
         if (e.ref >= 0) {
             st->nodes++;
-            const onode* n = &s->tlas.nodes[e.ref];
-            float en[2], ex[2];
-            int hitc[2];
-            for (int k = 0; k < 2; ++k) {
-                ray_box(&ray, n->c[k].lo, n->c[k].hi, &en[k], &ex[k]);
-                hitc[k] = !(ex[k] < en[k]);
-            }
-            if (hitc[0] && hitc[1]) {
-                int first = en[0] <= en[1] ? 0 : 1;
-                stack[sp++] = (sentry){n->c[1 - first].ref, en[1 - first]};
-                stack[sp++] = (sentry){n->c[first].ref, en[first]};
-            } else if (hitc[0]) {
-                stack[sp++] = (sentry){n->c[0].ref, en[0]};
-            } else if (hitc[1]) {
-                stack[sp++] = (sentry){n->c[1].ref, en[1]};
-            }
+            push_children(&s->tlas.nodes[e.ref], &ray, stack, &sp);
             continue;
         }
         int code = ~e.ref;
