@@ -986,6 +986,9 @@ struct igx_device {
     // off by default -- measured slower on the diamond (196 -> 230 ms per frame)
     // and neutral on primitives, S-deep and soup-1M
     bool spatial_splits = false;
+    // 1: build every BLAS here even when the scene carries the reference's own
+    // (igx_shape::ref_bvh, from the SceneDatabase adapter)
+    bool rebuild_bvh = false;
     // scene
     bool has_scene = false;
     std::vector<void*> scene_allocs;
@@ -1560,6 +1563,7 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
         dev->bvh_width_opt = (int)value;
     }
     else if (k == "spatial_splits") dev->spatial_splits = value != 0;
+    else if (k == "rebuild_bvh") dev->rebuild_bvh = value != 0;
     else if (k == "bvh_leaf_size") {
         if (value < 1 || value > 16) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "bvh_leaf_size must be in [1, 16]");
         dev->leaf_size = (int)value;
@@ -1607,6 +1611,14 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
                 bi.bmax[3 * f + a] = hi;
                 bi.centroid[3 * f + a] = 0.5f * (lo + hi);
             }
+        }
+        if (sh.ref_bvh && !dev->rebuild_bvh) {
+            // the reference loader's BLAS (Node2 + Tri1, TriMeshProvider.cpp:553-554)
+            std::string err;
+            if (!igx::bvh2_from_reference(sh.ref_bvh, sh.ref_bvh_bytes, m.num_faces, brs[s], err))
+                return fail(dev, IGX_ERR_INVALID_ARGUMENT, "shape " + std::to_string(s) + ": " + err);
+            blas_depth2 = std::max(blas_depth2, brs[s].depth);
+            continue;
         }
         try {
             if (dev->spatial_splits && m.num_faces <= SPATIAL_SPLIT_MAX_FACES) {

@@ -1,15 +1,26 @@
-// IG::Device facade over the igx_* C-ABI (include/igx.h).
+// IG::Device over the igx_* C-ABI (include/igx.h, include/igx_scene.h).
 //
-// Mirrors the reference plugin surface `IG::Device` (src/runtime/device/Device.h:14-74)
-// for the path this build covers: construction from SetupSettings, assignScene,
-// render one iteration, framebuffer access, clear, resize, statistics.  The
-// reference's tonemap/glare/imageinfo/bake entry points (Device.h:52-62) are
-// outside the hot path and are not provided.  Errors from the C-ABI become
-// std::runtime_error, which a Runtime turns into its bool/IG_LOG path
+// Same class, nested settings structs and member functions as the reference
+// plugin surface `IG::Device` (src/runtime/device/Device.h:14-74), so a runtime
+// written against it compiles against this header:
+//   * assignScene takes the reference's SceneSettings with a SceneDatabase*
+//     (table types in scene_database.h, same members as table/*.h); the tables
+//     reach the device through igx_scene_from_database;
+//   * render takes the TechniqueVariantShaderSet.  In the reference that is the
+//     technique variant's compiled shader code; igx has no shader JIT, so here
+//     the "shader set" is the shading tables the shaders were generated from
+//     (materials, lights, camera, technique: igx_shading_view).  The scene is
+//     uploaded on the first render after assignScene or with a new shader set,
+//     as the reference compiles and loads its shaders lazily;
+//   * the framebuffer, statistics, resize and release calls map one to one.
+// tonemap / evaluateGlare / imageinfo / bake (Device.h:66-69) are outside the
+// hot path and are not provided.  Errors from the C-ABI become
+// std::runtime_error, which a Runtime turns into its bool / IG_LOG path
 // (Runtime.cpp:159-162).
 #pragma once
 
 #include "igx.h"
+#include "scene_database.h"
 
 #include <cstdint>
 #include <stdexcept>
@@ -18,95 +29,188 @@
 
 namespace IG {
 
-struct SetupSettings {      // Device.h:18-23 (Target reduced to a HIP ordinal)
-    int Device = 0;
-    bool AcquireStats = false;
-    bool DebugTrace = false;
-    bool IsInteractive = false;
+// Target.h:19-68 reduced to what the device uses: a HIP ordinal
+class Target {
+public:
+    static Target makeGPU(int device = 0) { return Target(device); }
+    int device() const { return mDevice; }
+    bool isGPU() const { return true; }
+
+private:
+    explicit Target(int d) : mDevice(d) {}
+    int mDevice = 0;
 };
 
-struct SceneSettings {      // Device.h:25-30 (SceneDatabase -> igx_scene_desc)
-    const igx_scene_desc* Database = nullptr;
+struct Ray { // RuntimeStructs.h: org, dir, range (tmin, tmax)
+    float org[3];
+    float dir[3];
+    float range[2];
 };
+static_assert(sizeof(Ray) == 8 * sizeof(float), "ray-list layout of igx_render_params::rays");
 
-struct RenderSettings {     // Device.h:32-42
-    const float* rays = nullptr;   // ray-list mode (igtrace), 8 floats per ray
-    size_t ray_count = 0;
-    size_t spi = 8;
-    size_t width = 0, height = 0;
-    size_t iteration = 0;
-    size_t frame = 0;
-    int user_seed = 0;
-    int tile_size = 0, tile_offset = 0, tile_stride = 1;
+struct TechniqueVariantShaderSet {
+    igx_shading_view shading{};
 };
+struct TechniqueVariantInfo {};
+struct ParameterSet {};
 
-struct AOVAccessor {        // Device.h:44-47
-    const float* Data;
-    size_t IterationCount;
+// Statistics.h quantities the device fills (CameraRayCount, BounceRayCount,
+// ShadowRayCount; shadow rays counted when valid)
+class Statistics {
+public:
+    uint64_t cameraRayCount() const { return mStats.camera_rays; }
+    uint64_t bounceRayCount() const { return mStats.bounce_rays; }
+    uint64_t shadowRayCount() const { return mStats.shadow_rays; }
+    const igx_stats& raw() const { return mStats; }
+    igx_stats mStats{};
 };
 
 class Device {
 public:
+    struct SetupSettings { // Device.h:18-23
+        Target target = Target::makeGPU(0);
+        bool AcquireStats = false;
+        bool DebugTrace = false;
+        bool IsInteractive = false;
+    };
+
+    struct SceneSettings { // Device.h:25-30
+        SceneDatabase* database = nullptr;
+        const std::vector<std::string>* aov_map = nullptr;
+        const std::vector<std::string>* resource_map = nullptr;
+        const std::vector<int32_t>* entity_per_material = nullptr;
+    };
+
+    struct RenderSettings { // Device.h:32-42
+        const Ray* rays = nullptr; // non-null: width = number of rays, height = 1
+        size_t spi = 8;
+        size_t width = 0;
+        size_t height = 0;
+        size_t iteration = 0;
+        size_t frame = 0;
+        size_t user_seed = 0;
+        TechniqueVariantInfo info;
+        bool denoise = false;
+        // igx: tile sharding over ranks; 0 = whole film
+        int tile_size = 0, tile_offset = 0, tile_stride = 1;
+    };
+
+    struct AOVAccessor { // Device.h:44-47
+        float* Data;
+        size_t IterationCount;
+    };
+
     explicit Device(const SetupSettings& settings) : mSettings(settings) {
-        if (igx_create(settings.Device, &mDev) != IGX_OK || !mDev)
-            throw std::runtime_error("igx_create failed for HIP device " + std::to_string(settings.Device));
+        if (igx_create(settings.target.device(), &mDev) != IGX_OK || !mDev)
+            throw std::runtime_error("igx_create failed for HIP device " + std::to_string(settings.target.device()));
         if (settings.AcquireStats) check(igx_set_option(mDev, "timing", 1));
     }
     ~Device() {
+        releaseAll();
         if (mDev) igx_destroy(mDev);
     }
     Device(const Device&) = delete;
     Device& operator=(const Device&) = delete;
 
-    void assignScene(const SceneSettings& settings) { check(igx_upload_scene(mDev, settings.Database)); }
+    void assignScene(const SceneSettings& settings) {
+        if (!settings.database) throw std::runtime_error("igx: assignScene without a SceneDatabase");
+        mScene = settings;
+        mShaderSet = nullptr; // upload at the next render
+    }
 
-    void render(const RenderSettings& s) {
+    void render(const TechniqueVariantShaderSet& shader_set, const RenderSettings& s, const ParameterSet* = nullptr) {
+        if (!mScene.database) throw std::runtime_error("igx: render before assignScene");
+        if (mShaderSet != &shader_set) upload(shader_set);
         igx_render_params p{};
-        p.width = (int)s.width;
-        p.height = (int)s.height;
         p.spi = (int)s.spi;
         p.iteration = (int)s.iteration;
         p.frame = (int)s.frame;
-        p.seed = s.user_seed;
-        p.tile_size = s.tile_size;
-        p.tile_offset = s.tile_offset;
-        p.tile_stride = s.tile_stride;
-        p.num_rays = (int)s.ray_count;
-        p.rays = s.rays;
+        p.seed = (int)s.user_seed;
+        if (s.rays) { // ray-list mode (Runtime::trace, Runtime.cpp:385-407)
+            p.num_rays = (int)s.width;
+            p.rays = reinterpret_cast<const float*>(s.rays);
+        } else {
+            p.width = (int)s.width;
+            p.height = (int)s.height;
+            p.tile_size = s.tile_size;
+            p.tile_offset = s.tile_offset;
+            p.tile_stride = s.tile_stride;
+        }
         check(igx_render(mDev, &p));
-        mWidth = s.ray_count ? s.ray_count : s.width;
-        mHeight = s.ray_count ? 1 : s.height;
+        mWidth = s.width;
+        mHeight = s.rays ? 1 : s.height;
     }
 
+    void resize(size_t width, size_t height) {
+        mWidth = width;
+        mHeight = height;
+        check(igx_clear(mDev));
+    }
+
+    void releaseAll() {
+        if (mUploaded) igx_scene_free(mUploaded);
+        mUploaded = nullptr;
+        mShaderSet = nullptr;
+    }
+
+    Target target() const { return mSettings.target; }
+    size_t framebufferWidth() const { return mWidth; }
+    size_t framebufferHeight() const { return mHeight; }
+    bool isInteractive() const { return mSettings.IsInteractive; }
+
     AOVAccessor getFramebufferForHost(const std::string& name = "") {
-        if (!name.empty()) return AOVAccessor{nullptr, 0}; // only the colour framebuffer exists (Device.cpp:1303-1305)
+        if (!name.empty() && name != "Color") return AOVAccessor{nullptr, 0}; // only the colour AOV (Device.cpp:1303-1305)
         mHostFB.resize(mWidth * mHeight * 3);
         uint64_t iters = 0;
         check(igx_get_framebuffer(mDev, mHostFB.data(), mHostFB.size(), &iters));
         return AOVAccessor{mHostFB.data(), (size_t)iters};
     }
+    AOVAccessor getFramebufferForDevice(const std::string& name = "") {
+        if (!name.empty() && name != "Color") return AOVAccessor{nullptr, 0};
+        float* ptr = nullptr;
+        size_t n = 0;
+        uint64_t iters = 0;
+        check(igx_synchronize(mDev));
+        check(igx_framebuffer_device_ptr(mDev, &ptr, &n));
+        check(igx_get_framebuffer(mDev, nullptr, 0, &iters));
+        return AOVAccessor{ptr, (size_t)iters};
+    }
+    void clearFramebuffer(const std::string& = "") { check(igx_clear(mDev)); }
+    void clearAllFramebuffer() { check(igx_clear(mDev)); }
 
-    void clearFramebuffer() { check(igx_clear(mDev)); }
-
-    // render() only queues work; wait for it (timing, device-side reads)
-    void synchronize() { check(igx_synchronize(mDev)); }
-
-    igx_stats getStatistics() {
-        igx_stats s{};
-        check(igx_get_stats(mDev, &s));
-        return s;
+    const Statistics* getStatistics() {
+        check(igx_get_stats(mDev, &mStats.mStats));
+        return &mStats;
     }
 
+    // igx extras: render() only queues work; wait for it (timing, host reads)
+    void synchronize() { check(igx_synchronize(mDev)); }
     igx_device* handle() { return mDev; }
 
 private:
     void check(igx_status s) {
         if (s != IGX_OK) throw std::runtime_error(std::string("igx: ") + igx_last_error(mDev));
     }
+    void upload(const TechniqueVariantShaderSet& shader_set) {
+        DatabaseViewStorage view(*mScene.database);
+        char err[1024] = {0};
+        igx_scene* sc = igx_scene_from_database(&view.view, &shader_set.shading, err, sizeof(err));
+        if (!sc) throw std::runtime_error(std::string("igx: scene database: ") + err);
+        igx_status st = igx_upload_scene(mDev, igx_scene_get_desc(sc));
+        releaseAll();
+        mUploaded = sc;
+        check(st);
+        mShaderSet = &shader_set;
+    }
+
     SetupSettings mSettings;
+    SceneSettings mScene;
     igx_device* mDev = nullptr;
+    igx_scene* mUploaded = nullptr;
+    const TechniqueVariantShaderSet* mShaderSet = nullptr;
     size_t mWidth = 0, mHeight = 0;
     std::vector<float> mHostFB;
+    Statistics mStats;
 };
 
 } // namespace IG

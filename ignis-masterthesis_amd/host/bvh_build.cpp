@@ -7,6 +7,9 @@
 #include <stdexcept>
 #include <thread>
 #include <future>
+#include <cstring>
+#include <functional>
+#include <string>
 
 namespace igx {
 
@@ -582,6 +585,125 @@ Bvh4Result collapse_bvh4(const BvhBuildResult& in) {
     }
     res.stack_need = need[0];
     return res;
+}
+
+// ---------------------------------------------------------------------------
+// Reference GPU BLAS (Node2 + Tri1 blob) -> BvhBuildResult.
+// Node2 (traversal/mapping_gpu.art:3-7) stores the child boxes in the same
+// interleaving as BvhNode; children are inner index + 1 (> 0), ~first Tri1
+// (< 0) or 0 for a child the adapter cut out (BvhNAdapter.h:121-148).  A leaf
+// runs until the Tri1 whose prim_id has bit 31 set (TriBVHAdapter.h:148-158).
+// ---------------------------------------------------------------------------
+namespace {
+
+struct RefNode2 {
+    float b[12];
+    int32_t child[2];
+    int32_t pad[2];
+};
+static_assert(sizeof(RefNode2) == 64, "Node2 is 64 bytes");
+constexpr size_t kRefTri1Bytes = 48;
+
+} // namespace
+
+bool bvh2_from_reference(const uint8_t* blob, size_t bytes, uint32_t num_faces, BvhBuildResult& out, std::string& err) {
+    out = BvhBuildResult{};
+    if (!blob || bytes < 16) { err = "BLAS blob shorter than its header"; return false; }
+    uint32_t hdr[4];
+    std::memcpy(hdr, blob, 16);
+    const uint64_t nn = hdr[0], nt = hdr[1];
+    if (nn == 0 || nt == 0) { err = "BLAS blob without nodes or triangles"; return false; }
+    if (16 + nn * sizeof(RefNode2) + nt * kRefTri1Bytes > bytes) { err = "BLAS blob shorter than its node and triangle arrays"; return false; }
+    if (nt >= (uint64_t)kMaxLeafFirst) { err = "too many triangles for the leaf encoding"; return false; }
+    std::vector<RefNode2> rn(nn);
+    std::memcpy(rn.data(), blob + 16, nn * sizeof(RefNode2));
+    const uint8_t* tris = blob + 16 + nn * sizeof(RefNode2);
+    // slot -> face, and the leaf each slot starts
+    out.prim_order.resize(nt);
+    std::vector<uint8_t> ends(nt);
+    for (uint64_t s = 0; s < nt; ++s) {
+        uint32_t pid;
+        std::memcpy(&pid, tris + s * kRefTri1Bytes + 44, 4);
+        ends[s] = (pid >> 31) != 0;
+        pid &= 0x7FFFFFFFu;
+        if (pid >= num_faces) { err = "Tri1 prim_id beyond the mesh's faces"; return false; }
+        out.prim_order[s] = pid;
+    }
+    auto leaf_count = [&](uint64_t first, uint32_t& count) {
+        uint64_t s = first;
+        while (s < nt && !ends[s]) ++s;
+        if (s >= nt) return false;
+        count = (uint32_t)(s - first + 1);
+        return true;
+    };
+    const int max_leaf = 1 << kLeafCountBits;
+    // A reference leaf of more than max_leaf triangles becomes a balanced
+    // subtree of inner nodes over slices of it; every node of that subtree
+    // keeps the leaf's box (conservative: each slice lies inside it).
+    std::vector<int> ndepth; // levels below each output node (for the stack bound)
+    struct Item { int64_t src; int out; int depth; };
+    std::vector<Item> stack;
+    out.nodes.emplace_back();
+    stack.push_back({0, 0, 1});
+    std::vector<char> seen(nn, 0);
+    int depth = 1;
+    // child k of output node `o`: set box + ref, creating split-leaf nodes as needed
+    std::function<void(int, int, const float*, uint64_t, uint32_t, int)> put_leaf =
+        [&](int o, int k, const float* box, uint64_t first, uint32_t count, int d) {
+            float* dst = out.nodes[o].b + 6 * k;
+            std::memcpy(dst, box, 6 * sizeof(float));
+            if (count <= (uint32_t)max_leaf) {
+                out.nodes[o].ref[k] = encode_leaf((int32_t)first, (int32_t)count);
+                return;
+            }
+            const int idx = (int)out.nodes.size();
+            out.nodes.emplace_back();
+            out.nodes[o].ref[k] = idx;
+            depth = std::max(depth, d + 1);
+            const uint32_t half = count / 2;
+            put_leaf(idx, 0, box, first, half, d + 1);
+            put_leaf(idx, 1, box, first + half, count - half, d + 1);
+        };
+    bool root_leaf = false;
+    while (!stack.empty()) {
+        Item it = stack.back();
+        stack.pop_back();
+        if (it.src < 0 || (uint64_t)it.src >= nn) { err = "Node2 child index out of range"; return false; }
+        if (seen[it.src]++) { err = "Node2 graph is not a tree"; return false; }
+        depth = std::max(depth, it.depth);
+        RefNode2 n = rn[it.src];
+        // a cut-out child (0) repeats its sibling: harmless for closest and any hit
+        if (n.child[0] == 0 && n.child[1] == 0) { err = "Node2 without children"; return false; }
+        for (int k = 0; k < 2; ++k)
+            if (n.child[k] == 0) {
+                n.child[k] = n.child[1 - k];
+                std::memcpy(n.b + 6 * k, n.b + 6 * (1 - k), 6 * sizeof(float));
+                if (it.src == 0 && n.child[k] < 0) root_leaf = true; // root wrapping a single leaf (BvhNAdapter.h:94-98)
+            }
+        out.nodes[it.out].pad[0] = out.nodes[it.out].pad[1] = 0;
+        for (int k = 0; k < 2; ++k) {
+            const int32_t c = n.child[k];
+            if (c > 0) {
+                const int idx = (int)out.nodes.size();
+                out.nodes.emplace_back();
+                std::memcpy(out.nodes[it.out].b + 6 * k, n.b + 6 * k, 6 * sizeof(float));
+                out.nodes[it.out].ref[k] = idx;
+                stack.push_back({(int64_t)c - 1, idx, it.depth + 1});
+            } else {
+                const uint64_t first = (uint64_t)(~c);
+                uint32_t count = 0;
+                if (first >= nt || !leaf_count(first, count)) { err = "Tri1 leaf without its end marker"; return false; }
+                put_leaf(it.out, k, n.b + 6 * k, first, count, it.depth);
+            }
+        }
+    }
+    out.depth = depth;
+    out.max_leaf = max_leaf;
+    if (root_leaf && out.nodes.size() == 1 && out.nodes[0].ref[0] < 0) {
+        out.root_is_leaf = true;
+        out.root_leaf_ref = out.nodes[0].ref[0];
+    }
+    return true;
 }
 
 } // namespace igx

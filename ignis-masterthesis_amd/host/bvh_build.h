@@ -18,6 +18,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <string>
 #include <vector>
 
 namespace igx {
@@ -88,5 +89,12 @@ struct Bvh4Result {
 // inner grandchildren of its BVH2 node until it has four children (the
 // surface-area collapse of wide-BVH builders).  Leaf codes are kept.
 Bvh4Result collapse_bvh4(const BvhBuildResult& bvh2);
+
+// Read the reference's GPU BLAS (one FixTables["trimesh_primbvh"] entry:
+// u32 node_count, tri_count, 0, 0; Node2[]; Tri1[], TriMeshProvider.cpp:307-326)
+// into the device's BVH2 form: same boxes and topology, leaf codes over the
+// Tri1 slots, prim_order = each slot's prim_id.  Leaves above 16 triangles
+// become small subtrees.  false + err on a malformed blob.
+bool bvh2_from_reference(const uint8_t* blob, size_t bytes, uint32_t num_faces, BvhBuildResult& out, std::string& err);
 
 } // namespace igx

@@ -2,7 +2,10 @@
 // loads a scene, renders spp samples in iterations of spi on one GPU, prints
 // Msamples/s like the reference (cli/main.cpp:135, 172-178) plus Mrays/s, and
 // writes the averaged image as EXR (Image::save, Image.h:92-101), or PFM when
-// the output name ends in .pfm.
+// the output name ends in .pfm.  The scene reaches the device as the
+// reference's does: the loader's tables (SceneDatabase, serialize_scene) go
+// through IG::Device::assignScene, the shading tables through render's shader
+// set (Runtime.cpp:477-485, 343).
 #include "Device.h"
 #include "igx_scene.h"
 
@@ -46,29 +49,32 @@ int main(int argc, char** argv) {
     if (spp <= 0) spp = spi;
     int iters = (spp + spi - 1) / spi; // igcli rounds spp up to a multiple of spi (cli/main.cpp:110-113)
     try {
-        IG::SetupSettings ss;
-        ss.Device = device;
+        IG::SceneDatabase db;
+        IG::TechniqueVariantShaderSet shaders;
+        IG::serialize_scene(*desc, db, shaders.shading);
+        IG::Device::SetupSettings ss;
+        ss.target = IG::Target::makeGPU(device);
         IG::Device dev(ss);
-        IG::SceneSettings sc;
-        sc.Database = desc;
+        IG::Device::SceneSettings sc;
+        sc.database = &db;
         dev.assignScene(sc);
         std::vector<double> rates;
         double total_s = 0; // wall time of the render loop (cli/main.cpp:127-135)
         for (int it = 0; it < iters; ++it) {
-            IG::RenderSettings rs;
+            IG::Device::RenderSettings rs;
             rs.spi = spi;
             rs.width = desc->film_width;
             rs.height = desc->film_height;
             rs.iteration = it;
             rs.user_seed = seed;
             auto t0 = std::chrono::steady_clock::now();
-            dev.render(rs);
+            dev.render(shaders, rs, nullptr);
             dev.synchronize(); // render() only queues the iteration
             double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
             rates.push_back((double)spi * desc->film_width * desc->film_height / s / 1e6);
             total_s += s;
         }
-        igx_stats st = dev.getStatistics();
+        const igx_stats& st = dev.getStatistics()->raw();
         std::sort(rates.begin(), rates.end());
         double rays = (double)(st.camera_rays + st.bounce_rays + st.shadow_rays);
         std::printf("# %f %f %f Msamples/s\n", rates.front(), rates[rates.size() / 2], rates.back());
@@ -76,7 +82,7 @@ int main(int argc, char** argv) {
                     (unsigned long long)st.camera_rays, (unsigned long long)st.bounce_rays, (unsigned long long)st.shadow_rays,
                     total_s * 1e3);
         if (!out_path.empty()) {
-            IG::AOVAccessor acc = dev.getFramebufferForHost();
+            IG::Device::AOVAccessor acc = dev.getFramebufferForHost("");
             float inv = acc.IterationCount ? 1.0f / acc.IterationCount : 0.0f;
             const bool pfm = out_path.size() >= 4 && out_path.compare(out_path.size() - 4, 4, ".pfm") == 0;
             if (!pfm) {

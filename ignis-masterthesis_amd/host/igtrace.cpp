@@ -69,23 +69,27 @@ int main(int argc, char** argv) {
     if (!scene) { std::fprintf(stderr, "failed to load scene: %s\n", err); return 1; }
     int rc = 0;
     try {
-        IG::SetupSettings ss;
-        ss.Device = device;
+        IG::SceneDatabase db; // the loader's tables, as Runtime hands them over (Runtime.cpp:477-485)
+        IG::TechniqueVariantShaderSet shaders;
+        IG::serialize_scene(*igx_scene_get_desc(scene), db, shaders.shading);
+        IG::Device::SetupSettings ss;
+        ss.target = IG::Target::makeGPU(device);
         IG::Device dev(ss);
-        IG::SceneSettings sc;
-        sc.Database = igx_scene_get_desc(scene);
+        IG::Device::SceneSettings sc;
+        sc.database = &db;
         dev.assignScene(sc);
         const int iters = spp < 1 ? 1 : spp; // SPI fixed to 1 (trace/main.cpp:80)
         for (int it = 0; it < iters; ++it) {
-            IG::RenderSettings rs;
-            rs.rays = rays.data();
-            rs.ray_count = n;
+            IG::Device::RenderSettings rs; // Runtime::trace (Runtime.cpp:385-407): width = ray count
+            rs.rays = reinterpret_cast<const IG::Ray*>(rays.data());
+            rs.width = n;
+            rs.height = 1;
             rs.spi = 1;
             rs.iteration = it;
             rs.user_seed = seed;
-            dev.render(rs);
+            dev.render(shaders, rs, nullptr);
         }
-        IG::AOVAccessor acc = dev.getFramebufferForHost();
+        IG::Device::AOVAccessor acc = dev.getFramebufferForHost("");
         std::FILE* f = out_path.empty() ? stdout : std::fopen(out_path.c_str(), "w");
         if (!f) throw std::runtime_error("cannot write " + out_path);
         const float inv = acc.IterationCount ? 1.0f / (float)acc.IterationCount : 0.0f;

@@ -11,6 +11,7 @@
 #include "json.h"
 #include "linalg.h"
 #include "mesh.h"
+#include "scene_store.h"
 
 #include <cmath>
 #include <cstdio>
@@ -30,22 +31,12 @@ using igx::M4;
 using igx::TriMesh;
 using igx::V3;
 using igx::json::Value;
+using igx::SceneStore;
 
 namespace {
 
 constexpr float kPi = 3.14159265358979323846f;
 constexpr float kDeg2Rad = kPi / 180.0f;
-
-struct SceneStore {
-    igx_scene_desc desc{};
-    std::vector<std::vector<float>> vtx, nrm, tex;
-    std::vector<std::vector<uint32_t>> idx;
-    std::vector<igx_mesh> meshes;
-    std::vector<igx_shape> shapes;
-    std::vector<igx_entity> entities;
-    std::vector<igx_material> materials;
-    std::vector<igx_light> lights;
-};
 
 [[noreturn]] void fail(const std::string& m) { throw std::runtime_error(m); }
 
@@ -444,10 +435,6 @@ TriMesh setup_trimesh(const std::string& type, const Props& p, const std::string
 
 } // namespace
 
-struct igx_scene {
-    SceneStore store;
-};
-
 static void build_scene(SceneStore& S, const Value& doc, const std::string& base_dir) {
     // ---- film (Runtime.cpp:28-44) ----
     S.desc.film_width = 800;
@@ -647,6 +634,8 @@ static void build_scene(SceneStore& S, const Value& doc, const std::string& base
         igx_material m = bsdfs[mat_keys[mid].bsdf];
         m.light = -1;
         S.materials.push_back(m);
+        S.material_bsdf.push_back(mat_keys[mid].bsdf);
+        S.material_entity.push_back(mat_keys[mid].light_entity);
         for (const Value* e : groups[mid]) {
             Props ep{e};
             std::string name = ep.string("name");
@@ -678,6 +667,7 @@ static void build_scene(SceneStore& S, const Value& doc, const std::string& base
             for (int i = 0; i < 3; ++i) { ent.bbox_min[i] = eb.min[i]; ent.bbox_max[i] = eb.max[i]; }
             scene_bbox.extend(eb);
             entity_ids[name] = (int)S.entities.size();
+            S.entity_names.push_back(name);
             S.entities.push_back(ent);
         }
     }
@@ -892,16 +882,7 @@ static void build_scene(SceneStore& S, const Value& doc, const std::string& base
         S.desc.scene_bbox_min[i] = scene_bbox.empty() ? 0 : scene_bbox.min[i];
         S.desc.scene_bbox_max[i] = scene_bbox.empty() ? 0 : scene_bbox.max[i];
     }
-    S.desc.num_meshes = (uint32_t)S.meshes.size();
-    S.desc.meshes = S.meshes.data();
-    S.desc.num_shapes = (uint32_t)S.shapes.size();
-    S.desc.shapes = S.shapes.data();
-    S.desc.num_entities = (uint32_t)S.entities.size();
-    S.desc.entities = S.entities.data();
-    S.desc.num_materials = (uint32_t)S.materials.size();
-    S.desc.materials = S.materials.data();
-    S.desc.num_lights = (uint32_t)S.lights.size();
-    S.desc.lights = S.lights.data();
+    S.publish();
 }
 
 static void set_err(char* err, size_t len, const std::string& msg) {
@@ -942,3 +923,16 @@ extern "C" igx_scene* igx_scene_load_file(const char* path, char* err, size_t er
 
 extern "C" const igx_scene_desc* igx_scene_get_desc(const igx_scene* s) { return s ? &s->store.desc : nullptr; }
 extern "C" void igx_scene_free(igx_scene* s) { delete s; }
+
+extern "C" int32_t igx_scene_find_material(const igx_scene* s, const char* bsdf, const char* emissive_entity) {
+    if (!s || !bsdf) return -1;
+    const std::string e = emissive_entity ? emissive_entity : "";
+    for (size_t i = 0; i < s->store.material_bsdf.size(); ++i)
+        if (s->store.material_bsdf[i] == bsdf && s->store.material_entity[i] == e) return (int32_t)i;
+    return -1;
+}
+
+extern "C" const char* igx_scene_entity_name(const igx_scene* s, uint32_t entity) {
+    if (!s || entity >= s->store.entity_names.size()) return nullptr;
+    return s->store.entity_names[entity].c_str();
+}

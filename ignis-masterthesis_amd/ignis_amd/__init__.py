@@ -95,6 +95,17 @@ class Scene:
             raise IgxError(err.value.decode())
         return Scene(h)
 
+    @staticmethod
+    def from_database(db, shading):
+        """igx_scene_from_database: the reference's SceneDatabase tables
+        (`_native.DatabaseView`) plus the shading tables (`_native.ShadingView`);
+        the caller keeps the viewed buffers alive for the call."""
+        err = C.create_string_buffer(2048)
+        h = lib().igx_scene_from_database(C.byref(db), C.byref(shading), err, len(err))
+        if not h:
+            raise IgxError(err.value.decode())
+        return Scene(h)
+
     @property
     def desc_ptr(self):
         """Raw `const igx_scene_desc*` (for C consumers such as the oracle)."""

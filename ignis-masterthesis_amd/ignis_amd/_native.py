@@ -24,7 +24,7 @@ class Shape(C.Structure):
     _fields_ = [("type", C.c_int32), ("mesh", C.c_int32), ("sphere", C.c_float * 4),
                 ("bbox_min", C.c_float * 3), ("bbox_max", C.c_float * 3), ("is_plane", C.c_int32),
                 ("plane_origin", C.c_float * 3), ("plane_x", C.c_float * 3), ("plane_y", C.c_float * 3),
-                ("plane_tex", C.c_float * 8)]
+                ("plane_tex", C.c_float * 8), ("ref_bvh", C.c_void_p), ("ref_bvh_bytes", C.c_uint64)]
 
 
 class Entity(C.Structure):
@@ -75,6 +75,27 @@ class SceneDesc(C.Structure):
                 ("scene_bbox_min", C.c_float * 3), ("scene_bbox_max", C.c_float * 3)]
 
 
+class LookupEntry(C.Structure):
+    _fields_ = [("type_id", C.c_uint32), ("flags", C.c_uint32), ("offset", C.c_uint64)]
+
+
+class DbTable(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("bytes", C.c_uint64), ("lookups", C.POINTER(LookupEntry)), ("count", C.c_uint64)]
+
+
+class DatabaseView(C.Structure):
+    _fields_ = [("entities", DbTable), ("shapes", DbTable), ("trimesh_type_id", C.c_uint32),
+                ("sphere_type_id", C.c_uint32), ("trimesh_primbvh", DbTable),
+                ("scene_bvh_leaves", C.POINTER(DbTable)), ("num_scene_bvhs", C.c_uint32),
+                ("scene_bbox_min", C.c_float * 3), ("scene_bbox_max", C.c_float * 3)]
+
+
+class ShadingView(C.Structure):
+    _fields_ = [("film_width", C.c_int32), ("film_height", C.c_int32), ("camera", Camera), ("technique", Technique),
+                ("num_materials", C.c_uint32), ("materials", C.POINTER(Material)),
+                ("num_lights", C.c_uint32), ("lights", C.POINTER(Light))]
+
+
 # ---- igx.h ----------------------------------------------------------------
 
 class RenderParams(C.Structure):
@@ -109,6 +130,7 @@ class Stats(C.Structure):
 # every symbol include/igx.h and include/igx_scene.h declare
 EXPORTED_SYMBOLS = [
     "igx_scene_load_file", "igx_scene_load_string", "igx_scene_get_desc", "igx_scene_free", "igx_write_exr",
+    "igx_scene_from_database", "igx_scene_find_material", "igx_scene_entity_name",
     "igx_create", "igx_destroy", "igx_last_error", "igx_version", "igx_set_option", "igx_upload_scene",
     "igx_render", "igx_get_framebuffer", "igx_framebuffer_device_ptr", "igx_pack_tiles", "igx_clear",
     "igx_get_stats", "igx_reset_stats", "igx_trace_hits", "igx_trace_occlusion", "igx_synchronize",
@@ -131,6 +153,12 @@ def lib():
     L.igx_scene_load_file.restype = vp
     L.igx_scene_load_string.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_size_t]
     L.igx_scene_load_string.restype = vp
+    L.igx_scene_from_database.argtypes = [C.POINTER(DatabaseView), C.POINTER(ShadingView), C.c_char_p, C.c_size_t]
+    L.igx_scene_from_database.restype = vp
+    L.igx_scene_find_material.argtypes = [vp, C.c_char_p, C.c_char_p]
+    L.igx_scene_find_material.restype = C.c_int32
+    L.igx_scene_entity_name.argtypes = [vp, C.c_uint32]
+    L.igx_scene_entity_name.restype = C.c_char_p
     L.igx_scene_get_desc.argtypes = [vp]
     L.igx_scene_get_desc.restype = C.POINTER(SceneDesc)
     L.igx_scene_free.argtypes = [vp]

@@ -48,6 +48,14 @@ typedef struct igx_shape {
     int32_t is_plane;
     float plane_origin[3], plane_x[3], plane_y[3];
     float plane_tex[8];  /* 4 texcoords */
+    /* Optional prebuilt BLAS in the reference's GPU layout: one
+     * FixTables["trimesh_primbvh"] entry (TriMeshProvider.cpp:307-326, 361-369):
+     * u32 node_count, tri_count, 0, 0; Node2[node_count] (64 B,
+     * traversal/mapping_gpu.art:3-7; child > 0 inner index + 1, < 0 ~first Tri1,
+     * 0 empty); Tri1[tri_count] (48 B, shapes/trimesh.art:107-114; prim_id bit 31
+     * ends a leaf).  NULL: igx builds the BLAS itself (host/bvh_build.cpp). */
+    const uint8_t* ref_bvh;
+    uint64_t ref_bvh_bytes;
 } igx_shape;
 
 /* ---- entities ---------------------------------------------------------- */
@@ -162,6 +170,83 @@ igx_scene* igx_scene_load_file(const char* path, char* err, size_t err_len);
 igx_scene* igx_scene_load_string(const char* json, const char* base_dir, char* err, size_t err_len);
 const igx_scene_desc* igx_scene_get_desc(const igx_scene* scene);
 void igx_scene_free(igx_scene* scene);
+/* Names of a scene from igx_scene_load_*, for bindings that re-index its
+ * shading tables by the reference loader's ids: the
+ * material id of (BSDF name, emissive entity name or NULL/"" for a shared
+ * material, LoaderContext::Material, LoaderContext.h:19-27), -1 if absent;
+ * the name of entity `entity`, NULL if out of range (or for scenes built by
+ * igx_scene_from_database, which carry no names). */
+int32_t igx_scene_find_material(const igx_scene* scene, const char* bsdf, const char* emissive_entity);
+const char* igx_scene_entity_name(const igx_scene* scene, uint32_t entity);
+
+/* ---- the reference's SceneDatabase as plain C (Device::assignScene seam) --
+ * IG::Runtime hands its device a `SceneDatabase*` (Runtime.cpp:477-485,
+ * Device.h:25-30; table/SceneDatabase.h:13-20).  A binding passes views of the
+ * tables it holds; igx_scene_from_database turns them into an igx_scene whose
+ * desc equals what igx_scene_load_file builds from the same scene file. */
+
+/* DynTable lookup entry (table/DynTable.h:6-10), 16 bytes */
+typedef struct igx_lookup_entry {
+    uint32_t type_id;  /* ShapeProvider::id() for the "shapes" table */
+    uint32_t flags;
+    uint64_t offset;   /* byte offset of the record in the table data */
+} igx_lookup_entry;
+
+/* one DynTable / FixTable / SceneBVH byte array */
+typedef struct igx_db_table {
+    const uint8_t* data;
+    uint64_t bytes;
+    const igx_lookup_entry* lookups; /* DynTable only (NULL for a FixTable) */
+    uint64_t count;                  /* DynTable: lookup count; FixTable: entryCount() */
+} igx_db_table;
+
+typedef struct igx_database_view {
+    /* FixTables["entities"]: 36 x 4 B per entity, column-major toLocal 3x4,
+     * toGlobal 3x4, normal 3x3, u32 shape_id, u32 material_id, pad
+     * (LoaderEntity.cpp:155-162) */
+    igx_db_table entities;
+    /* DynTables["shapes"]: trimesh records (TriMeshProvider.cpp:583-598:
+     * u32 faces, vertices, normals, texcoords; bbox min.xyz, 0, max.xyz, 0;
+     * vertices and normals 16 B each; indices 4 x u32 per face; texcoords 8 B
+     * each) and sphere records (SphereProvider.cpp:40-47: origin.xyz, radius) */
+    igx_db_table shapes;
+    uint32_t trimesh_type_id;  /* lookup type_id of the trimesh provider */
+    uint32_t sphere_type_id;   /* lookup type_id of the sphere provider */
+    /* FixTables["trimesh_primbvh"]: GPU-target BLAS blobs (TriMeshProvider.cpp:
+     * 361-369); may be empty (igx then builds the BLAS itself) */
+    igx_db_table trimesh_primbvh;
+    /* SceneBVHs[provider].Leaves: EntityLeaf1 records (96 B, traversal/bvh.art:
+     * 52-61; SceneBVHAdapter.h:88-104) of every provider's TLAS.  They carry the
+     * entity visibility flags (LoaderEntity.cpp:120-128) and, in user[0..1],
+     * the float offset of the entity's BLAS in trimesh_primbvh */
+    const igx_db_table* scene_bvh_leaves;
+    uint32_t num_scene_bvhs;
+    float scene_bbox_min[3], scene_bbox_max[3]; /* SceneDatabase::SceneBBox */
+} igx_database_view;
+
+/* The part of a scene the reference compiles into shader code instead of
+ * tables (the TechniqueVariantShaderSet handed to Device::render, Device.h:52):
+ * film, camera, technique, the material of every material id
+ * (LoaderContext::Materials order, LoaderEntity.cpp:42-103) and the lights
+ * (area lights name their entity by its index in the entities table). */
+typedef struct igx_shading_view {
+    int32_t film_width, film_height;
+    igx_camera camera;
+    igx_technique technique;
+    uint32_t num_materials; const igx_material* materials;
+    uint32_t num_lights;    const igx_light* lights;
+} igx_shading_view;
+
+/* Build a scene from the reference's tables plus the shading view.  Plane
+ * shapes are recognised from the mesh records (TriMesh::getAsPlane, as
+ * TriMeshProvider.cpp:562 does); entity world boxes follow
+ * BoundingBox::transformed (LoaderEntity.cpp:141).  With a non-empty
+ * trimesh_primbvh, every trimesh shape carries its reference BLAS (ref_bvh),
+ * which igx_upload_scene then uses instead of building one (option
+ * "rebuild_bvh" = 1 ignores it).  Returns NULL and fills err on malformed
+ * tables (sizes, offsets, ids out of range). */
+igx_scene* igx_scene_from_database(const igx_database_view* db, const igx_shading_view* shading, char* err,
+                                   size_t err_len);
 
 /* Write a linear RGB image (row-major, 3 floats per pixel, each multiplied by
  * `scale`, e.g. 1/iteration count) as an uncompressed float OpenEXR file with

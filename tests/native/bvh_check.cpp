@@ -3,13 +3,21 @@
 // closest hit found through the built BVH2 -- binned SAH (build_bvh2) and
 // with spatial splits (build_sbvh2) -- equals brute force on random rays, for
 // scenes of long thin triangles (where spatial splits engage), large
-// overlapping triangles and a small-triangle soup.  Prints one line per case.
+// overlapping triangles and a small-triangle soup.  Also the reader of the
+// reference's GPU BLAS (bvh2_from_reference): a median-split tree written in
+// the Node2 + Tri1 layout of BvhNAdapter / TriBVHAdapter (inner child = index
+// + 1, leaf = ~first Tri1, bit 31 of prim_id ends a leaf, a root leaf wrapped
+// with a cut-out sibling), with leaves of up to 40 triangles, read back and
+// traced.  Prints one line per case.
 #include "bvh_build.h"
 
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <functional>
+#include <cstring>
 #include <random>
+#include <string>
 #include <vector>
 
 using namespace igx;
@@ -132,6 +140,73 @@ double sah(const BvhBuildResult& br) {
     return root > 0 ? 1.0 + cost / root : 0.0;
 }
 
+// Median-split tree over V in the reference's GPU BLAS layout (header, Node2[], Tri1[]).
+std::vector<uint8_t> write_reference_blob(const std::vector<float>& V, size_t max_leaf) {
+    struct N2 { float b[12]; int32_t child[2]; int32_t pad[2]; };
+    struct T1 { float v0[3]; int32_t p0; float e1[3]; int32_t p1; float e2[3]; int32_t prim; };
+    std::vector<N2> nodes;
+    std::vector<T1> tris;
+    const size_t n = V.size() / 9;
+    std::vector<uint32_t> idx(n);
+    for (size_t i = 0; i < n; ++i) idx[i] = (uint32_t)i;
+    auto box_of = [&](size_t first, size_t count, float* b) {
+        for (int a = 0; a < 3; ++a) { b[2 * a] = INFINITY; b[2 * a + 1] = -INFINITY; }
+        for (size_t i = first; i < first + count; ++i)
+            for (int k = 0; k < 3; ++k)
+                for (int a = 0; a < 3; ++a) {
+                    float x = V[9 * (size_t)idx[i] + 3 * k + a];
+                    b[2 * a] = std::min(b[2 * a], x);
+                    b[2 * a + 1] = std::max(b[2 * a + 1], x);
+                }
+    };
+    auto emit_leaf = [&](size_t first, size_t count) {
+        int32_t ref = ~(int32_t)tris.size();
+        for (size_t i = first; i < first + count; ++i) {
+            const float* t = &V[9 * (size_t)idx[i]];
+            T1 r{};
+            for (int a = 0; a < 3; ++a) { r.v0[a] = t[a]; r.e1[a] = t[a] - t[3 + a]; r.e2[a] = t[6 + a] - t[a]; }
+            r.prim = (int32_t)idx[i];
+            tris.push_back(r);
+        }
+        tris.back().prim |= (int32_t)0x80000000;
+        return ref;
+    };
+    std::function<void(size_t, size_t, int)> node = [&](size_t first, size_t count, int parent_slot) {
+        const size_t me = nodes.size();
+        nodes.emplace_back();
+        if (parent_slot >= 0) nodes[parent_slot / 2].child[parent_slot % 2] = (int32_t)me + 1;
+        float b[6];
+        box_of(first, count, b);
+        int axis = 0;
+        for (int a = 1; a < 3; ++a) if (b[2 * a + 1] - b[2 * a] > b[2 * axis + 1] - b[2 * axis]) axis = a;
+        auto cen = [&](uint32_t p) { return V[9 * (size_t)p + axis] + V[9 * (size_t)p + 3 + axis] + V[9 * (size_t)p + 6 + axis]; };
+        const size_t half = count / 2;
+        std::nth_element(idx.begin() + first, idx.begin() + first + half, idx.begin() + first + count,
+                         [&](uint32_t x, uint32_t y) { return cen(x) < cen(y); });
+        const size_t f[2] = {first, first + half}, c[2] = {half, count - half};
+        for (int k = 0; k < 2; ++k) {
+            box_of(f[k], c[k], nodes[me].b + 6 * k);
+            if (c[k] <= max_leaf) nodes[me].child[k] = emit_leaf(f[k], c[k]);
+            else node(f[k], c[k], (int)(2 * me + k));
+        }
+    };
+    if (n <= max_leaf) {  // root leaf: child 0 = the leaf, child 1 cut out (BvhNAdapter.h:94-98, 136-146)
+        nodes.emplace_back();
+        box_of(0, n, nodes[0].b);
+        nodes[0].child[0] = emit_leaf(0, n);
+        for (int a = 0; a < 3; ++a) { nodes[0].b[6 + 2 * a] = INFINITY; nodes[0].b[7 + 2 * a] = -INFINITY; }
+        nodes[0].child[1] = 0;
+    } else {
+        node(0, n, -1);
+    }
+    std::vector<uint8_t> blob(16 + nodes.size() * 64 + tris.size() * 48);
+    uint32_t hdr[4] = {(uint32_t)nodes.size(), (uint32_t)tris.size(), 0, 0};
+    std::memcpy(blob.data(), hdr, 16);
+    std::memcpy(blob.data() + 16, nodes.data(), nodes.size() * 64);
+    std::memcpy(blob.data() + 16 + nodes.size() * 64, tris.data(), tris.size() * 48);
+    return blob;
+}
+
 }  // namespace
 
 int main() {
@@ -162,12 +237,30 @@ int main() {
         }
         cases.push_back({"soup", V});
     }
+    {  // fewer triangles than one reference leaf: the wrapped root leaf
+        std::vector<float> V;
+        for (int i = 0; i < 12 * 9; ++i) V.push_back(U(rng));
+        cases.push_back({"tiny", V});
+    }
     int bad_total = 0;
     for (const Case& cs : cases) {
         const size_t n = cs.V.size() / 9;
         BvhBuildInput in = bounds(cs.V);
-        for (int split = 0; split < 2; ++split) {
-            BvhBuildResult br = split ? build_sbvh2(in, cs.V, 4) : build_bvh2(in, 4);
+        for (int split = 0; split < 4; ++split) {
+            BvhBuildResult br;
+            if (split < 2) {
+                br = split ? build_sbvh2(in, cs.V, 4) : build_bvh2(in, 4);
+            } else {  // the reference's GPU BLAS layout, leaves up to 4 / 40 triangles
+                std::vector<uint8_t> blob = write_reference_blob(cs.V, split == 2 ? 4 : 40);
+                std::string err;
+                if (!bvh2_from_reference(blob.data(), blob.size(), (uint32_t)n, br, err)) {
+                    std::printf("%s ref: %s\nFAIL\n", cs.name, err.c_str());
+                    return 1;
+                }
+                std::vector<uint8_t> cut(blob.begin(), blob.end() - 1);  // truncated blob must be refused
+                BvhBuildResult tmp;
+                if (bvh2_from_reference(cut.data(), cut.size(), (uint32_t)n, tmp, err)) ++bad_total;
+            }
             std::vector<char> seen(n, 0);
             for (uint32_t p : br.prim_order) seen[p] = 1;
             int missing = (int)std::count(seen.begin(), seen.end(), 0);
@@ -183,7 +276,7 @@ int main() {
                 if (a.prim != b.prim || !(a.t == b.t || (a.prim < 0 && b.prim < 0))) ++bad;
             }
             std::printf("%s %s refs %zu/%zu nodes %zu sah %.2f hits %d mismatches %d missing %d\n", cs.name,
-                        split ? "sbvh" : "bvh2", br.prim_order.size(), n, br.nodes.size(), sah(br), hits, bad, missing);
+                        split == 0 ? "bvh2" : split == 1 ? "sbvh" : split == 2 ? "ref4" : "ref40", br.prim_order.size(), n, br.nodes.size(), sah(br), hits, bad, missing);
             bad_total += bad + missing;
         }
     }

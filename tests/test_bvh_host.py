@@ -1,6 +1,8 @@
-"""Host BVH builders (CPU only): closest hits through the binned-SAH BVH2 and
-the spatial-split BVH equal brute force on random rays (tests/native/bvh_check.cpp,
-compiled here with g++ against host/bvh_build.cpp)."""
+"""Host BVH builders (CPU only): closest hits through the binned-SAH BVH2, the
+spatial-split BVH and the reader of the reference's GPU BLAS layout
+(bvh2_from_reference, Node2 + Tri1 trees with leaves of 4 and 40 triangles)
+equal brute force on random rays (tests/native/bvh_check.cpp, compiled here
+with g++ against host/bvh_build.cpp)."""
 import os
 import subprocess
 
@@ -16,7 +18,8 @@ def test_bvh_builders_match_brute_force(tmp_path):
     print(out.stdout)
     assert out.returncode == 0, out.stdout + out.stderr
     lines = [l.split() for l in out.stdout.splitlines() if " refs " in l]
-    assert len(lines) == 6
+    assert len(lines) == 16
+    assert {l[1] for l in lines} == {"bvh2", "sbvh", "ref4", "ref40"}
     # spatial splits engage on the thin triangles and lower their SAH cost
     sl = {l[1]: l for l in lines if l[0] == "slivers"}
     assert int(sl["sbvh"][3].split("/")[0]) > int(sl["bvh2"][3].split("/")[0])

@@ -695,3 +695,31 @@ def test_pack_tiles_rejects_a_film_that_is_not_the_framebuffer(device, diamond_p
     p.width, p.height, p.spi, p.tile_size, p.tile_offset, p.tile_stride = 400, 300, 4, 64, 0, 3
     with pytest.raises(ignis_amd.IgxError, match="does not match the framebuffer"):
         device.pack_tiles(p, buf.data_ptr(), buf.numel())
+
+
+@pytest.mark.parametrize("name,max_leaf", [("diamond_scene.json", 4), ("primitives.json", 4), ("materials.json", 40)])
+def test_database_adapter_renders_bit_identically(device, root, name, max_leaf):
+    """The reference's SceneDatabase tables (tests/refdb.py) through
+    igx_scene_from_database, traced over the reference-layout BLAS they carry
+    (Node2 + Tri1, leaves up to max_leaf triangles), render the same image bit
+    for bit as the JSON loader's scene over igx's own BVH (closest hits do not
+    depend on BVH topology: order-independent ties), and so do the same tables
+    with the BLAS rebuilt (option rebuild_bvh)."""
+    from refdb import RefDatabase
+
+    scene = ignis_amd.Scene.from_file(os.path.join(root, "scenes", name))
+    db, sv, keep = RefDatabase(scene, max_leaf=max_leaf).views()
+    adapted = ignis_amd.Scene.from_database(db, sv)
+    w, h, spi = 160, 120, 4
+    a = render_gpu(device, scene, w, h, spi)
+    b = render_gpu(device, adapted, w, h, spi)
+    ra = device.stats()
+    device.set_option("rebuild_bvh", 1)
+    try:
+        c = render_gpu(device, adapted, w, h, spi)
+    finally:
+        device.set_option("rebuild_bvh", 0)
+    assert np.isfinite(a).all() and a.mean() > 0
+    assert np.array_equal(a, b), f"max |diff| {np.abs(a - b).max()}"
+    assert np.array_equal(a, c)
+    assert ra["bvh_depth"] > 0
