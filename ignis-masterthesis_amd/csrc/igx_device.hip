@@ -111,6 +111,7 @@ struct FrameArgs {
     int chunk_iters;     // consecutive iterations (iter, iter + 1, ...) the chunk covers
     float inv_spi;
     int gen_n;           // > 0: this k_extend launch is bounce 0 and generates its n camera paths itself
+    int classify;        // surviving paths' stream class (see wave_append_paths): 0 all A, 1 B = inside a dielectric (eta != 1), 2 B = after a specular event
 };
 
 // path slot -> (local pixel, sample, iteration): slots run over the chunk's
@@ -154,8 +155,11 @@ static_assert(NSH == 64 && BLOCK % 64 == 0 && NSH % WAVES_PER_BLOCK == 0, "one s
 static_assert(BLOCK == TSTACK_STRIDE, "traversal stacks are laid out for BLOCK threads");
 
 // Records of all shards of a counter row: lane l reads shard l; wave-uniform.
+// A path-stream counter is two words (class A records from the front of the
+// shard, class B from its back, wave_append_paths); other streams leave the
+// second word 0.
 __device__ __forceinline__ int row_total(const int* row) {
-    int v = row[lane_id() * CSTRIDE];
+    int v = row[lane_id() * CSTRIDE] + row[lane_id() * CSTRIDE + 1];
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
     return __builtin_amdgcn_readfirstlane(v);
 }
@@ -182,19 +186,47 @@ __device__ __forceinline__ int gen_shard_count(int n, int s) {
     return (n >> 12) * 64 + (rem < 0 ? 0 : (rem > 64 ? 64 : rem));
 }
 
-// Wave-level compaction into two sharded streams: one returning atomic per
-// wave and stream (lanes 0 and 1 issue both in one instruction), positions
-// inside the wave by ballot prefix.  Needs every lane of the wave active.
-__device__ __forceinline__ void wave_append2(bool a, bool b, int* ca, int* cb, int& ia, int& ib) {
-    const int lane = lane_id();
-    const uint64_t ma = __ballot(a), mb = __ballot(b);
-    const uint64_t below = (1ull << lane) - 1ull;
-    const int want = lane == 0 ? __popcll(ma) : __popcll(mb);
-    int r = 0;
-    if (lane < 2 && want > 0) r = atomicAdd(lane == 0 ? ca : cb, want);
-    ia = __shfl(r, 0) + __popcll(ma & below);
-    ib = __shfl(r, 1) + __popcll(mb & below);
+// Records of path-stream shard s: `a` of class A at offsets [0, a) and n - a
+// of class B at offsets shard_cap - 1 down to shard_cap - (n - a); position
+// pos in [0, n) of the shard maps to stream index stream_index(s, pos, ...), so
+// consecutive positions, and so the 64 paths of one wave, share a class.
+struct ShardCount {
+    int a, n;
+};
+__device__ __forceinline__ ShardCount shard_count(const int* cnt, int s) {
+    const int a = uniform_load(cnt + s * CSTRIDE), b = uniform_load(cnt + s * CSTRIDE + 1);
+    return ShardCount{a, a + b};
 }
+__device__ __forceinline__ int stream_index(int s, int pos, int a, int shard_cap) {
+    return s * shard_cap + (pos < a ? pos : shard_cap - 1 - (pos - a));
+}
+
+// Wave-level compaction of the surviving paths (class A appended from the
+// front of the wave's shard, class B from its back: the next bounce's waves
+// then trace paths of one class, e.g. all inside a dielectric) and of the
+// shadow rays: one returning 64-bit atomic per stream (a/b counts in the two
+// words), lanes 0 and 1 issue both in one instruction; positions inside the
+// wave by ballot prefix.  Needs every lane of the wave active.
+__device__ __forceinline__ void wave_append_paths(bool alive, bool cls_b, bool shadow, int* cp, int* cs, int shard_cap,
+                                                  int& dst, int& sdst) {
+    const int lane = lane_id();
+    const uint64_t ma = __ballot(alive && !cls_b), mb = __ballot(alive && cls_b), ms = __ballot(shadow);
+    const uint64_t below = (1ull << lane) - 1ull;
+    const unsigned long long want = lane == 0 ? ((unsigned long long)__popcll(ma) | ((unsigned long long)__popcll(mb) << 32))
+                                              : (unsigned long long)__popcll(ms);
+    unsigned long long r = 0;
+    if (lane < 2 && want != 0) r = atomicAdd(reinterpret_cast<unsigned long long*>(lane == 0 ? cp : cs), want);
+    const int lo = (int)(uint32_t)r, hi = (int)(uint32_t)(r >> 32);
+    const int a0 = __shfl(lo, 0), b0 = __shfl(hi, 0), s0 = __shfl(lo, 1);
+    dst = cls_b ? shard_cap - 1 - (b0 + __popcll(mb & below)) : a0 + __popcll(ma & below);
+    sdst = s0 + __popcll(ms & below);
+}
+
+// stream class of a surviving path (FrameArgs::classify)
+__device__ __forceinline__ bool path_class_b(int classify, float eta, float inv_pdf) {
+    return classify == 1 ? eta != 1.0f : classify == 2 ? inv_pdf == 0.0f : false;
+}
+
 
 // ---------------------------------------------------------------------------
 // generate: camera rays (gpu_generate_rays, mapping_gpu.art:618-667;
@@ -482,7 +514,7 @@ __device__ __forceinline__ void flush_stats(const TraceStats& st, unsigned long 
 // ---------------------------------------------------------------------------
 // extend kernel: one bounce for every live path, compacted outputs.  Each
 // wave walks its shard of the input stream and appends survivors and shadow
-// rays to the same shard of the output streams (wave_append2): no block
+// rays to the same shard of the output streams (wave_append_paths): no block
 // barrier, so a wave whose rays finish early moves on to its next 64 paths.
 // ---------------------------------------------------------------------------
 template <int V, bool STATS, bool LDS>
@@ -499,7 +531,9 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : EXTEND_WAVES) 
     const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
     const WaveWork w = wave_work();
-    const int ns = gen ? gen_shard_count(fa.gen_n, w.s) : uniform_load(kc.cnt_in + w.s * CSTRIDE);
+    const ShardCount sc = gen ? ShardCount{gen_shard_count(fa.gen_n, w.s), gen_shard_count(fa.gen_n, w.s)}
+                              : shard_count(kc.cnt_in, w.s);
+    const int ns = sc.n;
     int* const c_out = kc.cnt_out + w.s * CSTRIDE;
     int* const c_sh = kc.cnt_shadow + w.s * CSTRIDE;
     for (int p0 = w.k * 64; p0 < ns; p0 += w.K * 64) {
@@ -523,7 +557,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : EXTEND_WAVES) 
                 ps.inv_pdf = 0;
                 ps.eta = 1.0f;
             } else {
-                ps = load_path(in, w.s * in.shard_cap + pos);
+                ps = load_path(in, stream_index(w.s, pos, sc.a, in.shard_cap));
             }
             if (ps.depth > 0) {
                 f3 Lacc;
@@ -533,7 +567,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : EXTEND_WAVES) 
             }
         }
         int dst, sdst;
-        wave_append2(alive, has_shadow, c_out, c_sh, dst, sdst);
+        wave_append_paths(alive, path_class_b(fa.classify, ps.eta, ps.inv_pdf), has_shadow, c_out, c_sh, out.shard_cap, dst, sdst);
         if (alive) store_path(out, w.s * out.shard_cap + dst, ps);
         if (has_shadow) {
             const int e = w.s * sh.shard_cap + sdst;
@@ -561,9 +595,10 @@ __global__ void __launch_bounds__(BLOCK, WAVES) k_trace(FrameArgs fa, SceneView 
     const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
     const WaveWork w = wave_work();
-    const int ns = uniform_load(cnt + w.s * CSTRIDE);
+    const ShardCount sc = shard_count(cnt, w.s);
+    const int ns = sc.n;
     for (int pos = w.k * 64 + lane_id(); pos < ns; pos += w.K * 64) {
-        const int i = w.s * in.shard_cap + pos;
+        const int i = stream_index(w.s, pos, sc.a, in.shard_cap);
         float4 p0 = in.p0[i], p1 = in.p1[i];
         int depth = (int)(__float_as_uint(p1.w) >> 24);
         int hit_ent = -1, hit_prim = -1;
@@ -591,12 +626,13 @@ __global__ void __launch_bounds__(BLOCK) k_shade(FrameArgs fa, SceneView sv, Pat
                                                  ShadowBuf sh, float4* L, KernelCounters kc, int tail_threshold) {
     if (row_total(kc.cnt_in) <= tail_threshold) return;
     const WaveWork w = wave_work();
-    const int ns = uniform_load(kc.cnt_in + w.s * CSTRIDE);
+    const ShardCount sc = shard_count(kc.cnt_in, w.s);
+    const int ns = sc.n;
     int* const c_out = kc.cnt_out + w.s * CSTRIDE;
     int* const c_sh = kc.cnt_shadow + w.s * CSTRIDE;
     for (int p0 = w.k * 64; p0 < ns; p0 += w.K * 64) {
         const int pos = p0 + lane_id();
-        const int i = w.s * in.shard_cap + pos;
+        const int i = stream_index(w.s, pos, sc.a, in.shard_cap);
         bool alive = false, has_shadow = false;
         PathState ps;
         ShadowRec sr;
@@ -613,7 +649,7 @@ __global__ void __launch_bounds__(BLOCK) k_shade(FrameArgs fa, SceneView sv, Pat
             }
         }
         int dst, sdst;
-        wave_append2(alive, has_shadow, c_out, c_sh, dst, sdst);
+        wave_append_paths(alive, path_class_b(fa.classify, ps.eta, ps.inv_pdf), has_shadow, c_out, c_sh, out.shard_cap, dst, sdst);
         if (alive) store_path(out, w.s * out.shard_cap + dst, ps);
         if (has_shadow) {
             const int e = w.s * sh.shard_cap + sdst;
@@ -644,9 +680,10 @@ __global__ void __launch_bounds__(BLOCK) k_finish(FrameArgs fa, SceneView gsv, P
     TraceStats sst{0, 0, 0, 0, 0, 0, 0};
     unsigned long long bounces = 0, shadows = 0;
     const WaveWork w = wave_work();
-    const int ns = uniform_load(cnt + w.s * CSTRIDE);
+    const ShardCount sc = shard_count(cnt, w.s);
+    const int ns = sc.n;
     for (int pos = w.k * 64 + lane_id(); pos < ns; pos += w.K * 64) {
-        PathState ps = load_path(in, w.s * in.shard_cap + pos);
+        PathState ps = load_path(in, stream_index(w.s, pos, sc.a, in.shard_cap));
         if (ps.depth <= 0) continue;
         for (;;) {
             f3 Lacc;
@@ -743,14 +780,14 @@ __global__ void __launch_bounds__(BLOCK, REFILL_WAVES) k_trace_refill(FrameArgs 
     const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
     const WaveWork w = wave_work();
-    const int ns = uniform_load(cnt + w.s * CSTRIDE);
-    const int base = w.s * in.shard_cap;
+    const ShardCount sc = shard_count(cnt, w.s);
+    const int ns = sc.n;
     const ShardSeq seq = shard_seq(w, ns);
     refill_loop<false, STATS, V>(
         sv, ts, seq.C, refill_min, [&](int c) { return seq(c); },
         [&](int pos, Trav& t) -> bool {
             if (pos >= ns) return false;
-            const int i = base + pos;
+            const int i = stream_index(w.s, pos, sc.a, in.shard_cap);
             const float4 p0 = in.p0[i], p1 = in.p1[i];
             const int depth = (int)(__float_as_uint(p1.w) >> 24);
             if (depth == 0) {
@@ -765,7 +802,7 @@ __global__ void __launch_bounds__(BLOCK, REFILL_WAVES) k_trace_refill(FrameArgs 
             return true;
         },
         [&](int pos, const Trav& t) {
-            const int i = base + pos;
+            const int i = stream_index(w.s, pos, sc.a, in.shard_cap);
             if (STATS && t.hit_ent >= 0) st.hits++;
             hits.h[i] = make_float4(t.tmax, t.hu, t.hv, __int_as_float(t.hit_ent));
             hits.prim[i] = t.hit_prim;
@@ -952,7 +989,7 @@ inline long long row_total(const Slot& s, int row) {
     if (row == 0) return s.n0;
     long long t = 0;
     const int* r = s.pinned + (size_t)row * CROW;
-    for (int k = 0; k < NSH; ++k) t += r[k * CSTRIDE];
+    for (int k = 0; k < NSH; ++k) t += r[k * CSTRIDE] + r[k * CSTRIDE + 1]; // class A + class B (wave_append_paths)
     return t;
 }
 
@@ -982,6 +1019,12 @@ struct igx_device {
     size_t table_bytes = 0;            // traversal tables (nodes, instances, triangles) of the current scene
     size_t shading_bytes = 0;          // shading tables (entities, vertices, normals, faces, materials, lights)
     int leaf_size = 4;
+    // stream class of surviving paths (FrameArgs::classify; option "path_classes"):
+    // paths inside a dielectric go to the back of their shard, so the next
+    // bounce's waves are all-inside or all-outside (diamond frame 152-155 ->
+    // 143-145 ms, S-deep 49.1 -> 47.5 ms per 8-iteration frame; bit-identical)
+    int classify_opt = 1;
+    float sah_node_cost = 1.0f;    // option "sah_node_cost_pct" (percent of one triangle test)
     // SBVH for BLAS up to SPATIAL_SPLIT_MAX_FACES triangles (option "spatial_splits"):
     // off by default -- measured slower on the diamond (196 -> 230 ms per frame)
     // and neutral on primitives, S-deep and soup-1M
@@ -1564,6 +1607,14 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     }
     else if (k == "spatial_splits") dev->spatial_splits = value != 0;
     else if (k == "rebuild_bvh") dev->rebuild_bvh = value != 0;
+    else if (k == "path_classes") {
+        if (value < 0 || value > 2) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "path_classes must be 0, 1 or 2");
+        dev->classify_opt = (int)value;
+    }
+    else if (k == "sah_node_cost_pct") {
+        if (value < 10 || value > 2000) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "sah_node_cost_pct must be in [10, 2000]");
+        dev->sah_node_cost = (float)value / 100.0f;
+    }
     else if (k == "bvh_leaf_size") {
         if (value < 1 || value > 16) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "bvh_leaf_size must be in [1, 16]");
         dev->leaf_size = (int)value;
@@ -1628,7 +1679,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
                         for (int a = 0; a < 3; ++a) tv[9 * (size_t)f + 3 * k + a] = m.vertices[3 * m.indices[3 * f + k] + a];
                 brs[s] = igx::build_sbvh2(bi, tv, dev->leaf_size);
             } else {
-                brs[s] = igx::build_bvh2(bi, dev->leaf_size);
+                brs[s] = igx::build_bvh2(bi, dev->leaf_size, 32, dev->sah_node_cost);
             }
         } catch (const std::exception& ex) {
             return fail(dev, IGX_ERR_INVALID_ARGUMENT, ex.what());
@@ -2021,6 +2072,7 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
     fa.frame = p->frame;
     fa.seed = p->seed;
     fa.inv_spi = 1.0f / (float)p->spi;
+    fa.classify = dev->classify_opt;
     long long local_pixels;
     if (list_mode) {
         // the previous ray list may still be read by a queued tail kernel
@@ -2345,11 +2397,25 @@ static igx_status trace_batch(igx_device* dev, const float* rays, int32_t n, uin
     HIPCHK(hipMalloc((void**)&d_tuv, (size_t)n * 3 * sizeof(float)));
     HIPCHK(hipMemcpy(d_rays, rays, (size_t)n * 8 * sizeof(float), hipMemcpyHostToDevice));
     int grid = grid_for(dev, n, MAX_BLOCKS_PER_CU);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (dev->timing) { // kernel time into ms_trace (traversal-only harness timing)
+        HIPCHK(hipEventCreate(&e0));
+        HIPCHK(hipEventCreate(&e1));
+        HIPCHK(hipEventRecord(e0, dev->stream));
+    }
 #define L_TH(S) hipLaunchKernelGGL(k_trace_hits<S>, dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, d_rays, n, flags, d_ep, d_tuv, any)
     IGX_DISPATCH_VARIANT(dev->variant, L_TH);
 #undef L_TH
     HIPCHK(hipGetLastError());
+    if (e1) HIPCHK(hipEventRecord(e1, dev->stream));
     HIPCHK(hipStreamSynchronize(dev->stream));
+    if (e1) {
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+        dev->stats.ms_trace += ms;
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    }
     HIPCHK(hipMemcpy(ent_prim, d_ep, (size_t)n * (any ? 1 : 2) * sizeof(int), hipMemcpyDeviceToHost));
     if (!any && tuv) HIPCHK(hipMemcpy(tuv, d_tuv, (size_t)n * 3 * sizeof(float), hipMemcpyDeviceToHost));
     (void)hipFree(d_rays);

@@ -9,6 +9,16 @@
 #include "device_math.h"
 #include "device_scene.h"
 
+// Branch-free BVH2 node step on scenes whose traversal stack fits the LDS column
+#ifndef IGX_BRANCHLESS
+#define IGX_BRANCHLESS 0
+#endif
+// Slab distances with packed FP32 FMAs (v_pk_fma_f32: a box's lo and hi bound
+// of one axis in one instruction)
+#ifndef IGX_PK_SLAB
+#define IGX_PK_SLAB 0
+#endif
+
 namespace igxd {
 
 struct SceneView {
@@ -171,6 +181,17 @@ __device__ __forceinline__ int node_step2(const SceneView& sv, const Trav& t, in
     const float4* np = sv.nodes + 4 * node;
     float4 a = np[0], b = np[1], c = np[2];
     int4 r = *reinterpret_cast<const int4*>(np + 3);
+#if IGX_PK_SLAB
+    // (lo, hi) of one axis per packed FMA; the same single-rounding fma per bound
+    const v2f ix = {t.idir.x, t.idir.x}, iy = {t.idir.y, t.idir.y}, iz = {t.idir.z, t.idir.z};
+    const v2f ox = {t.iorg.x, t.iorg.x}, oy = {t.iorg.y, t.iorg.y}, oz = {t.iorg.z, t.iorg.z};
+    const v2f px0 = pk_fma(v2f{a.x, a.y}, ix, ox), py0 = pk_fma(v2f{a.z, a.w}, iy, oy), pz0 = pk_fma(v2f{b.x, b.y}, iz, oz);
+    const v2f px1 = pk_fma(v2f{b.z, b.w}, ix, ox), py1 = pk_fma(v2f{c.x, c.y}, iy, oy), pz1 = pk_fma(v2f{c.z, c.w}, iz, oz);
+    float en0 = fmaxf(fmaxf(fminf(px0.x, px0.y), fminf(py0.x, py0.y)), fmaxf(fminf(pz0.x, pz0.y), t.tmin));
+    float ex0 = fminf(fminf(fmaxf(px0.x, px0.y), fmaxf(py0.x, py0.y)), fminf(fmaxf(pz0.x, pz0.y), t.tmax));
+    float en1 = fmaxf(fmaxf(fminf(px1.x, px1.y), fminf(py1.x, py1.y)), fmaxf(fminf(pz1.x, pz1.y), t.tmin));
+    float ex1 = fminf(fminf(fmaxf(px1.x, px1.y), fmaxf(py1.x, py1.y)), fminf(fmaxf(pz1.x, pz1.y), t.tmax));
+#else
     // child 0 box: lo (a.x, a.z, b.x) hi (a.y, a.w, b.y)
     // slab distances with explicit FMAs (the only contracted arithmetic
     // in the device code, built with -ffp-contract=off)
@@ -185,7 +206,21 @@ __device__ __forceinline__ int node_step2(const SceneView& sv, const Trav& t, in
     float s0z = fmaf(c.z, t.idir.z, t.iorg.z), s1z = fmaf(c.w, t.idir.z, t.iorg.z);
     float en1 = fmaxf(fmaxf(fminf(s0x, s1x), fminf(s0y, s1y)), fmaxf(fminf(s0z, s1z), t.tmin));
     float ex1 = fminf(fminf(fmaxf(s0x, s1x), fmaxf(s0y, s1y)), fminf(fmaxf(s0z, s1z), t.tmax));
+#endif
     bool h0 = en0 <= ex0, h1 = en1 <= ex1;
+#if IGX_BRANCHLESS
+    if constexpr (!SPILL) {
+        // one path for all lanes: the pop is a read of the top entry whatever
+        // the outcome, the push a store under the both-hit mask
+        const bool first0 = h0 && (!h1 || en0 < en1);
+        const int near = first0 ? r.x : r.y;
+        const int top = ts.lds[(sp - 1) * TSTACK_STRIDE];
+        if (h0 && h1) ts.lds[sp * TSTACK_STRIDE] = first0 ? r.y : r.x;
+        const bool any = h0 || h1;
+        sp += (h0 && h1) ? 1 : (any ? 0 : -1);
+        return any ? near : top;
+    }
+#endif
     if (h0 && h1) {
         bool first0 = en0 < en1;
         tpush<SPILL>(ts, sp, first0 ? r.y : r.x);
@@ -231,6 +266,29 @@ __device__ __forceinline__ int node_step4(const SceneView& sv, const Trav& t, in
     const float LY[4] = {ly.x, ly.y, ly.z, ly.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w};
     const float LZ[4] = {lz.x, lz.y, lz.z, lz.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
     int n = 0;
+#if IGX_PK_SLAB
+    // children (0, 1) and (2, 3) of one bound per packed FMA
+    const v2f ix = {t.idir.x, t.idir.x}, iy = {t.idir.y, t.idir.y}, iz = {t.idir.z, t.idir.z};
+    const v2f ox = {t.iorg.x, t.iorg.x}, oy = {t.iorg.y, t.iorg.y}, oz = {t.iorg.z, t.iorg.z};
+    const v2f LXa = pk_fma(v2f{lx.x, lx.y}, ix, ox), LXb = pk_fma(v2f{lx.z, lx.w}, ix, ox);
+    const v2f HXa = pk_fma(v2f{hx.x, hx.y}, ix, ox), HXb = pk_fma(v2f{hx.z, hx.w}, ix, ox);
+    const v2f LYa = pk_fma(v2f{ly.x, ly.y}, iy, oy), LYb = pk_fma(v2f{ly.z, ly.w}, iy, oy);
+    const v2f HYa = pk_fma(v2f{hy.x, hy.y}, iy, oy), HYb = pk_fma(v2f{hy.z, hy.w}, iy, oy);
+    const v2f LZa = pk_fma(v2f{lz.x, lz.y}, iz, oz), LZb = pk_fma(v2f{lz.z, lz.w}, iz, oz);
+    const v2f HZa = pk_fma(v2f{hz.x, hz.y}, iz, oz), HZb = pk_fma(v2f{hz.z, hz.w}, iz, oz);
+    const float TLX[4] = {LXa.x, LXa.y, LXb.x, LXb.y}, THX[4] = {HXa.x, HXa.y, HXb.x, HXb.y};
+    const float TLY[4] = {LYa.x, LYa.y, LYb.x, LYb.y}, THY[4] = {HYa.x, HYa.y, HYb.x, HYb.y};
+    const float TLZ[4] = {LZa.x, LZa.y, LZb.x, LZb.y}, THZ[4] = {HZa.x, HZa.y, HZb.x, HZb.y};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        float en = fmaxf(fmaxf(fminf(TLX[k], THX[k]), fminf(TLY[k], THY[k])), fmaxf(fminf(TLZ[k], THZ[k]), t.tmin));
+        float ex = fminf(fminf(fmaxf(TLX[k], THX[k]), fmaxf(TLY[k], THY[k])), fminf(fmaxf(TLZ[k], THZ[k]), t.tmax));
+        bool h = en <= ex;
+        d[k] = h ? en : INFINITY;
+        n += h ? 1 : 0;
+    }
+    (void)LX; (void)HX; (void)LY; (void)HY; (void)LZ; (void)HZ;
+#else
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         float nx, fx, ny, fy, nz, fz;
@@ -243,6 +301,7 @@ __device__ __forceinline__ int node_step4(const SceneView& sv, const Trav& t, in
         d[k] = h ? en : INFINITY;
         n += h ? 1 : 0;
     }
+#endif
     if (n == 0) return tpop<SPILL>(ts, sp);
     cswap(d[0], ref[0], d[1], ref[1]);
     cswap(d[2], ref[2], d[3], ref[3]);

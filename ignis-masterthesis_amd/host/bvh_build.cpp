@@ -40,6 +40,7 @@ struct Builder {
     const BvhBuildInput& in;
     int max_leaf;
     int bins;
+    float node_cost = 1.0f;     // SAH cost of a node step relative to one primitive test
     std::vector<uint32_t>& idx; // shared; each builder only touches its own ranges
     std::vector<TmpNode> nodes;
     int par_depth;              // subtrees above this depth are built on their own threads
@@ -104,9 +105,9 @@ struct Builder {
             }
         }
         float parent_area = box.half_area();
-        // leaf vs split: traversal cost 1, intersection cost 1 per primitive (relative)
+        // leaf vs split: node cost `node_cost`, intersection cost 1 per primitive (relative)
         float leaf_cost = (float)count;
-        float split_cost = best_axis >= 0 ? 1.0f + best_cost / std::max(parent_area, 1e-30f) : std::numeric_limits<float>::max();
+        float split_cost = best_axis >= 0 ? node_cost + best_cost / std::max(parent_area, 1e-30f) : std::numeric_limits<float>::max();
         if ((int)count <= max_leaf && leaf_cost <= split_cost) return me;
 
         uint32_t mid;
@@ -126,6 +127,7 @@ struct Builder {
         if (depth < par_depth && count >= 65536) {
             // left subtree on its own thread with its own node pool, merged after
             Builder sub(in, max_leaf, bins, idx, par_depth);
+            sub.node_cost = node_cost;
             auto fut = std::async(std::launch::async, [&sub, first, mid, depth] { return sub.build(first, mid - first, depth + 1); });
             r = build(mid, first + count - mid, depth + 1);
             int32_t sroot = fut.get();
@@ -204,7 +206,7 @@ void flatten(const std::vector<TmpNode>& tn, int32_t root, BvhBuildResult& res) 
 
 } // namespace
 
-BvhBuildResult build_bvh2(const BvhBuildInput& in, int max_leaf, int bins) {
+BvhBuildResult build_bvh2(const BvhBuildInput& in, int max_leaf, int bins, float node_cost) {
     if (max_leaf < 1 || max_leaf > (1 << kLeafCountBits)) throw std::invalid_argument("max_leaf out of range");
     BvhBuildResult res;
     const size_t n = in.count();
@@ -223,6 +225,7 @@ BvhBuildResult build_bvh2(const BvhBuildInput& in, int max_leaf, int bins) {
     // up to 2^4 concurrent subtree builders for large inputs
     const int par_depth = n >= 262144 ? 4 : 0;
     Builder b(in, max_leaf, bins, idx, par_depth);
+    b.node_cost = node_cost;
     b.nodes.reserve(2 * n / std::max(1, max_leaf) + 4);
     int32_t root = b.build(0, (uint32_t)n, 0);
     res.prim_order = std::move(idx);

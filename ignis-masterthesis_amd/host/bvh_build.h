@@ -53,8 +53,10 @@ struct BvhBuildResult {
     int32_t root_leaf_ref = 0;
 };
 
-// Build a BVH2 with binned SAH.  `max_leaf` caps primitives per leaf (<= 16).
-BvhBuildResult build_bvh2(const BvhBuildInput& in, int max_leaf, int bins = 32);
+// Build a BVH2 with binned SAH.  `max_leaf` caps primitives per leaf (<= 16);
+// `node_cost` is the SAH cost of a node step relative to one primitive test
+// (a split is kept when node_cost + SAH(children) < primitive count).
+BvhBuildResult build_bvh2(const BvhBuildInput& in, int max_leaf, int bins = 32, float node_cost = 1.0f);
 
 // Binned SAH with spatial splits (SBVH) over triangles: `tri9` holds the
 // three vertices of primitive i at [9 i, 9 i + 9).  A triangle may be

@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_PKG_DIR), "libigx.so")
+# IGX_LIB_PATH: a variant build of the same library (dev A/B runs, tools/ab_libs.sh)
+LIB_PATH = os.environ.get("IGX_LIB_PATH") or os.path.join(os.path.dirname(_PKG_DIR), "libigx.so")
 
 # ---- igx_scene.h ----------------------------------------------------------
 

@@ -331,6 +331,34 @@ def test_split_and_refill_invariance(device, root, name):
     assert imgs[0].sum() > 0
 
 
+@pytest.mark.parametrize("name", ["diamond_scene.json", "s_deep.json"])
+def test_path_class_invariance(device, root, name):
+    """Surviving paths split into two stream classes (inside a dielectric or
+    not, or after a specular event: front / back of each shard) render the same
+    image bit for bit with the same ray counts as one class, on the fused and
+    the split schedule, and through the tail kernel (tail threshold 0 / all)."""
+    sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", name))
+    imgs, counts = [], []
+    try:
+        device.upload(sc)
+        for classes, split, tail in [(0, -1, -1), (1, -1, -1), (2, -1, -1), (1, 1, -1), (1, 0, 0), (1, -1, 1 << 30)]:
+            device.set_option("path_classes", classes)
+            device.set_option("split", split)
+            device.set_option("tail_threshold", tail)
+            device.reset_stats()
+            imgs.append(render_gpu(device, sc, 112, 80, 4))
+            st = device.stats()
+            counts.append((st["camera_rays"], st["bounce_rays"], st["shadow_rays"]))
+    finally:
+        device.set_option("path_classes", 1)
+        device.set_option("split", -1)
+        device.set_option("tail_threshold", -1)
+    for im, c in zip(imgs[1:], counts[1:]):
+        np.testing.assert_array_equal(imgs[0], im)
+        assert c == counts[0]
+    assert imgs[0].sum() > 0
+
+
 @pytest.mark.parametrize("name", ["diamond_scene.json", "primitives.json", "s_deep.json", "s_soup_1m.json"])
 def test_occlusion_parity(device, root, name):
     sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", name))

@@ -1,0 +1,33 @@
+"""Dev tool: instrumented per-ray traversal statistics of one iteration
+(node / instance / triangle visits per closest-hit and shadow ray, wave-level
+node-loop and leaf-phase iterations per 64 rays, SIMD efficiency).
+usage: ray_stats.py [scene.json] [options json]"""
+import json, os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ignis-masterthesis_amd"))
+import ignis_amd
+
+scene = ignis_amd.Scene.from_file(os.path.join(ROOT, sys.argv[1] if len(sys.argv) > 1 else "scenes/diamond_scene.json"))
+W, H = scene.film_size
+dev = ignis_amd.Device(0)
+for k, v in (json.loads(sys.argv[2]) if len(sys.argv) > 2 else {}).items():
+    dev.set_option(k, v)
+dev.upload(scene)
+p = ignis_amd.RenderParams(); p.width, p.height, p.spi = W, H, 8
+dev.render(p); dev.synchronize()
+dev.reset_stats(); dev.set_option("instrument", 1); dev.clear()
+dev.render(p); dev.synchronize()
+s = dev.stats()
+n = s["camera_rays"] + s["bounce_rays"]
+ns = max(1, s["shadow_rays"])
+out = {"rays": n, "shadow_rays": s["shadow_rays"],
+       "nodes/ray": s["node_visits"] / n, "inst/ray": s["leaf_visits"] / n, "tris/ray": s["tri_tests"] / n,
+       "blas/ray": s["blas_enters"] / n,
+       "wave_node_iters/64rays": 64 * s["wave_node_iters"] / n, "wave_leaf_iters/64rays": 64 * s["wave_leaf_iters"] / n,
+       "simd_eff_nodes": s["node_visits"] / max(1, 64 * s["wave_node_iters"]),
+       "sh_nodes/ray": s["shadow_node_visits"] / ns, "sh_tris/ray": s["shadow_tri_tests"] / ns,
+       "sh_wave_node_iters/64rays": 64 * s["shadow_wave_node_iters"] / ns,
+       "sh_wave_leaf_iters/64rays": 64 * s["shadow_wave_leaf_iters"] / ns,
+       "depth": s["bvh_depth"], "width": s["bvh_width"], "lds_scene_bytes": s["lds_scene_bytes"],
+       "table_bytes": s["table_bytes"]}
+print(json.dumps({k: round(v, 3) if isinstance(v, float) else v for k, v in out.items()}))

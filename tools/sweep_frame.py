@@ -17,7 +17,7 @@ p.width, p.height, p.spi = W, H, 8
 for o in opts:
     for k, v in o.items():
         dev.set_option(k, v)
-    if any(k in ("bvh_width", "bvh_leaf_size", "spatial_splits") for k in o):
+    if any(k in ("bvh_width", "bvh_leaf_size", "spatial_splits", "sah_node_cost_pct", "rebuild_bvh") for k in o):
         dev.upload(scene)
     dev.clear()
     dev.render_iterations(p, iters)  # warm-up, buffers sized
@@ -37,7 +37,11 @@ for o in opts:
             best = (dt, s)
     dt, s = best
     rays = s["camera_rays"] + s["bounce_rays"] + s["shadow_rays"]
+    import hashlib
+    fb, _ = dev.framebuffer(W * H * 3)
+    md5 = hashlib.md5(fb.tobytes()).hexdigest()[:12]
     print(json.dumps({"opt": o, "ms_frame": round(dt * 1e3, 2), "Mrays/s": round(rays / dt / 1e6, 1),
                       "ext": round(s["ms_extend"], 2), "tr": round(s["ms_trace"], 2), "sh": round(s["ms_shadow"], 2),
-                      "fin": round(s["ms_finish"], 2), "gen": round(s["ms_generate"], 2), "res": round(s["ms_resolve"], 2), "tail_rays": s["tail_bounce_rays"] + s["tail_shadow_rays"]}), flush=True)
+                      "fin": round(s["ms_finish"], 2), "gen": round(s["ms_generate"], 2), "res": round(s["ms_resolve"], 2), "tail_rays": s["tail_bounce_rays"] + s["tail_shadow_rays"],
+                      "launches_ext": s["launches_extend"], "fb_md5": md5}), flush=True)
 dev.close()
