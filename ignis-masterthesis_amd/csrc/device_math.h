@@ -16,9 +16,6 @@ constexpr float INV_PI_ = 0.31830988618379067154f; // core/common.art:8
 struct f3 {
     float x, y, z;
 };
-// two fp32 lanes of one VGPR pair: v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32
-typedef float v2f __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ v2f pk_fma(v2f a, v2f b, v2f c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
 __device__ __forceinline__ f3 add(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
 __device__ __forceinline__ f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
@@ -44,6 +41,8 @@ __device__ __forceinline__ float safe_rcp(float x) {
 }
 // safe_div / safe_sqrt / clampf (core/common.art:167-171)
 __device__ __forceinline__ float safe_div(float a, float b) { return fabsf(b) <= FLT_EPS_ ? 0.0f : a / b; }
+// clamp (core/common.art, integer form)
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 __device__ __forceinline__ float safe_sqrt(float a) { return sqrtf(fmaxf(0.0f, a)); }
 __device__ __forceinline__ float safe_div_one(float a, float b) { return fabsf(b) <= FLT_EPS_ ? 1.0f : a / b; }
 __device__ __forceinline__ float clampf(float v, float l, float u) { return fminf(u, fmaxf(l, v)); }

@@ -28,6 +28,7 @@
 #include "device_scene.h"
 #include "igx_kernels.h"
 #include "../host/bvh_build.h"
+#include "../host/light_select.h"
 
 #include <hip/hip_runtime.h>
 
@@ -389,7 +390,8 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
             if (Lt.delta) continue;
             f3 emit = mk(Lt.radiance[0], Lt.radiance[1], Lt.radiance[2]);
             float pdf_s = 1 / (4 * PI_);
-            float mis = sv.nee ? 1 / (1 + ps.inv_pdf * (1.0f / (float)sv.num_lights) * pdf_s) : 1.0f;
+            const float sel = sv.selector == SEL_UNIFORM ? 1.0f / (float)sv.num_lights : select_pdf(sv, li, ps.o);
+            float mis = sv.nee ? 1 / (1 + ps.inv_pdf * sel * pdf_s) : 1.0f;
             Lacc = add(Lacc, handle_color(sv, mulf(mul(ps.contrib, emit), mis)));
             has_l = true;
         }
@@ -405,7 +407,8 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
             const DevLight& Lt = sv.lights[m.light];
             f3 emit = mk(Lt.radiance[0], Lt.radiance[1], Lt.radiance[2]);
             float pdf_s = light_pdf_direct_solid<FULL>(sv, Lt, ps.o, dt, tmax * tmax, hu, hv);
-            float mis = sv.nee ? 1 / (1 + ps.inv_pdf * (1.0f / (float)sv.num_lights) * pdf_s) : 1.0f;
+            const float sel = sv.selector == SEL_UNIFORM ? 1.0f / (float)sv.num_lights : select_pdf(sv, m.light, ps.o);
+            float mis = sv.nee ? 1 / (1 + ps.inv_pdf * sel * pdf_s) : 1.0f;
             Lacc = add(Lacc, handle_color(sv, mulf(mul(ps.contrib, emit), mis)));
             has_l = true;
         }
@@ -417,8 +420,8 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
     const bool specular = bsdf_is_specular<FULL>(m);
     // on_shadow (pathtracer.art:52-112)
     if (sv.nee && !specular && sv.num_lights > 0 && ps.depth + 1 <= sv.max_depth) {
-        int lid = sv.num_lights <= 1 ? 0 : rnd.next_i32(0, sv.num_lights - 1);
-        float sel_pdf = 1.0f / (float)sv.num_lights;
+        float sel_pdf;
+        const int lid = select_light(sv, rnd, s.point, sel_pdf);
         const DevLight& Lt = sv.lights[lid];
         DirectSample ls = light_sample_direct<FULL>(sv, Lt, rnd, s);
         float pdf_l_s = pdf_as_solid(ls.pdf_value, ls.pdf_solid, ls.cos, ls.dist * ls.dist) * sel_pdf;
@@ -1904,6 +1907,12 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
         }
     int num_infinite = 0;
     for (auto& l : lights) num_infinite += l.infinite;
+    // NEE selector tables over the finite lights, in device order (host/light_select.h)
+    std::vector<igx_light> finite_lights;
+    for (uint32_t l = 0; l < desc->num_lights; ++l)
+        if (light_remap[l] >= num_infinite) finite_lights.push_back(desc->lights[l]);
+    // (pass 1 above numbers the finite lights in desc order, so this is device order)
+    const igx::LightSelectTables lsel = igx::build_light_select(desc->technique.light_selector, (int)lights.size(), finite_lights);
     std::vector<DevMaterial> mats(desc->num_materials);
     for (uint32_t i = 0; i < desc->num_materials; ++i) {
         const igx_material& m = desc->materials[i];
@@ -1970,7 +1979,8 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     if ((st = upload(dev, nodes, &sv.nodes)) || (st = upload(dev, tris, &sv.tris)) || (st = upload(dev, inst, &sv.inst)) ||
         (st = upload(dev, spheres, &sv.spheres)) || (st = upload(dev, ent, &sv.ent)) || (st = upload(dev, vtx, &sv.vtx)) ||
         (st = upload(dev, nrm, &sv.nrm)) || (st = upload(dev, idx, &sv.idx)) || (st = upload(dev, mats, &sv.mats)) ||
-        (st = upload(dev, lights, &sv.lights))) {
+        (st = upload(dev, lights, &sv.lights)) || (st = upload(dev, lsel.cdf, &sv.sel_cdf)) ||
+        (st = upload(dev, lsel.hierarchy, &sv.sel_tree))) {
         free_scene(dev);
         return st;
     }
@@ -1989,6 +1999,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     }
     sv.num_lights = (int)lights.size();
     sv.num_infinite = num_infinite;
+    sv.selector = lsel.selector;
     // bbox_radius(scene_bbox) * 1.01 (light/env.art:75; core/bbox.art:24)
     float dx = desc->scene_bbox_max[0] - desc->scene_bbox_min[0];
     float dy = desc->scene_bbox_max[1] - desc->scene_bbox_min[1];

@@ -9,16 +9,6 @@
 #include "device_math.h"
 #include "device_scene.h"
 
-// Branch-free BVH2 node step on scenes whose traversal stack fits the LDS column
-#ifndef IGX_BRANCHLESS
-#define IGX_BRANCHLESS 0
-#endif
-// Slab distances with packed FP32 FMAs (v_pk_fma_f32: a box's lo and hi bound
-// of one axis in one instruction)
-#ifndef IGX_PK_SLAB
-#define IGX_PK_SLAB 0
-#endif
-
 namespace igxd {
 
 struct SceneView {
@@ -42,6 +32,9 @@ struct SceneView {
     int num_nodes, num_inst, num_tris; // table sizes (for staging the traversal tables in LDS)
     int* spill;            // traversal-stack overflow area of the launching stream (see TStack)
     int node_f4;           // float4s per BVH node (4: BVH2, 8: 4-wide)
+    int selector;          // NEE light selector in effect (IGX_SELECT_*; host/light_select.h)
+    const float* sel_cdf;  // simple: CDF over the finite lights ([c_1 .. c_{n-1}, 1])
+    const uint32_t* sel_tree; // hierarchy: codes (padded to 4), then 8 words per entry
 };
 
 // Copy the traversal tables (nodes, instances, triangles) of a small scene
@@ -181,17 +174,6 @@ __device__ __forceinline__ int node_step2(const SceneView& sv, const Trav& t, in
     const float4* np = sv.nodes + 4 * node;
     float4 a = np[0], b = np[1], c = np[2];
     int4 r = *reinterpret_cast<const int4*>(np + 3);
-#if IGX_PK_SLAB
-    // (lo, hi) of one axis per packed FMA; the same single-rounding fma per bound
-    const v2f ix = {t.idir.x, t.idir.x}, iy = {t.idir.y, t.idir.y}, iz = {t.idir.z, t.idir.z};
-    const v2f ox = {t.iorg.x, t.iorg.x}, oy = {t.iorg.y, t.iorg.y}, oz = {t.iorg.z, t.iorg.z};
-    const v2f px0 = pk_fma(v2f{a.x, a.y}, ix, ox), py0 = pk_fma(v2f{a.z, a.w}, iy, oy), pz0 = pk_fma(v2f{b.x, b.y}, iz, oz);
-    const v2f px1 = pk_fma(v2f{b.z, b.w}, ix, ox), py1 = pk_fma(v2f{c.x, c.y}, iy, oy), pz1 = pk_fma(v2f{c.z, c.w}, iz, oz);
-    float en0 = fmaxf(fmaxf(fminf(px0.x, px0.y), fminf(py0.x, py0.y)), fmaxf(fminf(pz0.x, pz0.y), t.tmin));
-    float ex0 = fminf(fminf(fmaxf(px0.x, px0.y), fmaxf(py0.x, py0.y)), fminf(fmaxf(pz0.x, pz0.y), t.tmax));
-    float en1 = fmaxf(fmaxf(fminf(px1.x, px1.y), fminf(py1.x, py1.y)), fmaxf(fminf(pz1.x, pz1.y), t.tmin));
-    float ex1 = fminf(fminf(fmaxf(px1.x, px1.y), fmaxf(py1.x, py1.y)), fminf(fmaxf(pz1.x, pz1.y), t.tmax));
-#else
     // child 0 box: lo (a.x, a.z, b.x) hi (a.y, a.w, b.y)
     // slab distances with explicit FMAs (the only contracted arithmetic
     // in the device code, built with -ffp-contract=off)
@@ -206,21 +188,7 @@ __device__ __forceinline__ int node_step2(const SceneView& sv, const Trav& t, in
     float s0z = fmaf(c.z, t.idir.z, t.iorg.z), s1z = fmaf(c.w, t.idir.z, t.iorg.z);
     float en1 = fmaxf(fmaxf(fminf(s0x, s1x), fminf(s0y, s1y)), fmaxf(fminf(s0z, s1z), t.tmin));
     float ex1 = fminf(fminf(fmaxf(s0x, s1x), fmaxf(s0y, s1y)), fminf(fmaxf(s0z, s1z), t.tmax));
-#endif
     bool h0 = en0 <= ex0, h1 = en1 <= ex1;
-#if IGX_BRANCHLESS
-    if constexpr (!SPILL) {
-        // one path for all lanes: the pop is a read of the top entry whatever
-        // the outcome, the push a store under the both-hit mask
-        const bool first0 = h0 && (!h1 || en0 < en1);
-        const int near = first0 ? r.x : r.y;
-        const int top = ts.lds[(sp - 1) * TSTACK_STRIDE];
-        if (h0 && h1) ts.lds[sp * TSTACK_STRIDE] = first0 ? r.y : r.x;
-        const bool any = h0 || h1;
-        sp += (h0 && h1) ? 1 : (any ? 0 : -1);
-        return any ? near : top;
-    }
-#endif
     if (h0 && h1) {
         bool first0 = en0 < en1;
         tpush<SPILL>(ts, sp, first0 ? r.y : r.x);
@@ -266,29 +234,6 @@ __device__ __forceinline__ int node_step4(const SceneView& sv, const Trav& t, in
     const float LY[4] = {ly.x, ly.y, ly.z, ly.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w};
     const float LZ[4] = {lz.x, lz.y, lz.z, lz.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
     int n = 0;
-#if IGX_PK_SLAB
-    // children (0, 1) and (2, 3) of one bound per packed FMA
-    const v2f ix = {t.idir.x, t.idir.x}, iy = {t.idir.y, t.idir.y}, iz = {t.idir.z, t.idir.z};
-    const v2f ox = {t.iorg.x, t.iorg.x}, oy = {t.iorg.y, t.iorg.y}, oz = {t.iorg.z, t.iorg.z};
-    const v2f LXa = pk_fma(v2f{lx.x, lx.y}, ix, ox), LXb = pk_fma(v2f{lx.z, lx.w}, ix, ox);
-    const v2f HXa = pk_fma(v2f{hx.x, hx.y}, ix, ox), HXb = pk_fma(v2f{hx.z, hx.w}, ix, ox);
-    const v2f LYa = pk_fma(v2f{ly.x, ly.y}, iy, oy), LYb = pk_fma(v2f{ly.z, ly.w}, iy, oy);
-    const v2f HYa = pk_fma(v2f{hy.x, hy.y}, iy, oy), HYb = pk_fma(v2f{hy.z, hy.w}, iy, oy);
-    const v2f LZa = pk_fma(v2f{lz.x, lz.y}, iz, oz), LZb = pk_fma(v2f{lz.z, lz.w}, iz, oz);
-    const v2f HZa = pk_fma(v2f{hz.x, hz.y}, iz, oz), HZb = pk_fma(v2f{hz.z, hz.w}, iz, oz);
-    const float TLX[4] = {LXa.x, LXa.y, LXb.x, LXb.y}, THX[4] = {HXa.x, HXa.y, HXb.x, HXb.y};
-    const float TLY[4] = {LYa.x, LYa.y, LYb.x, LYb.y}, THY[4] = {HYa.x, HYa.y, HYb.x, HYb.y};
-    const float TLZ[4] = {LZa.x, LZa.y, LZb.x, LZb.y}, THZ[4] = {HZa.x, HZa.y, HZb.x, HZb.y};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        float en = fmaxf(fmaxf(fminf(TLX[k], THX[k]), fminf(TLY[k], THY[k])), fmaxf(fminf(TLZ[k], THZ[k]), t.tmin));
-        float ex = fminf(fminf(fmaxf(TLX[k], THX[k]), fmaxf(TLY[k], THY[k])), fminf(fmaxf(TLZ[k], THZ[k]), t.tmax));
-        bool h = en <= ex;
-        d[k] = h ? en : INFINITY;
-        n += h ? 1 : 0;
-    }
-    (void)LX; (void)HX; (void)LY; (void)HY; (void)LZ; (void)HZ;
-#else
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         float nx, fx, ny, fy, nz, fz;
@@ -301,7 +246,6 @@ __device__ __forceinline__ int node_step4(const SceneView& sv, const Trav& t, in
         d[k] = h ? en : INFINITY;
         n += h ? 1 : 0;
     }
-#endif
     if (n == 0) return tpop<SPILL>(ts, sp);
     cswap(d[0], ref[0], d[1], ref[1]);
     cswap(d[2], ref[2], d[3], ref[3]);
@@ -858,6 +802,129 @@ __device__ __forceinline__ float light_pdf_direct_solid(const SceneView& sv, con
     }
     (void)cos; (void)dist2; (void)hu; (void)hv;
     return 1 / (4 * PI_); // env spherical: equal_area_sphere_pdf
+}
+
+// ---------------------------------------------------------------------------
+// NEE light selection (light/light_selector.art).  Lights are ordered infinite
+// first; finite light f is sv.lights[num_infinite + f].  "uniform" picks any
+// light with probability 1/n; "simple" samples the finite lights by a flux
+// CDF (make_cdf_light_selector, core/cdf.art:40-70) and "hierarchy" by a
+// light BVH walked from the shading point (make_hierarchy_light_selector,
+// light/light_hierarchy.art); with infinite lights both spend half the
+// probability on picking one of those uniformly.  Light counts are
+// compile-time constants in the reference's generated code, so a single
+// light costs no random draw (pick_light_id, make_light_hierarchy).
+// ---------------------------------------------------------------------------
+constexpr int SEL_UNIFORM = 0, SEL_SIMPLE = 1, SEL_HIERARCHY = 2;
+
+// make_cdf_1d (core/cdf.art:40-45): get(0) = 0, get(i) = cdf[i - 1]
+__device__ __forceinline__ float cdf_get(const float* cdf, int i) { return i == 0 ? 0.0f : cdf[i - 1]; }
+__device__ __forceinline__ int cdf_sample_discrete(const float* cdf, int n, float u, float& pdf) {
+    // interval::binary_search(n + 1, get(i) <= u) (core/interval.art:7-23)
+    int first = 0, len = n + 1;
+    while (len > 0) {
+        const int half = len / 2, middle = first + half;
+        if (cdf_get(cdf, middle) <= u) {
+            first = middle + 1;
+            len -= half + 1;
+        } else {
+            len = half;
+        }
+    }
+    const int off = min(clampi(first - 1, 0, n), n - 1);
+    pdf = cdf_get(cdf, off + 1) - cdf_get(cdf, off);
+    return off;
+}
+
+// light hierarchy entry (light_hierarchy::load_entry, light/light_hierarchy.art:24-37)
+struct LhEntry {
+    f3 pos, dir;
+    float flux;
+    int id;
+    bool has_dir, is_leaf;
+};
+__device__ __forceinline__ LhEntry lh_load(const uint32_t* entries, int id) {
+    const float4 e1 = *reinterpret_cast<const float4*>(entries + 8 * id);
+    const float4 e2 = *reinterpret_cast<const float4*>(entries + 8 * id + 4);
+    const int index = __float_as_int(e2.w);
+    return LhEntry{mk(e1.x, e1.y, e1.z), mk(e2.x, e2.y, e2.z), fabsf(e1.w), index < 0 ? -index - 1 : index,
+                   !signbit(e1.w), index >= 0};
+}
+// get_entry_cost / get_left_prop (light/light_hierarchy.art:39-56)
+__device__ __forceinline__ float lh_cost(const LhEntry& e, f3 pos) {
+    const f3 cdir = sub(e.pos, pos);
+    const float dist2 = dot(cdir, cdir);
+    const float cos_d = e.has_dir ? fabsf(dot(e.dir, normalize(cdir))) : 1.0f;
+    return safe_div(e.flux * cos_d, dist2);
+}
+__device__ __forceinline__ float lh_left_prop(const LhEntry& l, const LhEntry& r, f3 pos) {
+    const float cl = lh_cost(l, pos), cr = lh_cost(r, pos);
+    return 1 / (1 + cr / cl);
+}
+
+// sample one finite light (id in [0, nf)) and its selection pdf among the finite lights
+__device__ __forceinline__ int finite_select(const SceneView& sv, int nf, Rng& rnd, f3 from, float& pdf) {
+    if (sv.selector == SEL_SIMPLE) return cdf_sample_discrete(sv.sel_cdf, nf, rnd.next_f32(), pdf);
+    if (nf == 1) { // make_light_hierarchy, single light (light_hierarchy.art:104-108)
+        pdf = 1.0f;
+        return 0;
+    }
+    const uint32_t* data = sv.sel_tree + ((nf + 3) & ~3); // sample_light_id (light_hierarchy.art:63-78)
+    float p = 1.0f;
+    LhEntry e = lh_load(data, 0);
+    while (!e.is_leaf) {
+        const LhEntry l = lh_load(data, e.id), r = lh_load(data, e.id + 1);
+        const float prop = lh_left_prop(l, r, from);
+        const bool is_left = rnd.next_f32() < prop;
+        e = is_left ? l : r;
+        p *= is_left ? prop : 1 - prop;
+    }
+    pdf = p;
+    return e.id;
+}
+__device__ __forceinline__ float finite_select_pdf(const SceneView& sv, int nf, int f, f3 from) {
+    if (sv.selector == SEL_SIMPLE) return cdf_get(sv.sel_cdf, f + 1) - cdf_get(sv.sel_cdf, f);
+    if (nf == 1) return 1.0f;
+    uint32_t code = sv.sel_tree[f]; // compute_pdf (light_hierarchy.art:80-97)
+    const uint32_t* data = sv.sel_tree + ((nf + 3) & ~3);
+    float p = 1.0f;
+    LhEntry e = lh_load(data, 0);
+    while (!e.is_leaf) {
+        const LhEntry l = lh_load(data, e.id), r = lh_load(data, e.id + 1);
+        const float prop = lh_left_prop(l, r, from);
+        const bool is_left = (code & 0x1u) == 0;
+        e = is_left ? l : r;
+        p *= is_left ? prop : 1 - prop;
+        code >>= 1;
+    }
+    return p;
+}
+
+// LightSelector::sample: light index and selection pdf
+__device__ __forceinline__ int select_light(const SceneView& sv, Rng& rnd, f3 from, float& pdf) {
+    const int n = sv.num_lights, ninf = sv.num_infinite, nf = n - ninf;
+    if (sv.selector == SEL_UNIFORM) { // make_uniform_light_selector (light_selector.art:26-44)
+        pdf = 1.0f / (float)n;
+        return n <= 1 ? 0 : rnd.next_i32(0, n - 1);
+    }
+    if (ninf == 0) return finite_select(sv, nf, rnd, from, pdf);
+    const float q = rnd.next_f32();
+    if (q < 0.5f) { // infinite_ratio 0.5
+        pdf = (1 / (float)ninf) * 0.5f;
+        return ninf <= 1 ? 0 : rnd.next_i32(0, ninf - 1);
+    }
+    float p;
+    const int f = finite_select(sv, nf, rnd, from, p);
+    pdf = p * (1 - 0.5f);
+    return ninf + f;
+}
+// LightSelector::pdf of light `lid` seen from `from`
+__device__ __forceinline__ float select_pdf(const SceneView& sv, int lid, f3 from) {
+    const int n = sv.num_lights, ninf = sv.num_infinite, nf = n - ninf;
+    if (sv.selector == SEL_UNIFORM) return n == 0 ? 1.0f : 1.0f / (float)n;
+    if (ninf == 0) return finite_select_pdf(sv, nf, lid, from);
+    if (lid < ninf) return (1 / (float)ninf) * 0.5f;
+    return finite_select_pdf(sv, nf, lid - ninf, from) * (1 - 0.5f);
 }
 
 // ---------------------------------------------------------------------------

@@ -449,7 +449,7 @@ static void build_scene(SceneStore& S, const Value& doc, const std::string& base
     }
 
     // ---- technique (PathTechnique.cpp:8-17) ----
-    igx_technique tech{64, 2, 0.0f, 1};
+    igx_technique tech{64, 2, 0.0f, 1, IGX_SELECT_UNIFORM};
     if (const Value* t = doc.find("technique")) {
         Props tp{t};
         std::string type = tp.string("type", "path");
@@ -459,6 +459,10 @@ static void build_scene(SceneStore& S, const Value& doc, const std::string& base
         tech.clamp = tp.number("clamp", 0.0f);
         tech.nee = tp.boolean("nee", true) ? 1 : 0;
         if (tp.boolean("aov_mis", false)) fail("technique.aov_mis (advanced shadow handling) is not supported");
+        // PathTechnique.cpp (light_selector) -> LoaderLight::generateLightSelector (LoaderLight.cpp:423-453):
+        // "hierarchy" and "simple" select their sampler, anything else is the uniform selector
+        const std::string sel = tp.string("light_selector", "");
+        tech.light_selector = sel == "hierarchy" ? IGX_SELECT_HIERARCHY : sel == "simple" ? IGX_SELECT_SIMPLE : IGX_SELECT_UNIFORM;
     }
     S.desc.technique = tech;
 
@@ -708,6 +712,10 @@ static void build_scene(SceneStore& S, const Value& doc, const std::string& base
                     for (int i = 0; i < 3; ++i) { L.origin[i] = o[i]; L.x_axis[i] = xa[i]; L.y_axis[i] = ya[i]; L.normal[i] = n[i]; }
                     L.area = igx::norm(igx::cross(xa, ya));
                     host_area = L.area;
+                    // AreaLight.cpp:66-69: position at the plane's centre, direction its normal
+                    const V3 c = o + xa * 0.5f + ya * 0.5f;
+                    for (int i = 0; i < 3; ++i) { L.select_position[i] = c[i]; L.select_direction[i] = n[i]; }
+                    L.select_has_direction = 1;
                 } else if (opt && sphere) {
                     // AreaLight.cpp:71-79, 146-152: make_sphere_area_emitter; the emitter's own
                     // area is compute_ellipsoid_area (shapes/sphere.art:21-27, P = 1.6)
@@ -722,6 +730,8 @@ static void build_scene(SceneStore& S, const Value& doc, const std::string& base
                     L.radius = r;
                     L.area = ellipsoid(1.6f);
                     host_area = ellipsoid(1.6075f); // approximate_ellipsoid_area (AreaLight.cpp:24-33)
+                    const V3 c = igx::xform_point(t, sphere->origin); // AreaLight.cpp:74-77
+                    for (int i = 0; i < 3; ++i) L.select_position[i] = c[i];
                 } else if (is_tri) {
                     // AreaLight.cpp:80-90, 153-168: make_shape_area_emitter over the mesh
                     const igx::TriMesh& mesh = shapes[ent.shape].mesh;
@@ -732,6 +742,10 @@ static void build_scene(SceneStore& S, const Value& doc, const std::string& base
                     float w = scaled_len(V3(ls.x, 0, 0)), h = scaled_len(V3(0, ls.y, 0)), d = scaled_len(V3(0, 0, ls.z));
                     float half_area = ls.x * (ls.y + ls.z) + ls.y * ls.z;
                     host_area = igx::compute_area(mesh) * ((w * h + w * d + h * d) / half_area);
+                    // AreaLight.cpp:84-86: the transformed bbox centre
+                    const V3 c = igx::xform_point(t, V3((sh.bbox_min[0] + sh.bbox_max[0]) / 2, (sh.bbox_min[1] + sh.bbox_max[1]) / 2,
+                                                        (sh.bbox_min[2] + sh.bbox_max[2]) / 2));
+                    for (int i = 0; i < 3; ++i) L.select_position[i] = c[i];
                 } else {
                     fail("area light '" + name + "': entity '" + ename + "' is not triangular");
                 }
@@ -747,6 +761,9 @@ static void build_scene(SceneStore& S, const Value& doc, const std::string& base
                     rad = lp.color("radiance", V3(1, 1, 1));
                 }
                 for (int i = 0; i < 3; ++i) L.radiance[i] = rad[i];
+                // AreaLight::precompute / computeFlux (AreaLight.cpp:99-113): mean of the power colour
+                const V3 pw = lp.has("power") ? lp.color("power", V3(1, 1, 1)) : lp.color("radiance", V3(1, 1, 1)) * (host_area * kPi);
+                L.select_flux = (pw.x + pw.y + pw.z) / 3;
                 S.materials[ent.material].light = (int)S.lights.size();
             } else if (type == "env" || type == "constant" || type == "uniform") {
                 // EnvironmentLight.cpp:28-78: constant radiance bakes to a 1x1 texture -> make_environment_light
@@ -761,7 +778,9 @@ static void build_scene(SceneStore& S, const Value& doc, const std::string& base
                 V3 pos = lp.vec3("position", V3());
                 V3 I = lp.color("intensity", V3(1, 1, 1));
                 L.type = IGX_LIGHT_POINT;
-                for (int i = 0; i < 3; ++i) { L.origin[i] = pos[i]; L.radiance[i] = I[i]; }
+                for (int i = 0; i < 3; ++i) { L.origin[i] = pos[i]; L.radiance[i] = I[i]; L.select_position[i] = pos[i]; }
+                const V3 pw = I * (4 * kPi); // PointLight.cpp:16-30
+                L.select_flux = (pw.x + pw.y + pw.z) / 3;
             } else if (type == "spot") {
                 if (lp.has("power")) fail("spot light '" + name + "': 'power' is not supported");
                 V3 pos = lp.vec3("position", V3());
@@ -771,6 +790,11 @@ static void build_scene(SceneStore& S, const Value& doc, const std::string& base
                 for (int i = 0; i < 3; ++i) { L.origin[i] = pos[i]; L.normal[i] = dir[i]; L.radiance[i] = I[i]; }
                 L.cutoff = lp.number("cutoff", 30.0f) * kDeg2Rad;
                 L.falloff = lp.number("falloff", 20.0f) * kDeg2Rad;
+                // SpotLight.cpp:17-38: flux = mean(intensity) * 2 pi (1 - (cos cutoff + cos falloff) / 2)
+                const V3 pw = I * (2 * kPi * (1 - 0.5f * (std::cos(L.cutoff) + std::cos(L.falloff))));
+                L.select_flux = (pw.x + pw.y + pw.z) / 3;
+                for (int i = 0; i < 3; ++i) { L.select_position[i] = pos[i]; L.select_direction[i] = dir[i]; }
+                L.select_has_direction = 1;
             } else if (type == "directional" || type == "sun") {
                 // DirectionalLight.cpp:20-32, SunLight.cpp:24-46; direction via
                 // LoaderUtils::getEA(...).toDirectionYUp() (LoaderUtils.cpp:140-156)
@@ -796,15 +820,6 @@ static void build_scene(SceneStore& S, const Value& doc, const std::string& base
                 fail("light '" + name + "': unsupported light type '" + type + "'");
             }
             S.lights.push_back(L);
-        }
-    }
-    if (S.lights.size() > 1) {
-        // Multiple lights use the hierarchy/cdf selectors in the reference
-        // (LoaderLight.cpp:423-440); only the uniform selector is restated.
-        if (const Value* t = doc.find("technique")) {
-            Props tp{t};
-            std::string sel = tp.string("light_selector", "uniform");
-            if (sel != "uniform") fail("light_selector '" + sel + "' is not supported (uniform only)");
         }
     }
 

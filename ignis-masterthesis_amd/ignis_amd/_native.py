@@ -53,7 +53,8 @@ class Light(C.Structure):
     _fields_ = [("type", C.c_int32), ("entity", C.c_int32), ("radiance", C.c_float * 3),
                 ("origin", C.c_float * 3), ("x_axis", C.c_float * 3), ("y_axis", C.c_float * 3),
                 ("normal", C.c_float * 3), ("area", C.c_float), ("cutoff", C.c_float), ("falloff", C.c_float),
-                ("radius", C.c_float)]
+                ("radius", C.c_float), ("select_position", C.c_float * 3), ("select_direction", C.c_float * 3),
+                ("select_has_direction", C.c_int32), ("select_flux", C.c_float)]
 
 
 class Camera(C.Structure):
@@ -62,7 +63,8 @@ class Camera(C.Structure):
 
 
 class Technique(C.Structure):
-    _fields_ = [("max_depth", C.c_int32), ("min_depth", C.c_int32), ("clamp", C.c_float), ("nee", C.c_int32)]
+    _fields_ = [("max_depth", C.c_int32), ("min_depth", C.c_int32), ("clamp", C.c_float), ("nee", C.c_int32),
+                ("light_selector", C.c_int32)]
 
 
 class SceneDesc(C.Structure):

@@ -128,6 +128,13 @@ typedef struct igx_light {
     float area;            /* plane area; sphere: emitter area, compute_ellipsoid_area (shapes/sphere.art:21-27) */
     float cutoff, falloff; /* spot, radians; sun: cutoff = cosine of the sun's half angle */
     float radius;          /* sphere: object-space radius */
+    /* what the non-uniform light selectors know of a finite light
+     * (Light::position / direction / computeFlux, light/Light.h:22-23;
+     * AreaLight.cpp:46-112, PointLight.cpp:12-30, SpotLight.cpp:12-38) */
+    float select_position[3];
+    float select_direction[3];
+    int32_t select_has_direction;
+    float select_flux;     /* mean of the light's power colour */
 } igx_light;
 
 /* ---- camera / technique ------------------------------------------------ */
@@ -139,11 +146,16 @@ typedef struct igx_camera {
     float near_clip, far_clip;
 } igx_camera;
 
+/* light selection for next-event estimation (LoaderLight::generateLightSelector,
+ * LoaderLight.cpp:423-453; light/light_selector.art) */
+enum { IGX_SELECT_UNIFORM = 0, IGX_SELECT_SIMPLE = 1, IGX_SELECT_HIERARCHY = 2 };
+
 typedef struct igx_technique {
     int32_t max_depth;     /* PathTechnique.cpp:11, default 64 */
     int32_t min_depth;     /* default 2 */
     float clamp;           /* <= 0: no clamping */
     int32_t nee;           /* next-event estimation on */
+    int32_t light_selector;/* IGX_SELECT_*: "uniform" (default), "simple" (flux CDF), "hierarchy" (light BVH) */
 } igx_technique;
 
 typedef struct igx_scene_desc {

@@ -166,6 +166,8 @@ typedef struct {
     float sph[4];            /* sphere emitter: object-space centre, radius */
     float sph_area;          /* compute_ellipsoid_area (shapes/sphere.art:21-27) */
     int faces;               /* shape emitter: primitive_count */
+    float sel_pos[3], sel_dir[3], sel_flux; /* Light::position / direction / computeFlux */
+    int sel_has_dir;
 } olight;
 
 struct oracle_scene {
@@ -176,7 +178,229 @@ struct oracle_scene {
     int num_lights, num_infinite;
     int* mat_light;             /* remapped light index per material */
     float scene_radius;
+    int selector;               /* light selector in effect (IGX_SELECT_*) */
+    float* sel_cdf;             /* simple: CDF over the finite lights */
+    int* lh_codes;              /* hierarchy: per finite light, bit d = right at depth d */
+    float* lh_nodes;            /* hierarchy: 8 floats per node (pos, signed flux, dir, index bits) */
 };
+
+/* ---- NEE light selection (light/light_selector.art) ----------------------
+ * Finite light f is s->lights[num_infinite + f].  "simple": flux CDF
+ * (CDF::computeForArray, CDF.cpp:11-40; make_cdf_1d, core/cdf.art:40-45);
+ * "hierarchy": PointBvh (container/PointBvh.inl) turned into a light tree by
+ * LightHierarchy::setup (LightHierarchy.cpp:46-118), walked as in
+ * light/light_hierarchy.art.  One light or none, or no finite light: uniform
+ * (LoaderLight.cpp:423-453). */
+typedef struct { float lo[3], hi[3]; int axis; int index; } opnode; /* axis < 0: leaf of light `index` */
+
+static void pbox_extend(opnode* n, const float* p) {
+    for (int i = 0; i < 3; ++i) {
+        if (p[i] < n->lo[i]) n->lo[i] = p[i];
+        if (p[i] > n->hi[i]) n->hi[i] = p[i];
+    }
+}
+
+/* PointBvh::store: descend by the (grown) node's mid plane, split the leaf reached */
+static int pbvh_store(opnode* nodes, int count, int light, const float* p) {
+    if (count == 0) {
+        opnode n;
+        for (int i = 0; i < 3; ++i) n.lo[i] = n.hi[i] = p[i];
+        n.axis = -1;
+        n.index = 0;
+        nodes[0] = n;
+        return 1;
+    }
+    int at = 0;
+    for (;;) {
+        pbox_extend(&nodes[at], p);
+        if (nodes[at].axis < 0) break;
+        int ax = nodes[at].axis;
+        float mid = (nodes[at].hi[ax] + nodes[at].lo[ax]) / 2;
+        at = p[ax] < mid ? nodes[at].index : nodes[at].index + 1;
+    }
+    opnode box = nodes[at];
+    float d0 = box.hi[0] - box.lo[0], d1 = box.hi[1] - box.lo[1], d2 = box.hi[2] - box.lo[2];
+    int ax = 0;
+    float dm = d0;
+    if (d1 > dm) { ax = 1; dm = d1; }
+    if (d2 > dm) { ax = 2; dm = d2; }
+    float mid = dm / 2; /* PointBvh.inl: half the extent, compared with the coordinate */
+    int old_leaf = box.index;
+    nodes[at].index = count;
+    nodes[at].axis = ax;
+    opnode l = box, r = box;
+    float off = (box.hi[ax] - box.lo[ax]) * 0.5f;
+    l.hi[ax] -= off;
+    r.lo[ax] += off;
+    l.axis = r.axis = -1;
+    int new_left = p[ax] < mid;
+    l.index = new_left ? light : old_leaf;
+    r.index = new_left ? old_leaf : light;
+    nodes[count] = l;
+    nodes[count + 1] = r;
+    return count + 2;
+}
+
+/* populateInnerNodes: fills node entry `id` (8 floats), returns it in out[8] */
+static void lh_populate(const oracle_scene* s, const opnode* nodes, int id, uint32_t code, uint32_t depth, float* ent,
+                        int* codes, float* out) {
+    const opnode* n = &nodes[id];
+    float* e = ent + 8 * id;
+    if (n->axis < 0) {
+        const olight* L = &s->lights[s->num_infinite + n->index];
+        e[0] = L->sel_pos[0]; e[1] = L->sel_pos[1]; e[2] = L->sel_pos[2];
+        e[3] = L->sel_has_dir ? L->sel_flux : -L->sel_flux;
+        if (L->sel_has_dir) { e[4] = L->sel_dir[0]; e[5] = L->sel_dir[1]; e[6] = L->sel_dir[2]; }
+        else { e[4] = 0; e[5] = 0; e[6] = 1; }
+        int32_t lid = n->index;
+        memcpy(&e[7], &lid, 4);
+        codes[n->index] = (int)code;
+        memcpy(out, e, 32);
+        return;
+    }
+    float l[8], r[8];
+    lh_populate(s, nodes, n->index, code, depth + 1, ent, codes, l);
+    lh_populate(s, nodes, n->index + 1, code | (1u << depth), depth + 1, ent, codes, r);
+    e[0] = (n->hi[0] + n->lo[0]) / 2; e[1] = (n->hi[1] + n->lo[1]) / 2; e[2] = (n->hi[2] + n->lo[2]) / 2;
+    int32_t idx = -(n->index + 1);
+    memcpy(&e[7], &idx, 4);
+    if (l[3] < 0 && r[3] < 0) { e[4] = 0; e[5] = 0; e[6] = 1; e[3] = l[3] + r[3]; }
+    else if (l[3] < 0) { e[4] = 0; e[5] = 0; e[6] = 1; e[3] = -(-l[3] + r[3]); }
+    else if (r[3] < 0) { e[4] = 0; e[5] = 0; e[6] = 1; e[3] = -(l[3] - r[3]); }
+    else {
+        float d[3] = {l[4] + r[4], l[5] + r[5], l[6] + r[6]};
+        float len = sqrtf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+        e[4] = d[0] / len; e[5] = d[1] / len; e[6] = d[2] / len;
+        e[3] = l[3] + r[3];
+    }
+    memcpy(out, e, 32);
+}
+
+static void build_selector(oracle_scene* s, int selector) {
+    int nf = s->num_lights - s->num_infinite;
+    s->selector = IGX_SELECT_UNIFORM;
+    if (s->num_lights <= 1 || nf == 0) return;
+    if (selector == IGX_SELECT_SIMPLE) {
+        float* c = (float*)malloc(sizeof(float) * nf);
+        c[0] = s->lights[s->num_infinite].sel_flux;
+        for (int x = 1; x < nf; ++x) c[x] = c[x - 1] + s->lights[s->num_infinite + x].sel_flux;
+        float sum = c[nf - 1];
+        if (sum > 1e-5f) {
+            float inv = 1.0f / sum;
+            for (int x = 0; x < nf; ++x) c[x] *= inv;
+        } else {
+            float inv = 1.0f / (float)nf;
+            for (int x = 0; x < nf; ++x) c[x] = (float)x * inv;
+        }
+        c[nf - 1] = 1;
+        s->sel_cdf = c;
+        s->selector = IGX_SELECT_SIMPLE;
+    } else if (selector == IGX_SELECT_HIERARCHY) {
+        opnode* nodes = (opnode*)malloc(sizeof(opnode) * (2 * nf));
+        int count = 0;
+        for (int f = 0; f < nf; ++f) count = pbvh_store(nodes, count, f, s->lights[s->num_infinite + f].sel_pos);
+        s->lh_nodes = (float*)calloc((size_t)count * 8, sizeof(float));
+        s->lh_codes = (int*)calloc((size_t)nf, sizeof(int));
+        float root[8];
+        lh_populate(s, nodes, 0, 0, 0, s->lh_nodes, s->lh_codes, root);
+        free(nodes);
+        s->selector = IGX_SELECT_HIERARCHY;
+    }
+}
+
+static float cdf_at(const float* c, int i) { return i == 0 ? 0.0f : c[i - 1]; }
+
+typedef struct { v3 pos, dir; float flux; int id, has_dir, is_leaf; } olh_entry;
+static olh_entry lh_entry(const oracle_scene* s, int id) {
+    const float* e = s->lh_nodes + 8 * id;
+    int32_t index;
+    memcpy(&index, &e[7], 4);
+    olh_entry r = {V(e[0], e[1], e[2]), V(e[4], e[5], e[6]), fabsf(e[3]), index < 0 ? -index - 1 : index, !signbit(e[3]),
+                   index >= 0};
+    return r;
+}
+static float lh_cost(const olh_entry* e, v3 pos) {
+    v3 cdir = vsub(e->pos, pos);
+    float dist2 = vdot(cdir, cdir);
+    float cos_d = e->has_dir ? fabsf(vdot(e->dir, vnormalize(cdir))) : 1.0f;
+    return safe_div(e->flux * cos_d, dist2);
+}
+static float lh_prop(const olh_entry* l, const olh_entry* r, v3 pos) {
+    float cl = lh_cost(l, pos), cr = lh_cost(r, pos);
+    return 1 / (1 + cr / cl);
+}
+
+static int finite_select(const oracle_scene* s, rng_t* rnd, v3 from, float* pdf) {
+    int nf = s->num_lights - s->num_infinite;
+    if (s->selector == IGX_SELECT_SIMPLE) {
+        float u = rng_f32(rnd);
+        int first = 0, len = nf + 1; /* interval::binary_search */
+        while (len > 0) {
+            int half = len / 2, middle = first + half;
+            if (cdf_at(s->sel_cdf, middle) <= u) { first = middle + 1; len -= half + 1; }
+            else len = half;
+        }
+        int off = first - 1 < 0 ? 0 : (first - 1 > nf ? nf : first - 1);
+        if (off > nf - 1) off = nf - 1;
+        *pdf = cdf_at(s->sel_cdf, off + 1) - cdf_at(s->sel_cdf, off);
+        return off;
+    }
+    if (nf == 1) { *pdf = 1.0f; return 0; }
+    float p = 1.0f;
+    olh_entry e = lh_entry(s, 0);
+    while (!e.is_leaf) {
+        olh_entry l = lh_entry(s, e.id), r = lh_entry(s, e.id + 1);
+        float prop = lh_prop(&l, &r, from);
+        int left = rng_f32(rnd) < prop;
+        e = left ? l : r;
+        p *= left ? prop : 1 - prop;
+    }
+    *pdf = p;
+    return e.id;
+}
+static float finite_pdf(const oracle_scene* s, int f, v3 from) {
+    int nf = s->num_lights - s->num_infinite;
+    if (s->selector == IGX_SELECT_SIMPLE) return cdf_at(s->sel_cdf, f + 1) - cdf_at(s->sel_cdf, f);
+    if (nf == 1) return 1.0f;
+    uint32_t code = (uint32_t)s->lh_codes[f];
+    float p = 1.0f;
+    olh_entry e = lh_entry(s, 0);
+    while (!e.is_leaf) {
+        olh_entry l = lh_entry(s, e.id), r = lh_entry(s, e.id + 1);
+        float prop = lh_prop(&l, &r, from);
+        int left = (code & 1u) == 0;
+        e = left ? l : r;
+        p *= left ? prop : 1 - prop;
+        code >>= 1;
+    }
+    return p;
+}
+/* LightSelector::sample / pdf */
+static int select_light(const oracle_scene* s, rng_t* rnd, v3 from, float* pdf) {
+    int n = s->num_lights, ninf = s->num_infinite;
+    if (s->selector == IGX_SELECT_UNIFORM) {
+        *pdf = 1.0f / (float)n;
+        return n <= 1 ? 0 : rng_i32(rnd, 0, n - 1);
+    }
+    if (ninf == 0) return finite_select(s, rnd, from, pdf);
+    float q = rng_f32(rnd);
+    if (q < 0.5f) {
+        *pdf = (1 / (float)ninf) * 0.5f;
+        return ninf <= 1 ? 0 : rng_i32(rnd, 0, ninf - 1);
+    }
+    float p;
+    int f = finite_select(s, rnd, from, &p);
+    *pdf = p * (1 - 0.5f);
+    return ninf + f;
+}
+static float select_pdf(const oracle_scene* s, int lid, v3 from) {
+    int n = s->num_lights, ninf = s->num_infinite;
+    if (s->selector == IGX_SELECT_UNIFORM) return n == 0 ? 1.0f : 1.0f / (float)n;
+    if (ninf == 0) return finite_pdf(s, lid, from);
+    if (lid < ninf) return (1 / (float)ninf) * 0.5f;
+    return finite_pdf(s, lid - ninf, from) * (1 - 0.5f);
+}
+
 
 /* ---- binned-SAH BVH2, collapsed to 4-wide nodes --------------------------
  * The reference CPU device traverses BVH4 trees with Tri4 leaves built by
@@ -437,6 +661,10 @@ oracle_scene* oracle_scene_create(const igx_scene_desc* desc) {
             o->delta = L->type == IGX_LIGHT_POINT || L->type == IGX_LIGHT_SPOT || L->type == IGX_LIGHT_DIRECTIONAL ||
                        L->type == IGX_LIGHT_SUN;
             memcpy(o->rad, L->radiance, sizeof(o->rad));
+            memcpy(o->sel_pos, L->select_position, sizeof(o->sel_pos));
+            memcpy(o->sel_dir, L->select_direction, sizeof(o->sel_dir));
+            o->sel_flux = L->select_flux;
+            o->sel_has_dir = L->select_has_direction;
             memcpy(o->origin, L->origin, sizeof(o->origin));
             memcpy(o->normal, L->normal, sizeof(o->normal));
             if (L->type == IGX_LIGHT_PLANE) {
@@ -478,6 +706,7 @@ oracle_scene* oracle_scene_create(const igx_scene_desc* desc) {
     s->num_lights = k;
     s->num_infinite = 0;
     for (int i = 0; i < k; ++i) s->num_infinite += s->lights[i].infinite;
+    build_selector(s, desc->technique.light_selector);
     s->mat_light = (int*)malloc(sizeof(int) * (desc->num_materials ? desc->num_materials : 1));
     for (uint32_t m = 0; m < desc->num_materials; ++m) {
         int l = desc->materials[m].light;
@@ -502,6 +731,9 @@ void oracle_scene_free(oracle_scene* s) {
     free(s->tlas.nodes);
     free(s->tlas.order);
     free(s->lights);
+    free(s->sel_cdf);
+    free(s->lh_codes);
+    free(s->lh_nodes);
     free(s->mat_light);
     free(s);
 }
@@ -1646,7 +1878,7 @@ static v3 trace_path(const oracle_scene* s, const oracle_params* p, int x, int y
     v3 contrib = V(1, 1, 1);
     int depth = 1;
     v3 Lsum = V(0, 0, 0);
-    float sel_pdf = s->num_lights == 0 ? 1.0f : 1.0f / (float)s->num_lights;
+    const float uni_pdf = s->num_lights == 0 ? 1.0f : 1.0f / (float)s->num_lights;
     for (;;) {
         ohit h;
         trace_scene(s, &ray, 0, &h, &ps->tr);
@@ -1657,7 +1889,8 @@ static v3 trace_path(const oracle_scene* s, const oracle_params* p, int x, int y
                 if (L->delta) continue;
                 v3 emit = V(L->rad[0], L->rad[1], L->rad[2]);
                 float pdf_s = 1 / (4 * PI_);
-                float mis = tech->nee ? 1 / (1 + inv_pdf * sel_pdf * pdf_s) : 1.0f;
+                float sel = s->selector == IGX_SELECT_UNIFORM ? uni_pdf : select_pdf(s, li, ray.org);
+                float mis = tech->nee ? 1 / (1 + inv_pdf * sel * pdf_s) : 1.0f;
                 Lacc = vadd(Lacc, handle_color(s, vmulf(vmul(contrib, emit), mis)));
             }
             Lsum = vadd(Lsum, Lacc);
@@ -1673,7 +1906,8 @@ static v3 trace_path(const oracle_scene* s, const oracle_params* p, int x, int y
                 const olight* L = &s->lights[mlight];
                 v3 emit = V(L->rad[0], L->rad[1], L->rad[2]);
                 float pdf_s = area_pdf_direct_solid(s, L, ray.org, dt, h.t * h.t, h.u);
-                float mis = tech->nee ? 1 / (1 + inv_pdf * sel_pdf * pdf_s) : 1.0f;
+                float sel = s->selector == IGX_SELECT_UNIFORM ? uni_pdf : select_pdf(s, mlight, ray.org);
+                float mis = tech->nee ? 1 / (1 + inv_pdf * sel * pdf_s) : 1.0f;
                 Lacc = vadd(Lacc, handle_color(s, vmulf(vmul(contrib, emit), mis)));
             }
         }
@@ -1684,7 +1918,8 @@ static v3 trace_path(const oracle_scene* s, const oracle_params* p, int x, int y
         int specular = obsdf_specular(&bs);
         /* on_shadow */
         if (tech->nee && !specular && s->num_lights > 0 && depth + 1 <= tech->max_depth) {
-            int lid = s->num_lights <= 1 ? 0 : rng_i32(&r2, 0, s->num_lights - 1);
+            float sel_pdf;
+            int lid = select_light(s, &r2, surf.point, &sel_pdf);
             const olight* L = &s->lights[lid];
             odirect ls = light_sample_direct(s, L, &r2, &surf);
             float pdf_l_s = (ls.pdf_solid ? ls.pdf_value : ls.pdf_value * (ls.dist * ls.dist) / ls.cos) * sel_pdf;

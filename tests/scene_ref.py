@@ -264,6 +264,7 @@ def interpret(path):
         "film": (int(film[0]), int(film[1])),
         "technique": (int(tech.get("max_depth", 64)), int(tech.get("min_depth", 2)),
                       float(tech.get("clamp", 0.0)), bool(tech.get("nee", True))),
+        "light_selector": tech.get("light_selector", ""),
     }
     if "vfov" in cam:
         fov, vert = cam["vfov"], True
@@ -317,19 +318,29 @@ def interpret(path):
                 wc = corners @ T[:, :3].T + T[:, 3]
                 wn = np.linalg.det(T[:, :3]) * (np.linalg.inv(T[:, :3]).T @ n)  # orientation of the mapped face
                 rec.update(plane=True, corners=wc, normal=wn / np.linalg.norm(wn))
+                # Light::position / computeFlux of a plane emitter (AreaLight.cpp:66-69, 99-113)
+                area = np.linalg.norm(np.cross(wc[1] - wc[0], wc[2] - wc[0]))
+                if np.abs(np.dot(wc[3] - wc[0], wc[3] - wc[0]) - np.dot(wc[1] - wc[0], wc[1] - wc[0])
+                          - np.dot(wc[2] - wc[0], wc[2] - wc[0])) > 1e-3 * max(1.0, area):
+                    area = np.linalg.norm(np.cross(wc[1] - wc[0], wc[3] - wc[0]))  # corner order of the diagonal
+                rec.update(select_position=wc.mean(axis=0), select_flux=float(np.mean(rec["radiance"])) * area * math.pi)
             else:
                 rec["plane"] = False
             lights.append(rec)
         elif typ in ("env", "constant", "uniform"):
             lights.append({"type": "env", "radiance": _vec(l.get("radiance", 1.0)) * _vec(l.get("scale", 1.0))})
         elif typ == "point":
-            lights.append({"type": "point", "position": _vec(l.get("position"), [0, 0, 0]),
-                           "intensity": _vec(l.get("intensity", 1.0))})
+            I = _vec(l.get("intensity", 1.0))
+            lights.append({"type": "point", "position": _vec(l.get("position"), [0, 0, 0]), "intensity": I,
+                           "select_flux": float(np.mean(I)) * 4 * math.pi})  # PointLight.cpp:16-30
         elif typ == "spot":
             d = _vec(l.get("direction"), [0, 0, 1])
+            c_, f_ = math.radians(l.get("cutoff", 30)), math.radians(l.get("falloff", 20))
+            I = _vec(l.get("intensity", 1.0))
             lights.append({"type": "spot", "position": _vec(l.get("position"), [0, 0, 0]),
-                           "direction": d / np.linalg.norm(d), "intensity": _vec(l.get("intensity", 1.0)),
-                           "cutoff": math.radians(l.get("cutoff", 30)), "falloff": math.radians(l.get("falloff", 20))})
+                           "direction": d / np.linalg.norm(d), "intensity": I, "cutoff": c_, "falloff": f_,
+                           # SpotLight.cpp:17-38
+                           "select_flux": float(np.mean(I)) * 2 * math.pi * (1 - 0.5 * (math.cos(c_) + math.cos(f_)))})
         else:
             lights.append({"type": typ})
     out["lights"] = lights  # file order (the device puts infinite lights first itself)
@@ -363,6 +374,10 @@ def _check_light(i, L, rl, desc):
                     raise AssertionError(f"light {i}: plane corner {p.tolist()} not in {got.tolist()}")
             _close(L.normal[:], rl["normal"], f"light {i} plane normal")
             _close([L.area], [np.linalg.norm(np.cross(X, Y))], f"light {i} area")
+            _close(L.select_position[:], rl["select_position"], f"light {i} selector position")
+            _close(L.select_direction[:], rl["normal"], f"light {i} selector direction")
+            if not rl["power"]:
+                _close([L.select_flux], [rl["select_flux"]], f"light {i} selector flux", rtol=1e-4)
         elif L.type == 1:
             raise AssertionError(f"light {i}: plane emitter for a non-plane mesh")
     elif rl["type"] == "env":
@@ -374,6 +389,10 @@ def _check_light(i, L, rl, desc):
             raise AssertionError(f"light {i}: type {L.type}, expected point")
         _close(L.origin[:], rl["position"], f"light {i} position")
         _close(L.radiance[:], rl["intensity"], f"light {i} intensity")
+        _close(L.select_position[:], rl["position"], f"light {i} selector position")
+        _close([L.select_flux], [rl["select_flux"]], f"light {i} selector flux", rtol=1e-4)
+        if L.select_has_direction:
+            raise AssertionError(f"light {i}: a point light has no direction")
     elif rl["type"] == "spot":
         if L.type != 4:
             raise AssertionError(f"light {i}: type {L.type}, expected spot")
@@ -381,6 +400,8 @@ def _check_light(i, L, rl, desc):
         _close(L.normal[:], rl["direction"], f"light {i} direction")
         _close(L.radiance[:], rl["intensity"], f"light {i} intensity")
         _close([L.cutoff, L.falloff], [rl["cutoff"], rl["falloff"]], f"light {i} cone")
+        _close(L.select_direction[:], rl["direction"], f"light {i} selector direction")
+        _close([L.select_flux], [rl["select_flux"]], f"light {i} selector flux", rtol=1e-4)
 
 
 def check_desc(path, desc):
@@ -393,6 +414,10 @@ def check_desc(path, desc):
     if (t.max_depth, t.min_depth, t.nee != 0) != (ref["technique"][0], ref["technique"][1], ref["technique"][3]):
         raise AssertionError(f"technique {(t.max_depth, t.min_depth, t.nee)} vs {ref['technique']}")
     _close(t.clamp, ref["technique"][2], "technique.clamp")
+    # LoaderLight::generateLightSelector (LoaderLight.cpp:423-453): "hierarchy", "simple", else uniform
+    sel = ref["light_selector"]
+    if t.light_selector != {"hierarchy": 2, "simple": 1}.get(sel, 0):
+        raise AssertionError(f"technique.light_selector {t.light_selector} vs '{sel}'")
     c, rc = desc.camera, ref["camera"]
     _close(c.fov, rc["fov"], "camera.fov", rtol=1e-6)
     if bool(c.vertical_fov) != rc["vertical"]:

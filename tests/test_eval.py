@@ -93,9 +93,10 @@ def scene_from_doc(doc, base_dir):
     return ignis_amd.Scene.from_string(json.dumps(doc), base_dir)
 
 
-def pixel_coverage(device, scene, entity_name_index, grid=8):
+def pixel_coverage(tracer, scene, entity_name_index, grid=8):
     """Fraction of each pixel whose jittered camera ray (uniform pixel sampler,
-    sampler/pixel_sampler.art:4-10) first hits entity `entity_name_index`."""
+    sampler/pixel_sampler.art:4-10) first hits entity `entity_name_index`;
+    `tracer` is the HIP device or the oracle (trace_hits)."""
     import math
 
     w, h = scene.film_size
@@ -122,7 +123,7 @@ def pixel_coverage(device, scene, entity_name_index, grid=8):
             rays[:, 0:3] = eye
             rays[:, 3:6] = v.reshape(-1, 3)
             rays[:, 6], rays[:, 7] = c.near_clip, c.far_clip
-            ep, _ = device.trace_hits(rays, 1)
+            ep, _ = tracer.trace_hits(rays, 1)
             cov += (ep[:, 0] == entity_name_index).reshape(h, w)
     return cov / grid ** 2
 
@@ -187,6 +188,35 @@ def test_oracle_plane_d6_two_sided_lambert():
     expected = 2 * E.reference_image("plane-d6") - E.reference_image("plane-d1")
     err, _ = E.error_image(img, expected)
     assert err < E.eps_for("plane-d6") * (E.DEFAULT_SPP / spp), err
+
+
+def _multilight_floor(sc):
+    d = sc.desc
+    floor = [i for i in range(d.num_entities)
+             if d.materials[d.entities[i].material].kd[0] == pytest.approx(0.885809)]
+    assert len(floor) == 1
+    return floor[0], np.array(d.materials[d.entities[floor[0]].material].kd[:])
+
+
+@pytest.mark.parametrize("stem,selector", [("multilight-simple", 1), ("multilight-hierarchy", 2)])
+def test_oracle_multilight_light_selectors(stem, selector):
+    """CPU twin of the selector scenes: the oracle's flux-CDF ("simple") and
+    light-hierarchy selectors (its own restatement of CDF.cpp, PointBvh.inl,
+    LightHierarchy.cpp and light/light_selector.art, light_hierarchy.art)
+    against the reference image, with the back-side environment term of the
+    multilight scenes (see the module docstring), eps scaled by 1024/128."""
+    from oracle import oracle_py as O
+
+    spp = 128
+    sc = load(stem)
+    assert sc.desc.technique.light_selector == selector
+    floor, kd = _multilight_floor(sc)
+    cov = pixel_coverage(O.OracleScene(sc), sc, floor, grid=4)
+    img, bad = render_oracle(sc, spp)
+    expected = E.reference_image(stem) + 0.2 * kd[None, None, :] * cov[..., None]
+    err, _ = E.error_image(img, expected.astype(np.float32))
+    assert bad == 0
+    assert err < E.eps_for(stem) * (E.DEFAULT_SPP / spp), err
 
 
 def test_externals_replace_by_name():
@@ -264,13 +294,9 @@ def test_gpu_multilight_back_side_environment(device, stem):
         sc = load(stem)
     except ignis_amd.IgxError as e:
         pytest.skip(str(e))
-    d = sc.desc
-    floor = [i for i in range(d.num_entities)
-             if d.materials[d.entities[i].material].kd[0] == pytest.approx(0.885809)]
-    assert len(floor) == 1
-    kd = np.array(d.materials[d.entities[floor[0]].material].kd[:])
+    floor, kd = _multilight_floor(sc)
     device.upload(sc)
-    cov = pixel_coverage(device, sc, floor[0])
+    cov = pixel_coverage(device, sc, floor)
     img, _ = render_device(device, sc, E.DEFAULT_SPP)
     expected = E.reference_image(stem) + 0.2 * kd[None, None, :] * cov[..., None]
     err, _ = E.error_image(img, expected.astype(np.float32))
@@ -279,6 +305,7 @@ def test_gpu_multilight_back_side_environment(device, stem):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("stem", DIRECT + ["plane-d6", "cbox-d6", "flipped-prim-diffuse", "multilight",
+                                           "multilight-simple", "multilight-hierarchy",
                                            "three-planes-glass", "three-planes-interface"])
 def test_gpu_matches_oracle_on_evaluation_scenes(device, stem):
     """Same scene, seed and spi on the HIP device and the oracle: per-path
