@@ -22,7 +22,10 @@ constexpr int LEAF_COUNT_BITS = 4;
 // the spill area; bit 2 = the scene uses materials or lights beyond the basic
 // set (igx_kernels.h, bsdf_eval), compiled into the shading kernels only then.
 // The upload picks the variant per scene.
-constexpr int LDS_STACK = 16; // LDS traversal-stack entries per lane
+#ifndef IGX_LDS_STACK
+#define IGX_LDS_STACK 16
+#endif
+constexpr int LDS_STACK = IGX_LDS_STACK; // LDS traversal-stack entries per lane
 __host__ __device__ constexpr int variant_width(int v) { return (v & 2) ? 4 : 2; }
 __host__ __device__ constexpr bool variant_spill(int v) { return (v & 1) != 0; }
 __host__ __device__ constexpr bool variant_full(int v) { return (v & 4) != 0; }

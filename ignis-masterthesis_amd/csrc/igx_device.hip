@@ -33,7 +33,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
+#include <map>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -59,6 +61,12 @@ constexpr int MAX_BLOCKS_PER_CU = 8;  // 2048 threads per CU; grids never exceed
 constexpr int MAX_STACK = 128;        // traversal stack entries (LDS + spill) per ray
 constexpr int MAX_BOUNCES = 256;          // path depth is stored in 8 bits (p1.w, above the 24-bit RNG counter)
 constexpr long long MAX_CHUNK_PATHS = 1ll << 27; // paths per chunk (one wavefront), ~25 GB of stream buffers per slot
+// a path's slot in its chunk takes the low 27 bits of the slot word; the top
+// 5 carry 1 + the index of the enclosing entity it is in (at most 31 entities)
+constexpr int SLOT_BITS = 27;
+constexpr uint32_t SLOT_MASK = (1u << SLOT_BITS) - 1;
+constexpr int MAX_ENCLOSING = 31;
+static_assert(MAX_CHUNK_PATHS <= (1ll << SLOT_BITS), "path slots must fit the slot bits");
 constexpr long long PATH_SLOT_BYTES = 2 * 56 + 48 + 20 + 16; // two path buffers, shadow ray, hit record, radiance
 // Occupancy target (waves per SIMD) of k_extend, with global and with
 // LDS-staged traversal tables: 4 caps it at 128 VGPRs.  k_finish keeps the
@@ -85,7 +93,7 @@ constexpr int WAVES_PER_BLOCK = BLOCK / 64;
 constexpr int GRID_QUANTUM = NSH / WAVES_PER_BLOCK; // grids are multiples of this: every shard gets the same waves
 
 struct PathBuf {
-    float4* p0; // org.xyz, slot (int bits)
+    float4* p0; // org.xyz, slot (int bits; bits 27-31: 1 + the enclosing entity index the path is in, 0: none)
     float4* p1; // dir.xyz, rnd counter
     float4* p2; // contrib.rgb, inv_pdf
     float2* p3; // eta, RNG seed (uint bits): hashed once by k_generate, not per bounce
@@ -311,6 +319,7 @@ struct PathState {
     f3 contrib;
     float inv_pdf, eta;
     int slot, depth;
+    int inside; // index of the enclosing entity the path travels in (trace_enclosed), -1: none known
 };
 
 struct ShadowRec {
@@ -323,7 +332,9 @@ __device__ __forceinline__ PathState load_path(const PathBuf& in, int i) {
     PathState s;
     s.o = f3of(p0);
     s.d = f3of(p1);
-    s.slot = __float_as_int(p0.w);
+    const uint32_t sw = __float_as_uint(p0.w);
+    s.slot = (int)(sw & SLOT_MASK);
+    s.inside = (int)(sw >> SLOT_BITS) - 1;
     const uint32_t cd = __float_as_uint(p1.w);
     s.depth = (int)(cd >> 24);
     s.counter = cd & 0xFFFFFFu;
@@ -336,7 +347,7 @@ __device__ __forceinline__ PathState load_path(const PathBuf& in, int i) {
 }
 
 __device__ __forceinline__ void store_path(const PathBuf& out, int i, const PathState& s) {
-    out.p0[i] = make_float4(s.o.x, s.o.y, s.o.z, __int_as_float(s.slot));
+    out.p0[i] = make_float4(s.o.x, s.o.y, s.o.z, __uint_as_float((uint32_t)s.slot | ((uint32_t)(s.inside + 1) << SLOT_BITS)));
     out.p1[i] = make_float4(s.d.x, s.d.y, s.d.z, __uint_as_float(s.counter | ((uint32_t)s.depth << 24)));
     out.p2[i] = make_float4(s.contrib.x, s.contrib.y, s.contrib.z, s.inv_pdf);
     out.p3[i] = make_float2(s.eta, __uint_as_float(s.seed));
@@ -462,6 +473,17 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
     ps.inv_pdf = specular ? 0 : 1 / bs.pdf;
     ps.contrib = mulf(c2, 1 / rr);
     ps.eta = ps.eta * bs.eta;
+    // the entity the bounced ray travels in: entering an enclosing entity by
+    // transmission puts the path inside it, leaving by transmission or
+    // hitting anything else outside; a reflection inside keeps it inside
+    const int enc = sv.ent_enc[hit_ent];
+    if (enc < 0) {
+        ps.inside = -1;
+    } else if (dot(bs.in_dir, s.face_normal) * dot(rd, s.face_normal) > 0) { // continued through the surface
+        ps.inside = s.entering ? enc : -1;
+    } else if (ps.inside != enc) {
+        ps.inside = -1;
+    }
     ps.o = s.point;
     ps.d = bs.in_dir;
     ps.counter = rnd.counter;
@@ -480,7 +502,10 @@ __device__ __forceinline__ bool extend_step(const FrameArgs& fa, const SceneView
     ray_extent(fa, sv, ps.depth, ps.slot, tmin, tmax, rflags);
     int hit_ent, hit_prim;
     float hu = 0, hv = 0;
-    trace_ray<false, STATS, V>(sv, ps.o, ps.d, tmin, tmax, rflags, ts, hit_ent, hit_prim, hu, hv, st);
+    // a ray inside an enclosing entity hits it first: its BLAS alone decides
+    // (the full traversal from the TLAS root only when that finds nothing)
+    if (ps.inside < 0 || !trace_enclosed<STATS, V>(sv, ps.inside, ps.o, ps.d, tmin, tmax, rflags, ts, hit_ent, hit_prim, hu, hv, st))
+        trace_ray<false, STATS, V>(sv, ps.o, ps.d, tmin, tmax, rflags, ts, hit_ent, hit_prim, hu, hv, st);
     if (STATS && hit_ent >= 0) st.hits++;
     return shade_step<variant_full(V)>(fa, sv, ps, hit_ent, hit_prim, tmax, hu, hv, Lacc, has_l, has_shadow, sr);
 }
@@ -559,6 +584,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : EXTEND_WAVES) 
                 ps.contrib = mk(1, 1, 1); // init_pt_raypayload (technique/pathtracer.art:33-38)
                 ps.inv_pdf = 0;
                 ps.eta = 1.0f;
+                ps.inside = -1;
             } else {
                 ps = load_path(in, stream_index(w.s, pos, sc.a, in.shard_cap));
             }
@@ -609,7 +635,7 @@ __global__ void __launch_bounds__(BLOCK, WAVES) k_trace(FrameArgs fa, SceneView 
         if (depth > 0) {
             float tmin;
             uint32_t rflags;
-            ray_extent(fa, sv, depth, __float_as_int(p0.w), tmin, tmax, rflags);
+            ray_extent(fa, sv, depth, (int)(__float_as_uint(p0.w) & SLOT_MASK), tmin, tmax, rflags);
             trace_ray<false, STATS, V>(sv, f3of(p0), f3of(p1), tmin, tmax, rflags, ts, hit_ent, hit_prim, hu, hv, st);
             if (STATS && hit_ent >= 0) st.hits++;
         }
@@ -800,7 +826,7 @@ __global__ void __launch_bounds__(BLOCK, REFILL_WAVES) k_trace_refill(FrameArgs 
             }
             float tmin, tmax;
             uint32_t rflags;
-            ray_extent(fa, sv, depth, __float_as_int(p0.w), tmin, tmax, rflags);
+            ray_extent(fa, sv, depth, (int)(__float_as_uint(p0.w) & SLOT_MASK), tmin, tmax, rflags);
             trav_init(sv, t, f3of(p0), f3of(p1), tmin, tmax, rflags, ts);
             return true;
         },
@@ -1045,6 +1071,9 @@ struct igx_device {
     int bvh_width_opt = 0; // option "bvh_width": 0 = auto, 2, 4 (applies at the next upload)
     bool full_shading = false;     // the scene needs materials / lights beyond the basic set
     bool full_shading_opt = false; // option "full_shading": 1 = always compile-in the whole set
+    // option "enclosing": paths inside a closed, isolated dielectric trace
+    // only its BLAS (trace_enclosed); applies at the next upload
+    bool enclosing_opt = true;
     int scene_depth = 0;   // worst-case stack entries of the scene
     int* spill_main = nullptr; // spill columns of the main and tail streams
     int* spill_tail = nullptr;
@@ -1604,6 +1633,7 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
         dev->lds_scene_bytes = dev->has_scene && (int64_t)b <= value ? b : 0;
     }
     else if (k == "full_shading") dev->full_shading_opt = value != 0;
+    else if (k == "enclosing") dev->enclosing_opt = value != 0;
     else if (k == "bvh_width") {
         if (value != 0 && value != 2 && value != 4) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "bvh_width must be 0 (auto), 2 or 4");
         dev->bvh_width_opt = (int)value;
@@ -1629,6 +1659,27 @@ extern "C" igx_status igx_synchronize(igx_device* dev) {
     if (!dev) return IGX_ERR_INVALID_ARGUMENT;
     HIPCHK(hipSetDevice(dev->hip_device));
     return drain(dev);
+}
+
+// A closed triangle mesh: with vertices welded by position, every edge
+// borders exactly two faces (paths that enter it by transmission then hit it
+// again before leaving).  Checked up to 1 M faces.
+static bool closed_mesh(const igx_mesh& m) {
+    if (m.num_faces < 4 || m.num_faces > (1u << 20)) return false;
+    std::map<std::array<float, 3>, uint32_t> weld;
+    std::vector<uint32_t> id(m.num_vertices);
+    for (uint32_t v = 0; v < m.num_vertices; ++v)
+        id[v] = weld.emplace(std::array<float, 3>{m.vertices[3 * v], m.vertices[3 * v + 1], m.vertices[3 * v + 2]}, (uint32_t)weld.size()).first->second;
+    std::map<std::pair<uint32_t, uint32_t>, int> edges;
+    for (uint32_t f = 0; f < m.num_faces; ++f)
+        for (int k = 0; k < 3; ++k) {
+            uint32_t a = id[m.indices[3 * f + k]], b = id[m.indices[3 * f + (k + 1) % 3]];
+            if (a == b) return false;
+            ++edges[{std::min(a, b), std::max(a, b)}];
+        }
+    for (const auto& e : edges)
+        if (e.second != 2) return false;
+    return true;
 }
 
 extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* desc) {
@@ -1805,6 +1856,8 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
 
     // ---- TLAS over entities (leaf size 1), instance records ---------------
     std::vector<float4> inst, ent;
+    std::vector<int> ent_enc; // per entity: enclosing index or -1
+    std::vector<int2> enc_tab; // per enclosing index: entity, TLAS leaf slot
     int tlas_root = -1;
     int tlas_depth = 0;
     if (desc->num_entities > 0) {
@@ -1821,6 +1874,38 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
             float4 fi;
             std::memcpy(&fi, &info, 16);
             inst.push_back(fi);
+        }
+        // enclosing entities (trace_enclosed): a closed mesh of a non-thin
+        // dielectric whose world box keeps a margin from every other entity's
+        // box, at most MAX_ENCLOSING of them (ent_enc: index, enc_tab: entity and TLAS leaf slot)
+        ent_enc.assign(desc->num_entities, -1);
+        if (dev->enclosing_opt && desc->num_entities <= 4096) {
+            float slo[3], shi[3];
+            for (int a = 0; a < 3; ++a) { slo[a] = desc->scene_bbox_min[a]; shi[a] = desc->scene_bbox_max[a]; }
+            const float margin = 1e-4f * std::max({shi[0] - slo[0], shi[1] - slo[1], shi[2] - slo[2], 1e-6f});
+            std::vector<int> closed(desc->num_shapes, -1);
+            for (uint32_t slot = 0; slot < br.prim_order.size(); ++slot) {
+                const uint32_t e = br.prim_order[slot];
+                const igx_entity& en = desc->entities[e];
+                const igx_shape& sh = desc->shapes[en.shape];
+                const igx_material& mat = desc->materials[en.material];
+                if (sh.type != IGX_SHAPE_TRIMESH || mat.bsdf_type != IGX_BSDF_DIELECTRIC || mat.thin) continue;
+                if (closed[en.shape] < 0) closed[en.shape] = closed_mesh(desc->meshes[sh.mesh]) ? 1 : 0;
+                if (!closed[en.shape]) continue;
+                bool apart = true;
+                for (uint32_t o = 0; o < desc->num_entities && apart; ++o) {
+                    if (o == e) continue;
+                    const igx_entity& q = desc->entities[o];
+                    bool overlap = true;
+                    for (int a = 0; a < 3; ++a)
+                        overlap = overlap && q.bbox_min[a] <= en.bbox_max[a] + margin && en.bbox_min[a] <= q.bbox_max[a] + margin;
+                    apart = !overlap;
+                }
+                if (apart && (int)enc_tab.size() < MAX_ENCLOSING) {
+                    ent_enc[e] = (int)enc_tab.size();
+                    enc_tab.push_back(make_int2((int)e, (int)slot));
+                }
+            }
         }
         for (uint32_t e = 0; e < desc->num_entities; ++e) {
             const igx_entity& en = desc->entities[e];
@@ -1980,7 +2065,8 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
         (st = upload(dev, spheres, &sv.spheres)) || (st = upload(dev, ent, &sv.ent)) || (st = upload(dev, vtx, &sv.vtx)) ||
         (st = upload(dev, nrm, &sv.nrm)) || (st = upload(dev, idx, &sv.idx)) || (st = upload(dev, mats, &sv.mats)) ||
         (st = upload(dev, lights, &sv.lights)) || (st = upload(dev, lsel.cdf, &sv.sel_cdf)) ||
-        (st = upload(dev, lsel.hierarchy, &sv.sel_tree))) {
+        (st = upload(dev, lsel.hierarchy, &sv.sel_tree)) || (st = upload(dev, ent_enc, &sv.ent_enc)) ||
+        (st = upload(dev, enc_tab, &sv.enc))) {
         free_scene(dev);
         return st;
     }

@@ -32,6 +32,8 @@ struct SceneView {
     int num_nodes, num_inst, num_tris; // table sizes (for staging the traversal tables in LDS)
     int* spill;            // traversal-stack overflow area of the launching stream (see TStack)
     int node_f4;           // float4s per BVH node (4: BVH2, 8: 4-wide)
+    const int* ent_enc;    // per entity: its index among the enclosing entities (trace_enclosed), else -1
+    const int2* enc;       // per enclosing entity: entity id, TLAS leaf slot
     int selector;          // NEE light selector in effect (IGX_SELECT_*; host/light_select.h)
     const float* sel_cdf;  // simple: CDF over the finite lights ([c_1 .. c_{n-1}, 1])
     const uint32_t* sel_tree; // hierarchy: codes (padded to 4), then 8 words per entry
@@ -435,6 +437,58 @@ __device__ __forceinline__ bool trace_ray(const SceneView& sv, f3 o, f3 d, float
     hu = t.hu;
     hv = t.hv;
     return t.found;
+}
+
+// Closest hit of a ray that travels inside enclosing entity number `enc` (a closed,
+// non-thin dielectric mesh whose world box keeps a margin from every other
+// entity's box, igx_upload_scene).  The ray starts on the entity's surface,
+// i.e. in its box; along the ray the box is one interval from the start, every
+// hit on the entity lies in it and every other entity lies beyond it.  So a
+// hit the entity's BLAS finds is the closest hit of the whole scene -- the
+// same (t, u, v) the full traversal computes, from the same entity-space ray
+// (instance_test's transform).  Returns false (nothing written) when the
+// entity is not visible to the ray or its BLAS yields no hit; the caller then
+// traces the ray from the TLAS root.
+template <bool STATS, int V>
+__device__ __forceinline__ bool trace_enclosed(const SceneView& sv, int enc, f3 o, f3 d, float tmin, float& tmax,
+                                               uint32_t rflags, const TStack& ts, int& hit_ent, int& hit_prim, float& hu,
+                                               float& hv, TraceStats& st) {
+    const int slot = sv.enc[enc].y;
+    const float4* ip = sv.inst + 4 * slot;
+    const int4 info = *reinterpret_cast<const int4*>(ip + 3);
+    if ((rflags & RAY_TYPE_MASK) != ((rflags & (uint32_t)info.w) & RAY_TYPE_MASK)) return false;
+    const float4 m0 = ip[0], m1 = ip[1], m2 = ip[2];
+    Trav t;
+    t.o = o;
+    t.d = d;
+    t.lo = mk(m0.x * o.x + m0.y * o.y + m0.z * o.z + m0.w, m1.x * o.x + m1.y * o.y + m1.z * o.z + m1.w,
+              m2.x * o.x + m2.y * o.y + m2.z * o.z + m2.w);
+    t.ld = mk(m0.x * d.x + m0.y * d.y + m0.z * d.z, m1.x * d.x + m1.y * d.y + m1.z * d.z, m2.x * d.x + m2.y * d.y + m2.z * d.z);
+    t.idir = mk(safe_rcp(t.ld.x), safe_rcp(t.ld.y), safe_rcp(t.ld.z));
+    t.iorg = mk(-(t.lo.x * t.idir.x), -(t.lo.y * t.idir.y), -(t.lo.z * t.idir.z));
+    t.tmin = tmin;
+    t.tmax = tmax;
+    t.rflags = rflags;
+    t.cur_ent = info.x;
+    t.hit_ent = -1;
+    t.hit_prim = -1;
+    t.hu = 0;
+    t.hv = 0;
+    t.in_blas = true;
+    t.found = false;
+    ts.lds[0] = REF_EXIT;
+    t.sp = 1;
+    t.node = info.z; // BLAS root (or its only leaf)
+    if (STATS) { st.leaves++; st.blas++; }
+    while (!trav_step<false, STATS, V>(sv, t, ts, st)) {
+    }
+    if (!t.found) return false;
+    tmax = t.tmax;
+    hit_ent = t.hit_ent;
+    hit_prim = t.hit_prim;
+    hu = t.hu;
+    hv = t.hv;
+    return true;
 }
 
 // Persistent lanes with ray refill (Aila & Laine, "Understanding the

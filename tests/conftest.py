@@ -70,3 +70,18 @@ def emitter_scene(kind, max_depth=2, size=1000):
     ent = sc["entities"][-1]["name"]
     sc["lights"].append({"type": "area", "name": "Emitter", "entity": ent, "radiance": [1, 1, 1]})
     return sc
+
+
+def pytest_collection_modifyitems(config, items):
+    """With GPU tests selected, initialise torch's HIP runtime before any test
+    creates an igx device: torch (its own ROCm runtime) and libigx.so (the
+    image's) then share the GPU in one process, in the order bench.py uses."""
+    if not any(item.get_closest_marker("gpu") for item in items):
+        return
+    try:
+        import torch
+
+        if torch.cuda.is_available():
+            torch.zeros(1, device="cuda")
+    except Exception:  # no torch / no GPU: the GPU tests report it themselves
+        pass

@@ -359,6 +359,30 @@ def test_path_class_invariance(device, root, name):
     assert imgs[0].sum() > 0
 
 
+@pytest.mark.parametrize("name", ["diamond_scene.json", "materials.json", "s_deep.json"])
+def test_enclosing_shortcut_invariance(device, root, name):
+    """Paths inside a closed convex dielectric apart from every other entity
+    trace only its BLAS (trace_enclosed): the image and ray counts equal the
+    full traversal's bit for bit, through the wavefront and the tail kernel."""
+    sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", name))
+    imgs, counts = [], []
+    try:
+        for enclosing, tail in [(0, -1), (1, -1), (1, 0), (1, 1 << 30)]:
+            device.set_option("enclosing", enclosing)
+            device.set_option("tail_threshold", tail)
+            device.reset_stats()
+            imgs.append(render_gpu(device, sc, 112, 80, 4))
+            st = device.stats()
+            counts.append((st["camera_rays"], st["bounce_rays"], st["shadow_rays"]))
+    finally:
+        device.set_option("enclosing", 1)
+        device.set_option("tail_threshold", -1)
+    for im, c in zip(imgs[1:], counts[1:]):
+        np.testing.assert_array_equal(imgs[0], im)
+        assert c == counts[0]
+    assert imgs[0].sum() > 0
+
+
 @pytest.mark.parametrize("name", ["diamond_scene.json", "primitives.json", "s_deep.json", "s_soup_1m.json"])
 def test_occlusion_parity(device, root, name):
     sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", name))
