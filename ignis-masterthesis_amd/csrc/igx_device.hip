@@ -121,6 +121,7 @@ struct FrameArgs {
     float inv_spi;
     int gen_n;           // > 0: this k_extend launch is bounce 0 and generates its n camera paths itself
     int classify;        // surviving paths' stream class (see wave_append_paths): 0 all A, 1 B = inside a dielectric (eta != 1), 2 B = after a specular event
+    int dynamic;         // k_extend: waves take 64-path groups from per-shard work counters (KernelCounters::work)
 };
 
 // path slot -> (local pixel, sample, iteration): slots run over the chunk's
@@ -311,6 +312,7 @@ struct KernelCounters {
     int* cnt_out;
     int* cnt_shadow;
     unsigned long long* stats; // 9 counters (instrumentation)
+    int* work;                 // per-shard group counters of this bounce (FrameArgs::dynamic)
 };
 
 struct PathState {
@@ -539,6 +541,39 @@ __device__ __forceinline__ void flush_stats(const TraceStats& st, unsigned long 
     }
 }
 
+// Dynamic distribution of a launch's groups of 64 stream positions: the
+// wave takes the next group of shard s from that shard's counter (work +
+// s * CSTRIDE, one returning atomic per group); once s is exhausted it marks
+// s in the launch's mask of exhausted shards (work + CROW, 64 bits), reads the
+// mask (a coherent load: the scalar cache would hold it stale for the whole
+// launch) and moves on to the next shard still open.  Returns the group index
+// in shard s (s and n updated), or -1 once every shard is exhausted.  Waves
+// that drew short paths take more groups, so a launch no longer waits on the
+// wave with the slowest fixed share.
+template <class CountOf>
+__device__ __forceinline__ int take_group(int* work, int& s, uint64_t& done, int n, CountOf count_of) {
+    unsigned long long* const done_mask = reinterpret_cast<unsigned long long*>(work + CROW);
+    for (;;) {
+        if (!((done >> s) & 1ull)) {
+            int v = 0;
+            if (lane_id() == 0) v = atomicAdd(work + s * CSTRIDE, 1);
+            v = __shfl(v, 0);
+            if (v * 64 < n) return v;
+            if (lane_id() == 0) atomicOr(done_mask, 1ull << s);
+            done |= 1ull << s;
+        }
+        unsigned long long m = 0;
+        if (lane_id() == 0) m = __hip_atomic_load(done_mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        done |= (uint64_t)__shfl(m, 0);
+        const uint64_t open = ~done;
+        if (!open) return -1;
+        const int r = (s + 1) & (NSH - 1);
+        const uint64_t rot = (open >> r) | (r ? (open << (NSH - r)) : 0ull);
+        s = (r + __ffsll((unsigned long long)rot) - 1) & (NSH - 1);
+        n = count_of(s);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // extend kernel: one bounce for every live path, compacted outputs.  Each
 // wave walks its shard of the input stream and appends survivors and shadow
@@ -559,12 +594,33 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : EXTEND_WAVES) 
     const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
     const WaveWork w = wave_work();
-    const ShardCount sc = gen ? ShardCount{gen_shard_count(fa.gen_n, w.s), gen_shard_count(fa.gen_n, w.s)}
-                              : shard_count(kc.cnt_in, w.s);
-    const int ns = sc.n;
-    int* const c_out = kc.cnt_out + w.s * CSTRIDE;
-    int* const c_sh = kc.cnt_shadow + w.s * CSTRIDE;
-    for (int p0 = w.k * 64; p0 < ns; p0 += w.K * 64) {
+    // Groups of 64 positions of shard s: statically every K-th group from
+    // the wave's own (grid-stride), or (fa.dynamic) the next group a shard
+    // counter hands out, moving on to the following shards once the own is
+    // exhausted -- waves that drew fast paths take more groups, so a launch
+    // does not wait on the wave with the slowest share.  Survivors always go
+    // to the shard the group came from (its output never exceeds its input).
+    int s = w.s;
+    auto count_of = [&](int sh_) {
+        return gen ? ShardCount{gen_shard_count(fa.gen_n, sh_), gen_shard_count(fa.gen_n, sh_)} : shard_count(kc.cnt_in, sh_);
+    };
+    ShardCount sc = count_of(s);
+    uint64_t done = 0; // shards this wave knows to be exhausted (dynamic)
+    int p0 = w.k * 64;
+    for (;;) {
+        if (fa.dynamic) {
+            const int g = take_group(kc.work, s, done, sc.n, [&](int sh_) {
+                sc = count_of(sh_);
+                return sc.n;
+            });
+            if (g < 0) break;
+            p0 = g * 64;
+        } else if (p0 >= sc.n) {
+            break;
+        }
+        const int ns = sc.n;
+        int* const c_out = kc.cnt_out + s * CSTRIDE;
+        int* const c_sh = kc.cnt_shadow + s * CSTRIDE;
         const int pos = p0 + lane_id();
         bool alive = false, has_shadow = false;
         PathState ps;
@@ -572,7 +628,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : EXTEND_WAVES) 
         ps.depth = 0;
         if (pos < ns) {
             if (gen) { // inverse of gen_index
-                const int i = ((pos >> 6) << 12) | (w.s << 6) | (pos & 63);
+                const int i = ((pos >> 6) << 12) | (s << 6) | (pos & 63);
                 const GenPath g = gen_path(fa, sv, i);
                 L[i] = make_float4(0, 0, 0, 0);
                 ps.o = g.o;
@@ -586,7 +642,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : EXTEND_WAVES) 
                 ps.eta = 1.0f;
                 ps.inside = -1;
             } else {
-                ps = load_path(in, stream_index(w.s, pos, sc.a, in.shard_cap));
+                ps = load_path(in, stream_index(s, pos, sc.a, in.shard_cap));
             }
             if (ps.depth > 0) {
                 f3 Lacc;
@@ -597,13 +653,14 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : EXTEND_WAVES) 
         }
         int dst, sdst;
         wave_append_paths(alive, path_class_b(fa.classify, ps.eta, ps.inv_pdf), has_shadow, c_out, c_sh, out.shard_cap, dst, sdst);
-        if (alive) store_path(out, w.s * out.shard_cap + dst, ps);
+        if (alive) store_path(out, s * out.shard_cap + dst, ps);
         if (has_shadow) {
-            const int e = w.s * sh.shard_cap + sdst;
+            const int e = s * sh.shard_cap + sdst;
             sh.s0[e] = make_float4(sr.o.x, sr.o.y, sr.o.z, __int_as_float(ps.slot));
             sh.s1[e] = make_float4(sr.d.x, sr.d.y, sr.d.z, sr.tmax);
             sh.s2[e] = make_float4(sr.color.x, sr.color.y, sr.color.z, 0);
         }
+        if (!fa.dynamic) p0 += w.K * 64;
     }
     if (STATS) flush_stats<STATS>(st, kc.stats, 0, true);
 }
@@ -753,7 +810,7 @@ __global__ void __launch_bounds__(BLOCK) k_finish(FrameArgs fa, SceneView gsv, P
 // ---------------------------------------------------------------------------
 template <int V, bool STATS, bool LDS>
 __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, float4* L, const int* cnt,
-                                                  unsigned long long* stats) {
+                                                  unsigned long long* stats, int* work) {
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
@@ -761,9 +818,25 @@ __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, f
     const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
     const WaveWork w = wave_work();
-    const int ns = uniform_load(cnt + w.s * CSTRIDE);
-    for (int pos = w.k * 64 + lane_id(); pos < ns; pos += w.K * 64) {
-        const int i = w.s * sh.shard_cap + pos;
+    // groups of 64 shadow rays: grid-stride over the wave's own shard, or
+    // (work != nullptr) handed out by take_group
+    int s = w.s;
+    int ns = uniform_load(cnt + s * CSTRIDE);
+    uint64_t done = 0;
+    for (int p0 = w.k * 64;; p0 += w.K * 64) {
+        if (work) {
+            p0 = take_group(work, s, done, ns, [&](int sh_) {
+                ns = uniform_load(cnt + sh_ * CSTRIDE);
+                return ns;
+            });
+            if (p0 < 0) break;
+            p0 *= 64;
+        } else if (p0 >= ns) {
+            break;
+        }
+        const int pos = p0 + lane_id();
+        if (pos >= ns) continue;
+        const int i = s * sh.shard_cap + pos;
         float4 s0 = sh.s0[i], s1 = sh.s1[i];
         float tmax = s1.w;
         int e, p;
@@ -1007,7 +1080,10 @@ struct Slot {
     long long camera = 0;
 };
 
-constexpr int CTR_ROWS = 2 * MAX_BOUNCES + 4;
+// rows WORK_ROW0 + 4b: k_extend group counters of bounce b (take_group),
+// + 1: its mask of exhausted shards, + 2 / + 3: the same for k_shadow
+constexpr int WORK_ROW0 = 2 * MAX_BOUNCES + 4;
+constexpr int CTR_ROWS = WORK_ROW0 + 4 * MAX_BOUNCES;
 // BLAS with more triangles build without spatial splits (load time; their
 // triangles are small next to the scene in the suite's soups)
 constexpr uint32_t SPATIAL_SPLIT_MAX_FACES = 1u << 21;
@@ -1053,6 +1129,12 @@ struct igx_device {
     // bounce's waves are all-inside or all-outside (diamond frame 152-155 ->
     // 143-145 ms, S-deep 49.1 -> 47.5 ms per 8-iteration frame; bit-identical)
     int classify_opt = 1;
+    // option "dynamic" (bits): 1 = k_extend waves take their groups of 64
+    // paths from per-shard counters (take_group) instead of a fixed grid
+    // stride: diamond frame 142.4 -> 134.3 ms, materials 66.5 -> 54.6,
+    // primitives 36.8 -> 33.9, bit-identical images; 2 = the same for k_shadow
+    // (measured neutral to slightly slower: shadow rays cost about the same)
+    int dynamic_opt = 1;
     float sah_node_cost = 1.0f;    // option "sah_node_cost_pct" (percent of one triangle test)
     // SBVH for BLAS up to SPATIAL_SPLIT_MAX_FACES triangles (option "spatial_splits"):
     // off by default -- measured slower on the diamond (196 -> 230 ms per frame)
@@ -1310,7 +1392,7 @@ void launch_trace(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const
     else launch_trace_w<STATS, 1>(dev, s, grid, fa, in, cnt, tail);
 }
 template <bool STATS>
-void launch_shadow(igx_device* dev, Slot& s, int grid, const int* cnt) {
+void launch_shadow(igx_device* dev, Slot& s, int grid, const int* cnt, int* work) {
     if (use_refill(dev)) {
 #define L_SHR(S)                                                                                                        \
     if (dev->lds_scene_bytes)                                                                                            \
@@ -1324,12 +1406,12 @@ void launch_shadow(igx_device* dev, Slot& s, int grid, const int* cnt) {
         return;
     }
     if (dev->lds_scene_bytes) {
-#define L_SHL(S) hipLaunchKernelGGL((k_shadow<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->stream, dev->sv, s.sh, s.L, cnt, dev->dstats)
+#define L_SHL(S) hipLaunchKernelGGL((k_shadow<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->stream, dev->sv, s.sh, s.L, cnt, dev->dstats, work)
         IGX_DISPATCH_VARIANT(dev->variant, L_SHL);
 #undef L_SHL
         return;
     }
-#define L_SH(S) hipLaunchKernelGGL((k_shadow<S, STATS, false>), dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, s.sh, s.L, cnt, dev->dstats)
+#define L_SH(S) hipLaunchKernelGGL((k_shadow<S, STATS, false>), dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, s.sh, s.L, cnt, dev->dstats, work)
     IGX_DISPATCH_VARIANT(dev->variant, L_SH);
 #undef L_SH
 }
@@ -1421,7 +1503,7 @@ int shade_blocks_per_cu(bool full) { return full ? resident_blocks(k_shade<true>
     X int finish_blocks_per_cu<S>(int, size_t);
 #define IGX_TRACE_HELPERS(X, S)                                                                                      \
     X void launch_trace<S>(igx_device*, Slot&, int, const FrameArgs&, const PathBuf&, const int*, int);              \
-    X void launch_shadow<S>(igx_device*, Slot&, int, const int*);                                                    \
+    X void launch_shadow<S>(igx_device*, Slot&, int, const int*, int*);                                                    \
     X int trace_blocks_per_cu<S>(int, int, size_t, bool);                                                            \
     X int shadow_blocks_per_cu<S>(int, size_t, bool);
 #if IGX_PART == 1
@@ -1640,6 +1722,7 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     }
     else if (k == "spatial_splits") dev->spatial_splits = value != 0;
     else if (k == "rebuild_bvh") dev->rebuild_bvh = value != 0;
+    else if (k == "dynamic") dev->dynamic_opt = (int)(value & 3);
     else if (k == "path_classes") {
         if (value < 0 || value > 2) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "path_classes must be 0, 1 or 2");
         dev->classify_opt = (int)value;
@@ -2170,6 +2253,7 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
     fa.seed = p->seed;
     fa.inv_spi = 1.0f / (float)p->spi;
     fa.classify = dev->classify_opt;
+    fa.dynamic = dev->dynamic_opt & 1;
     long long local_pixels;
     if (list_mode) {
         // the previous ray list may still be read by a queued tail kernel
@@ -2274,6 +2358,8 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
         int* cnt = S.ctr; // row 2b: paths entering bounce b, row 2b+1: shadow rays of bounce b
         auto row = [&](int r) { return cnt + (size_t)r * CROW; };
         HIPCHK(hipMemsetAsync(S.ctr, 0, (size_t)(2 * max_bounces + 4) * CROW * sizeof(int), dev->stream));
+        if (dev->dynamic_opt)
+            HIPCHK(hipMemsetAsync(S.ctr + (size_t)WORK_ROW0 * CROW, 0, (size_t)4 * max_bounces * CROW * sizeof(int), dev->stream));
         // camera paths: built by bounce 0 of the fused k_extend when the chunk
         // runs through it (saves the 72 B/path round trip of k_generate)
         const bool fuse_gen = dev->fuse_generate && !split && n > tail;
@@ -2307,7 +2393,7 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
                 }
             }
             PathBuf in = (b & 1) ? S.pb : S.pa, out = (b & 1) ? S.pa : S.pb;
-            KernelCounters kc{row(2 * b), row(2 * (b + 1)), row(2 * b + 1), dev->dstats};
+            KernelCounters kc{row(2 * b), row(2 * (b + 1)), row(2 * b + 1), dev->dstats, row(WORK_ROW0 + 4 * b)};
             if (split) {
                 begin_timed(5, b, dev->stream);
                 if (inst) launch_trace<true>(dev, S, tr_grid, fa, in, row(2 * b), tail);
@@ -2325,8 +2411,9 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
                 end_timed(dev->stream);
             }
             begin_timed(1, b, dev->stream);
-            if (inst) launch_shadow<true>(dev, S, sh_grid, row(2 * b + 1));
-            else launch_shadow<false>(dev, S, sh_grid, row(2 * b + 1));
+            int* const sh_work = (dev->dynamic_opt & 2) ? row(WORK_ROW0 + 4 * b + 2) : nullptr;
+            if (inst) launch_shadow<true>(dev, S, sh_grid, row(2 * b + 1), sh_work);
+            else launch_shadow<false>(dev, S, sh_grid, row(2 * b + 1), sh_work);
             end_timed(dev->stream);
             HIPCHK(hipGetLastError());
             // shadow counts of bounce b and path counts entering bounce b+1 (adjacent rows)

@@ -383,6 +383,34 @@ def test_enclosing_shortcut_invariance(device, root, name):
     assert imgs[0].sum() > 0
 
 
+@pytest.mark.parametrize("name", ["diamond_scene.json", "primitives.json", "s_deep.json"])
+@pytest.mark.parametrize("film", [(112, 80), (640, 400)])
+def test_dynamic_groups_invariance(device, root, name, film):
+    """k_extend handing out groups of 64 paths through per-shard counters
+    (waves move on to the next open shard once their own is exhausted)
+    renders the same image bit for bit, with the same ray counts, as the
+    static grid-stride distribution: survivors stay in the shard they came
+    from and every path is taken exactly once."""
+    sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", name))
+    imgs, counts = [], []
+    try:
+        device.upload(sc)
+        for dynamic, tail in [(0, -1), (1, -1), (3, -1), (2, 0), (3, 0)]:
+            device.set_option("dynamic", dynamic)
+            device.set_option("tail_threshold", tail)
+            device.reset_stats()
+            imgs.append(render_gpu(device, sc, film[0], film[1], 4))
+            st = device.stats()
+            counts.append((st["camera_rays"], st["bounce_rays"], st["shadow_rays"]))
+    finally:
+        device.set_option("dynamic", 1)
+        device.set_option("tail_threshold", -1)
+    for im, c in zip(imgs[1:], counts[1:]):
+        np.testing.assert_array_equal(imgs[0], im)
+        assert c == counts[0]
+    assert imgs[0].sum() > 0
+
+
 @pytest.mark.parametrize("name", ["diamond_scene.json", "primitives.json", "s_deep.json", "s_soup_1m.json"])
 def test_occlusion_parity(device, root, name):
     sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", name))
