@@ -557,14 +557,15 @@ __device__ __forceinline__ int take_group(int* work, int& s, uint64_t& done, int
         if (!((done >> s) & 1ull)) {
             int v = 0;
             if (lane_id() == 0) v = atomicAdd(work + s * CSTRIDE, 1);
-            v = __shfl(v, 0);
+            v = __builtin_amdgcn_readfirstlane(v);
             if (v * 64 < n) return v;
             if (lane_id() == 0) atomicOr(done_mask, 1ull << s);
             done |= 1ull << s;
         }
         unsigned long long m = 0;
         if (lane_id() == 0) m = __hip_atomic_load(done_mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        done |= (uint64_t)__shfl(m, 0);
+        done |= (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)m) |
+                ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(m >> 32)) << 32);
         const uint64_t open = ~done;
         if (!open) return -1;
         const int r = (s + 1) & (NSH - 1);
@@ -860,36 +861,109 @@ __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, f
 #ifndef REFILL_WAVES
 #define REFILL_WAVES 6
 #endif
-struct ShardSeq {
-    int C; // positions in this wave's sequence (a multiple of 64)
-    int k, K;
-    __device__ __forceinline__ int operator()(int c) const { return (k + (c >> 6) * K) * 64 + (c & 63); }
+// The sequence of stream positions a persistent-lane wave walks
+// (refill_loop): virtual position c lies in virtual group c >> 6.  Static
+// (work == nullptr): virtual group j is group k + j * K of the wave's own
+// shard.  Dynamic: virtual groups come from take_group as the wave reaches
+// them.  A window of two slots holds the groups one refill can touch (a
+// refill takes at most 64 positions).  All members are wave-uniform.
+// CLASSES: the stream holds two path classes (stream_index); otherwise
+// position pos of shard s is stored at s * shard_cap + pos.
+template <bool CLASSES>
+struct GroupSeq {
+    const int* cnt;
+    int* work;
+    int shard_cap;
+    WaveWork w;
+    int s;
+    uint64_t done;
+    bool exhausted;
+    int j0;                          // virtual group of slot 0
+    int gs[2], gg[2], ga[2], gn[2]; // shard, group (< 0: empty slot), class-A count, count
+
+    __device__ __forceinline__ ShardCount count_of(int sh) const {
+        if constexpr (CLASSES) return shard_count(cnt, sh);
+        const int n = uniform_load(cnt + sh * CSTRIDE);
+        return ShardCount{n, n};
+    }
+    __device__ __forceinline__ void init(const int* cnt_, int* work_, int cap, const WaveWork& w_) {
+        cnt = cnt_;
+        work = work_;
+        shard_cap = cap;
+        w = w_;
+        s = w.s;
+        done = 0;
+        exhausted = false;
+        j0 = 0;
+        gg[0] = gg[1] = -1;
+    }
+    // load the next virtual group (j0 + k) into slot k
+    __device__ __forceinline__ bool fill(int k) {
+        if (exhausted) return false;
+        ShardCount sc = count_of(s);
+        int g;
+        if (work) {
+            g = take_group(work, s, done, sc.n, [&](int sh_) {
+                sc = count_of(sh_);
+                return sc.n;
+            });
+        } else {
+            g = w.k + (j0 + k) * w.K;
+            if (g * 64 >= sc.n) g = -1;
+        }
+        if (g < 0) {
+            exhausted = true;
+            return false;
+        }
+        gs[k] = s;
+        gg[k] = g;
+        ga[k] = sc.a;
+        gn[k] = sc.n;
+        return true;
+    }
+    // make positions [cursor, cursor + m) resolvable as far as groups remain;
+    // false once the sequence has nothing at cursor
+    __device__ __forceinline__ bool reserve(int cursor, int m) {
+        if (cursor >= (j0 + 1) * 64) { // slide the window
+            gs[0] = gs[1];
+            gg[0] = gg[1];
+            ga[0] = ga[1];
+            gn[0] = gn[1];
+            gg[1] = -1;
+            ++j0;
+        }
+        if (gg[0] < 0 && !fill(0)) return false;
+        if (cursor + m > (j0 + 1) * 64 && gg[1] < 0) fill(1);
+        return true;
+    }
+    // stream index of virtual position c (per lane); false: nothing there
+    __device__ __forceinline__ bool at(int c, int& i) const {
+        const int k = (c >> 6) - j0;
+        const int g = k ? gg[1] : gg[0];
+        if (g < 0) return false;
+        const int pos = g * 64 + (c & 63);
+        if (pos >= (k ? gn[1] : gn[0])) return false;
+        const int sh = k ? gs[1] : gs[0];
+        i = CLASSES ? stream_index(sh, pos, k ? ga[1] : ga[0], shard_cap) : sh * shard_cap + pos;
+        return true;
+    }
 };
-__device__ __forceinline__ ShardSeq shard_seq(const WaveWork& w, int ns) {
-    const int groups = (ns + 63) >> 6;
-    const int mine = w.k < groups ? (groups - w.k + w.K - 1) / w.K : 0;
-    return ShardSeq{mine * 64, w.k, w.K};
-}
 
 template <int V, bool STATS, bool LDS>
 __global__ void __launch_bounds__(BLOCK, REFILL_WAVES) k_trace_refill(FrameArgs fa, SceneView gsv, PathBuf in, HitBuf hits,
                                                                      const int* cnt, int tail_threshold,
-                                                                     unsigned long long* stats, int refill_min) {
+                                                                     unsigned long long* stats, int refill_min, int* work) {
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
     if (row_total(cnt) <= tail_threshold) return; // k_finish takes the remaining paths
     const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
-    const WaveWork w = wave_work();
-    const ShardCount sc = shard_count(cnt, w.s);
-    const int ns = sc.n;
-    const ShardSeq seq = shard_seq(w, ns);
+    GroupSeq<true> seq;
+    seq.init(cnt, work, in.shard_cap, wave_work());
     refill_loop<false, STATS, V>(
-        sv, ts, seq.C, refill_min, [&](int c) { return seq(c); },
-        [&](int pos, Trav& t) -> bool {
-            if (pos >= ns) return false;
-            const int i = stream_index(w.s, pos, sc.a, in.shard_cap);
+        sv, ts, seq, refill_min,
+        [&](int i, Trav& t) -> bool {
             const float4 p0 = in.p0[i], p1 = in.p1[i];
             const int depth = (int)(__float_as_uint(p1.w) >> 24);
             if (depth == 0) {
@@ -903,8 +977,7 @@ __global__ void __launch_bounds__(BLOCK, REFILL_WAVES) k_trace_refill(FrameArgs 
             trav_init(sv, t, f3of(p0), f3of(p1), tmin, tmax, rflags, ts);
             return true;
         },
-        [&](int pos, const Trav& t) {
-            const int i = stream_index(w.s, pos, sc.a, in.shard_cap);
+        [&](int i, const Trav& t) {
             if (STATS && t.hit_ent >= 0) st.hits++;
             hits.h[i] = make_float4(t.tmax, t.hu, t.hv, __int_as_float(t.hit_ent));
             hits.prim[i] = t.hit_prim;
@@ -915,29 +988,24 @@ __global__ void __launch_bounds__(BLOCK, REFILL_WAVES) k_trace_refill(FrameArgs 
 
 template <int V, bool STATS, bool LDS>
 __global__ void __launch_bounds__(BLOCK, REFILL_WAVES) k_shadow_refill(SceneView gsv, ShadowBuf sh, float4* L, const int* cnt,
-                                                                      unsigned long long* stats, int refill_min) {
+                                                                      unsigned long long* stats, int refill_min, int* work) {
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
     if (row_total(cnt) == 0) return;
     const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
-    const WaveWork w = wave_work();
-    const int ns = uniform_load(cnt + w.s * CSTRIDE);
-    const int base = w.s * sh.shard_cap;
-    const ShardSeq seq = shard_seq(w, ns);
+    GroupSeq<false> seq;
+    seq.init(cnt, work, sh.shard_cap, wave_work());
     refill_loop<true, STATS, V>(
-        sv, ts, seq.C, refill_min, [&](int c) { return seq(c); },
-        [&](int pos, Trav& t) -> bool {
-            if (pos >= ns) return false;
-            const int i = base + pos;
+        sv, ts, seq, refill_min,
+        [&](int i, Trav& t) -> bool {
             const float4 s0 = sh.s0[i], s1 = sh.s1[i];
             trav_init(sv, t, f3of(s0), f3of(s1), 0.001f, s1.w, RAY_SHADOW, ts);
             return true;
         },
-        [&](int pos, const Trav& t) {
+        [&](int i, const Trav& t) {
             if (t.found) return;
-            const int i = base + pos;
             add_radiance(L, __float_as_int(sh.s0[i].w), f3of(sh.s2[i]));
         },
         st);
@@ -1080,7 +1148,8 @@ struct Slot {
     long long camera = 0;
 };
 
-// rows WORK_ROW0 + 4b: k_extend group counters of bounce b (take_group),
+enum { DYN_EXTEND = 1, DYN_SHADOW = 2, DYN_REFILL_TRACE = 4, DYN_REFILL_SHADOW = 8 };
+// rows WORK_ROW0 + 4b: k_extend (or k_trace_refill) group counters of bounce b (take_group),
 // + 1: its mask of exhausted shards, + 2 / + 3: the same for k_shadow
 constexpr int WORK_ROW0 = 2 * MAX_BOUNCES + 4;
 constexpr int CTR_ROWS = WORK_ROW0 + 4 * MAX_BOUNCES;
@@ -1129,12 +1198,16 @@ struct igx_device {
     // bounce's waves are all-inside or all-outside (diamond frame 152-155 ->
     // 143-145 ms, S-deep 49.1 -> 47.5 ms per 8-iteration frame; bit-identical)
     int classify_opt = 1;
-    // option "dynamic" (bits): 1 = k_extend waves take their groups of 64
-    // paths from per-shard counters (take_group) instead of a fixed grid
-    // stride: diamond frame 142.4 -> 134.3 ms, materials 66.5 -> 54.6,
-    // primitives 36.8 -> 33.9, bit-identical images; 2 = the same for k_shadow
-    // (measured neutral to slightly slower: shadow rays cost about the same)
-    int dynamic_opt = 1;
+    // option "dynamic" (DYN_* bits): DYN_EXTEND = k_extend waves take their
+    // groups of 64 paths from per-shard counters (take_group) instead of a
+    // fixed grid stride: diamond frame 142.4 -> 134.3 ms, materials 66.5 ->
+    // 54.6, primitives 36.8 -> 33.9, bit-identical images; DYN_SHADOW = the
+    // same for k_shadow (measured neutral: shadow rays cost about the same);
+    // DYN_REFILL_TRACE / DYN_REFILL_SHADOW: the persistent-lane kernels
+    // draw their groups the same way (GroupSeq): soup-1M 8-iteration frame
+    // 452 -> 382 ms (k_shadow_refill 220 -> 164, k_trace_refill 205 -> 193),
+    // S-deep 52.7 -> 48.6 ms
+    int dynamic_opt = DYN_EXTEND | DYN_REFILL_TRACE | DYN_REFILL_SHADOW;
     float sah_node_cost = 1.0f;    // option "sah_node_cost_pct" (percent of one triangle test)
     // SBVH for BLAS up to SPATIAL_SPLIT_MAX_FACES triangles (option "spatial_splits"):
     // off by default -- measured slower on the diamond (196 -> 230 ms per frame)
@@ -1369,15 +1442,16 @@ void launch_trace_w(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, con
 #undef L_TR
 }
 template <bool STATS>
-void launch_trace(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const PathBuf& in, const int* cnt, int tail) {
+void launch_trace(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const PathBuf& in, const int* cnt, int tail,
+                  int* work) {
     if (use_refill(dev)) {
 #define L_TRR(S)                                                                                                        \
     if (dev->lds_scene_bytes)                                                                                            \
         hipLaunchKernelGGL((k_trace_refill<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->stream, fa, \
-                           dev->sv, in, s.hb, cnt, tail, dev->dstats, refill_min(dev));                                  \
+                           dev->sv, in, s.hb, cnt, tail, dev->dstats, refill_min(dev), work);                            \
     else                                                                                                                 \
         hipLaunchKernelGGL((k_trace_refill<S, STATS, false>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, s.hb, \
-                           cnt, tail, dev->dstats, refill_min(dev))
+                           cnt, tail, dev->dstats, refill_min(dev), work)
         IGX_DISPATCH_VARIANT(dev->variant, L_TRR);
 #undef L_TRR
         return;
@@ -1397,10 +1471,10 @@ void launch_shadow(igx_device* dev, Slot& s, int grid, const int* cnt, int* work
 #define L_SHR(S)                                                                                                        \
     if (dev->lds_scene_bytes)                                                                                            \
         hipLaunchKernelGGL((k_shadow_refill<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->stream,   \
-                           dev->sv, s.sh, s.L, cnt, dev->dstats, refill_min(dev));                                       \
+                           dev->sv, s.sh, s.L, cnt, dev->dstats, refill_min(dev), work);                                 \
     else                                                                                                                 \
         hipLaunchKernelGGL((k_shadow_refill<S, STATS, false>), dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, s.sh, s.L, \
-                           cnt, dev->dstats, refill_min(dev))
+                           cnt, dev->dstats, refill_min(dev), work)
         IGX_DISPATCH_VARIANT(dev->variant, L_SHR);
 #undef L_SHR
         return;
@@ -1502,7 +1576,7 @@ int shade_blocks_per_cu(bool full) { return full ? resident_blocks(k_shade<true>
     X void launch_finish<S>(igx_device*, Slot&, int, const FrameArgs&, const PathBuf&, const int*, int);             \
     X int finish_blocks_per_cu<S>(int, size_t);
 #define IGX_TRACE_HELPERS(X, S)                                                                                      \
-    X void launch_trace<S>(igx_device*, Slot&, int, const FrameArgs&, const PathBuf&, const int*, int);              \
+    X void launch_trace<S>(igx_device*, Slot&, int, const FrameArgs&, const PathBuf&, const int*, int, int*);              \
     X void launch_shadow<S>(igx_device*, Slot&, int, const int*, int*);                                                    \
     X int trace_blocks_per_cu<S>(int, int, size_t, bool);                                                            \
     X int shadow_blocks_per_cu<S>(int, size_t, bool);
@@ -1722,7 +1796,7 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     }
     else if (k == "spatial_splits") dev->spatial_splits = value != 0;
     else if (k == "rebuild_bvh") dev->rebuild_bvh = value != 0;
-    else if (k == "dynamic") dev->dynamic_opt = (int)(value & 3);
+    else if (k == "dynamic") dev->dynamic_opt = (int)(value & 15);
     else if (k == "path_classes") {
         if (value < 0 || value > 2) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "path_classes must be 0, 1 or 2");
         dev->classify_opt = (int)value;
@@ -2253,7 +2327,7 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
     fa.seed = p->seed;
     fa.inv_spi = 1.0f / (float)p->spi;
     fa.classify = dev->classify_opt;
-    fa.dynamic = dev->dynamic_opt & 1;
+    fa.dynamic = dev->dynamic_opt & DYN_EXTEND;
     long long local_pixels;
     if (list_mode) {
         // the previous ray list may still be read by a queued tail kernel
@@ -2396,8 +2470,9 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
             KernelCounters kc{row(2 * b), row(2 * (b + 1)), row(2 * b + 1), dev->dstats, row(WORK_ROW0 + 4 * b)};
             if (split) {
                 begin_timed(5, b, dev->stream);
-                if (inst) launch_trace<true>(dev, S, tr_grid, fa, in, row(2 * b), tail);
-                else launch_trace<false>(dev, S, tr_grid, fa, in, row(2 * b), tail);
+                int* const tr_work = (dev->dynamic_opt & DYN_REFILL_TRACE) ? row(WORK_ROW0 + 4 * b) : nullptr;
+                if (inst) launch_trace<true>(dev, S, tr_grid, fa, in, row(2 * b), tail, tr_work);
+                else launch_trace<false>(dev, S, tr_grid, fa, in, row(2 * b), tail, tr_work);
                 end_timed(dev->stream);
                 begin_timed(0, b, dev->stream);
                 launch_shade(dev, full, shade_grid, fa, in, S.hb, out, S.sh, S.L, kc, tail);
@@ -2411,7 +2486,8 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
                 end_timed(dev->stream);
             }
             begin_timed(1, b, dev->stream);
-            int* const sh_work = (dev->dynamic_opt & 2) ? row(WORK_ROW0 + 4 * b + 2) : nullptr;
+            int* const sh_work =
+                (dev->dynamic_opt & (use_refill(dev) ? DYN_REFILL_SHADOW : DYN_SHADOW)) ? row(WORK_ROW0 + 4 * b + 2) : nullptr;
             if (inst) launch_shadow<true>(dev, S, sh_grid, row(2 * b + 1), sh_work);
             else launch_shadow<false>(dev, S, sh_grid, row(2 * b + 1), sh_work);
             end_timed(dev->stream);

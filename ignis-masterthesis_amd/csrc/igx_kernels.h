@@ -496,28 +496,29 @@ __device__ __forceinline__ bool trace_enclosed(const SceneView& sv, int enc, f3 
 // ray positions; a lane whose ray is finished goes idle, and once at least
 // `refill_min` lanes are idle (or all are) the idle lanes take the next rays
 // of the sequence, so waves stop running long stretches with a handful of
-// active lanes.  No atomics: the sequence is fixed per wave (pos_of).
-// fetch(c, t) -> bool loads ray c into t (false: nothing to trace);
-// finish(c, t) consumes a finished ray.
-template <bool ANY, bool STATS, int V, typename PosOf, typename Fetch, typename Finish>
-__device__ __forceinline__ void refill_loop(const SceneView& sv, const TStack& ts, int C, int refill_min, PosOf pos_of,
-                                            Fetch fetch, Finish finish, TraceStats& st) {
+// active lanes.  seq.reserve(cursor, m) (wave-uniform) readies the next m
+// positions and is false once the sequence is exhausted; seq.at(c, i) maps
+// position c to a stream index (false: nothing there).
+// fetch(i, t) -> bool loads ray i into t (false: nothing to trace);
+// finish(i, t) consumes a finished ray.
+template <bool ANY, bool STATS, int V, typename Seq, typename Fetch, typename Finish>
+__device__ __forceinline__ void refill_loop(const SceneView& sv, const TStack& ts, Seq& seq, int refill_min, Fetch fetch,
+                                            Finish finish, TraceStats& st) {
     const int lane = (int)__lane_id();
     const uint64_t below = (1ull << lane) - 1ull;
     int cursor = 0; // wave-uniform
+    bool more = true; // wave-uniform: the sequence is not yet exhausted
     bool busy = false;
     int pos = 0;
     Trav t;
     for (;;) {
         const uint64_t idle = __ballot(!busy);
         const int nidle = __popcll(idle);
-        if (cursor < C && (nidle >= refill_min || nidle == 64)) {
+        if (more && (nidle >= refill_min || nidle == 64)) more = seq.reserve(cursor, nidle);
+        if (more && (nidle >= refill_min || nidle == 64)) {
             if (!busy) {
                 const int c = cursor + __popcll(idle & below);
-                if (c < C) {
-                    pos = pos_of(c);
-                    busy = fetch(pos, t);
-                }
+                if (seq.at(c, pos)) busy = fetch(pos, t);
             }
             cursor += nidle;
         } else if (nidle == 64) {

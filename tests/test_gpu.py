@@ -395,7 +395,7 @@ def test_dynamic_groups_invariance(device, root, name, film):
     imgs, counts = [], []
     try:
         device.upload(sc)
-        for dynamic, tail in [(0, -1), (1, -1), (3, -1), (2, 0), (3, 0)]:
+        for dynamic, tail in [(0, -1), (1, -1), (15, -1), (2, 0), (15, 0)]:
             device.set_option("dynamic", dynamic)
             device.set_option("tail_threshold", tail)
             device.reset_stats()
@@ -403,7 +403,7 @@ def test_dynamic_groups_invariance(device, root, name, film):
             st = device.stats()
             counts.append((st["camera_rays"], st["bounce_rays"], st["shadow_rays"]))
     finally:
-        device.set_option("dynamic", 1)
+        device.set_option("dynamic", 13)
         device.set_option("tail_threshold", -1)
     for im, c in zip(imgs[1:], counts[1:]):
         np.testing.assert_array_equal(imgs[0], im)
