@@ -496,6 +496,14 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
 // One bounce of one path: closest hit + shading.  Used by the tail kernel; the
 // wavefront runs the same two halves as k_trace + k_shade, so both produce
 // bit-identical paths.
+// Instrumentation of k_extend's phases: the wave's shader clock (s_memtime,
+// a read of the counter) since the previous mark is added to phase k; marks
+// sit at wave-uniform points.
+__device__ __forceinline__ void phase_mark(TraceStats& st, unsigned long long& last, int k) {
+    const unsigned long long now = __builtin_amdgcn_s_memtime();
+    st.cyc[k] += now - last;
+    last = now;
+}
 template <bool STATS, int V>
 __device__ __forceinline__ bool extend_step(const FrameArgs& fa, const SceneView& sv, const TStack& ts, PathState& ps, f3& Lacc,
                                             bool& has_l, bool& has_shadow, ShadowRec& sr, TraceStats& st) {
@@ -538,6 +546,8 @@ __device__ __forceinline__ void flush_stats(const TraceStats& st, unsigned long 
         if (with_hits) atomicAdd(&stats[8], h);
         atomicAdd(&stats[9 + (base / 4) * 2], wn);
         atomicAdd(&stats[10 + (base / 4) * 2], wl);
+        if (st.cyc[0] | st.cyc[1] | st.cyc[2] | st.cyc[3])
+            for (int k = 0; k < 4; ++k) atomicAdd(&stats[16 + k], st.cyc[k]);
     }
 }
 
@@ -608,6 +618,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : EXTEND_WAVES) 
     ShardCount sc = count_of(s);
     uint64_t done = 0; // shards this wave knows to be exhausted (dynamic)
     int p0 = w.k * 64;
+    unsigned long long t_last = STATS ? __builtin_amdgcn_s_memtime() : 0; // phase clocks (instrumented builds)
     for (;;) {
         if (fa.dynamic) {
             const int g = take_group(kc.work, s, done, sc.n, [&](int sh_) {
@@ -619,6 +630,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : EXTEND_WAVES) 
         } else if (p0 >= sc.n) {
             break;
         }
+        if (STATS) phase_mark(st, t_last, 3); // group distribution
         const int ns = sc.n;
         int* const c_out = kc.cnt_out + s * CSTRIDE;
         int* const c_sh = kc.cnt_shadow + s * CSTRIDE;
@@ -645,12 +657,35 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : EXTEND_WAVES) 
             } else {
                 ps = load_path(in, stream_index(s, pos, sc.a, in.shard_cap));
             }
-            if (ps.depth > 0) {
+            if (!STATS && ps.depth > 0) {
                 f3 Lacc;
                 bool has_l;
                 alive = extend_step<STATS, V>(fa, sv, ts, ps, Lacc, has_l, has_shadow, sr, st);
                 if (has_l) add_radiance(L, ps.slot, Lacc);
             }
+        }
+        if constexpr (STATS) {
+            // instrumented: extend_step's two halves with phase clocks between them
+            const bool act = pos < ns && ps.depth > 0;
+            int hit_ent = -1, hit_prim = -1;
+            float hu = 0, hv = 0, tmin = 0, tmax = 0;
+            uint32_t rflags = 0;
+            phase_mark(st, t_last, 0);
+            if (act) {
+                ray_extent(fa, sv, ps.depth, ps.slot, tmin, tmax, rflags);
+                if (ps.inside < 0 ||
+                    !trace_enclosed<STATS, V>(sv, ps.inside, ps.o, ps.d, tmin, tmax, rflags, ts, hit_ent, hit_prim, hu, hv, st))
+                    trace_ray<false, STATS, V>(sv, ps.o, ps.d, tmin, tmax, rflags, ts, hit_ent, hit_prim, hu, hv, st);
+                if (hit_ent >= 0) st.hits++;
+            }
+            phase_mark(st, t_last, 1);
+            if (act) {
+                f3 Lacc;
+                bool has_l;
+                alive = shade_step<variant_full(V)>(fa, sv, ps, hit_ent, hit_prim, tmax, hu, hv, Lacc, has_l, has_shadow, sr);
+                if (has_l) add_radiance(L, ps.slot, Lacc);
+            }
+            phase_mark(st, t_last, 2);
         }
         int dst, sdst;
         wave_append_paths(alive, path_class_b(fa.classify, ps.eta, ps.inv_pdf), has_shadow, c_out, c_sh, out.shard_cap, dst, sdst);
@@ -662,6 +697,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : EXTEND_WAVES) 
             sh.s2[e] = make_float4(sr.color.x, sr.color.y, sr.color.z, 0);
         }
         if (!fa.dynamic) p0 += w.K * 64;
+        if (STATS) phase_mark(st, t_last, 3);
     }
     if (STATS) flush_stats<STATS>(st, kc.stats, 0, true);
 }
@@ -861,6 +897,11 @@ __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, f
 #ifndef REFILL_WAVES
 #define REFILL_WAVES 6
 #endif
+// LDS-staged tables (<= 48 KB + the 16 KB stack per block) allow at most
+// 4 blocks per CU: the 6-wave VGPR cap would only force spills
+#ifndef REFILL_WAVES_LDS
+#define REFILL_WAVES_LDS 4
+#endif
 // The sequence of stream positions a persistent-lane wave walks
 // (refill_loop): virtual position c lies in virtual group c >> 6.  Static
 // (work == nullptr): virtual group j is group k + j * K of the wave's own
@@ -950,7 +991,7 @@ struct GroupSeq {
 };
 
 template <int V, bool STATS, bool LDS>
-__global__ void __launch_bounds__(BLOCK, REFILL_WAVES) k_trace_refill(FrameArgs fa, SceneView gsv, PathBuf in, HitBuf hits,
+__global__ void __launch_bounds__(BLOCK, LDS ? REFILL_WAVES_LDS : REFILL_WAVES) k_trace_refill(FrameArgs fa, SceneView gsv, PathBuf in, HitBuf hits,
                                                                      const int* cnt, int tail_threshold,
                                                                      unsigned long long* stats, int refill_min, int* work) {
     __shared__ int stack_mem[LDS_STACK * BLOCK];
@@ -987,7 +1028,7 @@ __global__ void __launch_bounds__(BLOCK, REFILL_WAVES) k_trace_refill(FrameArgs 
 }
 
 template <int V, bool STATS, bool LDS>
-__global__ void __launch_bounds__(BLOCK, REFILL_WAVES) k_shadow_refill(SceneView gsv, ShadowBuf sh, float4* L, const int* cnt,
+__global__ void __launch_bounds__(BLOCK, LDS ? REFILL_WAVES_LDS : REFILL_WAVES) k_shadow_refill(SceneView gsv, ShadowBuf sh, float4* L, const int* cnt,
                                                                       unsigned long long* stats, int refill_min, int* work) {
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
@@ -1729,12 +1770,12 @@ extern "C" igx_status igx_create(int hip_device, igx_device** out) {
         delete dev;
         return IGX_ERR_HIP;
     }
-    if (hipMalloc((void**)&dev->dstats, 16 * sizeof(unsigned long long)) != hipSuccess ||
+    if (hipMalloc((void**)&dev->dstats, 20 * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc((void**)&dev->tail_counts, 2 * sizeof(unsigned long long)) != hipSuccess) {
         delete dev;
         return IGX_ERR_OUT_OF_MEMORY;
     }
-    (void)hipMemset(dev->dstats, 0, 16 * sizeof(unsigned long long));
+    (void)hipMemset(dev->dstats, 0, 20 * sizeof(unsigned long long));
     (void)hipMemset(dev->tail_counts, 0, 2 * sizeof(unsigned long long));
     *out = dev;
     return IGX_OK;
@@ -2609,8 +2650,12 @@ extern "C" igx_status igx_get_stats(igx_device* dev, igx_stats* out) {
     *out = dev->stats;
     out->bvh_depth = dev->scene_depth;
     out->stack_entries = LDS_STACK;
-    unsigned long long h[16] = {0};
+    unsigned long long h[20] = {0};
     HIPCHK(hipMemcpy(h, dev->dstats, sizeof(h), hipMemcpyDeviceToHost));
+    out->extend_cycles_load = h[16];
+    out->extend_cycles_trace = h[17];
+    out->extend_cycles_shade = h[18];
+    out->extend_cycles_store = h[19];
     out->node_visits = h[0];
     out->leaf_visits = h[1];
     out->tri_tests = h[2];
@@ -2639,7 +2684,7 @@ extern "C" igx_status igx_reset_stats(igx_device* dev) {
     igx_status st = drain(dev);
     if (st != IGX_OK) return st;
     dev->stats = igx_stats{};
-    HIPCHK(hipMemset(dev->dstats, 0, 16 * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(dev->dstats, 0, 20 * sizeof(unsigned long long)));
     return IGX_OK;
 }
 

@@ -60,6 +60,8 @@ __device__ __forceinline__ SceneView stage_scene_lds(const SceneView& sv, float4
 struct TraceStats {
     uint32_t nodes, leaves, tris, blas, hits;
     uint32_t wnodes, wleaves; // wave-level iterations of the node loop / leaf phase (SIMD efficiency)
+    // k_extend phase clocks (wave-level, s_memtime): load, trace, shade, store
+    unsigned long long cyc[4] = {0, 0, 0, 0};
 };
 
 // true on the lowest active lane of the wave (counts one event per wave)
@@ -457,10 +459,10 @@ __device__ __forceinline__ bool trace_enclosed(const SceneView& sv, int enc, f3 
     const float4* ip = sv.inst + 4 * slot;
     const int4 info = *reinterpret_cast<const int4*>(ip + 3);
     if ((rflags & RAY_TYPE_MASK) != ((rflags & (uint32_t)info.w) & RAY_TYPE_MASK)) return false;
-    const float4 m0 = ip[0], m1 = ip[1], m2 = ip[2];
     Trav t;
     t.o = o;
     t.d = d;
+    const float4 m0 = ip[0], m1 = ip[1], m2 = ip[2];
     t.lo = mk(m0.x * o.x + m0.y * o.y + m0.z * o.z + m0.w, m1.x * o.x + m1.y * o.y + m1.z * o.z + m1.w,
               m2.x * o.x + m2.y * o.y + m2.z * o.z + m2.w);
     t.ld = mk(m0.x * d.x + m0.y * d.y + m0.z * d.z, m1.x * d.x + m1.y * d.y + m1.z * d.z, m2.x * d.x + m2.y * d.y + m2.z * d.z);

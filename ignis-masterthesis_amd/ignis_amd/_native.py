@@ -124,7 +124,9 @@ class Stats(C.Structure):
                 ("shadow_wave_node_iters", C.c_uint64), ("shadow_wave_leaf_iters", C.c_uint64),
                 ("bvh_width", C.c_int32), ("node_bytes", C.c_int32),
                 ("lds_scene_bytes", C.c_int32), ("shadow_blocks_per_cu", C.c_int32),
-                ("table_bytes", C.c_uint64), ("shading_bytes", C.c_uint64)]
+                ("table_bytes", C.c_uint64), ("shading_bytes", C.c_uint64),
+                ("extend_cycles_load", C.c_uint64), ("extend_cycles_trace", C.c_uint64),
+                ("extend_cycles_shade", C.c_uint64), ("extend_cycles_store", C.c_uint64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

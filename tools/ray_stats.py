@@ -30,4 +30,8 @@ out = {"rays": n, "shadow_rays": s["shadow_rays"],
        "sh_wave_leaf_iters/64rays": 64 * s["shadow_wave_leaf_iters"] / ns,
        "depth": s["bvh_depth"], "width": s["bvh_width"], "lds_scene_bytes": s["lds_scene_bytes"],
        "table_bytes": s["table_bytes"]}
+cyc = [s["extend_cycles_" + k] for k in ("load", "trace", "shade", "store")]
+if sum(cyc):  # share of k_extend's wave time per phase (instrumented build)
+    out.update({"ext_phase_" + k: c / sum(cyc) for k, c in zip(("load", "trace", "shade", "store"), cyc)})
+    out["ext_wave_cycles/64rays"] = 64 * sum(cyc) / max(1, s["extend_rays"])
 print(json.dumps({k: round(v, 3) if isinstance(v, float) else v for k, v in out.items()}))
