@@ -388,10 +388,22 @@ __device__ __forceinline__ void ray_extent(const FrameArgs& fa, const SceneView&
 // advances `ps` by one bounce.  Returns whether the path continues (ps then
 // holds the bounced ray); fills the radiance gathered at this vertex (Lacc,
 // has_l) and the NEE shadow ray (has_shadow, sr).
+#ifdef IGX_SHADE_PROBE
+// dev probe: per-lane shader clock since the lane's previous mark -> slot k
+#define SHADE_MARK(k)                                                                                                 \
+    if (probe) {                                                                                                       \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime();                                                 \
+        probe->cyc[k] += now_ - *probe_last;                                                                          \
+        *probe_last = now_;                                                                                           \
+    }
+#else
+#define SHADE_MARK(k)
+#endif
 template <bool FULL>
 __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView& sv, PathState& ps, int hit_ent,
                                            int hit_prim, float tmax, float hu, float hv, f3& Lacc, bool& has_l,
-                                           bool& has_shadow, ShadowRec& sr) {
+                                           bool& has_shadow, ShadowRec& sr, TraceStats* probe = nullptr,
+                                           unsigned long long* probe_last = nullptr) {
     Lacc = mk(0, 0, 0);
     has_l = false;
     has_shadow = false;
@@ -413,6 +425,7 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
     int mat_id;
     Surface s = surface_element(sv, hit_ent, hit_prim, tmax, hu, hv, ps.o, rd, mat_id);
     const DevMaterial& m = sv.mats[mat_id];
+    SHADE_MARK(1)
     // on_hit (pathtracer.art:114-134)
     if (m.light >= 0 && s.entering) {
         float dt = -dot(rd, s.local.n);
@@ -461,6 +474,7 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
             has_shadow = true;
         }
     }
+    SHADE_MARK(2)
     // on_bounce (pathtracer.art:165-200)
     if (!(ps.depth + 1 <= sv.max_depth)) return false;
     BsdfSample bs = bsdf_sample<FULL>(m, s, rnd, out_dir);
@@ -546,9 +560,18 @@ __device__ __forceinline__ void flush_stats(const TraceStats& st, unsigned long 
         if (with_hits) atomicAdd(&stats[8], h);
         atomicAdd(&stats[9 + (base / 4) * 2], wn);
         atomicAdd(&stats[10 + (base / 4) * 2], wl);
+#ifndef IGX_SHADE_PROBE
         if (st.cyc[0] | st.cyc[1] | st.cyc[2] | st.cyc[3])
             for (int k = 0; k < 4; ++k) atomicAdd(&stats[16 + k], st.cyc[k]);
+#endif
     }
+#ifdef IGX_SHADE_PROBE // per-lane marks: the lanes' sum / 64
+    for (int k = 0; k < 4; ++k) {
+        unsigned long long c = st.cyc[k];
+        for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off);
+        if (lane_id() == 0 && c) atomicAdd(&stats[16 + k], c / 64);
+    }
+#endif
 }
 
 // Dynamic distribution of a launch's groups of 64 stream positions: the
@@ -630,7 +653,11 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : EXTEND_WAVES) 
         } else if (p0 >= sc.n) {
             break;
         }
+#ifdef IGX_SHADE_PROBE
+        if (STATS) phase_mark(st, t_last, 0);
+#else
         if (STATS) phase_mark(st, t_last, 3); // group distribution
+#endif
         const int ns = sc.n;
         int* const c_out = kc.cnt_out + s * CSTRIDE;
         int* const c_sh = kc.cnt_shadow + s * CSTRIDE;
@@ -670,7 +697,11 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : EXTEND_WAVES) 
             int hit_ent = -1, hit_prim = -1;
             float hu = 0, hv = 0, tmin = 0, tmax = 0;
             uint32_t rflags = 0;
+#ifdef IGX_SHADE_PROBE
+            phase_mark(st, t_last, 0); // probe: everything outside shade_step -> 0
+#else
             phase_mark(st, t_last, 0);
+#endif
             if (act) {
                 ray_extent(fa, sv, ps.depth, ps.slot, tmin, tmax, rflags);
                 if (ps.inside < 0 ||
@@ -678,14 +709,27 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : EXTEND_WAVES) 
                     trace_ray<false, STATS, V>(sv, ps.o, ps.d, tmin, tmax, rflags, ts, hit_ent, hit_prim, hu, hv, st);
                 if (hit_ent >= 0) st.hits++;
             }
+#ifdef IGX_SHADE_PROBE
+            phase_mark(st, t_last, 0);
+#else
             phase_mark(st, t_last, 1);
+#endif
             if (act) {
                 f3 Lacc;
                 bool has_l;
+#ifdef IGX_SHADE_PROBE
+                alive = shade_step<variant_full(V)>(fa, sv, ps, hit_ent, hit_prim, tmax, hu, hv, Lacc, has_l, has_shadow, sr,
+                                                    &st, &t_last);
+#else
                 alive = shade_step<variant_full(V)>(fa, sv, ps, hit_ent, hit_prim, tmax, hu, hv, Lacc, has_l, has_shadow, sr);
+#endif
                 if (has_l) add_radiance(L, ps.slot, Lacc);
             }
+#ifdef IGX_SHADE_PROBE
+            phase_mark(st, t_last, 3); // bounce sampling and the rest
+#else
             phase_mark(st, t_last, 2);
+#endif
         }
         int dst, sdst;
         wave_append_paths(alive, path_class_b(fa.classify, ps.eta, ps.inv_pdf), has_shadow, c_out, c_sh, out.shard_cap, dst, sdst);
@@ -697,7 +741,11 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : EXTEND_WAVES) 
             sh.s2[e] = make_float4(sr.color.x, sr.color.y, sr.color.z, 0);
         }
         if (!fa.dynamic) p0 += w.K * 64;
+#ifdef IGX_SHADE_PROBE
+        if (STATS) phase_mark(st, t_last, 0);
+#else
         if (STATS) phase_mark(st, t_last, 3);
+#endif
     }
     if (STATS) flush_stats<STATS>(st, kc.stats, 0, true);
 }
