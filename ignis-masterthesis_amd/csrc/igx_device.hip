@@ -1298,6 +1298,8 @@ struct igx_device {
     // S-deep 52.7 -> 48.6 ms
     int dynamic_opt = DYN_EXTEND | DYN_REFILL_TRACE | DYN_REFILL_SHADOW;
     float sah_node_cost = 1.0f;    // option "sah_node_cost_pct" (percent of one triangle test)
+    int bvh_bins = 32;             // option "bvh_bins": SAH bins per axis of the BLAS builds (next upload)
+    int bvh_bins_tlas = 32;        // option "bvh_bins_tlas": the same for the TLAS
     // SBVH for BLAS up to SPATIAL_SPLIT_MAX_FACES triangles (option "spatial_splits"):
     // off by default -- measured slower on the diamond (196 -> 230 ms per frame)
     // and neutral on primitives, S-deep and soup-1M
@@ -1886,6 +1888,14 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     else if (k == "spatial_splits") dev->spatial_splits = value != 0;
     else if (k == "rebuild_bvh") dev->rebuild_bvh = value != 0;
     else if (k == "dynamic") dev->dynamic_opt = (int)(value & 15);
+    else if (k == "bvh_bins") {
+        if (value < 2 || value > 4096) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "bvh_bins must be in [2, 4096]");
+        dev->bvh_bins = (int)value;
+    }
+    else if (k == "bvh_bins_tlas") {
+        if (value < 2 || value > 4096) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "bvh_bins_tlas must be in [2, 4096]");
+        dev->bvh_bins_tlas = (int)value;
+    }
     else if (k == "path_classes") {
         if (value < 0 || value > 2) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "path_classes must be 0, 1 or 2");
         dev->classify_opt = (int)value;
@@ -1979,7 +1989,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
                         for (int a = 0; a < 3; ++a) tv[9 * (size_t)f + 3 * k + a] = m.vertices[3 * m.indices[3 * f + k] + a];
                 brs[s] = igx::build_sbvh2(bi, tv, dev->leaf_size);
             } else {
-                brs[s] = igx::build_bvh2(bi, dev->leaf_size, 32, dev->sah_node_cost);
+                brs[s] = igx::build_bvh2(bi, dev->leaf_size, dev->bvh_bins, dev->sah_node_cost);
             }
         } catch (const std::exception& ex) {
             return fail(dev, IGX_ERR_INVALID_ARGUMENT, ex.what());
@@ -2001,7 +2011,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
                 bi.centroid.push_back(0.5f * (en.bbox_min[a] + en.bbox_max[a]));
             }
         }
-        tlas_br = igx::build_bvh2(bi, 1);
+        tlas_br = igx::build_bvh2(bi, 1, dev->bvh_bins_tlas);
     }
     // Node width: BVH2 while its whole stack fits the LDS column (fewer,
     // cheaper node steps on small scenes), else 4-wide nodes (half the node

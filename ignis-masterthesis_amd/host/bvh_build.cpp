@@ -147,7 +147,31 @@ struct Builder {
     }
 };
 
-void set_child(BvhNode& n, int k, const Box& b, int32_t ref) {
+// Child boxes are written slightly enlarged, so that which triangles a ray
+// tests does not depend on how the builder grouped them.  Moeller-Trumbore
+// accepts barycentrics down to -FLT_EPSILON (intersection.art:71-101), i.e.
+// hits up to about 2 * FLT_EPSILON * (longest edge) outside the triangle and
+// its bounds, and the slab test's t carries float rounding relative to the
+// coordinates.  A box that misses such a hit by an ulp would make the closest
+// hit depend on the topology (a grouping that puts the triangle in a wider box
+// tests it, another does not).  Pad: 8 * FLT_EPSILON of the box's extent sum
+// plus 4 * FLT_EPSILON of the coordinate's magnitude, per side.
+Box pad_box(const Box& b) {
+    if (!(b.lo[0] <= b.hi[0] && b.lo[1] <= b.hi[1] && b.lo[2] <= b.hi[2])) return b; // empty child
+    const float eps = std::numeric_limits<float>::epsilon();
+    const float ext = (b.hi[0] - b.lo[0]) + (b.hi[1] - b.lo[1]) + (b.hi[2] - b.lo[2]);
+    Box r = b;
+    for (int a = 0; a < 3; ++a) {
+        const float mag = std::max(std::fabs(b.lo[a]), std::fabs(b.hi[a]));
+        const float pad = 8 * eps * ext + 4 * eps * mag;
+        r.lo[a] = b.lo[a] - pad;
+        r.hi[a] = b.hi[a] + pad;
+    }
+    return r;
+}
+
+void set_child(BvhNode& n, int k, const Box& box, int32_t ref) {
+    const Box b = pad_box(box);
     int o = k == 0 ? 0 : 6;
     // c0: [0]=lo.x [1]=hi.x [2]=lo.y [3]=hi.y [4]=lo.z [5]=hi.z ; c1 likewise at +6
     n.b[o + 0] = b.lo[0]; n.b[o + 1] = b.hi[0];
