@@ -1470,12 +1470,13 @@ int grid_for(igx_device* dev, long long items, int blocks_per_cu) {
 //  * traversal tables in LDS (<= 48 KB): fused k_extend, grid-stride k_shadow;
 //  * tables in global memory: shadow rays with persistent lanes (k_shadow_refill,
 //    a refill once refill_min lanes idle);
-//  * tables beyond one XCD's L2 (4 MiB): also split the bounce into k_trace
-//    (persistent lanes) + k_shade -- there every node step waits on an
-//    Infinity-Cache / HBM round trip, and a traversal-only kernel keeps more
-//    waves resident and lets lanes refill.  On cache-resident scenes the
-//    fused kernel is faster (no hit records, rays already coherent).
-constexpr size_t SPLIT_TABLE_BYTES = 4u << 20;
+//  * tables beyond 64 MiB: also split the bounce into k_trace (persistent
+//    lanes) + k_shade -- there most node steps wait on an Infinity-Cache /
+//    HBM round trip, and a traversal-only kernel keeps more waves resident
+//    and lets lanes refill.  Below, the fused kernel with dynamic groups is
+//    faster (no hit records): S-deep (18 MB of tables) 49.4 -> 46.9 ms per
+//    8-iteration frame fused, soup-1M (104 MB) 382 split vs 451 fused.
+constexpr size_t SPLIT_TABLE_BYTES = 64u << 20;
 inline int refill_min(const igx_device* dev) { return dev->refill_opt >= 0 ? dev->refill_opt : 16; }
 // auto: global-table scenes only; an explicit "refill" applies to LDS-staged scenes too
 inline bool use_refill(const igx_device* dev) {
