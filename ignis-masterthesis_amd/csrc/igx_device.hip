@@ -57,17 +57,17 @@ using namespace igxd;
 namespace igxh {
 
 constexpr int BLOCK = 256;
-constexpr int MAX_BLOCKS_PER_CU = 8;  // 2048 threads per CU; grids never exceed num_cus * this
-constexpr int MAX_STACK = 128;        // traversal stack entries (LDS + spill) per ray
+[[maybe_unused]] constexpr int MAX_BLOCKS_PER_CU = 8;  // 2048 threads per CU; grids never exceed num_cus * this
+[[maybe_unused]] constexpr int MAX_STACK = 128;        // traversal stack entries (LDS + spill) per ray
 constexpr int MAX_BOUNCES = 256;          // path depth is stored in 8 bits (p1.w, above the 24-bit RNG counter)
 constexpr long long MAX_CHUNK_PATHS = 1ll << 27; // paths per chunk (one wavefront), ~25 GB of stream buffers per slot
 // a path's slot in its chunk takes the low 27 bits of the slot word; the top
 // 5 carry 1 + the index of the enclosing entity it is in (at most 31 entities)
 constexpr int SLOT_BITS = 27;
 constexpr uint32_t SLOT_MASK = (1u << SLOT_BITS) - 1;
-constexpr int MAX_ENCLOSING = 31;
+[[maybe_unused]] constexpr int MAX_ENCLOSING = 31;
 static_assert(MAX_CHUNK_PATHS <= (1ll << SLOT_BITS), "path slots must fit the slot bits");
-constexpr long long PATH_SLOT_BYTES = 2 * 56 + 48 + 20 + 16; // two path buffers, shadow ray, hit record, radiance
+[[maybe_unused]] constexpr long long PATH_SLOT_BYTES = 2 * 56 + 48 + 20 + 16; // two path buffers, shadow ray, hit record, radiance
 // Occupancy target (waves per SIMD) of k_extend, with global and with
 // LDS-staged traversal tables: 4 caps it at 128 VGPRs.  k_finish keeps the
 // compiler's choice (it would spill).
@@ -90,7 +90,7 @@ constexpr int NSH = 64;             // shards per stream (one per lane of the co
 constexpr int CSTRIDE = 16;         // ints between two shard counters: one 64-B atomic line each
 constexpr int CROW = NSH * CSTRIDE; // ints per counter row (one row per stream and bounce)
 constexpr int WAVES_PER_BLOCK = BLOCK / 64;
-constexpr int GRID_QUANTUM = NSH / WAVES_PER_BLOCK; // grids are multiples of this: every shard gets the same waves
+[[maybe_unused]] constexpr int GRID_QUANTUM = NSH / WAVES_PER_BLOCK; // grids are multiples of this: every shard gets the same waves
 
 struct PathBuf {
     float4* p0; // org.xyz, slot (int bits; bits 27-31: 1 + the enclosing entity index the path is in, 0: none)
@@ -311,7 +311,7 @@ struct KernelCounters {
     int* cnt_in;
     int* cnt_out;
     int* cnt_shadow;
-    unsigned long long* stats; // 9 counters (instrumentation)
+    unsigned long long* stats; // instrumentation counters (igx_get_stats: visits 0-12, phase clocks 16-19)
     int* work;                 // per-shard group counters of this bounce (FrameArgs::dynamic)
 };
 
@@ -1244,8 +1244,8 @@ constexpr int WORK_ROW0 = 2 * MAX_BOUNCES + 4;
 constexpr int CTR_ROWS = WORK_ROW0 + 4 * MAX_BOUNCES;
 // BLAS with more triangles build without spatial splits (load time; their
 // triangles are small next to the scene in the suite's soups)
-constexpr uint32_t SPATIAL_SPLIT_MAX_FACES = 1u << 21;
-constexpr size_t CTR_INTS = (size_t)CTR_ROWS * CROW;
+[[maybe_unused]] constexpr uint32_t SPATIAL_SPLIT_MAX_FACES = 1u << 21;
+[[maybe_unused]] constexpr size_t CTR_INTS = (size_t)CTR_ROWS * CROW;
 
 // records in counter row `row` of the slot's host mirror (row 0: generated paths)
 inline long long row_total(const Slot& s, int row) {
