@@ -1245,6 +1245,9 @@ constexpr int CTR_ROWS = WORK_ROW0 + 4 * MAX_BOUNCES;
 // BLAS with more triangles build without spatial splits (load time; their
 // triangles are small next to the scene in the suite's soups)
 [[maybe_unused]] constexpr uint32_t SPATIAL_SPLIT_MAX_FACES = 1u << 21;
+// face instances (faces x entities using them) up to which the upload
+// precomputes world-space face normals (16 B each: at most 64 MB)
+[[maybe_unused]] constexpr size_t FACE_NORMAL_TABLE_MAX = 4u << 20;
 [[maybe_unused]] constexpr size_t CTR_INTS = (size_t)CTR_ROWS * CROW;
 
 // records in counter row `row` of the slot's host mirror (row 0: generated paths)
@@ -1297,6 +1300,9 @@ struct igx_device {
     // 452 -> 382 ms (k_shadow_refill 220 -> 164, k_trace_refill 205 -> 193),
     // S-deep 52.7 -> 48.6 ms
     int dynamic_opt = DYN_EXTEND | DYN_REFILL_TRACE | DYN_REFILL_SHADOW;
+    // option "face_normals": precomputed world-space face normals for scenes
+    // with at most FACE_NORMAL_TABLE_MAX face instances (next upload)
+    int face_normals_opt = 1;
     float sah_node_cost = 1.0f;    // option "sah_node_cost_pct" (percent of one triangle test)
     int bvh_bins = 32;             // option "bvh_bins": SAH bins per axis of the BLAS builds (next upload)
     int bvh_bins_tlas = 32;        // option "bvh_bins_tlas": the same for the TLAS
@@ -1889,6 +1895,7 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     else if (k == "spatial_splits") dev->spatial_splits = value != 0;
     else if (k == "rebuild_bvh") dev->rebuild_bvh = value != 0;
     else if (k == "dynamic") dev->dynamic_opt = (int)(value & 15);
+    else if (k == "face_normals") dev->face_normals_opt = value != 0;
     else if (k == "bvh_bins") {
         if (value < 2 || value > 4096) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "bvh_bins must be in [2, 4096]");
         dev->bvh_bins = (int)value;
@@ -2113,6 +2120,8 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
 
     // ---- TLAS over entities (leaf size 1), instance records ---------------
     std::vector<float4> inst, ent;
+    std::vector<int> ent_fn;       // per entity: first face-normal entry, -1 without a table
+    std::vector<float4> fn_tab;    // world-space unit face normals (surface_element)
     std::vector<int> ent_enc; // per entity: enclosing index or -1
     std::vector<int2> enc_tab; // per enclosing index: entity, TLAS leaf slot
     int tlas_root = -1;
@@ -2174,6 +2183,50 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
             float4 fi;
             std::memcpy(&fi, &info, 16);
             ent.push_back(fi);
+        }
+        // world-space unit face normals of every (mesh entity, face) when the
+        // scene has few face instances: surface_element then skips three vertex
+        // loads and transforms per hit.  make_triangle (core/triangle.art:11-26)
+        // on the entity's to_global rows, in float, same operation order.
+        size_t face_instances = 0;
+        for (uint32_t e = 0; e < desc->num_entities; ++e) {
+            const igx_shape& sh = desc->shapes[desc->entities[e].shape];
+            if (sh.type == IGX_SHAPE_TRIMESH && sh.mesh >= 0) face_instances += desc->meshes[sh.mesh].num_faces;
+        }
+        if (dev->face_normals_opt && face_instances > 0 && face_instances <= FACE_NORMAL_TABLE_MAX) {
+            ent_fn.assign(desc->num_entities, -1);
+            fn_tab.reserve(face_instances);
+            for (uint32_t e = 0; e < desc->num_entities; ++e) {
+                const igx_entity& en = desc->entities[e];
+                const igx_shape& sh = desc->shapes[en.shape];
+                if (sh.type != IGX_SHAPE_TRIMESH || sh.mesh < 0) continue;
+                const igx_mesh& m = desc->meshes[sh.mesh];
+                ent_fn[e] = (int)fn_tab.size();
+                const float* T = en.to_global;
+                auto xf = [&](uint32_t v, float out[3]) {
+                    const float* p = m.vertices + 3 * v;
+                    for (int r = 0; r < 3; ++r) {
+                        float acc = T[r * 4 + 0] * p[0];
+                        acc = acc + T[r * 4 + 1] * p[1];
+                        acc = acc + T[r * 4 + 2] * p[2];
+                        out[r] = acc + T[r * 4 + 3];
+                    }
+                };
+                for (uint32_t f = 0; f < m.num_faces; ++f) {
+                    float v0[3], v1[3], v2[3];
+                    xf(m.indices[3 * f], v0);
+                    xf(m.indices[3 * f + 1], v1);
+                    xf(m.indices[3 * f + 2], v2);
+                    const float e1[3] = {v1[0] - v0[0], v1[1] - v0[1], v1[2] - v0[2]};
+                    const float e2[3] = {v2[0] - v0[0], v2[1] - v0[1], v2[2] - v0[2]};
+                    const float n[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+                    float nn2 = n[0] * n[0];
+                    nn2 = nn2 + n[1] * n[1];
+                    nn2 = nn2 + n[2] * n[2];
+                    const float inv = 1 / std::sqrt(nn2);
+                    fn_tab.push_back(make_float4(n[0] * inv, n[1] * inv, n[2] * inv, 0));
+                }
+            }
         }
     }
 
@@ -2323,10 +2376,12 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
         (st = upload(dev, nrm, &sv.nrm)) || (st = upload(dev, idx, &sv.idx)) || (st = upload(dev, mats, &sv.mats)) ||
         (st = upload(dev, lights, &sv.lights)) || (st = upload(dev, lsel.cdf, &sv.sel_cdf)) ||
         (st = upload(dev, lsel.hierarchy, &sv.sel_tree)) || (st = upload(dev, ent_enc, &sv.ent_enc)) ||
-        (st = upload(dev, enc_tab, &sv.enc))) {
+        (st = upload(dev, enc_tab, &sv.enc)) || (st = upload(dev, ent_fn, &sv.ent_fn)) ||
+        (st = upload(dev, fn_tab, &sv.fn_tab))) {
         free_scene(dev);
         return st;
     }
+    if (fn_tab.empty()) sv.fn_tab = nullptr; // surface_element computes the normals
     sv.tlas_root = tlas_root;
     sv.num_nodes = (int)(nodes.size() / nf4);
     sv.node_f4 = nf4;
@@ -2338,7 +2393,8 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
         dev->lds_scene_bytes = (int64_t)b <= dev->lds_scene_max ? b : 0;
         dev->table_bytes = b;
         dev->shading_bytes = ent.size() * sizeof(ent[0]) + vtx.size() * sizeof(vtx[0]) + nrm.size() * sizeof(nrm[0]) +
-                             idx.size() * sizeof(idx[0]) + mats.size() * sizeof(DevMaterial) + lights.size() * sizeof(lights[0]);
+                             idx.size() * sizeof(idx[0]) + mats.size() * sizeof(DevMaterial) + lights.size() * sizeof(lights[0]) +
+                             fn_tab.size() * sizeof(fn_tab[0]);
     }
     sv.num_lights = (int)lights.size();
     sv.num_infinite = num_infinite;

@@ -37,6 +37,10 @@ struct SceneView {
     int selector;          // NEE light selector in effect (IGX_SELECT_*; host/light_select.h)
     const float* sel_cdf;  // simple: CDF over the finite lights ([c_1 .. c_{n-1}, 1])
     const uint32_t* sel_tree; // hierarchy: codes (padded to 4), then 8 words per entry
+    // world-space unit face normals per (entity, face), precomputed at upload
+    // for scenes with few face instances (nullptr otherwise): fn_tab[ent_fn[e] + prim]
+    const int* ent_fn;
+    const float4* fn_tab;
 };
 
 // Copy the traversal tables (nodes, instances, triangles) of a small scene
@@ -572,14 +576,20 @@ __device__ __forceinline__ Surface surface_element(const SceneView& sv, int ent_
         return s;
     }
     int4 f = sv.idx[info.w + prim];
-    f3 v0 = xform_point_rows(g0, g1, g2, f3of(sv.vtx[info.z + f.x]));
-    f3 v1 = xform_point_rows(g0, g1, g2, f3of(sv.vtx[info.z + f.y]));
-    f3 v2 = xform_point_rows(g0, g1, g2, f3of(sv.vtx[info.z + f.z]));
-    // make_triangle (core/triangle.art:11-26)
-    f3 e1 = sub(v1, v0), e2 = sub(v2, v0);
-    f3 n = cross(e1, e2);
-    float nn = len(n);
-    f3 fn = mulf(n, 1 / nn);
+    f3 fn;
+    if (sv.fn_tab) {
+        // the upload computed the same make_triangle normal on the host
+        fn = f3of(sv.fn_tab[sv.ent_fn[ent_id] + prim]);
+    } else {
+        f3 v0 = xform_point_rows(g0, g1, g2, f3of(sv.vtx[info.z + f.x]));
+        f3 v1 = xform_point_rows(g0, g1, g2, f3of(sv.vtx[info.z + f.y]));
+        f3 v2 = xform_point_rows(g0, g1, g2, f3of(sv.vtx[info.z + f.z]));
+        // make_triangle (core/triangle.art:11-26)
+        f3 e1 = sub(v1, v0), e2 = sub(v2, v0);
+        f3 n = cross(e1, e2);
+        float nn = len(n);
+        fn = mulf(n, 1 / nn);
+    }
     f3 ln = lerp2(f3of(sv.nrm[info.z + f.x]), f3of(sv.nrm[info.z + f.y]), f3of(sv.nrm[info.z + f.z]), hu, hv);
     f3 normal = normalize(xform_dir_rows(n0, n1, n2, ln));
     s.entering = dot(rd, fn) <= 0;

@@ -383,6 +383,24 @@ def test_enclosing_shortcut_invariance(device, root, name):
     assert imgs[0].sum() > 0
 
 
+@pytest.mark.parametrize("name", ["diamond_scene.json", "materials.json"])
+def test_face_normal_table_invariance(device, root, name):
+    """World-space face normals precomputed at upload (the host restates
+    make_triangle in float with the device's operation order) render the
+    same image bit for bit as normals computed per hit."""
+    sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", name))
+    imgs = []
+    try:
+        for fnt in (0, 1):
+            device.set_option("face_normals", fnt)
+            device.upload(sc)
+            imgs.append(render_gpu(device, sc, 160, 120, 4))
+    finally:
+        device.set_option("face_normals", 1)
+    np.testing.assert_array_equal(imgs[0], imgs[1])
+    assert imgs[0].sum() > 0
+
+
 @pytest.mark.parametrize("name", ["diamond_scene.json", "primitives.json", "s_deep.json"])
 @pytest.mark.parametrize("film", [(112, 80), (640, 400)])
 def test_dynamic_groups_invariance(device, root, name, film):
