@@ -363,7 +363,9 @@ def main():
         if n_gpus == 1 and args.suite:
             # other scenes of SURVEY.md §8d, incl. the HBM roofline scene of record (S-soup-16M)
             suite = [suite_line(ignis_amd, 0, os.path.join(ROOT, "scenes", f), spi, n, size)
-                     for f, n, size in (("primitives.json", 8, None), ("s_deep.json", 4, None), ("s_soup_1m.json", 2, None),
+                     for f, n, size in (("primitives.json", 8, None),
+                                        # config 4 stand-in at its stated 1024 spp (128 iterations x spi 8)
+                                        ("s_deep.json", 128, None), ("s_soup_1m.json", 2, None),
                                         ("s_soup_16m.json", 1, None),
                                         # config 5 stand-in: S-deep at 4096x4096, 64 spp
                                         ("s_deep.json", 8, (4096, 4096)))]

@@ -812,6 +812,43 @@ def test_config5_tile_shard_gather_equals_single_device(root, n_shards):
         dev.close()
 
 
+def test_config4_s_deep_1024spp_full_size(device, root):
+    """BASELINE config 4 stand-in at its stated sample count:
+    S-deep (4096 instances) at 1000x1000, 1024 spp = 128 iterations of spi 8.
+    Size-independent properties at full size: the one-call frame equals the
+    frame of two 64-iteration calls bit for bit (iteration offsets, chunking
+    and the tail are exact over 128 M-path wavefronts), and the two
+    independent 512-spp halves agree in RunEvaluations' metric (the estimator
+    is converging, no NaN/inf, no biased half)."""
+    sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", "s_deep.json"))
+    w, h = sc.film_size
+    assert (w, h) == (1000, 1000)
+    p = ignis_amd.RenderParams()
+    p.width, p.height, p.spi = w, h, 8
+    device.upload(sc)
+    device.set_option("capacity", 0)
+    device.clear()
+    device.reset_stats()
+    p.iteration = 0
+    device.render_iterations(p, 128)
+    full, it = device.framebuffer(w * h * 3)
+    assert it == 128
+    assert device.stats()["camera_rays"] == w * h * 1024
+    halves = []
+    device.clear()
+    for k in range(2):
+        p.iteration = 64 * k
+        device.render_iterations(p, 64)
+        acc, _ = device.framebuffer(w * h * 3)
+        halves.append(acc.copy())
+    np.testing.assert_array_equal(full, halves[1])
+    first = halves[0] / 64
+    second = (halves[1] - halves[0]) / 64
+    assert np.isfinite(full).all() and full.mean() > 0
+    assert rel_mse(second.reshape(h, w, 3), first.reshape(h, w, 3)) < 5e-2
+    assert abs(first.mean() - second.mean()) <= 2e-2 * first.mean()
+
+
 def test_pack_tiles_rejects_a_film_that_is_not_the_framebuffer(device, diamond_path):
     """igx_pack_tiles reads dev->fb through the tile table: a film larger than
     the allocated framebuffer must be refused, not read out of bounds."""
