@@ -30,6 +30,22 @@ __host__ __device__ constexpr int variant_width(int v) { return (v & 2) ? 4 : 2;
 __host__ __device__ constexpr bool variant_spill(int v) { return (v & 1) != 0; }
 __host__ __device__ constexpr bool variant_full(int v) { return (v & 4) != 0; }
 __host__ __device__ constexpr int node_f4(int width) { return width == 4 ? 8 : 4; }
+// LDS-staged node tables keep one float4 of padding per node (BVH2 nodes 80 B,
+// 4-wide 144 B apart): lanes that read the same float4 of different nodes then
+// hit different 16-B bank groups (an odd multiple of 16 B cycles through all
+// 16 groups of the 256-B bank period) instead of the two groups a 64/128-B
+// stride maps every node to.  Bit 3 of the variant selects that stride; the
+// kernels set it on their LDS-staged SceneView only.
+#ifndef IGX_LDS_NODE_PAD
+#define IGX_LDS_NODE_PAD 0
+#endif
+__host__ __device__ constexpr bool variant_ldspad(int v) { return (v & 8) != 0; }
+__host__ __device__ constexpr int lds_variant(int v, bool lds) { return (lds && IGX_LDS_NODE_PAD) ? (v | 8) : v; }
+__host__ __device__ constexpr int lds_node_pad() { return IGX_LDS_NODE_PAD ? 1 : 0; }
+// Bit 4: if-if stepping (trav_step advances one inner node or one leaf per
+// call) -- set only on k_shadow_refill launches for scenes on the split
+// schedule (igx_device.hip, use_shadow_ifif).
+__host__ __device__ constexpr bool variant_ifif(int v) { return (v & 16) != 0; }
 
 // Instance record (one per TLAS leaf slot): 64 B
 //   row0..row2: to_local 3x4 (row-major, xyz = linear row, w = translation)

@@ -614,9 +614,10 @@ __device__ __forceinline__ int take_group(int* work, int& s, uint64_t& done, int
 // rays to the same shard of the output streams (wave_append_paths): no block
 // barrier, so a wave whose rays finish early moves on to its next 64 paths.
 // ---------------------------------------------------------------------------
-template <int V, bool STATS, bool LDS>
+template <int V0, bool STATS, bool LDS>
 __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : EXTEND_WAVES) k_extend(FrameArgs fa, SceneView gsv, PathBuf in, PathBuf out, ShadowBuf sh,
                                                   float4* L, KernelCounters kc, int tail_threshold) {
+    constexpr int V = lds_variant(V0, LDS); // LDS-staged nodes: padded stride (device_scene.h)
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
@@ -756,9 +757,10 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : EXTEND_WAVES) 
 // for high occupancy (the latency of the dependent node loads is what bounds
 // it); each lane writes its own hit record (same index as its path).
 // ---------------------------------------------------------------------------
-template <int V, bool STATS, int WAVES, bool LDS>
+template <int V0, bool STATS, int WAVES, bool LDS>
 __global__ void __launch_bounds__(BLOCK, WAVES) k_trace(FrameArgs fa, SceneView gsv, PathBuf in, HitBuf hits,
                                                       const int* cnt, int tail_threshold, unsigned long long* stats) {
+    constexpr int V = lds_variant(V0, LDS); // LDS-staged nodes: padded stride (device_scene.h)
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
@@ -837,10 +839,11 @@ __global__ void __launch_bounds__(BLOCK) k_shade(FrameArgs fa, SceneView sv, Pat
 // empty per-bounce launches.  Same per-path arithmetic and the same radiance
 // accumulation order as the wavefront kernels.
 // ---------------------------------------------------------------------------
-template <int V, bool STATS, bool LDS>
+template <int V0, bool STATS, bool LDS>
 __global__ void __launch_bounds__(BLOCK) k_finish(FrameArgs fa, SceneView gsv, PathBuf in, float4* L, const int* cnt,
                                                   int tail_threshold, unsigned long long* stats,
                                                   unsigned long long* tail_counts) {
+    constexpr int V = lds_variant(V0, LDS); // LDS-staged nodes: padded stride (device_scene.h)
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
@@ -893,9 +896,10 @@ __global__ void __launch_bounds__(BLOCK) k_finish(FrameArgs fa, SceneView gsv, P
 // shadow: any-hit traversal; on miss add the NEE contribution
 // (gpu_traverse_secondary, mapping_gpu.art:70-112; on_shadow_miss, pathtracer.art:202-209)
 // ---------------------------------------------------------------------------
-template <int V, bool STATS, bool LDS>
+template <int V0, bool STATS, bool LDS>
 __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, float4* L, const int* cnt,
                                                   unsigned long long* stats, int* work) {
+    constexpr int V = lds_variant(V0, LDS); // LDS-staged nodes: padded stride (device_scene.h)
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
@@ -1038,10 +1042,11 @@ struct GroupSeq {
     }
 };
 
-template <int V, bool STATS, bool LDS>
+template <int V0, bool STATS, bool LDS>
 __global__ void __launch_bounds__(BLOCK, LDS ? REFILL_WAVES_LDS : REFILL_WAVES) k_trace_refill(FrameArgs fa, SceneView gsv, PathBuf in, HitBuf hits,
                                                                      const int* cnt, int tail_threshold,
                                                                      unsigned long long* stats, int refill_min, int* work) {
+    constexpr int V = lds_variant(V0, LDS); // LDS-staged nodes: padded stride (device_scene.h)
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
@@ -1075,9 +1080,10 @@ __global__ void __launch_bounds__(BLOCK, LDS ? REFILL_WAVES_LDS : REFILL_WAVES) 
     if (STATS) flush_stats<STATS>(st, stats, 0, true);
 }
 
-template <int V, bool STATS, bool LDS>
+template <int V0, bool STATS, bool LDS>
 __global__ void __launch_bounds__(BLOCK, LDS ? REFILL_WAVES_LDS : REFILL_WAVES) k_shadow_refill(SceneView gsv, ShadowBuf sh, float4* L, const int* cnt,
                                                                       unsigned long long* stats, int refill_min, int* work) {
+    constexpr int V = lds_variant(V0, LDS); // LDS-staged nodes: padded stride (device_scene.h)
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
@@ -1280,6 +1286,7 @@ struct igx_device {
     int split_opt = -1;      // k_trace + k_shade per bounce instead of the fused k_extend (-1: auto = global-table scenes)
     int trace_waves = 5;     // occupancy target of k_trace (5 waves per SIMD, anything else = compiler's choice)
     int refill_opt = -1;     // persistent-lane trace / shadow, refilled once this many lanes idle (0: off, -1: auto = 16)
+    int shadow_ifif_opt = -1; // if-if stepping in k_shadow_refill (-1: auto = split-schedule scenes)
     int64_t lds_scene_max = 48 * 1024; // stage traversal tables in LDS when they fit (0 = never)
     size_t lds_scene_bytes = 0;        // bytes staged per block for the current scene (0 = global tables)
     size_t table_bytes = 0;            // traversal tables (nodes, instances, triangles) of the current scene
@@ -1491,6 +1498,14 @@ inline bool use_refill(const igx_device* dev) {
 inline bool use_split(const igx_device* dev) {
     return dev->split_opt >= 0 ? dev->split_opt != 0 : (dev->lds_scene_bytes == 0 && dev->table_bytes > SPLIT_TABLE_BYTES);
 }
+// if-if stepping for the persistent-lane shadow kernel (variant bit 4): on the
+// big-table scenes of the split schedule a lane at a leaf no longer waits for
+// the wave's slowest inner-node walk (any-hit rays end at their first
+// occluder, so their lengths vary most); on S-deep-sized tables the while-while
+// loop is faster.  Option "shadow_ifif": -1 auto, 0 off, 1 on.
+inline bool use_shadow_ifif(const igx_device* dev) {
+    return dev->shadow_ifif_opt >= 0 ? dev->shadow_ifif_opt != 0 : use_split(dev);
+}
 
 // Launch helpers dispatching on the scene's traversal variant.
 #define IGX_DISPATCH_VARIANT(v, MACRO)        \
@@ -1573,7 +1588,12 @@ void launch_shadow(igx_device* dev, Slot& s, int grid, const int* cnt, int* work
     else                                                                                                                 \
         hipLaunchKernelGGL((k_shadow_refill<S, STATS, false>), dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, s.sh, s.L, \
                            cnt, dev->dstats, refill_min(dev), work)
-        IGX_DISPATCH_VARIANT(dev->variant, L_SHR);
+#define L_SHRI(S)                                                                                                       \
+    hipLaunchKernelGGL((k_shadow_refill<S | 16, STATS, false>), dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, s.sh, s.L, \
+                       cnt, dev->dstats, refill_min(dev), work)
+        if (!dev->lds_scene_bytes && use_shadow_ifif(dev)) IGX_DISPATCH_VARIANT(dev->variant, L_SHRI);
+        else IGX_DISPATCH_VARIANT(dev->variant, L_SHR);
+#undef L_SHRI
 #undef L_SHR
         return;
     }
@@ -1876,6 +1896,10 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
         if (value < -1 || value > 1) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "split must be -1 (auto), 0 or 1");
         dev->split_opt = (int)value;
     }
+    else if (k == "shadow_ifif") {
+        if (value < -1 || value > 1) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "shadow_ifif must be -1 (auto), 0 or 1");
+        dev->shadow_ifif_opt = (int)value;
+    }
     else if (k == "trace_waves") dev->trace_waves = (int)value;
     else if (k == "refill") {
         if (value < -1 || value > 64) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "refill must be -1 (auto) or in [0, 64]");
@@ -1883,7 +1907,8 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     }
     else if (k == "lds_scene_max") {
         dev->lds_scene_max = value;
-        size_t b = ((size_t)dev->sv.num_nodes * dev->sv.node_f4 + (size_t)dev->sv.num_inst * 4 + (size_t)dev->sv.num_tris * 3) * 16;
+        size_t b = ((size_t)dev->sv.num_nodes * (dev->sv.node_f4 + lds_node_pad()) + (size_t)dev->sv.num_inst * 4 +
+                    (size_t)dev->sv.num_tris * 3) * 16; // LDS layout (stage_scene_lds)
         dev->lds_scene_bytes = dev->has_scene && (int64_t)b <= value ? b : 0;
     }
     else if (k == "full_shading") dev->full_shading_opt = value != 0;
@@ -2390,7 +2415,8 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     sv.num_tris = (int)(tris.size() / 3);
     {
         size_t b = ((size_t)sv.num_nodes * nf4 + (size_t)sv.num_inst * 4 + (size_t)sv.num_tris * 3) * 16;
-        dev->lds_scene_bytes = (int64_t)b <= dev->lds_scene_max ? b : 0;
+        const size_t bl = b + (size_t)sv.num_nodes * lds_node_pad() * 16; // LDS layout (stage_scene_lds)
+        dev->lds_scene_bytes = (int64_t)bl <= dev->lds_scene_max ? bl : 0;
         dev->table_bytes = b;
         dev->shading_bytes = ent.size() * sizeof(ent[0]) + vtx.size() * sizeof(vtx[0]) + nrm.size() * sizeof(nrm[0]) +
                              idx.size() * sizeof(idx[0]) + mats.size() * sizeof(DevMaterial) + lights.size() * sizeof(lights[0]) +

@@ -49,8 +49,9 @@ struct SceneView {
 // path, which the divergent node fetches otherwise keep busy.
 template <int BLOCK_>
 __device__ __forceinline__ SceneView stage_scene_lds(const SceneView& sv, float4* lds) {
-    const int n4 = sv.num_nodes * sv.node_f4, i4 = sv.num_inst * 4, t3 = sv.num_tris * 3;
-    for (int k = threadIdx.x; k < n4; k += BLOCK_) lds[k] = sv.nodes[k];
+    const int nf = sv.node_f4, sh = nf == 8 ? 3 : 2, ns = nf + lds_node_pad(); // node stride in LDS (float4)
+    const int n4 = sv.num_nodes * ns, i4 = sv.num_inst * 4, t3 = sv.num_tris * 3;
+    for (int k = threadIdx.x; k < sv.num_nodes * nf; k += BLOCK_) lds[(k >> sh) * ns + (k & (nf - 1))] = sv.nodes[k];
     for (int k = threadIdx.x; k < i4; k += BLOCK_) lds[n4 + k] = sv.inst[k];
     for (int k = threadIdx.x; k < t3; k += BLOCK_) lds[n4 + i4 + k] = sv.tris[k];
     __syncthreads();
@@ -172,14 +173,14 @@ __device__ __forceinline__ void trav_init(const SceneView& sv, Trav& t, f3 o, f3
 // Slab test of both children of BVH2 node `node` (intersect_ray_box,
 // intersection.art:170-181, with ray.tmin folded in).  Returns the next node
 // (nearer child first; the other is pushed) or the popped entry.
-template <bool STATS, bool SPILL>
+template <bool STATS, bool SPILL, int NS>
 __device__ __forceinline__ int node_step2(const SceneView& sv, const Trav& t, int node, const TStack& ts, int& sp,
                                          TraceStats& st) {
     if (STATS) {
         st.nodes++;
         if (first_active_lane()) st.wnodes++;
     }
-    const float4* np = sv.nodes + 4 * node;
+    const float4* np = sv.nodes + NS * node;
     float4 a = np[0], b = np[1], c = np[2];
     int4 r = *reinterpret_cast<const int4*>(np + 3);
     // child 0 box: lo (a.x, a.z, b.x) hi (a.y, a.w, b.y)
@@ -226,14 +227,14 @@ __device__ __forceinline__ void cswap(float& da, int& ra, float& db, int& rb) {
     da = td;
     ra = tr;
 }
-template <bool STATS, bool SPILL>
+template <bool STATS, bool SPILL, int NS>
 __device__ __forceinline__ int node_step4(const SceneView& sv, const Trav& t, int node, const TStack& ts, int& sp,
                                           TraceStats& st) {
     if (STATS) {
         st.nodes++;
         if (first_active_lane()) st.wnodes++;
     }
-    const float4* np = sv.nodes + 8 * node;
+    const float4* np = sv.nodes + NS * node;
     const float4 lx = np[0], hx = np[1], ly = np[2], hy = np[3], lz = np[4], hz = np[5];
     const int4 r = *reinterpret_cast<const int4*>(np + 6);
     float d[4];
@@ -269,8 +270,9 @@ __device__ __forceinline__ int node_step4(const SceneView& sv, const Trav& t, in
 template <bool STATS, int V>
 __device__ __forceinline__ int node_step(const SceneView& sv, const Trav& t, int node, const TStack& ts, int& sp,
                                          TraceStats& st) {
-    if constexpr (variant_width(V) == 4) return node_step4<STATS, variant_spill(V)>(sv, t, node, ts, sp, st);
-    else return node_step2<STATS, variant_spill(V)>(sv, t, node, ts, sp, st);
+    constexpr int PAD = variant_ldspad(V) ? 1 : 0;
+    if constexpr (variant_width(V) == 4) return node_step4<STATS, variant_spill(V), 8 + PAD>(sv, t, node, ts, sp, st);
+    else return node_step2<STATS, variant_spill(V), 4 + PAD>(sv, t, node, ts, sp, st);
 }
 
 // Back from a BLAS: restore the world ray (recomputed: cheaper than keeping
@@ -377,7 +379,17 @@ __device__ __forceinline__ bool trav_step(const SceneView& sv, Trav& t, const TS
     int node = t.node;
     int sp = t.sp;
     constexpr bool SPILL = variant_spill(V);
-    while (node >= 0) node = node_step<STATS, V>(sv, t, node, ts, sp, st);
+    if constexpr (variant_ifif(V)) {
+        // if-if: one inner node per call, so a lane that reached a leaf does
+        // not idle until every lane of the wave has reached one
+        if (node >= 0) {
+            t.node = node_step<STATS, V>(sv, t, node, ts, sp, st);
+            t.sp = sp;
+            return false;
+        }
+    } else {
+        while (node >= 0) node = node_step<STATS, V>(sv, t, node, ts, sp, st);
+    }
     if (node == REF_EXIT) {
         t.node = node;
         t.sp = sp;

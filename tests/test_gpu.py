@@ -312,11 +312,14 @@ def test_split_and_refill_invariance(device, root, name):
     try:
         device.upload(sc)
         # global tables, then (diamond) LDS-staged tables with explicit split / refill
-        runs = [(0, 0, 0), (0, 1, 0), (0, 1, 16), (0, 0, 8), (0, -1, -1), (48 * 1024, 1, 16), (48 * 1024, 0, 32)]
-        for lds, split, refill in runs:
+        # (lds_scene_max, split, refill, shadow_ifif): if-if stepping of the persistent-lane shadow kernel too
+        runs = [(0, 0, 0, -1), (0, 1, 0, -1), (0, 1, 16, 0), (0, 1, 16, 1), (0, 0, 8, 1), (0, -1, -1, -1),
+                (48 * 1024, 1, 16, -1), (48 * 1024, 0, 32, -1)]
+        for lds, split, refill, ifif in runs:
             device.set_option("lds_scene_max", lds)
             device.set_option("split", split)
             device.set_option("refill", refill)
+            device.set_option("shadow_ifif", ifif)
             device.reset_stats()
             imgs.append(render_gpu(device, sc, 112, 80, 4))
             st = device.stats()
@@ -324,6 +327,7 @@ def test_split_and_refill_invariance(device, root, name):
     finally:
         device.set_option("split", -1)
         device.set_option("refill", -1)
+        device.set_option("shadow_ifif", -1)
         device.set_option("lds_scene_max", 48 * 1024)
     for im, c in zip(imgs[1:], counts[1:]):
         np.testing.assert_array_equal(imgs[0], im)
