@@ -949,6 +949,10 @@ __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, f
 #ifndef REFILL_WAVES
 #define REFILL_WAVES 6
 #endif
+// the if-if shadow kernel (split-schedule scenes) needs fewer registers
+#ifndef SHADOW_IFIF_WAVES
+#define SHADOW_IFIF_WAVES 6
+#endif
 // LDS-staged tables (<= 48 KB + the 16 KB stack per block) allow at most
 // 4 blocks per CU: the 6-wave VGPR cap would only force spills
 #ifndef REFILL_WAVES_LDS
@@ -1081,7 +1085,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? REFILL_WAVES_LDS : REFILL_WAVES) 
 }
 
 template <int V0, bool STATS, bool LDS>
-__global__ void __launch_bounds__(BLOCK, LDS ? REFILL_WAVES_LDS : REFILL_WAVES) k_shadow_refill(SceneView gsv, ShadowBuf sh, float4* L, const int* cnt,
+__global__ void __launch_bounds__(BLOCK, LDS ? REFILL_WAVES_LDS : (variant_ifif(V0) ? SHADOW_IFIF_WAVES : REFILL_WAVES)) k_shadow_refill(SceneView gsv, ShadowBuf sh, float4* L, const int* cnt,
                                                                       unsigned long long* stats, int refill_min, int* work) {
     constexpr int V = lds_variant(V0, LDS); // LDS-staged nodes: padded stride (device_scene.h)
     __shared__ int stack_mem[LDS_STACK * BLOCK];
