@@ -74,6 +74,13 @@ static_assert(MAX_CHUNK_PATHS <= (1ll << SLOT_BITS), "path slots must fit the sl
 #ifndef EXTEND_WAVES
 #define EXTEND_WAVES 4
 #endif
+// the full shading variant on global tables: 3 waves per SIMD (no spills)
+// instead of 4 (~150 spilled VGPRs): materials frame 55.3 -> 54.0 ms; the
+// basic variant stays at 4 (S-deep 31.5 -> 36.1, primitives 22.0 -> 24.3 ms
+// at 3), profiles/r02_ab_extend_waves.log
+#ifndef EXTEND_WAVES_FULL
+#define EXTEND_WAVES_FULL 3
+#endif
 #ifndef EXTEND_WAVES_LDS
 #define EXTEND_WAVES_LDS 4
 #endif
@@ -615,7 +622,7 @@ __device__ __forceinline__ int take_group(int* work, int& s, uint64_t& done, int
 // barrier, so a wave whose rays finish early moves on to its next 64 paths.
 // ---------------------------------------------------------------------------
 template <int V0, bool STATS, bool LDS>
-__global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : EXTEND_WAVES) k_extend(FrameArgs fa, SceneView gsv, PathBuf in, PathBuf out, ShadowBuf sh,
+__global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(V0) ? EXTEND_WAVES_FULL : EXTEND_WAVES)) k_extend(FrameArgs fa, SceneView gsv, PathBuf in, PathBuf out, ShadowBuf sh,
                                                   float4* L, KernelCounters kc, int tail_threshold) {
     constexpr int V = lds_variant(V0, LDS); // LDS-staged nodes: padded stride (device_scene.h)
     __shared__ int stack_mem[LDS_STACK * BLOCK];
