@@ -55,6 +55,9 @@ def parse():
 # Tables up to half the 256 MiB Infinity Cache count as on-chip: a table stays resident only while it and
 # everything streamed between two uses of a line fit the cache (MI355X_MICROARCH.md, Infinity Cache)
 MALL_BYTES = 128 << 20
+# N > 1: device memory per handle for its two stream slots (a rank holds two
+# handles); 20 GB bounds a chunk at 51 M paths, 196 B each per slot
+SLOT_BUDGET_MB = int(os.environ.get("IGX_SLOT_BUDGET_MB", "20000"))
 
 
 def algorithmic_bytes(inst, st):
@@ -107,6 +110,28 @@ def load_pmc(n_gpus, scene="diamond_scene", kernel="extend"):
         return None
 
 
+def load_rocprof(scene_key, split):
+    """Average duration (us) of the dominant kernel in the newest committed
+    rocprofv3 --kernel-trace --stats summary of the same workload:
+    profiles/rNN_kernel_stats.csv (headline diamond) or
+    profiles/rNN_<key>_kernel_stats.csv (suite lines, tools/gpu_profile_suite.sh)."""
+    import csv
+    import re
+    pat = re.compile(r"^r(\d\d)_kernel_stats\.csv$" if scene_key == "diamond_scene" else
+                     r"^r(\d\d)_" + re.escape(scene_key) + r"_kernel_stats\.csv$")
+    d = os.path.join(ROOT, "profiles")
+    files = sorted((f for f in os.listdir(d) if pat.match(f)), key=lambda f: int(pat.match(f).group(1)))
+    if not files:
+        return None
+    want = "k_trace_refill<" if split else "k_extend<"
+    with open(os.path.join(d, files[-1])) as f:
+        for r in csv.DictReader(f):
+            if want in r["Name"]:
+                return {"file": "profiles/" + files[-1], "avg_us": round(float(r["AverageNs"]) / 1e3, 2),
+                        "calls": int(r["Calls"])}
+    return None
+
+
 def roofline(dev, st, render_one, n_gpus, scene_key):
     """Roofline object of the dominant kernel: algorithmic HBM bytes (visit
     counts from an instrumented, untimed pass) over its HIP-event launch time,
@@ -153,6 +178,12 @@ def roofline(dev, st, render_one, n_gpus, scene_key):
         "avg_launch_us": round(avg_launch_s * 1e6, 2),
         "launches": launches,
     }
+    rp = load_rocprof(scene_key, split) if n_gpus == 1 else None
+    if rp:
+        # the same quantities over the committed rocprof average of the same kernel and workload
+        t = rp["avg_us"] * 1e-6
+        out["rocprof"] = dict(rp, frac=round(alg_bytes / launches / t / 1e9 / HBM_PEAK_GBS, 4),
+                              frac_traffic=round(traffic / t / 1e9 / HBM_PEAK_GBS, 4) if traffic else None)
     out["limiter"] = (f"not HBM: tables on chip, node loop at {simd:.0%} SIMD efficiency (divergent per-lane "
                       "traversal; VALU-issue bound, profiles/r01_pmc_diamond.md)" if resident else
                       f"dependent node-fetch latency: {simd:.0%} SIMD efficiency, L2 hit rate ~44% "
@@ -186,7 +217,8 @@ def suite_line(ignis_amd, dev_index, path, spi, iters, size=None):
     st = dev.stats()
     dev.set_option("timing", 0)
     rays = st["camera_rays"] + st["bounce_rays"] + st["shadow_rays"]
-    key = os.path.splitext(os.path.basename(path))[0]
+    # profiles/ key of the suite line: scene stem, plus the film size when overridden (config 5: s_deep_4096)
+    key = os.path.splitext(os.path.basename(path))[0] + (f"_{size[0]}" if size else "")
     line = {"scene": os.path.basename(path), "width": W, "height": H, "spi": spi, "iterations": iters,
             "value": round(rays / dt / 1e6, 2), "unit": "Mrays/s", "ms_per_iteration": round(dt / iters * 1e3, 3),
             "load_and_build_s": round(t_load, 2), "bvh_depth": st["bvh_depth"],
@@ -196,9 +228,36 @@ def suite_line(ignis_amd, dev_index, path, spi, iters, size=None):
     return line
 
 
+def launch_ranks(args):
+    """`bench.py --gpus N` (N > 1) started without a launcher: run N ranks as a
+    child `torch.distributed.run` (one process per GPU, rendezvous on
+    127.0.0.1) with the same arguments, relay its output (rank 0 prints the
+    JSON line) and return its exit code.  Runs before anything touches the
+    GPU, and starts a child instead of replacing this process."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: launch one rank per GPU "
+                         f"(torch.distributed.run --nproc-per-node {args.gpus}) or drop the launcher")
+    if os.environ.get("IGX_BENCH_LAUNCH_PROBE") == "1":
+        # launcher test hook (tests/test_bench_launch.py): report the rank layout, touch no GPU
+        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "world": world, "gpus": args.gpus}), flush=True)
+        return None
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     n_gpus = max(world, 1)
@@ -256,6 +315,10 @@ def main():
     if n_gpus > 1:
         devs.append(ignis_amd.Device(gpu))
         devs[1].upload(scene)
+        # each handle's stream slots sized to the rank's share: two handles in
+        # 2 x SLOT_BUDGET_MB (the auto size is a quarter of HBM per handle)
+        for d in devs:
+            d.set_option("slot_budget_mb", SLOT_BUDGET_MB)
     pending = []
     count = [0]
 
@@ -394,7 +457,9 @@ def main():
                 "workload": f"{os.path.basename(args.scene)} {W}x{H}, {iters * spi} spp = {iters} iterations x spi {spi}, path tracer max_depth {scene.desc.technique.max_depth}, seed 0",
                 "scene": os.path.basename(args.scene),
                 "width": W, "height": H, "spp": iters * spi, "spi": spi,
-                "parallelism": f"tile-shard x{n_gpus} ({tile}x{tile} tiles round-robin) + RCCL gather to rank 0" if n_gpus > 1 else "single GPU",
+                "parallelism": (f"tile-shard x{n_gpus} ({tile}x{tile} tiles round-robin) + "
+                                + ("gloo (rehearsal: every rank on GPU 0)" if rehearsal else "RCCL gather to rank 0"))
+                if n_gpus > 1 else "single GPU",
             },
             "msamples_per_s": round(samples / elapsed / 1e6, 2),
             "rays": {"camera": int(totals[1]), "bounce": int(totals[2]), "shadow": int(totals[3])},
@@ -408,6 +473,8 @@ def main():
         }
         if frame_check is not None:
             result["frame_equals_single_gpu"] = frame_check
+        result["slot_bytes_per_handle"] = [int(d.stats()["slot_bytes"]) for d in devs]
+        result["backend"] = ("gloo (rehearsal)" if rehearsal else "nccl (RCCL)") if n_gpus > 1 else None
         print(json.dumps(result), flush=True)
     if dist:
         dist.barrier()
@@ -417,16 +484,35 @@ def main():
     return result
 
 
+def cgroup_cpu_quota():
+    """CPUs' worth of time the cgroup grants this process (cgroup v2 cpu.max,
+    or v1 cfs quota / period), None when unlimited."""
+    for path, split in (("/sys/fs/cgroup/cpu.max", None),
+                        ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "/sys/fs/cgroup/cpu/cpu.cfs_period_us")):
+        try:
+            if split is None:
+                q, per = open(path).read().split()[:2]
+            else:
+                q, per = open(path).read().strip(), open(split).read().strip()
+            if q in ("max", "-1"):
+                return None
+            return max(1, int(math.ceil(int(q) / int(per))))
+        except (OSError, ValueError):
+            continue
+    return None
+
+
 def cpu_threads():
-    """Threads of the CPU baseline: the reference CPU device uses
-    hardware_concurrency (Device.cpp:347).  Here that is the CPUs this process
-    may run on (affinity / cgroup cpuset), capped by OMP_NUM_THREADS, which the
-    GPU boxes set to the job's CPU share (the machine has many more)."""
-    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    omp = os.environ.get("OMP_NUM_THREADS")
-    if omp and omp.isdigit() and int(omp) > 0:
-        n = min(n, int(omp))
-    return max(1, n)
+    """Threads of the CPU baseline.  The reference CPU device runs TBB with
+    hardware_concurrency threads (Device.cpp:347), which counts the CPUs the
+    process may run on (affinity) and ignores OMP_NUM_THREADS; so does this.
+    The GPU boxes grant the job a cgroup CPU quota (cpu.max 1600000/100000 =
+    16 CPUs) on a 256-CPU affinity mask: more threads than the quota are
+    throttled to the same CPU time, so the baseline runs min(affinity, quota)
+    threads and reports both numbers.  Returns (threads, affinity, quota)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = cgroup_cpu_quota()
+    return max(1, min(aff, quota) if quota else aff), aff, quota
 
 
 def cpu_model():
@@ -449,7 +535,7 @@ def cpu_baseline(scene, dev, W, H, spi, target_s):
     12 runs take about target_s; value = the median run.  Also the per-pixel
     parity of the GPU band (iteration 0)."""
     from oracle import oracle_py as O
-    threads = cpu_threads()
+    threads, affinity, quota = cpu_threads()
     orc = O.OracleScene(scene)
     # calibrate on 8 rows, then size the band for ~target_s / 12 per run
     y0 = H // 2
@@ -473,10 +559,14 @@ def cpu_baseline(scene, dev, W, H, spi, target_s):
         "cores": threads,
         "kind": "port",
         "min_med_max": [round(rates[0], 3), round(med, 3), round(rates[-1], 3)],
+        "per_thread": round(med / threads, 3),
         "cpu_model": cpu_model(),
         "machine_logical_cpus": os.cpu_count(),
+        "hardware_concurrency": affinity,
+        "cgroup_cpu_quota": quota,
         "sample": f"oracle/oracle.c (restated reference CPU device, SAH BVH4 + Tri4 leaves), {threads} threads "
-                  f"(the job's CPU share of a {os.cpu_count()}-CPU {cpu_model()} host), rows {y0}-{y0 + rows} of the "
+                  f"(hardware_concurrency {affinity} on a {cpu_model()} host, cgroup CPU quota "
+                  f"{quota if quota else 'none'}: min of the two), rows {y0}-{y0 + rows} of the "
                   f"{W}x{H} frame, 2 warm-up + 10 timed runs of one iteration (spi {spi}) each, "
                   f"{sum(t for _, t in runs):.1f} s timed",
     }

@@ -1291,6 +1291,10 @@ struct igx_device {
     bool timing = false;
     bool instrument = false;
     int64_t capacity_opt = 0;
+    // option "slot_budget_mb": device memory the two stream slots of this
+    // handle may take (0 = auto: a quarter of the device memory).  A rank of
+    // a multi-GPU render holds two handles (bench.py), each sized to its share
+    int64_t slot_budget_mb = 0;
     int64_t tail_opt = -1;   // paths at or below which k_finish takes over (-1 = auto)
     int64_t tail_last_opt = -1; // the same for the last chunk of a render call, whose tail overlaps nothing (-1 = tail_opt)
     bool fuse_generate = true; // bounce 0 of the fused k_extend builds its camera paths (no k_generate pass)
@@ -1900,6 +1904,10 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     if (k == "timing") dev->timing = value != 0;
     else if (k == "instrument") dev->instrument = value != 0;
     else if (k == "capacity") dev->capacity_opt = value;
+    else if (k == "slot_budget_mb") {
+        if (value < 0) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "slot_budget_mb must be >= 0 (0 = auto)");
+        dev->slot_budget_mb = value;
+    }
     else if (k == "tail_threshold") dev->tail_opt = value;
     else if (k == "tail_threshold_last") dev->tail_last_opt = value;
     else if (k == "fuse_generate") dev->fuse_generate = value != 0;
@@ -2084,7 +2092,8 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
             for (auto nd : br.nodes) {
                 for (int k = 0; k < 2; ++k) {
                     if (nd.ref[k] >= 0) nd.ref[k] += node_off;
-                    else if (nd.b[k * 6] <= nd.b[k * 6 + 1]) nd.ref[k] = move_leaf(nd.ref[k]); // empty children keep -1
+                    else if (nd.ref[k] != igx::kEmptyRef && nd.b[k * 6] <= nd.b[k * 6 + 1])
+                        nd.ref[k] = move_leaf(nd.ref[k]); // empty and absent children keep their code
                 }
                 float4 f[4];
                 std::memcpy(f, &nd, 64);
@@ -2559,11 +2568,14 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
     // (MI355X: 128 M paths, 2 x 25 GB).  Fewer, larger chunks leave fewer
     // tails that overlap nothing: diamond frame 193 -> 179 ms, S-deep 4096^2
     // 865 -> 823 ms from 32 M to 128 M paths (tools/sweep_frame.py)
+    const long long slot_budget = dev->slot_budget_mb > 0 ? dev->slot_budget_mb * (1ll << 20) : (long long)(dev->mem_total / 4);
     long long auto_chunk_paths = 1ll << 24;
-    while (auto_chunk_paths < MAX_CHUNK_PATHS && 2 * (2 * auto_chunk_paths) * PATH_SLOT_BYTES <= (long long)(dev->mem_total / 4))
+    while (auto_chunk_paths < MAX_CHUNK_PATHS && 2 * (2 * auto_chunk_paths) * PATH_SLOT_BYTES <= slot_budget)
         auto_chunk_paths *= 2;
+    if (dev->slot_budget_mb > 0) // an explicit budget also bounds the chunk below 16 M paths
+        auto_chunk_paths = std::max<long long>(1ll << 20, std::min<long long>(auto_chunk_paths, slot_budget / (2 * PATH_SLOT_BYTES)));
     long long cap = dev->capacity_opt > 0 ? dev->capacity_opt
-                                          : (count > 1 ? auto_chunk_paths : std::min<long long>(total_paths, 1ll << 24));
+                                          : (count > 1 ? auto_chunk_paths : std::min<long long>({total_paths, 1ll << 24, auto_chunk_paths}));
     cap = std::min<long long>(cap, MAX_CHUNK_PATHS);
     cap = std::max<long long>(p->spi, (cap / p->spi) * p->spi);
     const long long chunk_pixels_max = std::min<long long>(cap, total_paths) / p->spi;
@@ -2827,6 +2839,8 @@ extern "C" igx_status igx_get_stats(igx_device* dev, igx_stats* out) {
     out->shadow_blocks_per_cu = dev->has_scene ? shadow_blocks_per_cu<false>(dev->variant, dev->lds_scene_bytes, use_refill(dev)) : 0;
     out->table_bytes = dev->table_bytes;
     out->shading_bytes = dev->shading_bytes;
+    out->slot_bytes = 0;
+    for (const Slot& s : dev->slots) out->slot_bytes += (uint64_t)s.shard_cap * NSH * (2 * 56 + 48 + 20) + (uint64_t)s.cap * 16;
     return IGX_OK;
 }
 

@@ -571,8 +571,8 @@ Bvh4Result collapse_bvh4(const BvhBuildResult& in) {
         res.depth = std::max(res.depth, it.depth);
         Child2 kids[4];
         int nk = 0;
-        kids[nk++] = child_of(in.nodes[it.src], 0);
-        kids[nk++] = child_of(in.nodes[it.src], 1);
+        for (int k = 0; k < 2; ++k) // an absent BVH2 child (kEmptyRef, bvh2_from_reference) stays absent
+            if (in.nodes[it.src].ref[k] != kEmptyRef) kids[nk++] = child_of(in.nodes[it.src], k);
         while (nk < 4) {
             int best = -1;
             float best_area = -1;
@@ -674,11 +674,26 @@ bool bvh2_from_reference(const uint8_t* blob, size_t bytes, uint32_t num_faces, 
     stack.push_back({0, 0, 1});
     std::vector<char> seen(nn, 0);
     int depth = 1;
+    // child boxes get the same pad as igx's own builder (pad_box, set_child),
+    // so closest hits through an imported tree do not depend on its grouping
+    // either; Node2 keeps a child box as lo.x, hi.x, lo.y, hi.y, lo.z, hi.z
+    auto put_box = [&](int o, int k, const float* box) {
+        Box b;
+        for (int a = 0; a < 3; ++a) {
+            b.lo[a] = box[2 * a];
+            b.hi[a] = box[2 * a + 1];
+        }
+        const Box p = pad_box(b);
+        float* dst = out.nodes[o].b + 6 * k;
+        for (int a = 0; a < 3; ++a) {
+            dst[2 * a] = p.lo[a];
+            dst[2 * a + 1] = p.hi[a];
+        }
+    };
     // child k of output node `o`: set box + ref, creating split-leaf nodes as needed
     std::function<void(int, int, const float*, uint64_t, uint32_t, int)> put_leaf =
         [&](int o, int k, const float* box, uint64_t first, uint32_t count, int d) {
-            float* dst = out.nodes[o].b + 6 * k;
-            std::memcpy(dst, box, 6 * sizeof(float));
+            put_box(o, k, box);
             if (count <= (uint32_t)max_leaf) {
                 out.nodes[o].ref[k] = encode_leaf((int32_t)first, (int32_t)count);
                 return;
@@ -699,21 +714,29 @@ bool bvh2_from_reference(const uint8_t* blob, size_t bytes, uint32_t num_faces, 
         if (seen[it.src]++) { err = "Node2 graph is not a tree"; return false; }
         depth = std::max(depth, it.depth);
         RefNode2 n = rn[it.src];
-        // a cut-out child (0) repeats its sibling: harmless for closest and any hit
+        // a cut-out child (0) repeats its sibling: harmless for closest and any
+        // hit -- except under the root wrapping a single leaf
+        // (BvhNAdapter.h:94-98), where the copy would be expanded a second time
+        // when the leaf splits into a subtree: that child becomes absent instead
         if (n.child[0] == 0 && n.child[1] == 0) { err = "Node2 without children"; return false; }
+        int absent = -1;
         for (int k = 0; k < 2; ++k)
             if (n.child[k] == 0) {
                 n.child[k] = n.child[1 - k];
                 std::memcpy(n.b + 6 * k, n.b + 6 * (1 - k), 6 * sizeof(float));
-                if (it.src == 0 && n.child[k] < 0) root_leaf = true; // root wrapping a single leaf (BvhNAdapter.h:94-98)
+                if (it.src == 0 && n.child[k] < 0) {
+                    root_leaf = true;
+                    absent = k;
+                }
             }
         out.nodes[it.out].pad[0] = out.nodes[it.out].pad[1] = 0;
         for (int k = 0; k < 2; ++k) {
             const int32_t c = n.child[k];
+            if (k == absent) continue;
             if (c > 0) {
                 const int idx = (int)out.nodes.size();
                 out.nodes.emplace_back();
-                std::memcpy(out.nodes[it.out].b + 6 * k, n.b + 6 * k, 6 * sizeof(float));
+                put_box(it.out, k, n.b + 6 * k);
                 out.nodes[it.out].ref[k] = idx;
                 stack.push_back({(int64_t)c - 1, idx, it.depth + 1});
             } else {
@@ -722,6 +745,12 @@ bool bvh2_from_reference(const uint8_t* blob, size_t bytes, uint32_t num_faces, 
                 if (first >= nt || !leaf_count(first, count)) { err = "Tri1 leaf without its end marker"; return false; }
                 put_leaf(it.out, k, n.b + 6 * k, first, count, it.depth);
             }
+        }
+        if (absent >= 0) {
+            // +inf bounds: no slab test accepts the child (as absent 4-wide children)
+            float* dst = out.nodes[it.out].b + 6 * absent;
+            for (int a = 0; a < 6; ++a) dst[a] = INFINITY;
+            out.nodes[it.out].ref[absent] = kEmptyRef;
         }
     }
     out.depth = depth;

@@ -189,6 +189,9 @@ static void build_from_tables(SceneStore& S, const igx_database_view& db, const 
         Reader bv{db.trimesh_primbvh.data, db.trimesh_primbvh.bytes, "trimesh_primbvh"};
         for (size_t s = 0; s < S.shapes.size(); ++s) {
             if (S.shapes[s].type != IGX_SHAPE_TRIMESH || shape_blas[s] == ~0ull) continue;
+            // offsets count floats: refuse one beyond the table before scaling it
+            // (a huge user word would wrap and select the wrong bytes)
+            if (shape_blas[s] > db.trimesh_primbvh.bytes / 4) fail("trimesh_primbvh: BLAS offset beyond the table");
             const uint64_t o = shape_blas[s] * 4;
             const uint64_t nn = bv.at<uint32_t>(o), nt = bv.at<uint32_t>(o + 4);
             const uint64_t len = 16 + 64 * nn + 48 * nt;

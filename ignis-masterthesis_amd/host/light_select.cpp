@@ -144,6 +144,24 @@ LightSelectTables build_light_select(int selector, int light_count, const std::v
             leaves.push_back(e);
             store(nodes, leaves.size() - 1, e.pos);
         }
+        // a leaf's code keeps one bit per level (bit d: right at depth d), so
+        // the walk (light/light_hierarchy.art) is defined for at most 32
+        // levels; the insertion-built tree can get deeper with clustered or
+        // geometrically spaced lights (the reference leaves this as a TODO and
+        // shifts past the word).  Such a scene gets the flux CDF instead:
+        // also unbiased, and the same lights weighted by the same flux.
+        std::vector<std::pair<size_t, uint32_t>> todo{{0, 0}};
+        uint32_t deepest = 0;
+        while (!todo.empty()) {
+            const auto [id, d] = todo.back();
+            todo.pop_back();
+            deepest = std::max(deepest, d);
+            if (nodes[id].axis >= 0) {
+                todo.push_back({(size_t)nodes[id].index, d + 1});
+                todo.push_back({(size_t)nodes[id].index + 1, d + 1});
+            }
+        }
+        if (deepest > 32) return build_light_select(IGX_SELECT_SIMPLE, light_count, finite);
         std::vector<Entry> entries(nodes.size());
         std::vector<uint32_t> codes(n, 0);
         populate(0, 0, 0, nodes, leaves, entries, codes);

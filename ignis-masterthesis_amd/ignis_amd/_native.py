@@ -126,7 +126,8 @@ class Stats(C.Structure):
                 ("lds_scene_bytes", C.c_int32), ("shadow_blocks_per_cu", C.c_int32),
                 ("table_bytes", C.c_uint64), ("shading_bytes", C.c_uint64),
                 ("extend_cycles_load", C.c_uint64), ("extend_cycles_trace", C.c_uint64),
-                ("extend_cycles_shade", C.c_uint64), ("extend_cycles_store", C.c_uint64)]
+                ("extend_cycles_shade", C.c_uint64), ("extend_cycles_store", C.c_uint64),
+                ("slot_bytes", C.c_uint64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

@@ -1,0 +1,42 @@
+"""bench.py's multi-GPU launch contract, on CPU (no GPU call): `bench.py --gpus N`
+started without a launcher runs N ranks itself as a child torch.distributed.run,
+and a launcher whose WORLD_SIZE disagrees with --gpus is refused.  The
+IGX_BENCH_LAUNCH_PROBE hook makes every rank print its layout and exit before
+anything touches the GPU."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["IGX_BENCH_LAUNCH_PROBE"] = "1"
+    env.update(kw)
+    return env
+
+
+def test_gpus_n_launches_n_ranks():
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--steps", "1"], env=_env(), capture_output=True, text=True,
+                       timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert sorted(x["rank"] for x in lines) == [0, 1]
+    assert all(x["world"] == 2 and x["gpus"] == 2 for x in lines)
+
+
+def test_single_gpu_needs_no_launcher():
+    r = subprocess.run([sys.executable, BENCH], env=_env(), capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert lines == [{"rank": 0, "world": 1, "gpus": 1}]
+
+
+def test_world_size_mismatch_is_refused():
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "4"], env=_env(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    assert "WORLD_SIZE=2 but --gpus 4" in r.stderr

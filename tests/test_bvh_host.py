@@ -24,3 +24,15 @@ def test_bvh_builders_match_brute_force(tmp_path):
     sl = {l[1]: l for l in lines if l[0] == "slivers"}
     assert int(sl["sbvh"][3].split("/")[0]) > int(sl["bvh2"][3].split("/")[0])
     assert float(sl["sbvh"][7]) < float(sl["bvh2"][7])
+
+
+def test_light_hierarchy_depth_guard(tmp_path):
+    """A light tree deeper than the 32-bit left/right codes falls back to the
+    flux CDF selector (tests/native/light_select_check.cpp, g++ against
+    host/light_select.cpp)."""
+    exe = str(tmp_path / "light_select_check")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", HOST, "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "native", "light_select_check.cpp"), os.path.join(HOST, "light_select.cpp"),
+                    "-o", exe], check=True)
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0 and out.stdout.strip().endswith("ok"), out.stdout + out.stderr

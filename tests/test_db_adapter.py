@@ -146,6 +146,14 @@ def test_malformed_tables_are_refused():
         r.primbvh.data = r.primbvh.data[:40]
     _corrupt(short_blas, "beyond the end")
 
+    def huge_blas_offset(r):
+        # user2 (high word of the BLAS offset in floats) with bit 30 set: offset * 4
+        # wraps to the low word's bytes unless the offset is checked first
+        recs = np.frombuffer(bytes(r.leaves), np.uint32).copy().reshape(-1, 24)
+        recs[:, 23] |= 0x40000000
+        r.leaves[:] = recs.tobytes()
+    _corrupt(huge_blas_offset, "BLAS offset beyond the table")
+
 
 def test_corrupted_transform_is_seen():
     """A changed toGlobal column in the entity table shows up in the desc (the

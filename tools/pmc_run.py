@@ -2,7 +2,8 @@
 (default diamond 1000x1000, spi 8), batched by igx_render_iterations like the
 bench, without timing or instrumentation, so every k_extend dispatch is the
 same kernel with the same path count the bench times.
-Usage: pmc_run.py [iterations] [scene file under scenes/] [device options as JSON]"""
+Usage: pmc_run.py [iterations] [scene file under scenes/] [device options as JSON] [square film size]
+(the size overrides the scene's film as bench.py's suite does for the config-5 stand-in)"""
 import os
 import sys
 
@@ -13,6 +14,8 @@ import ignis_amd  # noqa: E402
 iters = int(sys.argv[1]) if len(sys.argv) > 1 else 2
 scene = ignis_amd.Scene.from_file(os.path.join(ROOT, "scenes", sys.argv[2] if len(sys.argv) > 2 else "diamond_scene.json"))
 W, H = scene.film_size
+if len(sys.argv) > 4 and int(sys.argv[4]) > 0:
+    W = H = int(sys.argv[4])
 dev = ignis_amd.Device(0)
 import json  # noqa: E402
 for k, v in (json.loads(sys.argv[3]) if len(sys.argv) > 3 else {}).items():

@@ -52,7 +52,7 @@ def pmc_file(kernel, scene):
     return f"pmc_{k}.json" if scene == "diamond_scene" else f"pmc_{k}_{scene}.json"
 
 
-def pmc(fetch_dir, write_dir, kernel="k_extend", scene="diamond_scene"):
+def pmc(fetch_dir, write_dir, kernel="k_extend", scene="diamond_scene", workload=None):
     def per_dispatch(d, counter):
         f = find(d, "*counter_collection.csv")
         if not f:
@@ -72,7 +72,7 @@ def pmc(fetch_dir, write_dir, kernel="k_extend", scene="diamond_scene"):
     write = sum(ws.values()) / len(ws)
     res = {
         "kernel": kernel,
-        "workload": f"tools/pmc_run.py: {scene}.json 1000x1000, spi 8 (the bench's iterations)",
+        "workload": workload or f"tools/pmc_run.py: {scene}.json 1000x1000, spi 8 (the bench's iterations)",
         "dispatches_fetch_pass": len(fs), "dispatches_write_pass": len(ws),
         "fetch_size_kib_per_launch": round(fetch, 1),
         "write_size_kib_per_launch": round(write, 1),
@@ -125,7 +125,34 @@ def calibration(fetch_dir, write_dir, trace_dir, log, tag):
     print(json.dumps(res, indent=1))
 
 
+def suite(tag):
+    """profiles for every suite line (tools/gpu_profile_suite.sh): rocprof kernel
+    stats as profiles/<tag>_<key>_kernel_stats.{csv,md} and the dominant
+    kernel's PMC traffic as profiles/pmc_<kernel>_<key>.json (bench.py load_pmc)."""
+    out = os.path.join(ROOT, "gpurun_out")
+    for d in sorted(glob.glob(os.path.join(out, "suite_*"))):
+        key = os.path.basename(d)[len("suite_"):]
+        f = find(os.path.join(d, "trace"), "*kernel_stats.csv")
+        if not f:
+            print("no trace for", key)
+            continue
+        kernel_stats(os.path.join(d, "trace"), f"{tag}_{key}")
+        names = [short(r["Name"]) for r in csv.DictReader(open(f))]
+        # split-schedule scenes: the persistent-lane closest-hit kernel dominates
+        kernel = "k_trace" if any("k_trace" in n for n in names) else "k_extend"
+        args = ""
+        for line in open(os.path.join(out, "suite.log")) if os.path.exists(os.path.join(out, "suite.log")) else []:
+            if line.startswith(f"== {key}:"):
+                args = line.split(":", 1)[1].strip()
+        pmc(os.path.join(d, "fetch"), os.path.join(d, "write"), kernel=kernel, scene=key,
+            workload=f"tools/{args or 'pmc_run.py'} (the suite line's scene, film and iterations, spi 8); "
+                     f"rocprof kernel stats: profiles/{tag}_{key}_kernel_stats.md")
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[1] == "suite":
+        suite(sys.argv[2])
+        sys.exit(0)
     tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
     out = os.path.join(ROOT, "gpurun_out")
     kernel_stats(os.path.join(out, "prof"), tag)
