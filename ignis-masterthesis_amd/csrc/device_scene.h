@@ -46,6 +46,13 @@ __host__ __device__ constexpr int lds_node_pad() { return IGX_LDS_NODE_PAD ? 1 :
 // call) -- set only on k_shadow_refill launches for scenes on the split
 // schedule (igx_device.hip, use_shadow_ifif).
 __host__ __device__ constexpr bool variant_ifif(int v) { return (v & 16) != 0; }
+// Bit 5: the node tables stay in global memory, but the hottest nodes (the
+// first SceneView::tree_n of the node array, igx_upload_scene's hot order)
+// are staged in LDS (the treelet); node steps below that index read LDS.
+// Set by every kernel instantiation that does not stage the whole table.
+constexpr int VARIANT_TREE = 32;
+__host__ __device__ constexpr bool variant_tree(int v) { return (v & VARIANT_TREE) != 0; }
+__host__ __device__ constexpr int kernel_variant(int v, bool lds) { return lds ? lds_variant(v, true) : (v | VARIANT_TREE); }
 
 // Instance record (one per TLAS leaf slot): 64 B
 //   row0..row2: to_local 3x4 (row-major, xyz = linear row, w = translation)

@@ -239,10 +239,6 @@ __device__ __forceinline__ void wave_append_paths(bool alive, bool cls_b, bool s
     sdst = s0 + __popcll(ms & below);
 }
 
-// stream class of a surviving path (FrameArgs::classify)
-__device__ __forceinline__ bool path_class_b(int classify, float eta, float inv_pdf) {
-    return classify == 1 ? eta != 1.0f : classify == 2 ? inv_pdf == 0.0f : false;
-}
 
 
 // ---------------------------------------------------------------------------
@@ -335,6 +331,34 @@ struct ShadowRec {
     f3 o, d, color;
     float tmax;
 };
+
+// stream class of a surviving path (FrameArgs::classify): 1 B = inside a
+// dielectric (eta != 1); 2 B = after a specular event; 3 B = inside a
+// dielectric or its next ray crosses the world box of an enclosing entity
+// (the paths whose traversal enters a large BLAS and that will likely shade
+// a dielectric), A = the rest (wall-to-wall paths: short walks, diffuse)
+__device__ __forceinline__ bool crosses_enclosing_box(const SceneView& sv, f3 o, f3 d) {
+    const f3 id = mk(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
+    bool hit = false;
+    for (int k = 0; k < sv.num_enc && !hit; ++k) {
+        const float4 lo = sv.enc_box[2 * k], hi = sv.enc_box[2 * k + 1];
+        const float ax = (lo.x - o.x) * id.x, bx = (hi.x - o.x) * id.x;
+        const float ay = (lo.y - o.y) * id.y, by = (hi.y - o.y) * id.y;
+        const float az = (lo.z - o.z) * id.z, bz = (hi.z - o.z) * id.z;
+        const float en = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+        const float ex = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+        hit = en <= ex && ex >= 0.0f;
+    }
+    return hit;
+}
+__device__ __forceinline__ bool path_class_b(int classify, const SceneView& sv, const PathState& ps) {
+    switch (classify) {
+    case 1: return ps.eta != 1.0f;
+    case 2: return ps.inv_pdf == 0.0f;
+    case 3: return ps.eta != 1.0f || crosses_enclosing_box(sv, ps.o, ps.d);
+    default: return false;
+    }
+}
 
 __device__ __forceinline__ PathState load_path(const PathBuf& in, int i) {
     float4 p0 = in.p0[i], p1 = in.p1[i], p2 = in.p2[i];
@@ -624,7 +648,7 @@ __device__ __forceinline__ int take_group(int* work, int& s, uint64_t& done, int
 template <int V0, bool STATS, bool LDS>
 __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(V0) ? EXTEND_WAVES_FULL : EXTEND_WAVES)) k_extend(FrameArgs fa, SceneView gsv, PathBuf in, PathBuf out, ShadowBuf sh,
                                                   float4* L, KernelCounters kc, int tail_threshold) {
-    constexpr int V = lds_variant(V0, LDS); // LDS-staged nodes: padded stride (device_scene.h)
+    constexpr int V = kernel_variant(V0, LDS); // LDS-staged nodes: padded stride; global tables: treelet (device_scene.h)
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
@@ -633,7 +657,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
     // shard order, built here instead of being read from the input stream.
     const bool gen = fa.gen_n > 0;
     if (!gen && row_total(kc.cnt_in) <= tail_threshold) return; // k_finish takes the remaining paths (block-uniform)
-    const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
+    const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : stage_treelet<BLOCK>(gsv, lds_scene);
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
     const WaveWork w = wave_work();
     // Groups of 64 positions of shard s: statically every K-th group from
@@ -740,7 +764,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
 #endif
         }
         int dst, sdst;
-        wave_append_paths(alive, path_class_b(fa.classify, ps.eta, ps.inv_pdf), has_shadow, c_out, c_sh, out.shard_cap, dst, sdst);
+        wave_append_paths(alive, path_class_b(fa.classify, sv, ps), has_shadow, c_out, c_sh, out.shard_cap, dst, sdst);
         if (alive) store_path(out, s * out.shard_cap + dst, ps);
         if (has_shadow) {
             const int e = s * sh.shard_cap + sdst;
@@ -767,12 +791,12 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
 template <int V0, bool STATS, int WAVES, bool LDS>
 __global__ void __launch_bounds__(BLOCK, WAVES) k_trace(FrameArgs fa, SceneView gsv, PathBuf in, HitBuf hits,
                                                       const int* cnt, int tail_threshold, unsigned long long* stats) {
-    constexpr int V = lds_variant(V0, LDS); // LDS-staged nodes: padded stride (device_scene.h)
+    constexpr int V = kernel_variant(V0, LDS); // LDS-staged nodes: padded stride; global tables: treelet (device_scene.h)
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
     if (row_total(cnt) <= tail_threshold) return; // k_finish takes the remaining paths
-    const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
+    const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : stage_treelet<BLOCK>(gsv, lds_scene);
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
     const WaveWork w = wave_work();
     const ShardCount sc = shard_count(cnt, w.s);
@@ -829,7 +853,7 @@ __global__ void __launch_bounds__(BLOCK) k_shade(FrameArgs fa, SceneView sv, Pat
             }
         }
         int dst, sdst;
-        wave_append_paths(alive, path_class_b(fa.classify, ps.eta, ps.inv_pdf), has_shadow, c_out, c_sh, out.shard_cap, dst, sdst);
+        wave_append_paths(alive, path_class_b(fa.classify, sv, ps), has_shadow, c_out, c_sh, out.shard_cap, dst, sdst);
         if (alive) store_path(out, w.s * out.shard_cap + dst, ps);
         if (has_shadow) {
             const int e = w.s * sh.shard_cap + sdst;
@@ -850,13 +874,13 @@ template <int V0, bool STATS, bool LDS>
 __global__ void __launch_bounds__(BLOCK) k_finish(FrameArgs fa, SceneView gsv, PathBuf in, float4* L, const int* cnt,
                                                   int tail_threshold, unsigned long long* stats,
                                                   unsigned long long* tail_counts) {
-    constexpr int V = lds_variant(V0, LDS); // LDS-staged nodes: padded stride (device_scene.h)
+    constexpr int V = kernel_variant(V0, LDS); // LDS-staged nodes: padded stride; global tables: treelet (device_scene.h)
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
     const int n = row_total(cnt);
     if (n > tail_threshold || n == 0) return; // the wavefront kernels own this bounce
-    const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
+    const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : stage_treelet<BLOCK>(gsv, lds_scene);
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
     TraceStats sst{0, 0, 0, 0, 0, 0, 0};
     unsigned long long bounces = 0, shadows = 0;
@@ -906,12 +930,12 @@ __global__ void __launch_bounds__(BLOCK) k_finish(FrameArgs fa, SceneView gsv, P
 template <int V0, bool STATS, bool LDS>
 __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, float4* L, const int* cnt,
                                                   unsigned long long* stats, int* work) {
-    constexpr int V = lds_variant(V0, LDS); // LDS-staged nodes: padded stride (device_scene.h)
+    constexpr int V = kernel_variant(V0, LDS); // LDS-staged nodes: padded stride; global tables: treelet (device_scene.h)
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
     if (row_total(cnt) == 0) return;
-    const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
+    const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : stage_treelet<BLOCK>(gsv, lds_scene);
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
     const WaveWork w = wave_work();
     // groups of 64 shadow rays: grid-stride over the wave's own shard, or
@@ -1057,12 +1081,12 @@ template <int V0, bool STATS, bool LDS>
 __global__ void __launch_bounds__(BLOCK, LDS ? REFILL_WAVES_LDS : REFILL_WAVES) k_trace_refill(FrameArgs fa, SceneView gsv, PathBuf in, HitBuf hits,
                                                                      const int* cnt, int tail_threshold,
                                                                      unsigned long long* stats, int refill_min, int* work) {
-    constexpr int V = lds_variant(V0, LDS); // LDS-staged nodes: padded stride (device_scene.h)
+    constexpr int V = kernel_variant(V0, LDS); // LDS-staged nodes: padded stride; global tables: treelet (device_scene.h)
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
     if (row_total(cnt) <= tail_threshold) return; // k_finish takes the remaining paths
-    const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
+    const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : stage_treelet<BLOCK>(gsv, lds_scene);
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
     GroupSeq<true> seq;
     seq.init(cnt, work, in.shard_cap, wave_work());
@@ -1094,12 +1118,12 @@ __global__ void __launch_bounds__(BLOCK, LDS ? REFILL_WAVES_LDS : REFILL_WAVES) 
 template <int V0, bool STATS, bool LDS>
 __global__ void __launch_bounds__(BLOCK, LDS ? REFILL_WAVES_LDS : (variant_ifif(V0) ? SHADOW_IFIF_WAVES : REFILL_WAVES)) k_shadow_refill(SceneView gsv, ShadowBuf sh, float4* L, const int* cnt,
                                                                       unsigned long long* stats, int refill_min, int* work) {
-    constexpr int V = lds_variant(V0, LDS); // LDS-staged nodes: padded stride (device_scene.h)
+    constexpr int V = kernel_variant(V0, LDS); // LDS-staged nodes: padded stride; global tables: treelet (device_scene.h)
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
     if (row_total(cnt) == 0) return;
-    const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : gsv;
+    const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : stage_treelet<BLOCK>(gsv, lds_scene);
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
     GroupSeq<false> seq;
     seq.init(cnt, work, sh.shard_cap, wave_work());
@@ -1266,6 +1290,9 @@ constexpr int CTR_ROWS = WORK_ROW0 + 4 * MAX_BOUNCES;
 // precomputes world-space face normals (16 B each: at most 64 MB)
 [[maybe_unused]] constexpr size_t FACE_NORMAL_TABLE_MAX = 4u << 20;
 [[maybe_unused]] constexpr size_t CTR_INTS = (size_t)CTR_ROWS * CROW;
+// nodes moved to the front of the node array in hot order at upload (the
+// largest treelet a kernel may stage: 160 KB of LDS / 128-B nodes)
+[[maybe_unused]] constexpr size_t TREELET_FRONT = 1280;
 
 // records in counter row `row` of the slot's host mirror (row 0: generated paths)
 inline long long row_total(const Slot& s, int row) {
@@ -1295,6 +1322,14 @@ struct igx_device {
     // handle may take (0 = auto: a quarter of the device memory).  A rank of
     // a multi-GPU render holds two handles (bench.py), each sized to its share
     int64_t slot_budget_mb = 0;
+    // LDS treelet (stage_treelet) on global-table scenes: nodes staged per
+    // kernel (the largest prefix of the hot order that keeps the kernel's
+    // register-bound occupancy), recomputed when the scene or option changes.
+    // Option "treelet": -1 auto, 0 off, n > 0 at most n nodes
+    int64_t treelet_opt = -1;
+    int treelet_kernels = 7; // option "treelet_kernels": bit 1 k_extend, 2 k_trace_refill, 4 k_shadow / k_shadow_refill
+    bool tree_dirty = true;
+    int tree_ext = 0, tree_trace = 0, tree_shadow = 0, tree_fin = 0;
     int64_t tail_opt = -1;   // paths at or below which k_finish takes over (-1 = auto)
     int64_t tail_last_opt = -1; // the same for the last chunk of a render call, whose tail overlaps nothing (-1 = tail_opt)
     bool fuse_generate = true; // bounce 0 of the fused k_extend builds its camera paths (no k_generate pass)
@@ -1311,7 +1346,10 @@ struct igx_device {
     // paths inside a dielectric go to the back of their shard, so the next
     // bounce's waves are all-inside or all-outside (diamond frame 152-155 ->
     // 143-145 ms, S-deep 49.1 -> 47.5 ms per 8-iteration frame; bit-identical)
-    int classify_opt = 1;
+    // 3: also paths whose next ray crosses an enclosing entity's world box
+    // (diamond frame 132.5 -> 119.3 ms, k_extend 1770 -> 1591 us per launch,
+    // bit-identical)
+    int classify_opt = 3;
     // option "dynamic" (DYN_* bits): DYN_EXTEND = k_extend waves take their
     // groups of 64 paths from per-shard counters (take_group) instead of a
     // fixed grid stride: diamond frame 142.4 -> 134.3 ms, materials 66.5 ->
@@ -1505,6 +1543,8 @@ int grid_for(igx_device* dev, long long items, int blocks_per_cu) {
 //    faster (no hit records): S-deep (18 MB of tables) 49.4 -> 46.9 ms per
 //    8-iteration frame fused, soup-1M (104 MB) 382 split vs 451 fused.
 constexpr size_t SPLIT_TABLE_BYTES = 64u << 20;
+// dynamic LDS of a global-table kernel that stages `nodes` treelet nodes
+inline size_t tree_bytes(const igx_device* dev, int nodes) { return (size_t)nodes * node_f4(dev->bvh_width) * 16; }
 inline int refill_min(const igx_device* dev) { return dev->refill_opt >= 0 ? dev->refill_opt : 16; }
 // auto: global-table scenes only; an explicit "refill" applies to LDS-staged scenes too
 inline bool use_refill(const igx_device* dev) {
@@ -1556,7 +1596,9 @@ void launch_extend(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, cons
 #undef L_EXTL
         return;
     }
-#define L_EXT(S) hipLaunchKernelGGL((k_extend<S, STATS, false>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, out, s.sh, s.L, kc, tail)
+    SceneView tsv = dev->sv;
+    tsv.tree_n = dev->tree_ext;
+#define L_EXT(S) hipLaunchKernelGGL((k_extend<S, STATS, false>), dim3(grid), dim3(BLOCK), tree_bytes(dev, tsv.tree_n), dev->stream, fa, tsv, in, out, s.sh, s.L, kc, tail)
     IGX_DISPATCH_VARIANT8(dev->variant, L_EXT);
 #undef L_EXT
 }
@@ -1572,14 +1614,16 @@ void launch_trace_w(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, con
 template <bool STATS>
 void launch_trace(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const PathBuf& in, const int* cnt, int tail,
                   int* work) {
+    SceneView tsv = dev->sv;
+    tsv.tree_n = dev->tree_trace;
     if (use_refill(dev)) {
 #define L_TRR(S)                                                                                                        \
     if (dev->lds_scene_bytes)                                                                                            \
         hipLaunchKernelGGL((k_trace_refill<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->stream, fa, \
                            dev->sv, in, s.hb, cnt, tail, dev->dstats, refill_min(dev), work);                            \
     else                                                                                                                 \
-        hipLaunchKernelGGL((k_trace_refill<S, STATS, false>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, s.hb, \
-                           cnt, tail, dev->dstats, refill_min(dev), work)
+        hipLaunchKernelGGL((k_trace_refill<S, STATS, false>), dim3(grid), dim3(BLOCK), tree_bytes(dev, tsv.tree_n), dev->stream, \
+                           fa, tsv, in, s.hb, cnt, tail, dev->dstats, refill_min(dev), work)
         IGX_DISPATCH_VARIANT(dev->variant, L_TRR);
 #undef L_TRR
         return;
@@ -1595,17 +1639,19 @@ void launch_trace(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const
 }
 template <bool STATS>
 void launch_shadow(igx_device* dev, Slot& s, int grid, const int* cnt, int* work) {
+    SceneView tsv = dev->sv;
+    tsv.tree_n = dev->tree_shadow;
     if (use_refill(dev)) {
 #define L_SHR(S)                                                                                                        \
     if (dev->lds_scene_bytes)                                                                                            \
         hipLaunchKernelGGL((k_shadow_refill<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->stream,   \
                            dev->sv, s.sh, s.L, cnt, dev->dstats, refill_min(dev), work);                                 \
     else                                                                                                                 \
-        hipLaunchKernelGGL((k_shadow_refill<S, STATS, false>), dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, s.sh, s.L, \
-                           cnt, dev->dstats, refill_min(dev), work)
+        hipLaunchKernelGGL((k_shadow_refill<S, STATS, false>), dim3(grid), dim3(BLOCK), tree_bytes(dev, tsv.tree_n), dev->stream, \
+                           tsv, s.sh, s.L, cnt, dev->dstats, refill_min(dev), work)
 #define L_SHRI(S)                                                                                                       \
-    hipLaunchKernelGGL((k_shadow_refill<S | 16, STATS, false>), dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, s.sh, s.L, \
-                       cnt, dev->dstats, refill_min(dev), work)
+    hipLaunchKernelGGL((k_shadow_refill<S | 16, STATS, false>), dim3(grid), dim3(BLOCK), tree_bytes(dev, tsv.tree_n), dev->stream, \
+                       tsv, s.sh, s.L, cnt, dev->dstats, refill_min(dev), work)
         if (!dev->lds_scene_bytes && use_shadow_ifif(dev)) IGX_DISPATCH_VARIANT(dev->variant, L_SHRI);
         else IGX_DISPATCH_VARIANT(dev->variant, L_SHR);
 #undef L_SHRI
@@ -1618,7 +1664,7 @@ void launch_shadow(igx_device* dev, Slot& s, int grid, const int* cnt, int* work
 #undef L_SHL
         return;
     }
-#define L_SH(S) hipLaunchKernelGGL((k_shadow<S, STATS, false>), dim3(grid), dim3(BLOCK), 0, dev->stream, dev->sv, s.sh, s.L, cnt, dev->dstats, work)
+#define L_SH(S) hipLaunchKernelGGL((k_shadow<S, STATS, false>), dim3(grid), dim3(BLOCK), tree_bytes(dev, tsv.tree_n), dev->stream, tsv, s.sh, s.L, cnt, dev->dstats, work)
     IGX_DISPATCH_VARIANT(dev->variant, L_SH);
 #undef L_SH
 }
@@ -1626,13 +1672,14 @@ template <bool STATS>
 void launch_finish(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const PathBuf& in, const int* cnt, int tail) {
     SceneView tsv = dev->sv;
     tsv.spill = dev->spill_tail; // k_finish runs concurrently with the main stream's kernels
+    tsv.tree_n = dev->tree_fin;
     if (dev->lds_scene_bytes) {
 #define L_FINL(S) hipLaunchKernelGGL((k_finish<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->tail_stream, fa, tsv, in, s.L, cnt, tail, dev->dstats, dev->tail_counts)
         IGX_DISPATCH_VARIANT8(dev->variant, L_FINL);
 #undef L_FINL
         return;
     }
-#define L_FIN(S) hipLaunchKernelGGL((k_finish<S, STATS, false>), dim3(grid), dim3(BLOCK), 0, dev->tail_stream, fa, tsv, in, s.L, cnt, tail, dev->dstats, dev->tail_counts)
+#define L_FIN(S) hipLaunchKernelGGL((k_finish<S, STATS, false>), dim3(grid), dim3(BLOCK), tree_bytes(dev, tsv.tree_n), dev->tail_stream, fa, tsv, in, s.L, cnt, tail, dev->dstats, dev->tail_counts)
     IGX_DISPATCH_VARIANT8(dev->variant, L_FIN);
 #undef L_FIN
 }
@@ -1644,7 +1691,7 @@ int resident_blocks(K kernel, size_t dyn_lds = 0) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, BLOCK, dyn_lds) != hipSuccess || nb < 1) nb = 1;
     return nb;
 }
-#define IGX_RES1(K, V, ...) return lds ? resident_blocks(K<V, __VA_ARGS__, true>, lds) : resident_blocks(K<V, __VA_ARGS__, false>)
+#define IGX_RES1(K, V, ...) return lds ? resident_blocks(K<V, __VA_ARGS__, true>, lds) : resident_blocks(K<V, __VA_ARGS__, false>, tree)
 #define IGX_RESIDENT(K, ...)                                         \
     do {                                                             \
         switch (v & 3) {                                             \
@@ -1669,16 +1716,16 @@ int resident_blocks(K kernel, size_t dyn_lds = 0) {
     } while (0)
 #define IGX_RESIDENT_G(K) IGX_RESIDENT(K, STATS)
 template <bool STATS>
-int extend_blocks_per_cu(int v, size_t lds) { IGX_RESIDENT8(k_extend, STATS); }
+int extend_blocks_per_cu(int v, size_t lds, size_t tree) { IGX_RESIDENT8(k_extend, STATS); }
 template <bool STATS>
-int shadow_blocks_per_cu(int v, size_t lds, bool refill) {
+int shadow_blocks_per_cu(int v, size_t lds, bool refill, size_t tree) {
     if (refill) IGX_RESIDENT_G(k_shadow_refill);
     IGX_RESIDENT(k_shadow, STATS);
 }
 template <bool STATS>
-int finish_blocks_per_cu(int v, size_t lds) { IGX_RESIDENT8(k_finish, STATS); }
+int finish_blocks_per_cu(int v, size_t lds, size_t tree) { IGX_RESIDENT8(k_finish, STATS); }
 template <bool STATS>
-int trace_blocks_per_cu(int v, int waves, size_t lds, bool refill) {
+int trace_blocks_per_cu(int v, int waves, size_t lds, bool refill, size_t tree) {
     if (refill) IGX_RESIDENT_G(k_trace_refill);
     if (lds) IGX_RESIDENT(k_trace, STATS, 1);
     if (waves == 5) IGX_RESIDENT(k_trace, STATS, 5);
@@ -1704,15 +1751,15 @@ int shade_blocks_per_cu(bool full) { return full ? resident_blocks(k_shade<true>
 #define IGX_EXTEND_HELPERS(X, S)                                                                                     \
     X void launch_extend<S>(igx_device*, Slot&, int, const FrameArgs&, const PathBuf&, const PathBuf&,               \
                             const KernelCounters&, int);                                                             \
-    X int extend_blocks_per_cu<S>(int, size_t);
+    X int extend_blocks_per_cu<S>(int, size_t, size_t);
 #define IGX_FINISH_HELPERS(X, S)                                                                                     \
     X void launch_finish<S>(igx_device*, Slot&, int, const FrameArgs&, const PathBuf&, const int*, int);             \
-    X int finish_blocks_per_cu<S>(int, size_t);
+    X int finish_blocks_per_cu<S>(int, size_t, size_t);
 #define IGX_TRACE_HELPERS(X, S)                                                                                      \
     X void launch_trace<S>(igx_device*, Slot&, int, const FrameArgs&, const PathBuf&, const int*, int, int*);              \
     X void launch_shadow<S>(igx_device*, Slot&, int, const int*, int*);                                                    \
-    X int trace_blocks_per_cu<S>(int, int, size_t, bool);                                                            \
-    X int shadow_blocks_per_cu<S>(int, size_t, bool);
+    X int trace_blocks_per_cu<S>(int, int, size_t, bool, size_t);                                                    \
+    X int shadow_blocks_per_cu<S>(int, size_t, bool, size_t);
 #if IGX_PART == 1
 IGX_EXTEND_HELPERS(template, true)
 IGX_EXTEND_HELPERS(template, false)
@@ -1785,6 +1832,36 @@ igx_status drain(igx_device* dev) {
     dev->stats.tail_bounce_rays += tc[0];
     dev->stats.tail_shadow_rays += tc[1];
     return IGX_OK;
+}
+
+// Treelet size of every global-table kernel: the largest prefix of the hot
+// node order (order_hot_nodes) whose LDS copy keeps the kernel's resident
+// blocks per CU (set by its register budget) -- the treelet takes LDS that
+// would otherwise stay unused.  Binary search over hipOccupancy answers.
+void configure_treelet(igx_device* dev) {
+    dev->tree_ext = dev->tree_trace = dev->tree_shadow = dev->tree_fin = 0;
+    dev->tree_dirty = false;
+    if (!dev->has_scene || dev->lds_scene_bytes || dev->treelet_opt == 0) return;
+    int cap = (int)std::min<size_t>(TREELET_FRONT, (size_t)dev->sv.num_nodes);
+    if (dev->treelet_opt > 0) cap = (int)std::min<int64_t>(cap, dev->treelet_opt);
+    const int v = dev->variant;
+    const bool refill = use_refill(dev);
+    auto fit = [&](auto blocks) {
+        const int nb0 = blocks((size_t)0);
+        int lo = 0, hi = cap;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) / 2;
+            if (blocks(tree_bytes(dev, mid)) >= nb0) lo = mid;
+            else hi = mid - 1;
+        }
+        return lo;
+    };
+    if (dev->treelet_kernels & 1) dev->tree_ext = fit([&](size_t t) { return extend_blocks_per_cu<false>(v, 0, t); });
+    if (refill && (dev->treelet_kernels & 2))
+        dev->tree_trace = fit([&](size_t t) { return trace_blocks_per_cu<false>(v, dev->trace_waves, 0, true, t); });
+    if (dev->treelet_kernels & 4) dev->tree_shadow = fit([&](size_t t) { return shadow_blocks_per_cu<false>(v, 0, refill, t); });
+    // k_finish: none -- the tail kernel overlaps the next chunk's kernels, and
+    // LDS it holds keeps their blocks off the CU (soup-1M frame +4 % with one)
 }
 
 long long valid_pixels_in_chunk(const FrameArgs& fa) {
@@ -1901,9 +1978,16 @@ extern "C" const char* igx_last_error(const igx_device* dev) { return dev ? dev-
 extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t value) {
     if (!dev || !key) return IGX_ERR_INVALID_ARGUMENT;
     std::string k(key);
+    dev->tree_dirty = true; // schedule options change which kernels run, and so their treelets
     if (k == "timing") dev->timing = value != 0;
     else if (k == "instrument") dev->instrument = value != 0;
     else if (k == "capacity") dev->capacity_opt = value;
+    else if (k == "treelet") {
+        if (value < -1) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "treelet must be -1 (auto), 0 (off) or a node count");
+        dev->treelet_opt = value;
+        dev->tree_dirty = true;
+    }
+    else if (k == "treelet_kernels") dev->treelet_kernels = (int)(value & 7);
     else if (k == "slot_budget_mb") {
         if (value < 0) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "slot_budget_mb must be >= 0 (0 = auto)");
         dev->slot_budget_mb = value;
@@ -1949,7 +2033,7 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
         dev->bvh_bins_tlas = (int)value;
     }
     else if (k == "path_classes") {
-        if (value < 0 || value > 2) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "path_classes must be 0, 1 or 2");
+        if (value < 0 || value > 3) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "path_classes must be 0, 1, 2 or 3");
         dev->classify_opt = (int)value;
     }
     else if (k == "sah_node_cost_pct") {
@@ -1972,6 +2056,119 @@ extern "C" igx_status igx_synchronize(igx_device* dev) {
 // A closed triangle mesh: with vertices welded by position, every edge
 // borders exactly two faces (paths that enter it by transmission then hit it
 // again before leaving).  Checked up to 1 M faces.
+// Hot order of the node array for the LDS treelet (stage_treelet): the
+// `front` inner nodes a ray most likely visits move to indices [0, front), so
+// a kernel stages any prefix of the array as its treelet.  Visit likelihood
+// follows the surface-area heuristic: the TLAS root has 1; a child has its
+// parent's times the child box's area over the union of the sibling boxes
+// (the chance a ray through the parent also crosses the child); a BLAS root
+// collects the likelihood of every TLAS leaf that instances it.  The other
+// nodes keep their relative (depth-first) order.  Every inner-node reference
+// (node children, instance BLAS roots, the TLAS root) is renumbered; the
+// traversal result does not depend on node numbering.
+static void order_hot_nodes(std::vector<float4>& nodes, int nf4, std::vector<float4>& inst, int& tlas_root, size_t front) {
+    const size_t nn = nodes.size() / nf4;
+    if (nn == 0 || front == 0) return;
+    const int width = nf4 == 8 ? 4 : 2;
+    auto ref = [&](size_t n, int k) -> int32_t& {
+        return reinterpret_cast<int32_t*>(&nodes[n * nf4])[width == 4 ? 24 + k : 12 + k];
+    };
+    auto box = [&](size_t n, int k, float lo[3], float hi[3]) {
+        const float* f = reinterpret_cast<const float*>(&nodes[n * nf4]);
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = width == 4 ? f[8 * a + k] : f[6 * k + 2 * a];
+            hi[a] = width == 4 ? f[8 * a + 4 + k] : f[6 * k + 2 * a + 1];
+        }
+    };
+    auto half_area = [](const float lo[3], const float hi[3]) -> double {
+        for (int a = 0; a < 3; ++a)
+            if (!std::isfinite(lo[a]) || !std::isfinite(hi[a]) || lo[a] > hi[a]) return 0.0;
+        const double dx = (double)hi[0] - lo[0], dy = (double)hi[1] - lo[1], dz = (double)hi[2] - lo[2];
+        return dx * dy + dy * dz + dz * dx;
+    };
+    // children of node n with the node's likelihood pn: f(child ref, child likelihood)
+    auto children = [&](size_t n, double pn, auto&& f) {
+        float ulo[3] = {INFINITY, INFINITY, INFINITY}, uhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        double ak[4] = {0, 0, 0, 0};
+        for (int k = 0; k < width; ++k) {
+            float lo[3], hi[3];
+            box(n, k, lo, hi);
+            ak[k] = half_area(lo, hi);
+            if (ak[k] <= 0) continue;
+            for (int a = 0; a < 3; ++a) {
+                ulo[a] = std::min(ulo[a], lo[a]);
+                uhi[a] = std::max(uhi[a], hi[a]);
+            }
+        }
+        const double ua = half_area(ulo, uhi);
+        for (int k = 0; k < width; ++k) {
+            const int32_t r = ref(n, k);
+            if (r == igx::kEmptyRef || ak[k] <= 0) continue;
+            f(r, ua > 0 ? pn * std::min(1.0, ak[k] / ua) : pn);
+        }
+    };
+    std::vector<double> p(nn, 0.0), pblas(nn, 0.0);
+    auto instances = [&](int32_t leaf, double pl) { // TLAS leaf: its instances' BLAS roots
+        const int code = ~leaf;
+        const int first = code >> igx::kLeafCountBits, count = (code & ((1 << igx::kLeafCountBits) - 1)) + 1;
+        for (int k = 0; k < count; ++k) {
+            int4 info;
+            std::memcpy(&info, &inst[4 * (size_t)(first + k) + 3], 16);
+            if (info.y == 0 && info.z >= 0 && (size_t)info.z < nn) pblas[info.z] += pl;
+        }
+    };
+    std::vector<std::pair<int32_t, double>> todo;
+    if (tlas_root >= 0) todo.push_back({tlas_root, 1.0});
+    else if (!inst.empty()) instances(tlas_root, 1.0); // one entity: the root is its leaf
+    while (!todo.empty()) { // TLAS (a tree)
+        const auto [n, pn] = todo.back();
+        todo.pop_back();
+        p[n] += pn;
+        children((size_t)n, pn, [&](int32_t r, double pc) {
+            if (r >= 0) todo.push_back({r, pc});
+            else instances(r, pc);
+        });
+    }
+    for (size_t r = 0; r < nn; ++r) { // every BLAS from its root (a BLAS is a tree; shared BLAS summed at the root)
+        if (pblas[r] <= 0) continue;
+        todo.push_back({(int32_t)r, pblas[r]});
+        while (!todo.empty()) {
+            const auto [n, pn] = todo.back();
+            todo.pop_back();
+            p[n] += pn;
+            children((size_t)n, pn, [&](int32_t c, double pc) {
+                if (c >= 0) todo.push_back({c, pc});
+            });
+        }
+    }
+    std::vector<int32_t> order(nn);
+    for (size_t i = 0; i < nn; ++i) order[i] = (int32_t)i;
+    front = std::min(front, nn);
+    std::partial_sort(order.begin(), order.begin() + front, order.end(), [&](int32_t a, int32_t b) {
+        return p[a] != p[b] ? p[a] > p[b] : a < b;
+    });
+    std::vector<int32_t> newidx(nn, -1);
+    for (size_t i = 0; i < front; ++i) newidx[order[i]] = (int32_t)i;
+    int32_t next = (int32_t)front;
+    for (size_t i = 0; i < nn; ++i)
+        if (newidx[i] < 0) newidx[i] = next++;
+    std::vector<float4> out(nodes.size());
+    for (size_t i = 0; i < nn; ++i) std::copy(&nodes[i * nf4], &nodes[i * nf4] + nf4, &out[(size_t)newidx[i] * nf4]);
+    nodes.swap(out);
+    for (size_t i = 0; i < nn; ++i)
+        for (int k = 0; k < width; ++k)
+            if (ref(i, k) >= 0) ref(i, k) = newidx[ref(i, k)];
+    for (size_t slot = 0; slot < inst.size() / 4; ++slot) {
+        int4 info;
+        std::memcpy(&info, &inst[4 * slot + 3], 16);
+        if (info.y == 0 && info.z >= 0) {
+            info.z = newidx[info.z];
+            std::memcpy(&inst[4 * slot + 3], &info, 16);
+        }
+    }
+    if (tlas_root >= 0) tlas_root = newidx[tlas_root];
+}
+
 static bool closed_mesh(const igx_mesh& m) {
     if (m.num_faces < 4 || m.num_faces > (1u << 20)) return false;
     std::map<std::array<float, 3>, uint32_t> weld;
@@ -2169,6 +2366,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     std::vector<float4> fn_tab;    // world-space unit face normals (surface_element)
     std::vector<int> ent_enc; // per entity: enclosing index or -1
     std::vector<int2> enc_tab; // per enclosing index: entity, TLAS leaf slot
+    std::vector<float4> enc_box; // per enclosing index: world box lo, hi
     int tlas_root = -1;
     int tlas_depth = 0;
     if (desc->num_entities > 0) {
@@ -2215,6 +2413,8 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
                 if (apart && (int)enc_tab.size() < MAX_ENCLOSING) {
                     ent_enc[e] = (int)enc_tab.size();
                     enc_tab.push_back(make_int2((int)e, (int)slot));
+                    enc_box.push_back(make_float4(en.bbox_min[0], en.bbox_min[1], en.bbox_min[2], 0));
+                    enc_box.push_back(make_float4(en.bbox_max[0], en.bbox_max[1], en.bbox_max[2], 0));
                 }
             }
         }
@@ -2413,6 +2613,9 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
         mats[i] = d;
     }
 
+    // hot nodes first: any prefix of the node array is a treelet (stage_treelet)
+    order_hot_nodes(nodes, nf4, inst, tlas_root, TREELET_FRONT);
+
     // ---- upload ----------------------------------------------------------
     SceneView sv{};
     igx_status st;
@@ -2421,7 +2624,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
         (st = upload(dev, nrm, &sv.nrm)) || (st = upload(dev, idx, &sv.idx)) || (st = upload(dev, mats, &sv.mats)) ||
         (st = upload(dev, lights, &sv.lights)) || (st = upload(dev, lsel.cdf, &sv.sel_cdf)) ||
         (st = upload(dev, lsel.hierarchy, &sv.sel_tree)) || (st = upload(dev, ent_enc, &sv.ent_enc)) ||
-        (st = upload(dev, enc_tab, &sv.enc)) || (st = upload(dev, ent_fn, &sv.ent_fn)) ||
+        (st = upload(dev, enc_tab, &sv.enc)) || (st = upload(dev, enc_box, &sv.enc_box)) || (st = upload(dev, ent_fn, &sv.ent_fn)) ||
         (st = upload(dev, fn_tab, &sv.fn_tab))) {
         free_scene(dev);
         return st;
@@ -2432,6 +2635,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     sv.node_f4 = nf4;
     dev->bvh_width = width;
     sv.num_inst = (int)(inst.size() / 4);
+    sv.num_enc = (int)enc_tab.size();
     sv.num_tris = (int)(tris.size() / 3);
     {
         size_t b = ((size_t)sv.num_nodes * nf4 + (size_t)sv.num_inst * 4 + (size_t)sv.num_tris * 3) * 16;
@@ -2482,6 +2686,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
         return st;
     }
     dev->has_scene = true;
+    dev->tree_dirty = true;
     return IGX_OK;
 }
 
@@ -2586,16 +2791,20 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
     const bool inst = dev->instrument;
     const int sd = dev->variant;
     const size_t ldsb = dev->lds_scene_bytes;
-    const int ext_bpc = inst ? extend_blocks_per_cu<true>(sd, ldsb) : extend_blocks_per_cu<false>(sd, ldsb);
+    if (dev->tree_dirty) configure_treelet(dev);
+    const int ext_bpc = inst ? extend_blocks_per_cu<true>(sd, ldsb, tree_bytes(dev, dev->tree_ext))
+                             : extend_blocks_per_cu<false>(sd, ldsb, tree_bytes(dev, dev->tree_ext));
     const bool refill = use_refill(dev);
-    const int tr_bpc = inst ? trace_blocks_per_cu<true>(sd, dev->trace_waves, dev->lds_scene_bytes, refill)
-                            : trace_blocks_per_cu<false>(sd, dev->trace_waves, dev->lds_scene_bytes, refill);
+    const size_t tr_tree = refill ? tree_bytes(dev, dev->tree_trace) : 0;
+    const int tr_bpc = inst ? trace_blocks_per_cu<true>(sd, dev->trace_waves, dev->lds_scene_bytes, refill, tr_tree)
+                            : trace_blocks_per_cu<false>(sd, dev->trace_waves, dev->lds_scene_bytes, refill, tr_tree);
     const bool full = variant_full(sd);
     const int shade_bpc = shade_blocks_per_cu(full);
     const bool split = use_split(dev);
-    const int sh_bpc = inst ? shadow_blocks_per_cu<true>(sd, dev->lds_scene_bytes, refill)
-                            : shadow_blocks_per_cu<false>(sd, dev->lds_scene_bytes, refill);
-    const int fin_bpc = inst ? finish_blocks_per_cu<true>(sd, ldsb) : finish_blocks_per_cu<false>(sd, ldsb);
+    const int sh_bpc = inst ? shadow_blocks_per_cu<true>(sd, dev->lds_scene_bytes, refill, tree_bytes(dev, dev->tree_shadow))
+                            : shadow_blocks_per_cu<false>(sd, dev->lds_scene_bytes, refill, tree_bytes(dev, dev->tree_shadow));
+    const int fin_bpc = inst ? finish_blocks_per_cu<true>(sd, ldsb, tree_bytes(dev, dev->tree_fin))
+                             : finish_blocks_per_cu<false>(sd, ldsb, tree_bytes(dev, dev->tree_fin));
 
     for (int it0 = 0; it0 < count; it0 += iters_per_chunk)
     for (long long px0 = 0; px0 < local_pixels; px0 += chunk_pixels_max) {
@@ -2736,6 +2945,13 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
     return IGX_OK;
 }
 
+extern "C" igx_status igx_set_camera(igx_device* dev, const igx_camera* camera) {
+    if (!dev || !camera) return IGX_ERR_INVALID_ARGUMENT;
+    // queued chunks read the camera from their kernel arguments: no drain needed
+    dev->cam_desc = *camera;
+    return IGX_OK;
+}
+
 extern "C" igx_status igx_render(igx_device* dev, const igx_render_params* p) { return render_impl(dev, p, 1); }
 
 extern "C" igx_status igx_render_iterations(igx_device* dev, const igx_render_params* p, int32_t count) {
@@ -2836,7 +3052,13 @@ extern "C" igx_status igx_get_stats(igx_device* dev, igx_stats* out) {
     out->bvh_width = dev->bvh_width;
     out->node_bytes = node_f4(dev->bvh_width) * 16;
     out->lds_scene_bytes = (int32_t)dev->lds_scene_bytes;
-    out->shadow_blocks_per_cu = dev->has_scene ? shadow_blocks_per_cu<false>(dev->variant, dev->lds_scene_bytes, use_refill(dev)) : 0;
+    if (dev->has_scene && dev->tree_dirty) configure_treelet(dev);
+    out->shadow_blocks_per_cu = dev->has_scene ? shadow_blocks_per_cu<false>(dev->variant, dev->lds_scene_bytes, use_refill(dev),
+                                                                            tree_bytes(dev, dev->tree_shadow)) : 0;
+    out->treelet_nodes[0] = dev->tree_ext;
+    out->treelet_nodes[1] = dev->tree_trace;
+    out->treelet_nodes[2] = dev->tree_shadow;
+    out->treelet_nodes[3] = dev->tree_fin;
     out->table_bytes = dev->table_bytes;
     out->shading_bytes = dev->shading_bytes;
     out->slot_bytes = 0;

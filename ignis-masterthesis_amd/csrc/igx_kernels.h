@@ -30,10 +30,16 @@ struct SceneView {
     int max_depth, min_depth, nee;
     float clamp;
     int num_nodes, num_inst, num_tris; // table sizes (for staging the traversal tables in LDS)
+    // treelet: nodes [0, tree_n) of `nodes` (the hottest, igx_upload_scene's
+    // hot order) staged in LDS at `tree` by stage_treelet (variant_tree kernels)
+    const float4* tree;
+    int tree_n;
     int* spill;            // traversal-stack overflow area of the launching stream (see TStack)
     int node_f4;           // float4s per BVH node (4: BVH2, 8: 4-wide)
     const int* ent_enc;    // per entity: its index among the enclosing entities (trace_enclosed), else -1
     const int2* enc;       // per enclosing entity: entity id, TLAS leaf slot
+    const float4* enc_box; // per enclosing entity: world box lo.xyz, hi.xyz (path classes, option path_classes 3)
+    int num_enc;
     int selector;          // NEE light selector in effect (IGX_SELECT_*; host/light_select.h)
     const float* sel_cdf;  // simple: CDF over the finite lights ([c_1 .. c_{n-1}, 1])
     const uint32_t* sel_tree; // hierarchy: codes (padded to 4), then 8 words per entry
@@ -59,6 +65,23 @@ __device__ __forceinline__ SceneView stage_scene_lds(const SceneView& sv, float4
     l.nodes = lds;
     l.inst = lds + n4;
     l.tris = lds + n4 + i4;
+    return l;
+}
+
+// Stage the treelet (the scene's first tree_n nodes, the ones rays visit
+// most: the top of the TLAS and of the busiest BLAS) in LDS for a kernel
+// whose tables stay in global memory; node steps below tree_n then read LDS
+// instead of waiting on an L2 / Infinity-Cache round trip.  Block-uniform:
+// every thread of the block calls it before any divergent code.
+template <int BLOCK_>
+__device__ __forceinline__ SceneView stage_treelet(const SceneView& sv, float4* lds) {
+    SceneView l = sv;
+    l.tree = lds;
+    if (sv.tree_n > 0) {
+        const int n4 = sv.tree_n * sv.node_f4;
+        for (int k = threadIdx.x; k < n4; k += BLOCK_) lds[k] = sv.nodes[k];
+        __syncthreads();
+    }
     return l;
 }
 
@@ -173,16 +196,19 @@ __device__ __forceinline__ void trav_init(const SceneView& sv, Trav& t, f3 o, f3
 // Slab test of both children of BVH2 node `node` (intersect_ray_box,
 // intersection.art:170-181, with ray.tmin folded in).  Returns the next node
 // (nearer child first; the other is pushed) or the popped entry.
-template <bool STATS, bool SPILL, int NS>
+template <bool STATS, bool SPILL, int NS, bool TREE>
 __device__ __forceinline__ int node_step2(const SceneView& sv, const Trav& t, int node, const TStack& ts, int& sp,
                                          TraceStats& st) {
     if (STATS) {
         st.nodes++;
         if (first_active_lane()) st.wnodes++;
     }
-    const float4* np = sv.nodes + NS * node;
-    float4 a = np[0], b = np[1], c = np[2];
-    int4 r = *reinterpret_cast<const int4*>(np + 3);
+    // treelet nodes (TREE, node < tree_n) come from LDS: one generic (flat)
+    // load sequence serves both address spaces, so the two sources share
+    // registers (a branch per source cost the 80-VGPR persistent-lane kernels spills)
+    const float4* np = (TREE && node < sv.tree_n ? sv.tree : sv.nodes) + NS * node;
+    const float4 a = np[0], b = np[1], c = np[2];
+    const int4 r = *reinterpret_cast<const int4*>(np + 3);
     // child 0 box: lo (a.x, a.z, b.x) hi (a.y, a.w, b.y)
     // slab distances with explicit FMAs (the only contracted arithmetic
     // in the device code, built with -ffp-contract=off)
@@ -227,14 +253,14 @@ __device__ __forceinline__ void cswap(float& da, int& ra, float& db, int& rb) {
     da = td;
     ra = tr;
 }
-template <bool STATS, bool SPILL, int NS>
+template <bool STATS, bool SPILL, int NS, bool TREE>
 __device__ __forceinline__ int node_step4(const SceneView& sv, const Trav& t, int node, const TStack& ts, int& sp,
                                           TraceStats& st) {
     if (STATS) {
         st.nodes++;
         if (first_active_lane()) st.wnodes++;
     }
-    const float4* np = sv.nodes + NS * node;
+    const float4* np = (TREE && node < sv.tree_n ? sv.tree : sv.nodes) + NS * node; // see node_step2
     const float4 lx = np[0], hx = np[1], ly = np[2], hy = np[3], lz = np[4], hz = np[5];
     const int4 r = *reinterpret_cast<const int4*>(np + 6);
     float d[4];
@@ -271,8 +297,8 @@ template <bool STATS, int V>
 __device__ __forceinline__ int node_step(const SceneView& sv, const Trav& t, int node, const TStack& ts, int& sp,
                                          TraceStats& st) {
     constexpr int PAD = variant_ldspad(V) ? 1 : 0;
-    if constexpr (variant_width(V) == 4) return node_step4<STATS, variant_spill(V), 8 + PAD>(sv, t, node, ts, sp, st);
-    else return node_step2<STATS, variant_spill(V), 4 + PAD>(sv, t, node, ts, sp, st);
+    if constexpr (variant_width(V) == 4) return node_step4<STATS, variant_spill(V), 8 + PAD, variant_tree(V)>(sv, t, node, ts, sp, st);
+    else return node_step2<STATS, variant_spill(V), 4 + PAD, variant_tree(V)>(sv, t, node, ts, sp, st);
 }
 
 // Back from a BLAS: restore the world ray (recomputed: cheaper than keeping

@@ -10,8 +10,20 @@
 //     technique variant's compiled shader code; igx has no shader JIT, so here
 //     the "shader set" is the shading tables the shaders were generated from
 //     (materials, lights, camera, technique: igx_shading_view).  The scene is
-//     uploaded on the first render after assignScene or with a new shader set,
-//     as the reference compiles and loads its shaders lazily;
+//     uploaded on the first render after assignScene and whenever the shading
+//     tables' contents change (materials, lights, technique, film; a copy of
+//     the last uploaded ones is compared, so a set edited in place or a new
+//     set at a freed one's address is seen), as the reference compiles and
+//     loads its shaders lazily.  A camera change alone does not re-upload: it
+//     reaches the device through igx_set_camera;
+//   * render's ParameterSet (RuntimeStructs.h:56-70) carries the runtime's
+//     camera orientation (__camera_eye / __camera_dir / __camera_up,
+//     Runtime::setCameraOrientationParameter, Runtime.cpp:700-705), which
+//     overrides the shading view's camera; its other parameters drive the
+//     reference's shading networks, which igx does not have, and are ignored;
+//   * capture_shading builds the shader set of an in-memory scene
+//     (igx_objscene_*, the `const Scene*` of Runtime::loadFromScene) without a
+//     file;
 //   * the framebuffer, statistics, resize and release calls map one to one.
 // tonemap / evaluateGlare / imageinfo / bake (Device.h:66-69) are outside the
 // hot path and are not provided.  Errors from the C-ABI become
@@ -22,9 +34,12 @@
 #include "igx.h"
 #include "scene_database.h"
 
+#include <array>
 #include <cstdint>
+#include <cstring>
 #include <stdexcept>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 namespace IG {
@@ -52,7 +67,34 @@ struct TechniqueVariantShaderSet {
     igx_shading_view shading{};
 };
 struct TechniqueVariantInfo {};
-struct ParameterSet {};
+using Vector3f = std::array<float, 3>;
+using Vector4f = std::array<float, 4>;
+struct ParameterSet { // RuntimeStructs.h:56-70
+    std::unordered_map<std::string, int> IntParameters;
+    std::unordered_map<std::string, float> FloatParameters;
+    std::unordered_map<std::string, Vector3f> VectorParameters;
+    std::unordered_map<std::string, Vector4f> ColorParameters;
+    bool empty() const { return IntParameters.empty() && FloatParameters.empty() && VectorParameters.empty() && ColorParameters.empty(); }
+};
+
+// The shader set of a scene igx loaded itself (igx_scene_load_* or, for the
+// reference's in-memory scenes, igx_scene_from_objects): its film, camera,
+// technique, materials and lights.  The views point into `scene`, which must
+// outlive the shader set.
+inline TechniqueVariantShaderSet capture_shading(const igx_scene* scene) {
+    const igx_scene_desc* d = igx_scene_get_desc(scene);
+    if (!d) throw std::runtime_error("igx: capture_shading without a scene");
+    TechniqueVariantShaderSet s;
+    s.shading.film_width = d->film_width;
+    s.shading.film_height = d->film_height;
+    s.shading.camera = d->camera;
+    s.shading.technique = d->technique;
+    s.shading.num_materials = d->num_materials;
+    s.shading.materials = d->materials;
+    s.shading.num_lights = d->num_lights;
+    s.shading.lights = d->lights;
+    return s;
+}
 
 // Statistics.h quantities the device fills (CameraRayCount, BounceRayCount,
 // ShadowRayCount; shadow rays counted when valid)
@@ -115,12 +157,26 @@ public:
     void assignScene(const SceneSettings& settings) {
         if (!settings.database) throw std::runtime_error("igx: assignScene without a SceneDatabase");
         mScene = settings;
-        mShaderSet = nullptr; // upload at the next render
+        releaseAll(); // upload at the next render
     }
 
-    void render(const TechniqueVariantShaderSet& shader_set, const RenderSettings& s, const ParameterSet* = nullptr) {
+    void render(const TechniqueVariantShaderSet& shader_set, const RenderSettings& s, const ParameterSet* params = nullptr) {
         if (!mScene.database) throw std::runtime_error("igx: render before assignScene");
-        if (mShaderSet != &shader_set) upload(shader_set);
+        if (!mUploaded || !mLast.same(shader_set.shading)) upload(shader_set);
+        igx_camera cam = shader_set.shading.camera;
+        if (params) { // the runtime's camera orientation (Runtime.cpp:700-705)
+            auto put = [&](const char* key, float* dst) {
+                auto it = params->VectorParameters.find(key);
+                if (it != params->VectorParameters.end()) std::memcpy(dst, it->second.data(), 3 * sizeof(float));
+            };
+            put("__camera_eye", cam.eye);
+            put("__camera_dir", cam.dir);
+            put("__camera_up", cam.up);
+        }
+        if (std::memcmp(&cam, &mCamera, sizeof(cam)) != 0) {
+            check(igx_set_camera(mDev, &cam));
+            mCamera = cam;
+        }
         igx_render_params p{};
         p.spi = (int)s.spi;
         p.iteration = (int)s.iteration;
@@ -150,7 +206,7 @@ public:
     void releaseAll() {
         if (mUploaded) igx_scene_free(mUploaded);
         mUploaded = nullptr;
-        mShaderSet = nullptr;
+        mLast = ShadingCopy{};
     }
 
     Target target() const { return mSettings.target; }
@@ -200,14 +256,41 @@ private:
         releaseAll();
         mUploaded = sc;
         check(st);
-        mShaderSet = &shader_set;
+        mLast.take(shader_set.shading);
+        mCamera = shader_set.shading.camera; // igx_upload_scene set it
     }
+
+    // a copy of the shading tables last uploaded (the camera aside: it does
+    // not need an upload), to see in-place edits and reused addresses
+    struct ShadingCopy {
+        bool valid = false;
+        int32_t film_width = 0, film_height = 0;
+        igx_technique technique{};
+        std::vector<igx_material> materials;
+        std::vector<igx_light> lights;
+        void take(const igx_shading_view& v) {
+            valid = true;
+            film_width = v.film_width;
+            film_height = v.film_height;
+            technique = v.technique;
+            materials.assign(v.materials, v.materials + v.num_materials);
+            lights.assign(v.lights, v.lights + v.num_lights);
+        }
+        bool same(const igx_shading_view& v) const {
+            return valid && film_width == v.film_width && film_height == v.film_height &&
+                   std::memcmp(&technique, &v.technique, sizeof(technique)) == 0 && materials.size() == v.num_materials &&
+                   lights.size() == v.num_lights &&
+                   (materials.empty() || std::memcmp(materials.data(), v.materials, materials.size() * sizeof(igx_material)) == 0) &&
+                   (lights.empty() || std::memcmp(lights.data(), v.lights, lights.size() * sizeof(igx_light)) == 0);
+        }
+    };
 
     SetupSettings mSettings;
     SceneSettings mScene;
     igx_device* mDev = nullptr;
     igx_scene* mUploaded = nullptr;
-    const TechniqueVariantShaderSet* mShaderSet = nullptr;
+    ShadingCopy mLast;
+    igx_camera mCamera{};
     size_t mWidth = 0, mHeight = 0;
     std::vector<float> mHostFB;
     Statistics mStats;

@@ -951,3 +951,154 @@ extern "C" const char* igx_scene_entity_name(const igx_scene* s, uint32_t entity
     if (!s || entity >= s->store.entity_names.size()) return nullptr;
     return s->store.entity_names[entity].c_str();
 }
+
+// ---------------------------------------------------------------------------
+// In-memory scenes (IG::Scene object model, include/igx_scene.h): the objects
+// become the same document load_document builds from JSON, so build_scene
+// reads both with one set of semantics.
+// ---------------------------------------------------------------------------
+struct igx_objscene {
+    Value doc;
+    std::string base_dir;
+    std::vector<std::pair<std::string, std::string>> objs; // handle -> (category, name); anonymous: name empty
+};
+
+namespace {
+
+const char* object_category(int32_t t) {
+    switch (t) {
+    case IGX_OBJ_BSDF: return "bsdfs";
+    case IGX_OBJ_CAMERA: return "camera";
+    case IGX_OBJ_ENTITY: return "entities";
+    case IGX_OBJ_FILM: return "film";
+    case IGX_OBJ_LIGHT: return "lights";
+    case IGX_OBJ_MEDIUM: return "media";
+    case IGX_OBJ_SHAPE: return "shapes";
+    case IGX_OBJ_TECHNIQUE: return "technique";
+    case IGX_OBJ_TEXTURE: return "textures";
+    case IGX_OBJ_PARAMETER: return "parameters";
+    default: return nullptr;
+    }
+}
+
+bool anonymous_category(const std::string& c) { return c == "camera" || c == "film" || c == "technique"; }
+
+Value* find_object(igx_objscene* sc, int32_t h) {
+    if (!sc || h < 0 || (size_t)h >= sc->objs.size()) return nullptr;
+    const auto& [cat, name] = sc->objs[(size_t)h];
+    for (auto& kv : sc->doc.obj) {
+        if (kv.first != cat) continue;
+        if (anonymous_category(cat)) return &kv.second;
+        for (auto& o : kv.second.arr) {
+            const Value* n = o.find("name");
+            if (n && n->str == name) return &o;
+        }
+    }
+    return nullptr;
+}
+
+Value number_value(double x) {
+    Value v;
+    v.type = Value::Number;
+    v.num = x;
+    return v;
+}
+
+} // namespace
+
+extern "C" igx_objscene* igx_objscene_create(const char* base_dir) {
+    auto* s = new igx_objscene();
+    s->doc.type = Value::Object;
+    s->base_dir = base_dir ? base_dir : ".";
+    return s;
+}
+
+extern "C" void igx_objscene_free(igx_objscene* s) { delete s; }
+
+extern "C" int32_t igx_objscene_add(igx_objscene* sc, int32_t type, const char* plugin_type, const char* name,
+                                    const char* base_dir) {
+    const char* cat = object_category(type);
+    if (!sc || !cat) return -1;
+    Value obj;
+    obj.type = Value::Object;
+    Value t;
+    t.type = Value::String;
+    t.str = plugin_type ? plugin_type : "";
+    obj.obj.emplace_back("type", t);
+    Value bd;
+    bd.type = Value::String;
+    bd.str = base_dir ? base_dir : sc->base_dir;
+    obj.obj.emplace_back("__base_dir", bd);
+    std::string nm;
+    if (!anonymous_category(cat)) {
+        if (!name || !*name) return -1; // named objects need a name (Scene::add*)
+        nm = name;
+        Value n;
+        n.type = Value::String;
+        n.str = nm;
+        obj.obj.emplace_back("name", n);
+        put_named(category(sc->doc, cat), obj);
+    } else {
+        set_key(sc->doc, cat, &obj);
+    }
+    sc->objs.emplace_back(cat, nm);
+    return (int32_t)sc->objs.size() - 1;
+}
+
+extern "C" int32_t igx_objscene_set_property(igx_objscene* sc, int32_t h, const char* key, int32_t type, const void* data,
+                                             uint64_t count) {
+    Value* obj = find_object(sc, h);
+    if (!obj || !key || (!data && type != IGX_PROP_INTEGER_ARRAY && type != IGX_PROP_NUMBER_ARRAY)) return -1;
+    const std::string k = key;
+    if (k == "type" || k == "name" || k == "__base_dir") return -1; // set by igx_objscene_add
+    Value v;
+    auto floats = [&](const float* f, size_t n) {
+        v.type = Value::Array;
+        for (size_t i = 0; i < n; ++i) v.arr.push_back(number_value(f[i]));
+    };
+    switch (type) {
+    case IGX_PROP_BOOL:
+        v.type = Value::Bool;
+        v.b = *static_cast<const int32_t*>(data) != 0;
+        break;
+    case IGX_PROP_INTEGER: v = number_value(*static_cast<const int32_t*>(data)); break;
+    case IGX_PROP_NUMBER: v = number_value(*static_cast<const float*>(data)); break;
+    case IGX_PROP_STRING:
+        v.type = Value::String;
+        v.str = static_cast<const char*>(data);
+        break;
+    case IGX_PROP_TRANSFORM: floats(static_cast<const float*>(data), 16); break;
+    case IGX_PROP_VECTOR2: floats(static_cast<const float*>(data), 2); break;
+    case IGX_PROP_VECTOR3: floats(static_cast<const float*>(data), 3); break;
+    case IGX_PROP_NUMBER_ARRAY: floats(static_cast<const float*>(data), (size_t)count); break;
+    case IGX_PROP_INTEGER_ARRAY:
+        v.type = Value::Array;
+        for (uint64_t i = 0; i < count; ++i) v.arr.push_back(number_value(static_cast<const int32_t*>(data)[i]));
+        break;
+    default: return -1;
+    }
+    for (auto& kv : obj->obj)
+        if (kv.first == k) {
+            kv.second = v;
+            return 0;
+        }
+    obj->obj.emplace_back(k, v);
+    return 0;
+}
+
+extern "C" igx_scene* igx_scene_from_objects(const igx_objscene* sc, char* err, size_t err_len) {
+    if (!sc) { set_err(err, err_len, "null object scene"); return nullptr; }
+    try {
+        auto* s = new igx_scene();
+        try {
+            build_scene(s->store, sc->doc, sc->base_dir);
+        } catch (...) {
+            delete s;
+            throw;
+        }
+        return s;
+    } catch (const std::exception& e) {
+        set_err(err, err_len, e.what());
+        return nullptr;
+    }
+}

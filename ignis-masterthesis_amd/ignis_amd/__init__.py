@@ -96,6 +96,16 @@ class Scene:
         return Scene(h)
 
     @staticmethod
+    def from_objects(objects):
+        """igx_scene_from_objects: a scene built object by object
+        (`ObjectScene`, the reference's in-memory IG::Scene)."""
+        err = C.create_string_buffer(2048)
+        h = lib().igx_scene_from_objects(objects._h, err, len(err))
+        if not h:
+            raise IgxError(err.value.decode())
+        return Scene(h)
+
+    @staticmethod
     def from_database(db, shading):
         """igx_scene_from_database: the reference's SceneDatabase tables
         (`_native.DatabaseView`) plus the shading tables (`_native.ShadingView`);
@@ -123,6 +133,103 @@ class Scene:
     def close(self):
         if self._h:
             lib().igx_scene_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class ObjectScene:
+    """The reference's in-memory scene (IG::Scene: technique, camera, film and
+    named bsdfs / shapes / lights / entities / textures / media, each a
+    SceneObject of SceneProperty values) built through the igx_objscene_* C-ABI,
+    the way a binding forwards the `const Scene*` that Runtime::loadFromScene
+    receives (Runtime.cpp:183-199)."""
+
+    OBJ = {"bsdfs": 0, "camera": 1, "entities": 2, "film": 3, "lights": 4, "media": 5, "shapes": 6, "technique": 7,
+           "textures": 8, "parameters": 9}
+    BOOL, INTEGER, NUMBER, STRING, TRANSFORM, VECTOR2, VECTOR3, INTEGER_ARRAY, NUMBER_ARRAY = range(1, 10)
+
+    def __init__(self, base_dir=None):
+        self._h = lib().igx_objscene_create(os.fsencode(base_dir) if base_dir else None)
+
+    def add(self, category, plugin_type, name=None, base_dir=None):
+        h = lib().igx_objscene_add(self._h, self.OBJ[category], plugin_type.encode(), name.encode() if name else None,
+                                   os.fsencode(base_dir) if base_dir else None)
+        if h < 0:
+            raise IgxError(f"igx_objscene_add({category}, {plugin_type}, {name}) refused")
+        return h
+
+    def set(self, obj, key, ptype, value):
+        if ptype == self.STRING:
+            buf = C.create_string_buffer(value.encode())
+            data, n = C.cast(buf, C.c_void_p), 1
+        elif ptype in (self.BOOL, self.INTEGER, self.INTEGER_ARRAY):
+            vals = [int(v) for v in (value if isinstance(value, (list, tuple)) else [value])]
+            buf = (C.c_int32 * max(1, len(vals)))(*vals)
+            data, n = C.cast(buf, C.c_void_p), len(vals)
+        else:
+            vals = [float(v) for v in (value if isinstance(value, (list, tuple)) else [value])]
+            buf = (C.c_float * max(1, len(vals)))(*vals)
+            data, n = C.cast(buf, C.c_void_p), len(vals)
+        if lib().igx_objscene_set_property(self._h, obj, key.encode(), ptype, data, n) != 0:
+            raise IgxError(f"igx_objscene_set_property({key}) refused")
+
+    def set_value(self, obj, key, v):
+        """A JSON value typed as the reference parser types it (getProperty, Parser.cpp:281-318)."""
+        if isinstance(v, bool):
+            self.set(obj, key, self.BOOL, int(v))
+        elif isinstance(v, str):
+            self.set(obj, key, self.STRING, v)
+        elif isinstance(v, int):
+            self.set(obj, key, self.INTEGER, v)
+        elif isinstance(v, float):
+            self.set(obj, key, self.NUMBER, v)
+        elif isinstance(v, list):
+            if len(v) == 2:
+                self.set(obj, key, self.VECTOR2, v)
+            elif len(v) == 3:
+                self.set(obj, key, self.VECTOR3, v)
+            elif len(v) in (9, 12, 16):
+                m = [[1.0 if i == j else 0.0 for j in range(4)] for i in range(4)]
+                for i in range(3 if len(v) != 16 else 4):
+                    for j in range(3 if len(v) == 9 else 4):
+                        m[i][j] = float(v[i * (3 if len(v) == 9 else 4) + j])
+                self.set(obj, key, self.TRANSFORM, [x for row in m for x in row])
+            else:
+                raise IgxError(f"property '{key}': an array of {len(v)} is not a scene property")
+        elif isinstance(v, dict) and "values" in v:
+            ints = str(v.get("type", "")) in ("int", "integer")
+            self.set(obj, key, self.INTEGER_ARRAY if ints else self.NUMBER_ARRAY, v["values"])
+        else:
+            raise IgxError(f"property '{key}': unsupported value {v!r}")
+
+    @staticmethod
+    def from_dict(scene, base_dir=None):
+        """Every object of a scene dict (the JSON schema), as a binding would
+        forward the parsed IG::Scene's objects."""
+        o = ObjectScene(base_dir)
+        for cat in ("technique", "camera", "film"):
+            if cat in scene:
+                d = scene[cat]
+                h = o.add(cat, d.get("type", ""))
+                for k, v in d.items():
+                    if k != "type":
+                        o.set_value(h, k, v)
+        for cat in ("textures", "bsdfs", "shapes", "lights", "media", "entities"):
+            for d in scene.get(cat, []):
+                h = o.add(cat, d.get("type", ""), d["name"])
+                for k, v in d.items():
+                    if k not in ("type", "name"):
+                        o.set_value(h, k, v)
+        return o
+
+    def close(self):
+        if self._h:
+            lib().igx_objscene_free(self._h)
             self._h = None
 
     def __del__(self):

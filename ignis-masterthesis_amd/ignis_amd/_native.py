@@ -127,10 +127,11 @@ class Stats(C.Structure):
                 ("table_bytes", C.c_uint64), ("shading_bytes", C.c_uint64),
                 ("extend_cycles_load", C.c_uint64), ("extend_cycles_trace", C.c_uint64),
                 ("extend_cycles_shade", C.c_uint64), ("extend_cycles_store", C.c_uint64),
-                ("slot_bytes", C.c_uint64)]
+                ("slot_bytes", C.c_uint64), ("treelet_nodes", C.c_int32 * 4)]
 
     def as_dict(self):
-        return {name: getattr(self, name) for name, _ in self._fields_}
+        return {name: (list(getattr(self, name)) if isinstance(getattr(self, name), C.Array) else getattr(self, name))
+                for name, _ in self._fields_}
 
 
 # every symbol include/igx.h and include/igx_scene.h declare
@@ -140,7 +141,8 @@ EXPORTED_SYMBOLS = [
     "igx_create", "igx_destroy", "igx_last_error", "igx_version", "igx_set_option", "igx_upload_scene",
     "igx_render", "igx_get_framebuffer", "igx_framebuffer_device_ptr", "igx_pack_tiles", "igx_clear",
     "igx_get_stats", "igx_reset_stats", "igx_trace_hits", "igx_trace_occlusion", "igx_synchronize",
-    "igx_render_iterations",
+    "igx_render_iterations", "igx_objscene_create", "igx_objscene_free", "igx_objscene_add",
+    "igx_objscene_set_property", "igx_scene_from_objects", "igx_set_camera",
 ]
 
 _lib = None
@@ -169,6 +171,17 @@ def lib():
     L.igx_scene_get_desc.restype = C.POINTER(SceneDesc)
     L.igx_scene_free.argtypes = [vp]
     L.igx_scene_free.restype = None
+    L.igx_objscene_create.argtypes = [C.c_char_p]
+    L.igx_objscene_create.restype = vp
+    L.igx_objscene_free.argtypes = [vp]
+    L.igx_objscene_free.restype = None
+    L.igx_objscene_add.argtypes = [vp, C.c_int32, C.c_char_p, C.c_char_p, C.c_char_p]
+    L.igx_objscene_add.restype = C.c_int32
+    L.igx_objscene_set_property.argtypes = [vp, C.c_int32, C.c_char_p, C.c_int32, C.c_void_p, C.c_uint64]
+    L.igx_objscene_set_property.restype = C.c_int32
+    L.igx_scene_from_objects.argtypes = [vp, C.c_char_p, C.c_size_t]
+    L.igx_scene_from_objects.restype = vp
+    L.igx_set_camera.argtypes = [vp, C.POINTER(Camera)]
     L.igx_write_exr.argtypes = [C.c_char_p, C.POINTER(C.c_float), C.c_int32, C.c_int32, C.c_int32, C.c_float]
     L.igx_write_exr.restype = C.c_int
     L.igx_create.argtypes = [C.c_int, C.POINTER(vp)]

@@ -191,6 +191,48 @@ void igx_scene_free(igx_scene* scene);
 int32_t igx_scene_find_material(const igx_scene* scene, const char* bsdf, const char* emissive_entity);
 const char* igx_scene_entity_name(const igx_scene* scene, uint32_t entity);
 
+/* ---- in-memory scenes: the reference's IG::Scene object model ------------
+ * Runtime::loadFromString / loadFromScene parse (or receive) an IG::Scene and
+ * call load({}, scene) without a file (Runtime.cpp:164-199).  A binding that
+ * holds such a `const Scene*` (Scene.h: technique, camera, film and named
+ * textures / bsdfs / shapes / lights / media / entities, each a SceneObject
+ * with a plugin type and SceneProperty values, SceneObject.h, SceneProperty.h)
+ * rebuilds it here object by object and property by property, and
+ * igx_scene_from_objects reads it with the same semantics as the JSON loader
+ * -- no file and no second parse.  An in-memory JSON string goes through
+ * igx_scene_load_string. */
+typedef struct igx_objscene igx_objscene;
+/* SceneObject::Type (SceneObject.h:10-22) */
+enum {
+    IGX_OBJ_BSDF = 0, IGX_OBJ_CAMERA = 1, IGX_OBJ_ENTITY = 2, IGX_OBJ_FILM = 3, IGX_OBJ_LIGHT = 4, IGX_OBJ_MEDIUM = 5,
+    IGX_OBJ_SHAPE = 6, IGX_OBJ_TECHNIQUE = 7, IGX_OBJ_TEXTURE = 8, IGX_OBJ_PARAMETER = 9
+};
+/* SceneProperty::Type (SceneProperty.h:17-28) and the data each takes:
+ * BOOL, INTEGER: int32_t[1]; NUMBER: float[1]; STRING: a NUL-terminated char*;
+ * TRANSFORM: float[16], row-major 4x4 (Eigen's Transformf::matrix() is
+ * column-major: transpose it); VECTOR2 float[2]; VECTOR3 float[3];
+ * INTEGER_ARRAY int32_t[count]; NUMBER_ARRAY float[count] */
+enum {
+    IGX_PROP_BOOL = 1, IGX_PROP_INTEGER = 2, IGX_PROP_NUMBER = 3, IGX_PROP_STRING = 4, IGX_PROP_TRANSFORM = 5,
+    IGX_PROP_VECTOR2 = 6, IGX_PROP_VECTOR3 = 7, IGX_PROP_INTEGER_ARRAY = 8, IGX_PROP_NUMBER_ARRAY = 9
+};
+/* `base_dir` resolves relative file names (mesh files) of objects added
+ * without their own directory (SceneObject::baseDir); may be NULL. */
+igx_objscene* igx_objscene_create(const char* base_dir);
+void igx_objscene_free(igx_objscene* scene);
+/* Add an object (Scene::addBSDF / setCamera / ...): a named object replaces
+ * one of the same type and name; camera, film and technique ignore `name` and
+ * replace the previous one.  `base_dir` may be NULL.  Returns the object's
+ * handle (>= 0) or -1 for an unknown type. */
+int32_t igx_objscene_add(igx_objscene* scene, int32_t object_type, const char* plugin_type, const char* name,
+                         const char* base_dir);
+/* SceneObject::setProperty: 0 on success, -1 for a bad handle, type or data. */
+int32_t igx_objscene_set_property(igx_objscene* scene, int32_t object, const char* key, int32_t property_type,
+                                  const void* data, uint64_t count);
+/* Load the object scene like igx_scene_load_string loads a JSON scene.
+ * Returns NULL and fills err on unsupported or malformed objects. */
+igx_scene* igx_scene_from_objects(const igx_objscene* scene, char* err, size_t err_len);
+
 /* ---- the reference's SceneDatabase as plain C (Device::assignScene seam) --
  * IG::Runtime hands its device a `SceneDatabase*` (Runtime.cpp:477-485,
  * Device.h:25-30; table/SceneDatabase.h:13-20).  A binding passes views of the

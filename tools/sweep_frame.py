@@ -43,5 +43,5 @@ for o in opts:
     print(json.dumps({"opt": o, "ms_frame": round(dt * 1e3, 2), "Mrays/s": round(rays / dt / 1e6, 1),
                       "ext": round(s["ms_extend"], 2), "tr": round(s["ms_trace"], 2), "sh": round(s["ms_shadow"], 2),
                       "fin": round(s["ms_finish"], 2), "gen": round(s["ms_generate"], 2), "res": round(s["ms_resolve"], 2), "tail_rays": s["tail_bounce_rays"] + s["tail_shadow_rays"],
-                      "launches_ext": s["launches_extend"], "fb_md5": md5}), flush=True)
+                      "launches_ext": s["launches_extend"], "treelet": s.get("treelet_nodes"), "fb_md5": md5}), flush=True)
 dev.close()
