@@ -129,6 +129,7 @@ struct FrameArgs {
     int gen_n;           // > 0: this k_extend launch is bounce 0 and generates its n camera paths itself
     int classify;        // surviving paths' stream class (see wave_append_paths): 0 all A, 1 B = inside a dielectric (eta != 1), 2 B = after a specular event
     int dynamic;         // k_extend: waves take 64-path groups from per-shard work counters (KernelCounters::work)
+    int shadow_classes;  // shadow rays crossing an enclosing entity's box go to the back of their shard (shadow_class_b)
 };
 
 // path slot -> (local pixel, sample, iteration): slots run over the chunk's
@@ -224,19 +225,20 @@ __device__ __forceinline__ int stream_index(int s, int pos, int a, int shard_cap
 // shadow rays: one returning 64-bit atomic per stream (a/b counts in the two
 // words), lanes 0 and 1 issue both in one instruction; positions inside the
 // wave by ballot prefix.  Needs every lane of the wave active.
-__device__ __forceinline__ void wave_append_paths(bool alive, bool cls_b, bool shadow, int* cp, int* cs, int shard_cap,
-                                                  int& dst, int& sdst) {
+__device__ __forceinline__ void wave_append_paths(bool alive, bool cls_b, bool shadow, bool sh_b, int* cp, int* cs,
+                                                  int shard_cap, int sh_cap, int& dst, int& sdst) {
     const int lane = lane_id();
-    const uint64_t ma = __ballot(alive && !cls_b), mb = __ballot(alive && cls_b), ms = __ballot(shadow);
+    const uint64_t ma = __ballot(alive && !cls_b), mb = __ballot(alive && cls_b);
+    const uint64_t sa = __ballot(shadow && !sh_b), sb = __ballot(shadow && sh_b);
     const uint64_t below = (1ull << lane) - 1ull;
     const unsigned long long want = lane == 0 ? ((unsigned long long)__popcll(ma) | ((unsigned long long)__popcll(mb) << 32))
-                                              : (unsigned long long)__popcll(ms);
+                                              : ((unsigned long long)__popcll(sa) | ((unsigned long long)__popcll(sb) << 32));
     unsigned long long r = 0;
     if (lane < 2 && want != 0) r = atomicAdd(reinterpret_cast<unsigned long long*>(lane == 0 ? cp : cs), want);
     const int lo = (int)(uint32_t)r, hi = (int)(uint32_t)(r >> 32);
-    const int a0 = __shfl(lo, 0), b0 = __shfl(hi, 0), s0 = __shfl(lo, 1);
+    const int a0 = __shfl(lo, 0), b0 = __shfl(hi, 0), s0 = __shfl(lo, 1), t0 = __shfl(hi, 1);
     dst = cls_b ? shard_cap - 1 - (b0 + __popcll(mb & below)) : a0 + __popcll(ma & below);
-    sdst = s0 + __popcll(ms & below);
+    sdst = sh_b ? sh_cap - 1 - (t0 + __popcll(sb & below)) : s0 + __popcll(sa & below);
 }
 
 
@@ -337,8 +339,13 @@ struct ShadowRec {
 // dielectric or its next ray crosses the world box of an enclosing entity
 // (the paths whose traversal enters a large BLAS and that will likely shade
 // a dielectric), A = the rest (wall-to-wall paths: short walks, diffuse)
+// (the class only orders the stream, so the slab test may use the hardware
+// reciprocal, v_rcp_f32, instead of three IEEE divisions)
+__device__ __forceinline__ f3 fast_rcp3(f3 d) {
+    return mk(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
+}
 __device__ __forceinline__ bool crosses_enclosing_box(const SceneView& sv, f3 o, f3 d) {
-    const f3 id = mk(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
+    const f3 id = fast_rcp3(d);
     bool hit = false;
     for (int k = 0; k < sv.num_enc && !hit; ++k) {
         const float4 lo = sv.enc_box[2 * k], hi = sv.enc_box[2 * k + 1];
@@ -348,6 +355,24 @@ __device__ __forceinline__ bool crosses_enclosing_box(const SceneView& sv, f3 o,
         const float en = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
         const float ex = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
         hit = en <= ex && ex >= 0.0f;
+    }
+    return hit;
+}
+// shadow-ray class (FrameArgs::classify 3): B = the segment [0, tmax] of the
+// shadow ray crosses an enclosing entity's box (its any-hit walk enters that
+// BLAS), A = the rest; stored like the path classes (shard front / back)
+__device__ __forceinline__ bool shadow_class_b(int enabled, const SceneView& sv, f3 o, f3 d, float tmax) {
+    if (!enabled) return false;
+    const f3 id = fast_rcp3(d);
+    bool hit = false;
+    for (int k = 0; k < sv.num_enc && !hit; ++k) {
+        const float4 lo = sv.enc_box[2 * k], hi = sv.enc_box[2 * k + 1];
+        const float ax = (lo.x - o.x) * id.x, bx = (hi.x - o.x) * id.x;
+        const float ay = (lo.y - o.y) * id.y, by = (hi.y - o.y) * id.y;
+        const float az = (lo.z - o.z) * id.z, bz = (hi.z - o.z) * id.z;
+        const float en = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+        const float ex = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+        hit = en <= ex && ex >= 0.0f && en <= tmax;
     }
     return hit;
 }
@@ -764,7 +789,9 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
 #endif
         }
         int dst, sdst;
-        wave_append_paths(alive, path_class_b(fa.classify, sv, ps), has_shadow, c_out, c_sh, out.shard_cap, dst, sdst);
+        wave_append_paths(alive, path_class_b(fa.classify, sv, ps), has_shadow,
+                          has_shadow && shadow_class_b(fa.shadow_classes, sv, sr.o, sr.d, sr.tmax), c_out, c_sh, out.shard_cap,
+                          sh.shard_cap, dst, sdst);
         if (alive) store_path(out, s * out.shard_cap + dst, ps);
         if (has_shadow) {
             const int e = s * sh.shard_cap + sdst;
@@ -853,7 +880,9 @@ __global__ void __launch_bounds__(BLOCK) k_shade(FrameArgs fa, SceneView sv, Pat
             }
         }
         int dst, sdst;
-        wave_append_paths(alive, path_class_b(fa.classify, sv, ps), has_shadow, c_out, c_sh, out.shard_cap, dst, sdst);
+        wave_append_paths(alive, path_class_b(fa.classify, sv, ps), has_shadow,
+                          has_shadow && shadow_class_b(fa.shadow_classes, sv, sr.o, sr.d, sr.tmax), c_out, c_sh, out.shard_cap,
+                          sh.shard_cap, dst, sdst);
         if (alive) store_path(out, w.s * out.shard_cap + dst, ps);
         if (has_shadow) {
             const int e = w.s * sh.shard_cap + sdst;
@@ -941,22 +970,22 @@ __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, f
     // groups of 64 shadow rays: grid-stride over the wave's own shard, or
     // (work != nullptr) handed out by take_group
     int s = w.s;
-    int ns = uniform_load(cnt + s * CSTRIDE);
+    ShardCount sc = shard_count(cnt, s); // two shadow classes (wave_append_paths)
     uint64_t done = 0;
     for (int p0 = w.k * 64;; p0 += w.K * 64) {
         if (work) {
-            p0 = take_group(work, s, done, ns, [&](int sh_) {
-                ns = uniform_load(cnt + sh_ * CSTRIDE);
-                return ns;
+            p0 = take_group(work, s, done, sc.n, [&](int sh_) {
+                sc = shard_count(cnt, sh_);
+                return sc.n;
             });
             if (p0 < 0) break;
             p0 *= 64;
-        } else if (p0 >= ns) {
+        } else if (p0 >= sc.n) {
             break;
         }
         const int pos = p0 + lane_id();
-        if (pos >= ns) continue;
-        const int i = s * sh.shard_cap + pos;
+        if (pos >= sc.n) continue;
+        const int i = stream_index(s, pos, sc.a, sh.shard_cap);
         float4 s0 = sh.s0[i], s1 = sh.s1[i];
         float tmax = s1.w;
         int e, p;
@@ -1125,7 +1154,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? REFILL_WAVES_LDS : (variant_ifif(
     if (row_total(cnt) == 0) return;
     const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : stage_treelet<BLOCK>(gsv, lds_scene);
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
-    GroupSeq<false> seq;
+    GroupSeq<true> seq; // two shadow classes (wave_append_paths)
     seq.init(cnt, work, sh.shard_cap, wave_work());
     refill_loop<true, STATS, V>(
         sv, ts, seq, refill_min,
@@ -1327,7 +1356,10 @@ struct igx_device {
     // register-bound occupancy), recomputed when the scene or option changes.
     // Option "treelet": -1 auto, 0 off, n > 0 at most n nodes
     int64_t treelet_opt = -1;
-    int treelet_kernels = 7; // option "treelet_kernels": bit 1 k_extend, 2 k_trace_refill, 4 k_shadow / k_shadow_refill
+    // option "treelet_kernels": bit 1 k_extend, 2 k_trace_refill, 4 k_shadow / k_shadow_refill.  Default 5:
+    // primitives 8.89 -> 8.37, S-deep 48.2 -> 45.8, soup-1M 187.9 -> 184.9 ms per frame; the persistent-lane
+    // trace kernel loses with one (soup-1M trace 100.9 -> 102.6 ms), its top nodes stay L2 hits anyway
+    int treelet_kernels = 5;
     bool tree_dirty = true;
     int tree_ext = 0, tree_trace = 0, tree_shadow = 0, tree_fin = 0;
     int64_t tail_opt = -1;   // paths at or below which k_finish takes over (-1 = auto)
@@ -1350,6 +1382,10 @@ struct igx_device {
     // (diamond frame 132.5 -> 119.3 ms, k_extend 1770 -> 1591 us per launch,
     // bit-identical)
     int classify_opt = 3;
+    // option "shadow_classes": shadow rays whose segment crosses an enclosing
+    // entity's box apart from the rest (shadow_class_b), 0/1: diamond shadow
+    // time 26.9 -> 21.7 ms per frame, frame 121.1 -> 118.4 ms, bit-identical
+    int shadow_classes_opt = 1;
     // option "dynamic" (DYN_* bits): DYN_EXTEND = k_extend waves take their
     // groups of 64 paths from per-shard counters (take_group) instead of a
     // fixed grid stride: diamond frame 142.4 -> 134.3 ms, materials 66.5 ->
@@ -1988,6 +2024,7 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
         dev->tree_dirty = true;
     }
     else if (k == "treelet_kernels") dev->treelet_kernels = (int)(value & 7);
+    else if (k == "shadow_classes") dev->shadow_classes_opt = value != 0;
     else if (k == "slot_budget_mb") {
         if (value < 0) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "slot_budget_mb must be >= 0 (0 = auto)");
         dev->slot_budget_mb = value;
@@ -2734,6 +2771,7 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
     fa.seed = p->seed;
     fa.inv_spi = 1.0f / (float)p->spi;
     fa.classify = dev->classify_opt;
+    fa.shadow_classes = dev->shadow_classes_opt;
     fa.dynamic = dev->dynamic_opt & DYN_EXTEND;
     long long local_pixels;
     if (list_mode) {

@@ -492,6 +492,64 @@ def test_full_size_window_parity(device, diamond_path):
     assert np.isfinite(g).all() and (g >= 0).all()
 
 
+def test_config2_diamond_256spp_band_matches_cpu_device(device, diamond_path):
+    """BASELINE config 2 at its stated size: diamond 1000x1000, 256 spp = 32
+    iterations x spi 8 (the bench's frame), rendered whole on the GPU in one
+    render_iterations call (the bench's chunking); the oracle accumulates the
+    same 32 iterations over a 48-row band.  Diamond contract of SURVEY.md §8c."""
+    sc = ignis_amd.Scene.from_file(diamond_path)
+    W = H = 1000
+    device.upload(sc)
+    device.set_option("capacity", 0)
+    device.clear()
+    p = ignis_amd.RenderParams()
+    p.width, p.height, p.spi = W, H, 8
+    device.render_iterations(p, 32)
+    g, it = device.framebuffer(W * H * 3)
+    assert it == 32
+    y0, y1 = 476, 524
+    orc = O.OracleScene(sc)
+    o = np.zeros(W * H * 3, np.float32)
+    for k in range(32):
+        orc.render(W, H, 8, iteration=k, threads=16, window=(0, y0, W, y1), fb=o)
+    gb = g.reshape(H, W, 3)[y0:y1] / 32
+    ob = o.reshape(H, W, 3)[y0:y1] / 32
+    assert rel_mse(gb, ob) <= 5e-3
+    close = np.abs(gb - ob) <= 1e-2 * np.maximum(np.abs(ob), 1e-2)
+    assert close.mean() >= 0.99, close.mean()
+    assert np.isfinite(g).all() and (g >= 0).all()
+
+
+def test_config3_primitives_256spp_matches_cpu_device(device, primitives_path):
+    """BASELINE config 3 at its stated size: primitives.json (mixed BSDFs),
+    1000x1000, 256 spp = 32 iterations x spi 8, whole frame on the GPU and on
+    the oracle (max_depth 2 keeps the oracle cheap); primitives contract
+    (RelSE <= 1e-3, >= 99 % of pixels within 1e-3 relative) and ray counts."""
+    sc = ignis_amd.Scene.from_file(primitives_path)
+    W = H = 1000
+    device.upload(sc)
+    device.set_option("capacity", 0)
+    device.clear()
+    device.reset_stats()
+    p = ignis_amd.RenderParams()
+    p.width, p.height, p.spi = W, H, 8
+    device.render_iterations(p, 32)
+    g, it = device.framebuffer(W * H * 3)
+    assert it == 32
+    st = device.stats()
+    orc = O.OracleScene(sc)
+    o = np.zeros(W * H * 3, np.float32)
+    rays = 0
+    for k in range(32):
+        _, ost = orc.render(W, H, 8, iteration=k, threads=16, fb=o)
+        rays += ost["camera_rays"] + ost["bounce_rays"] + ost["shadow_rays"]
+    assert rel_mse(g / 32, o / 32) <= 1e-3
+    close = np.abs(g - o) <= 1e-3 * np.maximum(np.abs(o), 1e-3)
+    assert close.mean() >= 0.99, close.mean()
+    gpu_rays = st["camera_rays"] + st["bounce_rays"] + st["shadow_rays"]
+    assert abs(gpu_rays - rays) / rays < 1e-3, (gpu_rays, rays)
+
+
 def test_config1_diamond_64spp_matches_cpu_device(device, diamond_path):
     """BASELINE config 1 (diamond, 1000x1000, 64 spp = 8 iterations x spi 8,
     seed 0) rendered whole by the HIP device and by the oracle (the restated
