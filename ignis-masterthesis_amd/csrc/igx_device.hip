@@ -953,6 +953,130 @@ __global__ void __launch_bounds__(BLOCK) k_finish(FrameArgs fa, SceneView gsv, P
 }
 
 // ---------------------------------------------------------------------------
+// tail kernel with lane pairs (global-table scenes): on the soups a tail
+// path's bounce is two dependent walks through HBM-resident tables (closest
+// hit, then the NEE shadow ray), and the longest path sets the tail's length.
+// Both rays of a bounce start at the same shading point and do not depend on
+// each other, so here the even lane of a pair carries the path and traces its
+// closest hits while the odd lane traces the path's shadow rays: the two walks
+// overlap, and both lanes step through the same instructions (per-lane any-hit
+// flag, trav_step_core).  Radiance is added in the wavefront's order (emission
+// of bounce k, shadow ray of bounce k, emission of bounce k + 1), so the image
+// is bit-identical to k_finish.
+// ---------------------------------------------------------------------------
+template <int V0, bool STATS>
+__global__ void __launch_bounds__(BLOCK) k_finish_pairs(FrameArgs fa, SceneView gsv, PathBuf in, float4* L, const int* cnt,
+                                                        int tail_threshold, unsigned long long* stats,
+                                                        unsigned long long* tail_counts) {
+    constexpr int V = kernel_variant(V0, false);
+    __shared__ int stack_mem[LDS_STACK * BLOCK];
+    extern __shared__ float4 lds_scene[];
+    const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
+    const int n = row_total(cnt);
+    if (n > tail_threshold || n == 0) return; // the wavefront kernels own this bounce
+    const SceneView sv = stage_treelet<BLOCK>(gsv, lds_scene);
+    TraceStats st{0, 0, 0, 0, 0, 0, 0};
+    TraceStats sst{0, 0, 0, 0, 0, 0, 0};
+    unsigned long long bounces = 0, shadows = 0;
+    const WaveWork w = wave_work();
+    const ShardCount sc = shard_count(cnt, w.s);
+    const int ns = sc.n;
+    const int lane = lane_id(), partner = lane ^ 1;
+    const bool path_lane = (lane & 1) == 0;
+    for (int pos0 = w.k * 32; pos0 < ns; pos0 += w.K * 32) { // 32 paths per wave and pass
+        const int pos = pos0 + (lane >> 1);
+        PathState ps;
+        ps.depth = 0;
+        if (path_lane && pos < ns) ps = load_path(in, stream_index(w.s, pos, sc.a, in.shard_cap));
+        bool tracing = path_lane && pos < ns && ps.depth > 0; // path lane: its current ray needs a closest hit
+        bool sh_trace = false;                                  // odd lane: a shadow ray to trace
+        bool had_shadow = false;                                // path lane: its last shadow ray is out
+        ShadowRec sr;
+        f3 so = mk(0, 0, 0), sd = mk(0, 0, 1);
+        float stmax = 0;
+        int hit_ent = -1, hit_prim = -1;
+        float hu = 0, hv = 0, htmax = 0;
+        for (;;) {
+            // ---- both walks of the pair ----
+            Trav t;
+            bool busy = false, enclosed = false;
+            TraceStats& tst = path_lane ? st : sst;
+            if (tracing) {
+                float tmin, tmax;
+                uint32_t rflags;
+                ray_extent(fa, sv, ps.depth, ps.slot, tmin, tmax, rflags);
+                enclosed = ps.inside >= 0 && trav_init_enclosed<STATS>(sv, t, ps.inside, ps.o, ps.d, tmin, tmax, rflags, ts, tst);
+                if (!enclosed) trav_init(sv, t, ps.o, ps.d, tmin, tmax, rflags, ts);
+                busy = true;
+            } else if (sh_trace) {
+                trav_init(sv, t, so, sd, 0.001f, stmax, RAY_SHADOW, ts);
+                busy = true;
+            }
+            for (;;) {
+                while (__ballot(busy)) {
+                    if (busy && trav_step_core<2, STATS, V>(sv, t, ts, tst, !path_lane)) busy = false;
+                }
+                // an enclosed walk that found nothing: the full traversal from the TLAS root
+                if (!(tracing && enclosed && !t.found)) break;
+                float tmin, tmax;
+                uint32_t rflags;
+                ray_extent(fa, sv, ps.depth, ps.slot, tmin, tmax, rflags);
+                trav_init(sv, t, ps.o, ps.d, tmin, tmax, rflags, ts);
+                enclosed = false;
+                busy = true;
+            }
+            if (tracing) {
+                htmax = t.tmax;
+                hit_ent = t.hit_ent;
+                hit_prim = t.hit_prim;
+                hu = t.hu;
+                hv = t.hv;
+                if (STATS && hit_ent >= 0) st.hits++;
+            }
+            // ---- the shadow ray's verdict back to its path lane ----
+            const bool occluded = __shfl(sh_trace && t.found, partner) != 0;
+            if (path_lane && had_shadow && !occluded) add_radiance(L, ps.slot, sr.color);
+            if (!__ballot(tracing)) break;
+            // ---- shade the hits (path lanes) ----
+            bool cont = false, has_shadow = false;
+            if (tracing) {
+                f3 Lacc;
+                bool has_l;
+                cont = shade_step<variant_full(V)>(fa, sv, ps, hit_ent, hit_prim, htmax, hu, hv, Lacc, has_l, has_shadow, sr);
+                if (has_l) add_radiance(L, ps.slot, Lacc);
+                if (has_shadow) ++shadows;
+                if (cont) ++bounces;
+            }
+            tracing = cont;
+            had_shadow = has_shadow;
+            // ---- hand the shadow ray to the odd lane ----
+            const float ox = __shfl(sr.o.x, partner), oy = __shfl(sr.o.y, partner), oz = __shfl(sr.o.z, partner);
+            const float dx = __shfl(sr.d.x, partner), dy = __shfl(sr.d.y, partner), dz = __shfl(sr.d.z, partner);
+            const float tm = __shfl(sr.tmax, partner);
+            const bool ph = __shfl(has_shadow, partner) != 0;
+            if (!path_lane) {
+                sh_trace = ph;
+                so = mk(ox, oy, oz);
+                sd = mk(dx, dy, dz);
+                stmax = tm;
+            }
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        bounces += __shfl_down(bounces, off);
+        shadows += __shfl_down(shadows, off);
+    }
+    if (lane_id() == 0 && (bounces | shadows)) {
+        atomicAdd(&tail_counts[0], bounces);
+        atomicAdd(&tail_counts[1], shadows);
+    }
+    if (STATS) {
+        flush_stats<STATS>(st, stats, 0, true);
+        flush_stats<STATS>(sst, stats, 4, false);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // shadow: any-hit traversal; on miss add the NEE contribution
 // (gpu_traverse_secondary, mapping_gpu.art:70-112; on_shadow_miss, pathtracer.art:202-209)
 // ---------------------------------------------------------------------------
@@ -1355,6 +1479,7 @@ struct igx_device {
     // kernel (the largest prefix of the hot order that keeps the kernel's
     // register-bound occupancy), recomputed when the scene or option changes.
     // Option "treelet": -1 auto, 0 off, n > 0 at most n nodes
+    int tail_pairs_opt = -1;  // k_finish_pairs on global-table scenes (-1 auto = on, 0 off, 1 on)
     int64_t treelet_opt = -1;
     // option "treelet_kernels": bit 1 k_extend, 2 k_trace_refill, 4 k_shadow / k_shadow_refill.  Default 5:
     // primitives 8.89 -> 8.37, S-deep 48.2 -> 45.8, soup-1M 187.9 -> 184.9 ms per frame; the persistent-lane
@@ -1579,6 +1704,10 @@ int grid_for(igx_device* dev, long long items, int blocks_per_cu) {
 //    faster (no hit records): S-deep (18 MB of tables) 49.4 -> 46.9 ms per
 //    8-iteration frame fused, soup-1M (104 MB) 382 split vs 451 fused.
 constexpr size_t SPLIT_TABLE_BYTES = 64u << 20;
+// tail kernel with lane pairs (k_finish_pairs) on global-table scenes; option "tail_pairs" (-1 auto, 0, 1)
+inline bool use_tail_pairs(const igx_device* dev) {
+    return dev->lds_scene_bytes == 0 && (dev->tail_pairs_opt < 0 ? true : dev->tail_pairs_opt != 0);
+}
 // dynamic LDS of a global-table kernel that stages `nodes` treelet nodes
 inline size_t tree_bytes(const igx_device* dev, int nodes) { return (size_t)nodes * node_f4(dev->bvh_width) * 16; }
 inline int refill_min(const igx_device* dev) { return dev->refill_opt >= 0 ? dev->refill_opt : 16; }
@@ -1715,6 +1844,12 @@ void launch_finish(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, cons
 #undef L_FINL
         return;
     }
+    if (use_tail_pairs(dev)) {
+#define L_FINP(S) hipLaunchKernelGGL((k_finish_pairs<S, STATS>), dim3(grid), dim3(BLOCK), tree_bytes(dev, tsv.tree_n), dev->tail_stream, fa, tsv, in, s.L, cnt, tail, dev->dstats, dev->tail_counts)
+        IGX_DISPATCH_VARIANT8(dev->variant, L_FINP);
+#undef L_FINP
+        return;
+    }
 #define L_FIN(S) hipLaunchKernelGGL((k_finish<S, STATS, false>), dim3(grid), dim3(BLOCK), tree_bytes(dev, tsv.tree_n), dev->tail_stream, fa, tsv, in, s.L, cnt, tail, dev->dstats, dev->tail_counts)
     IGX_DISPATCH_VARIANT8(dev->variant, L_FIN);
 #undef L_FIN
@@ -1759,7 +1894,21 @@ int shadow_blocks_per_cu(int v, size_t lds, bool refill, size_t tree) {
     IGX_RESIDENT(k_shadow, STATS);
 }
 template <bool STATS>
-int finish_blocks_per_cu(int v, size_t lds, size_t tree) { IGX_RESIDENT8(k_finish, STATS); }
+int finish_blocks_per_cu(int v, size_t lds, size_t tree, bool pairs) {
+    if (!lds && pairs) {
+        switch (v) {
+        case 0: return resident_blocks(k_finish_pairs<0, STATS>, tree);
+        case 1: return resident_blocks(k_finish_pairs<1, STATS>, tree);
+        case 2: return resident_blocks(k_finish_pairs<2, STATS>, tree);
+        case 3: return resident_blocks(k_finish_pairs<3, STATS>, tree);
+        case 4: return resident_blocks(k_finish_pairs<4, STATS>, tree);
+        case 5: return resident_blocks(k_finish_pairs<5, STATS>, tree);
+        case 6: return resident_blocks(k_finish_pairs<6, STATS>, tree);
+        default: return resident_blocks(k_finish_pairs<7, STATS>, tree);
+        }
+    }
+    IGX_RESIDENT8(k_finish, STATS);
+}
 template <bool STATS>
 int trace_blocks_per_cu(int v, int waves, size_t lds, bool refill, size_t tree) {
     if (refill) IGX_RESIDENT_G(k_trace_refill);
@@ -1790,7 +1939,7 @@ int shade_blocks_per_cu(bool full) { return full ? resident_blocks(k_shade<true>
     X int extend_blocks_per_cu<S>(int, size_t, size_t);
 #define IGX_FINISH_HELPERS(X, S)                                                                                     \
     X void launch_finish<S>(igx_device*, Slot&, int, const FrameArgs&, const PathBuf&, const int*, int);             \
-    X int finish_blocks_per_cu<S>(int, size_t, size_t);
+    X int finish_blocks_per_cu<S>(int, size_t, size_t, bool);
 #define IGX_TRACE_HELPERS(X, S)                                                                                      \
     X void launch_trace<S>(igx_device*, Slot&, int, const FrameArgs&, const PathBuf&, const int*, int, int*);              \
     X void launch_shadow<S>(igx_device*, Slot&, int, const int*, int*);                                                    \
@@ -2025,6 +2174,10 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     }
     else if (k == "treelet_kernels") dev->treelet_kernels = (int)(value & 7);
     else if (k == "shadow_classes") dev->shadow_classes_opt = value != 0;
+    else if (k == "tail_pairs") {
+        if (value < -1 || value > 1) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "tail_pairs must be -1 (auto), 0 or 1");
+        dev->tail_pairs_opt = (int)value;
+    }
     else if (k == "slot_budget_mb") {
         if (value < 0) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "slot_budget_mb must be >= 0 (0 = auto)");
         dev->slot_budget_mb = value;
@@ -2447,6 +2600,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
                         overlap = overlap && q.bbox_min[a] <= en.bbox_max[a] + margin && en.bbox_min[a] <= q.bbox_max[a] + margin;
                     apart = !overlap;
                 }
+                static_assert(MAX_ENCLOSING <= MAX_ENC_BOXES, "enclosing boxes are staged in LDS (stage_enc_boxes)");
                 if (apart && (int)enc_tab.size() < MAX_ENCLOSING) {
                     ent_enc[e] = (int)enc_tab.size();
                     enc_tab.push_back(make_int2((int)e, (int)slot));
@@ -2841,8 +2995,9 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
     const bool split = use_split(dev);
     const int sh_bpc = inst ? shadow_blocks_per_cu<true>(sd, dev->lds_scene_bytes, refill, tree_bytes(dev, dev->tree_shadow))
                             : shadow_blocks_per_cu<false>(sd, dev->lds_scene_bytes, refill, tree_bytes(dev, dev->tree_shadow));
-    const int fin_bpc = inst ? finish_blocks_per_cu<true>(sd, ldsb, tree_bytes(dev, dev->tree_fin))
-                             : finish_blocks_per_cu<false>(sd, ldsb, tree_bytes(dev, dev->tree_fin));
+    const bool pairs = use_tail_pairs(dev);
+    const int fin_bpc = inst ? finish_blocks_per_cu<true>(sd, ldsb, tree_bytes(dev, dev->tree_fin), pairs)
+                             : finish_blocks_per_cu<false>(sd, ldsb, tree_bytes(dev, dev->tree_fin), pairs);
 
     for (int it0 = 0; it0 < count; it0 += iters_per_chunk)
     for (long long px0 = 0; px0 < local_pixels; px0 += chunk_pixels_max) {
@@ -2874,7 +3029,8 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
         // lanes loop over several long paths each and it outlasts the
         // overlapping chunk (diamond 32M-path chunks: 500K -> 196K tail paths,
         // 204.6 -> 195.0 ms per frame, tools/sweep_frame.py)
-        const long long fin_lanes = (long long)fin_bpc * dev->num_cus * BLOCK;
+        // paths one pass of the tail kernel holds (lane pairs: one path per two lanes)
+        const long long fin_lanes = (long long)fin_bpc * dev->num_cus * BLOCK / (pairs ? 2 : 1);
         const bool last_chunk = it0 + iters_per_chunk >= count && px0 + chunk_pixels_max >= local_pixels;
         const int64_t topt = last_chunk && dev->tail_last_opt >= 0 ? dev->tail_last_opt : dev->tail_opt;
         int tail = topt >= 0 ? (int)std::min<int64_t>(topt, 1 << 30)
@@ -2901,7 +3057,7 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
         const int shade_grid = grid_for(dev, n, shade_bpc);
         S.split = split;
         const int sh_grid = grid_for(dev, n, sh_bpc);
-        const int fin_grid = grid_for(dev, std::min<long long>(n, tail), fin_bpc);
+        const int fin_grid = grid_for(dev, std::min<long long>(n, tail) * (pairs ? 2 : 1), fin_bpc);
         // Wavefront bounces on the main stream.  The host learns counts two
         // bounces late (async copies, no per-bounce sync); the device gates
         // k_extend off once the count is <= tail, and the host then queues

@@ -53,6 +53,17 @@ struct SceneView {
 // into LDS, laid out back to back, and point a block-local view at them: the
 // node loop then reads LDS (~50-cycle ds_read) instead of the vector-memory
 // path, which the divergent node fetches otherwise keep busy.
+// The enclosing entities' world boxes (path / shadow-ray classes, read by
+// every lane at every append): a small LDS copy, so the class test does not
+// wait on dependent global loads (they cost k_extend ~10 % of its wave time).
+constexpr int MAX_ENC_BOXES = 32;
+template <int BLOCK_>
+__device__ __forceinline__ const float4* stage_enc_boxes(const SceneView& sv) {
+    __shared__ float4 enc_box_lds[2 * MAX_ENC_BOXES];
+    for (int k = threadIdx.x; k < 2 * sv.num_enc; k += BLOCK_) enc_box_lds[k] = sv.enc_box[k];
+    return enc_box_lds;
+}
+
 template <int BLOCK_>
 __device__ __forceinline__ SceneView stage_scene_lds(const SceneView& sv, float4* lds) {
     const int nf = sv.node_f4, sh = nf == 8 ? 3 : 2, ns = nf + lds_node_pad(); // node stride in LDS (float4)
@@ -60,8 +71,10 @@ __device__ __forceinline__ SceneView stage_scene_lds(const SceneView& sv, float4
     for (int k = threadIdx.x; k < sv.num_nodes * nf; k += BLOCK_) lds[(k >> sh) * ns + (k & (nf - 1))] = sv.nodes[k];
     for (int k = threadIdx.x; k < i4; k += BLOCK_) lds[n4 + k] = sv.inst[k];
     for (int k = threadIdx.x; k < t3; k += BLOCK_) lds[n4 + i4 + k] = sv.tris[k];
+    const float4* eb = stage_enc_boxes<BLOCK_>(sv);
     __syncthreads();
     SceneView l = sv;
+    l.enc_box = eb;
     l.nodes = lds;
     l.inst = lds + n4;
     l.tris = lds + n4 + i4;
@@ -77,9 +90,10 @@ template <int BLOCK_>
 __device__ __forceinline__ SceneView stage_treelet(const SceneView& sv, float4* lds) {
     SceneView l = sv;
     l.tree = lds;
-    if (sv.tree_n > 0) {
+    if (sv.tree_n > 0 || sv.num_enc > 0) {
         const int n4 = sv.tree_n * sv.node_f4;
         for (int k = threadIdx.x; k < n4; k += BLOCK_) lds[k] = sv.nodes[k];
+        l.enc_box = stage_enc_boxes<BLOCK_>(sv);
         __syncthreads();
     }
     return l;
@@ -399,9 +413,12 @@ __device__ __forceinline__ void tri_test(const SceneView& sv, Trav& t, int slot,
 
 // One traversal step (while-while): inner nodes down to a leaf, then that
 // leaf or the BLAS return marker.  Returns true once the ray is finished
-// (stack exhausted, or the first hit for ANY).
-template <bool ANY, bool STATS, int V>
-__device__ __forceinline__ bool trav_step(const SceneView& sv, Trav& t, const TStack& ts, TraceStats& st) {
+// (stack exhausted, or the first hit for any-hit rays).  ANYM: 0 closest
+// hit, 1 any hit, 2 per lane (`any_rt`), so that closest-hit and any-hit rays
+// of one wave step through the same instructions (k_finish_pairs).
+template <int ANYM, bool STATS, int V>
+__device__ __forceinline__ bool trav_step_core(const SceneView& sv, Trav& t, const TStack& ts, TraceStats& st, bool any_rt) {
+    const bool ANY = ANYM == 2 ? any_rt : ANYM == 1;
     int node = t.node;
     int sp = t.sp;
     constexpr bool SPILL = variant_spill(V);
@@ -466,6 +483,11 @@ __device__ __forceinline__ bool trav_step(const SceneView& sv, Trav& t, const TS
     return false;
 }
 
+template <bool ANY, bool STATS, int V>
+__device__ __forceinline__ bool trav_step(const SceneView& sv, Trav& t, const TStack& ts, TraceStats& st) {
+    return trav_step_core<ANY ? 1 : 0, STATS, V>(sv, t, ts, st, false);
+}
+
 // Whole-ray traversal (used by the tail kernel and the hit-level harness).
 template <bool ANY, bool STATS, int V>
 __device__ __forceinline__ bool trace_ray(const SceneView& sv, f3 o, f3 d, float tmin, float& tmax, uint32_t rflags,
@@ -493,15 +515,15 @@ __device__ __forceinline__ bool trace_ray(const SceneView& sv, f3 o, f3 d, float
 // (instance_test's transform).  Returns false (nothing written) when the
 // entity is not visible to the ray or its BLAS yields no hit; the caller then
 // traces the ray from the TLAS root.
-template <bool STATS, int V>
-__device__ __forceinline__ bool trace_enclosed(const SceneView& sv, int enc, f3 o, f3 d, float tmin, float& tmax,
-                                               uint32_t rflags, const TStack& ts, int& hit_ent, int& hit_prim, float& hu,
-                                               float& hv, TraceStats& st) {
+// Traversal state of trace_enclosed's BLAS-only walk; false when the entity
+// is not visible to the ray (nothing to walk).
+template <bool STATS>
+__device__ __forceinline__ bool trav_init_enclosed(const SceneView& sv, Trav& t, int enc, f3 o, f3 d, float tmin, float tmax,
+                                                   uint32_t rflags, const TStack& ts, TraceStats& st) {
     const int slot = sv.enc[enc].y;
     const float4* ip = sv.inst + 4 * slot;
     const int4 info = *reinterpret_cast<const int4*>(ip + 3);
     if ((rflags & RAY_TYPE_MASK) != ((rflags & (uint32_t)info.w) & RAY_TYPE_MASK)) return false;
-    Trav t;
     t.o = o;
     t.d = d;
     const float4 m0 = ip[0], m1 = ip[1], m2 = ip[2];
@@ -524,6 +546,14 @@ __device__ __forceinline__ bool trace_enclosed(const SceneView& sv, int enc, f3 
     t.sp = 1;
     t.node = info.z; // BLAS root (or its only leaf)
     if (STATS) { st.leaves++; st.blas++; }
+    return true;
+}
+template <bool STATS, int V>
+__device__ __forceinline__ bool trace_enclosed(const SceneView& sv, int enc, f3 o, f3 d, float tmin, float& tmax,
+                                               uint32_t rflags, const TStack& ts, int& hit_ent, int& hit_prim, float& hu,
+                                               float& hv, TraceStats& st) {
+    Trav t;
+    if (!trav_init_enclosed<STATS>(sv, t, enc, o, d, tmin, tmax, rflags, ts, st)) return false;
     while (!trav_step<false, STATS, V>(sv, t, ts, st)) {
     }
     if (!t.found) return false;
