@@ -584,8 +584,7 @@ __device__ __forceinline__ bool extend_step(const FrameArgs& fa, const SceneView
     float hu = 0, hv = 0;
     // a ray inside an enclosing entity hits it first: its BLAS alone decides
     // (the full traversal from the TLAS root only when that finds nothing)
-    if (ps.inside < 0 || !trace_enclosed<STATS, V>(sv, ps.inside, ps.o, ps.d, tmin, tmax, rflags, ts, hit_ent, hit_prim, hu, hv, st))
-        trace_ray<false, STATS, V>(sv, ps.o, ps.d, tmin, tmax, rflags, ts, hit_ent, hit_prim, hu, hv, st);
+    trace_path_ray<STATS, V>(sv, ps.inside, ps.o, ps.d, tmin, tmax, rflags, ts, hit_ent, hit_prim, hu, hv, st);
     if (STATS && hit_ent >= 0) st.hits++;
     return shade_step<variant_full(V)>(fa, sv, ps, hit_ent, hit_prim, tmax, hu, hv, Lacc, has_l, has_shadow, sr);
 }
@@ -761,9 +760,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
 #endif
             if (act) {
                 ray_extent(fa, sv, ps.depth, ps.slot, tmin, tmax, rflags);
-                if (ps.inside < 0 ||
-                    !trace_enclosed<STATS, V>(sv, ps.inside, ps.o, ps.d, tmin, tmax, rflags, ts, hit_ent, hit_prim, hu, hv, st))
-                    trace_ray<false, STATS, V>(sv, ps.o, ps.d, tmin, tmax, rflags, ts, hit_ent, hit_prim, hu, hv, st);
+                trace_path_ray<STATS, V>(sv, ps.inside, ps.o, ps.d, tmin, tmax, rflags, ts, hit_ent, hit_prim, hu, hv, st);
                 if (hit_ent >= 0) st.hits++;
             }
 #ifdef IGX_SHADE_PROBE

@@ -565,6 +565,33 @@ __device__ __forceinline__ bool trace_enclosed(const SceneView& sv, int enc, f3 
     return true;
 }
 
+// Closest hit of a path's ray: rays inside enclosing entity `inside` (>= 0)
+// walk that entity's BLAS first (trace_enclosed), the rest from the TLAS
+// root -- in ONE loop, so that a wave holding both kinds steps them together
+// (two loops one after the other ran the wave's enclosed lanes and then its
+// other lanes, each half idle).  An enclosed walk that finds nothing falls back
+// to the full traversal (rare: a ray grazing out through a crack).
+template <bool STATS, int V>
+__device__ __forceinline__ void trace_path_ray(const SceneView& sv, int inside, f3 o, f3 d, float tmin, float& tmax,
+                                               uint32_t rflags, const TStack& ts, int& hit_ent, int& hit_prim, float& hu,
+                                               float& hv, TraceStats& st) {
+    Trav t;
+    bool enclosed = inside >= 0 && trav_init_enclosed<STATS>(sv, t, inside, o, d, tmin, tmax, rflags, ts, st);
+    if (!enclosed) trav_init(sv, t, o, d, tmin, tmax, rflags, ts);
+    for (;;) {
+        while (!trav_step<false, STATS, V>(sv, t, ts, st)) {
+        }
+        if (!enclosed || t.found) break;
+        trav_init(sv, t, o, d, tmin, tmax, rflags, ts);
+        enclosed = false;
+    }
+    tmax = t.tmax;
+    hit_ent = t.hit_ent;
+    hit_prim = t.hit_prim;
+    hu = t.hu;
+    hv = t.hv;
+}
+
 // Persistent lanes with ray refill (Aila & Laine, "Understanding the
 // efficiency of ray traversal on GPUs", 2009): a wave walks a sequence of C
 // ray positions; a lane whose ray is finished goes idle, and once at least
