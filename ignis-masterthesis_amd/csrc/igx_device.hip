@@ -1545,8 +1545,11 @@ struct igx_device {
     // only its BLAS (trace_enclosed); applies at the next upload
     bool enclosing_opt = true;
     int scene_depth = 0;   // worst-case stack entries of the scene
-    int* spill_main = nullptr; // spill columns of the main and tail streams
+    int* spill_main = nullptr; // spill columns of the main, tail and shadow streams
     int* spill_tail = nullptr;
+    int* spill_shadow = nullptr;
+    hipStream_t shadow_stream = nullptr; // split schedule: shadow rays of bounce b overlap the trace of bounce b + 1
+    int overlap_shadow_opt = 1;           // option "overlap_shadow" (0/1)
     // streams
     Slot slots[2];
     int next_slot = 0;
@@ -1593,7 +1596,7 @@ igx_status upload(igx_device* dev, const std::vector<T>& v, const T** out) {
 void free_scene(igx_device* dev) {
     for (void* p : dev->scene_allocs) (void)hipFree(p);
     dev->scene_allocs.clear();
-    dev->spill_main = dev->spill_tail = nullptr;
+    dev->spill_main = dev->spill_tail = dev->spill_shadow = nullptr;
     dev->has_scene = false;
 }
 
@@ -1610,8 +1613,8 @@ igx_status configure_stack(igx_device* dev) {
     const int extra = std::max(0, need - LDS_STACK);
     dev->variant = (dev->bvh_width == 4 ? 2 : 0) | (extra > 0 ? 1 : 0) | (dev->full_shading ? 4 : 0);
     const size_t threads = (size_t)max_grid(dev) * BLOCK;
-    for (int k = 0; k < 2; ++k) {
-        int*& old = k == 0 ? dev->spill_main : dev->spill_tail;
+    for (int k = 0; k < 3; ++k) {
+        int*& old = k == 0 ? dev->spill_main : k == 1 ? dev->spill_tail : dev->spill_shadow;
         if (old) {
             auto it = std::find(dev->scene_allocs.begin(), dev->scene_allocs.end(), (void*)old);
             if (it != dev->scene_allocs.end()) dev->scene_allocs.erase(it);
@@ -1621,7 +1624,7 @@ igx_status configure_stack(igx_device* dev) {
         void* p = nullptr;
         HIPCHK(hipMalloc(&p, std::max<size_t>(16, (size_t)extra * threads * sizeof(int))));
         dev->scene_allocs.push_back(p);
-        (k == 0 ? dev->spill_main : dev->spill_tail) = static_cast<int*>(p);
+        (k == 0 ? dev->spill_main : k == 1 ? dev->spill_tail : dev->spill_shadow) = static_cast<int*>(p);
     }
     dev->sv.spill = dev->spill_main;
     return IGX_OK;
@@ -1800,19 +1803,20 @@ void launch_trace(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const
     else launch_trace_w<STATS, 1>(dev, s, grid, fa, in, cnt, tail);
 }
 template <bool STATS>
-void launch_shadow(igx_device* dev, Slot& s, int grid, const int* cnt, int* work) {
+void launch_shadow(igx_device* dev, Slot& s, int grid, const int* cnt, int* work, hipStream_t strm) {
     SceneView tsv = dev->sv;
     tsv.tree_n = dev->tree_shadow;
+    if (strm != dev->stream) tsv.spill = dev->spill_shadow; // concurrent with the main stream's kernels
     if (use_refill(dev)) {
 #define L_SHR(S)                                                                                                        \
     if (dev->lds_scene_bytes)                                                                                            \
-        hipLaunchKernelGGL((k_shadow_refill<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->stream,   \
-                           dev->sv, s.sh, s.L, cnt, dev->dstats, refill_min(dev), work);                                 \
+        hipLaunchKernelGGL((k_shadow_refill<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, strm,   \
+                           tsv, s.sh, s.L, cnt, dev->dstats, refill_min(dev), work);                                 \
     else                                                                                                                 \
-        hipLaunchKernelGGL((k_shadow_refill<S, STATS, false>), dim3(grid), dim3(BLOCK), tree_bytes(dev, tsv.tree_n), dev->stream, \
+        hipLaunchKernelGGL((k_shadow_refill<S, STATS, false>), dim3(grid), dim3(BLOCK), tree_bytes(dev, tsv.tree_n), strm, \
                            tsv, s.sh, s.L, cnt, dev->dstats, refill_min(dev), work)
 #define L_SHRI(S)                                                                                                       \
-    hipLaunchKernelGGL((k_shadow_refill<S | 16, STATS, false>), dim3(grid), dim3(BLOCK), tree_bytes(dev, tsv.tree_n), dev->stream, \
+    hipLaunchKernelGGL((k_shadow_refill<S | 16, STATS, false>), dim3(grid), dim3(BLOCK), tree_bytes(dev, tsv.tree_n), strm, \
                        tsv, s.sh, s.L, cnt, dev->dstats, refill_min(dev), work)
         if (!dev->lds_scene_bytes && use_shadow_ifif(dev)) IGX_DISPATCH_VARIANT(dev->variant, L_SHRI);
         else IGX_DISPATCH_VARIANT(dev->variant, L_SHR);
@@ -1821,12 +1825,12 @@ void launch_shadow(igx_device* dev, Slot& s, int grid, const int* cnt, int* work
         return;
     }
     if (dev->lds_scene_bytes) {
-#define L_SHL(S) hipLaunchKernelGGL((k_shadow<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->stream, dev->sv, s.sh, s.L, cnt, dev->dstats, work)
+#define L_SHL(S) hipLaunchKernelGGL((k_shadow<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, strm, tsv, s.sh, s.L, cnt, dev->dstats, work)
         IGX_DISPATCH_VARIANT(dev->variant, L_SHL);
 #undef L_SHL
         return;
     }
-#define L_SH(S) hipLaunchKernelGGL((k_shadow<S, STATS, false>), dim3(grid), dim3(BLOCK), tree_bytes(dev, tsv.tree_n), dev->stream, tsv, s.sh, s.L, cnt, dev->dstats, work)
+#define L_SH(S) hipLaunchKernelGGL((k_shadow<S, STATS, false>), dim3(grid), dim3(BLOCK), tree_bytes(dev, tsv.tree_n), strm, tsv, s.sh, s.L, cnt, dev->dstats, work)
     IGX_DISPATCH_VARIANT(dev->variant, L_SH);
 #undef L_SH
 }
@@ -1939,7 +1943,7 @@ int shade_blocks_per_cu(bool full) { return full ? resident_blocks(k_shade<true>
     X int finish_blocks_per_cu<S>(int, size_t, size_t, bool);
 #define IGX_TRACE_HELPERS(X, S)                                                                                      \
     X void launch_trace<S>(igx_device*, Slot&, int, const FrameArgs&, const PathBuf&, const int*, int, int*);              \
-    X void launch_shadow<S>(igx_device*, Slot&, int, const int*, int*);                                                    \
+    X void launch_shadow<S>(igx_device*, Slot&, int, const int*, int*, hipStream_t);                                       \
     X int trace_blocks_per_cu<S>(int, int, size_t, bool, size_t);                                                    \
     X int shadow_blocks_per_cu<S>(int, size_t, bool, size_t);
 #if IGX_PART == 1
@@ -2005,6 +2009,7 @@ igx_status drain(igx_device* dev) {
     igx_status st;
     if ((st = harvest(dev, dev->slots[0])) || (st = harvest(dev, dev->slots[1]))) return st;
     HIPCHK(hipStreamSynchronize(dev->stream));
+    HIPCHK(hipStreamSynchronize(dev->shadow_stream));
     HIPCHK(hipStreamSynchronize(dev->tail_stream));
     unsigned long long tc[2] = {0, 0};
     HIPCHK(hipMemcpy(tc, dev->tail_counts, sizeof(tc), hipMemcpyDeviceToHost));
@@ -2117,7 +2122,8 @@ extern "C" igx_status igx_create(int hip_device, igx_device** out) {
         dev->mem_total = prop.totalGlobalMem;
     }
     if (hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&dev->tail_stream, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&dev->tail_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&dev->shadow_stream, hipStreamNonBlocking) != hipSuccess) {
         delete dev;
         return IGX_ERR_HIP;
     }
@@ -2137,6 +2143,7 @@ extern "C" igx_status igx_destroy(igx_device* dev) {
     (void)hipSetDevice(dev->hip_device);
     if (dev->stream) (void)hipStreamSynchronize(dev->stream);
     if (dev->tail_stream) (void)hipStreamSynchronize(dev->tail_stream);
+    if (dev->shadow_stream) (void)hipStreamSynchronize(dev->shadow_stream);
     free_scene(dev);
     for (auto& s : dev->slots) {
         free_slot_buffers(s);
@@ -2151,6 +2158,7 @@ extern "C" igx_status igx_destroy(igx_device* dev) {
     if (dev->ray_list) (void)hipFree(dev->ray_list);
     if (dev->stream) (void)hipStreamDestroy(dev->stream);
     if (dev->tail_stream) (void)hipStreamDestroy(dev->tail_stream);
+    if (dev->shadow_stream) (void)hipStreamDestroy(dev->shadow_stream);
     delete dev;
     return IGX_OK;
 }
@@ -2171,6 +2179,7 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     }
     else if (k == "treelet_kernels") dev->treelet_kernels = (int)(value & 7);
     else if (k == "shadow_classes") dev->shadow_classes_opt = value != 0;
+    else if (k == "overlap_shadow") dev->overlap_shadow_opt = value != 0;
     else if (k == "tail_pairs") {
         if (value < -1 || value > 1) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "tail_pairs must be -1 (auto), 0 or 1");
         dev->tail_pairs_opt = (int)value;
@@ -3062,6 +3071,13 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
         S.bounce_ev.clear();
         int switch_b = -1;
         S.launched = 0;
+        // split schedule: the shadow rays of bounce b run on the shadow stream,
+        // overlapping the trace of bounce b + 1 (independent: both come from
+        // shade(b)); shade(b + 1) waits for them, as both add to the radiance
+        // slots, so the additions keep their order and the image is unchanged
+        const bool overlap = split && dev->overlap_shadow_opt;
+        hipStream_t sh_strm = overlap ? dev->shadow_stream : dev->stream;
+        hipEvent_t sh_done = nullptr; // the last shadow launch on the shadow stream
         if (n <= tail) switch_b = 0;
         for (int b = 0; switch_b < 0 && b < max_bounces; ++b) {
             if (b >= 2) {
@@ -3079,6 +3095,7 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
                 if (inst) launch_trace<true>(dev, S, tr_grid, fa, in, row(2 * b), tail, tr_work);
                 else launch_trace<false>(dev, S, tr_grid, fa, in, row(2 * b), tail, tr_work);
                 end_timed(dev->stream);
+                if (sh_done) HIPCHK(hipStreamWaitEvent(dev->stream, sh_done, 0));
                 begin_timed(0, b, dev->stream);
                 launch_shade(dev, full, shade_grid, fa, in, S.hb, out, S.sh, S.L, kc, tail);
                 end_timed(dev->stream);
@@ -3090,12 +3107,21 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
                 else launch_extend<false>(dev, S, ext_grid, fb, in, out, kc, tail);
                 end_timed(dev->stream);
             }
-            begin_timed(1, b, dev->stream);
+            if (overlap) {
+                hipEvent_t shaded = slot_event(S);
+                HIPCHK(hipEventRecord(shaded, dev->stream));
+                HIPCHK(hipStreamWaitEvent(sh_strm, shaded, 0));
+            }
+            begin_timed(1, b, sh_strm);
             int* const sh_work =
                 (dev->dynamic_opt & (use_refill(dev) ? DYN_REFILL_SHADOW : DYN_SHADOW)) ? row(WORK_ROW0 + 4 * b + 2) : nullptr;
-            if (inst) launch_shadow<true>(dev, S, sh_grid, row(2 * b + 1), sh_work);
-            else launch_shadow<false>(dev, S, sh_grid, row(2 * b + 1), sh_work);
-            end_timed(dev->stream);
+            if (inst) launch_shadow<true>(dev, S, sh_grid, row(2 * b + 1), sh_work, sh_strm);
+            else launch_shadow<false>(dev, S, sh_grid, row(2 * b + 1), sh_work, sh_strm);
+            end_timed(sh_strm);
+            if (overlap) {
+                sh_done = slot_event(S);
+                HIPCHK(hipEventRecord(sh_done, sh_strm));
+            }
             HIPCHK(hipGetLastError());
             // shadow counts of bounce b and path counts entering bounce b+1 (adjacent rows)
             HIPCHK(hipMemcpyAsync(S.pinned + (size_t)(2 * b + 1) * CROW, row(2 * b + 1), 2 * CROW * sizeof(int), hipMemcpyDeviceToHost, dev->stream));
@@ -3112,7 +3138,9 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
                 if (row_total(S, 2 * b) <= tail) { switch_b = b; break; }
         }
         S.switch_bounce = switch_b;
-        // tail + resolve on the tail stream, after the main stream reached this point
+        // tail + resolve on the tail stream, after the main stream (and the
+        // shadow stream's last launch) reached this point
+        if (sh_done) HIPCHK(hipStreamWaitEvent(dev->stream, sh_done, 0));
         hipEvent_t reach = slot_event(S);
         HIPCHK(hipEventRecord(reach, dev->stream));
         HIPCHK(hipStreamWaitEvent(dev->tail_stream, reach, 0));
