@@ -51,6 +51,13 @@ __host__ __device__ constexpr bool variant_ifif(int v) { return (v & 16) != 0; }
 // are staged in LDS (the treelet); node steps below that index read LDS.
 // Set by every kernel instantiation that does not stage the whole table.
 constexpr int VARIANT_TREE = 32;
+// Bit 6: speculative while-while (trav_step_core): a lane that reaches a BLAS
+// leaf postpones it and keeps walking inner nodes until every active lane of
+// the wave holds a leaf (Aila & Laine 2009) -- more node fetches in flight per
+// wave on latency-bound scenes.  Set on k_trace_refill launches only (option
+// "speculative").
+constexpr int VARIANT_SPEC = 64;
+__host__ __device__ constexpr bool variant_spec(int v) { return (v & VARIANT_SPEC) != 0; }
 __host__ __device__ constexpr bool variant_tree(int v) { return (v & VARIANT_TREE) != 0; }
 __host__ __device__ constexpr int kernel_variant(int v, bool lds) { return lds ? lds_variant(v, true) : (v | VARIANT_TREE); }
 

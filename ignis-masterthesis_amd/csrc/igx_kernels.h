@@ -430,6 +430,28 @@ __device__ __forceinline__ bool trav_step_core(const SceneView& sv, Trav& t, con
             t.sp = sp;
             return false;
         }
+    } else if constexpr (variant_spec(V)) {
+        // speculative while-while: the first BLAS leaf a lane meets is
+        // postponed and the lane keeps popping and walking inner nodes until
+        // no active lane is still walking without a postponed leaf; then the
+        // postponed leaf is tested, its pending entry pushed back.  Leaves are
+        // tested in a different order than depth-first; the closest hit does
+        // not depend on the order (accept_hit), an any-hit ray stops at any hit
+        bool post = false;
+        int leaf = 0;
+        while (node >= 0) {
+            node = node_step<STATS, V>(sv, t, node, ts, sp, st);
+            if (!post && t.in_blas && is_leaf_ref(node)) {
+                post = true;
+                leaf = node;
+                node = tpop<SPILL>(ts, sp);
+            }
+            if (__ballot(!post && node >= 0) == 0) break;
+        }
+        if (post) {
+            tpush<SPILL>(ts, sp, node);
+            node = leaf;
+        }
     } else {
         while (node >= 0) node = node_step<STATS, V>(sv, t, node, ts, sp, st);
     }
