@@ -223,6 +223,25 @@ def suite_line(ignis_amd, dev_index, path, spi, iters, size=None):
             "value": round(rays / dt / 1e6, 2), "unit": "Mrays/s", "ms_per_iteration": round(dt / iters * 1e3, 3),
             "load_and_build_s": round(t_load, 2), "bvh_depth": st["bvh_depth"],
             "roofline": roofline(dev, st, lambda: dev.render(p), 1, key)}
+    if st["launches_trace"] > 0:
+        # split schedule: k_trace_refill shares the chip with the shadow rays of the
+        # previous bounce (option overlap_shadow), so its launch durations include
+        # shared time; the same iterations once more with the overlap off give the
+        # kernel's own duration (not timed for `value`)
+        r = line["roofline"]
+        dev.reset_stats()
+        dev.set_option("timing", 1)
+        dev.set_option("overlap_shadow", 0)
+        dev.render_iterations(p, iters)
+        si = dev.stats()
+        dev.set_option("overlap_shadow", 1)
+        dev.set_option("timing", 0)
+        t_iso = si["ms_trace"] / 1e3 / max(1, si["launches_trace"])
+        per_launch = r["algorithmic_bytes_per_launch"]
+        r["isolated"] = {"avg_launch_us": round(t_iso * 1e6, 2),
+                         "frac": round(per_launch / t_iso / 1e9 / HBM_PEAK_GBS, 4) if t_iso > 0 else None,
+                         "frac_traffic": round(r["traffic"] / t_iso / 1e9 / HBM_PEAK_GBS, 4) if t_iso > 0 and r["traffic"] else None,
+                         "note": "k_trace_refill alone (overlap_shadow 0): its own launch duration"}
     dev.close()
     del scene
     return line
