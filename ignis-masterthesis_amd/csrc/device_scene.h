@@ -57,6 +57,13 @@ constexpr int VARIANT_TREE = 32;
 // wave on latency-bound scenes.  Set on k_trace_refill launches only (option
 // "speculative").
 constexpr int VARIANT_SPEC = 64;
+// Bit 7: quantised 4-wide nodes (64 B, node_step4q; host Bvh4QNode) instead of
+// the 128-B 4-wide nodes -- half the node bytes per visit on scenes whose
+// tables stay in global memory.  Set by the upload with bit 1 (option
+// "bvh_quantize").
+constexpr int VARIANT_Q4 = 128;
+__host__ __device__ constexpr bool variant_q4(int v) { return (v & VARIANT_Q4) != 0; }
+constexpr int32_t REF_EMPTY = (int32_t)0x80000002; // absent child of a 4-wide node (host kEmptyRef)
 __host__ __device__ constexpr bool variant_spec(int v) { return (v & VARIANT_SPEC) != 0; }
 __host__ __device__ constexpr bool variant_tree(int v) { return (v & VARIANT_TREE) != 0; }
 __host__ __device__ constexpr int kernel_variant(int v, bool lds) { return lds ? lds_variant(v, true) : (v | VARIANT_TREE); }

@@ -1130,6 +1130,10 @@ __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, f
 #ifndef REFILL_WAVES
 #define REFILL_WAVES 6
 #endif
+// with quantised nodes a node step holds 16 VGPRs of node data instead of 32
+#ifndef REFILL_WAVES_Q4
+#define REFILL_WAVES_Q4 6
+#endif
 // the if-if shadow kernel (split-schedule scenes) needs fewer registers
 #ifndef SHADOW_IFIF_WAVES
 #define SHADOW_IFIF_WAVES 6
@@ -1228,7 +1232,7 @@ struct GroupSeq {
 };
 
 template <int V0, bool STATS, bool LDS>
-__global__ void __launch_bounds__(BLOCK, LDS ? REFILL_WAVES_LDS : REFILL_WAVES) k_trace_refill(FrameArgs fa, SceneView gsv, PathBuf in, HitBuf hits,
+__global__ void __launch_bounds__(BLOCK, LDS ? REFILL_WAVES_LDS : (variant_q4(V0) ? REFILL_WAVES_Q4 : REFILL_WAVES)) k_trace_refill(FrameArgs fa, SceneView gsv, PathBuf in, HitBuf hits,
                                                                      const int* cnt, int tail_threshold,
                                                                      unsigned long long* stats, int refill_min, int* work) {
     constexpr int V = kernel_variant(V0, LDS); // LDS-staged nodes: padded stride; global tables: treelet (device_scene.h)
@@ -1538,6 +1542,9 @@ struct igx_device {
     igx_camera cam_desc{};
     int variant = 0;       // traversal variant of the scene (device_scene.h: width, spill)
     int bvh_width = 2;     // node width of the uploaded tables
+    bool quantized = false; // the 4-wide nodes are quantised (Bvh4QNode, 64 B; variant bit 7)
+    int quantize_opt = -1;  // option "bvh_quantize": -1 auto (4-wide scenes whose tables stay in global memory), 0, 1
+    int nf4 = 4;            // float4s per node of the uploaded tables
     int bvh_width_opt = 0; // option "bvh_width": 0 = auto, 2, 4 (applies at the next upload)
     bool full_shading = false;     // the scene needs materials / lights beyond the basic set
     bool full_shading_opt = false; // option "full_shading": 1 = always compile-in the whole set
@@ -1614,7 +1621,7 @@ int max_grid(const igx_device* dev) {
 igx_status configure_stack(igx_device* dev) {
     const int need = dev->scene_depth;
     const int extra = std::max(0, need - LDS_STACK);
-    dev->variant = (dev->bvh_width == 4 ? 2 : 0) | (extra > 0 ? 1 : 0) | (dev->full_shading ? 4 : 0);
+    dev->variant = (dev->bvh_width == 4 ? 2 : 0) | (extra > 0 ? 1 : 0) | (dev->full_shading ? 4 : 0) | (dev->quantized ? VARIANT_Q4 : 0);
     const size_t threads = (size_t)max_grid(dev) * BLOCK;
     for (int k = 0; k < 3; ++k) {
         int*& old = k == 0 ? dev->spill_main : k == 1 ? dev->spill_tail : dev->spill_shadow;
@@ -1712,7 +1719,7 @@ inline bool use_tail_pairs(const igx_device* dev) {
     return dev->lds_scene_bytes == 0 && (dev->tail_pairs_opt < 0 ? true : dev->tail_pairs_opt != 0);
 }
 // dynamic LDS of a global-table kernel that stages `nodes` treelet nodes
-inline size_t tree_bytes(const igx_device* dev, int nodes) { return (size_t)nodes * node_f4(dev->bvh_width) * 16; }
+inline size_t tree_bytes(const igx_device* dev, int nodes) { return (size_t)nodes * dev->nf4 * 16; }
 inline int refill_min(const igx_device* dev) { return dev->refill_opt >= 0 ? dev->refill_opt : 16; }
 // auto: global-table scenes only; an explicit "refill" applies to LDS-staged scenes too
 inline bool use_refill(const igx_device* dev) {
@@ -1731,19 +1738,22 @@ inline bool use_shadow_ifif(const igx_device* dev) {
 }
 
 // Launch helpers dispatching on the scene's traversal variant.
+// (bit 7, VARIANT_Q4: quantised 4-wide nodes, only with bit 1)
 #define IGX_DISPATCH_VARIANT(v, MACRO)        \
     do {                                      \
-        switch ((v) & 3) {                    \
+        switch ((v) & (3 | VARIANT_Q4)) {     \
         case 0: MACRO(0); break;              \
         case 1: MACRO(1); break;              \
         case 2: MACRO(2); break;              \
-        default: MACRO(3); break;             \
+        case 3: MACRO(3); break;              \
+        case 2 | VARIANT_Q4: MACRO(130); break; \
+        default: MACRO(131); break;           \
         }                                     \
     } while (0)
 // shading kernels also dispatch on the material/light feature bit
 #define IGX_DISPATCH_VARIANT8(v, MACRO)       \
     do {                                      \
-        switch (v) {                          \
+        switch ((v) & (7 | VARIANT_Q4)) {     \
         case 0: MACRO(0); break;              \
         case 1: MACRO(1); break;              \
         case 2: MACRO(2); break;              \
@@ -1751,7 +1761,11 @@ inline bool use_shadow_ifif(const igx_device* dev) {
         case 4: MACRO(4); break;              \
         case 5: MACRO(5); break;              \
         case 6: MACRO(6); break;              \
-        default: MACRO(7); break;             \
+        case 7: MACRO(7); break;              \
+        case 2 | VARIANT_Q4: MACRO(130); break; \
+        case 3 | VARIANT_Q4: MACRO(131); break; \
+        case 6 | VARIANT_Q4: MACRO(134); break; \
+        default: MACRO(135); break;           \
         }                                     \
     } while (0)
 
@@ -1874,16 +1888,18 @@ int resident_blocks(K kernel, size_t dyn_lds = 0) {
 #define IGX_RES1(K, V, ...) return lds ? resident_blocks(K<V, __VA_ARGS__, true>, lds) : resident_blocks(K<V, __VA_ARGS__, false>, tree)
 #define IGX_RESIDENT(K, ...)                                         \
     do {                                                             \
-        switch (v & 3) {                                             \
+        switch (v & (3 | VARIANT_Q4)) {                              \
         case 0: IGX_RES1(K, 0, __VA_ARGS__);                         \
         case 1: IGX_RES1(K, 1, __VA_ARGS__);                         \
         case 2: IGX_RES1(K, 2, __VA_ARGS__);                         \
-        default: IGX_RES1(K, 3, __VA_ARGS__);                        \
+        case 3: IGX_RES1(K, 3, __VA_ARGS__);                         \
+        case 2 | VARIANT_Q4: IGX_RES1(K, 130, __VA_ARGS__);          \
+        default: IGX_RES1(K, 131, __VA_ARGS__);                      \
         }                                                            \
     } while (0)
 #define IGX_RESIDENT8(K, ...)                                        \
     do {                                                             \
-        switch (v) {                                                 \
+        switch (v & (7 | VARIANT_Q4)) {                              \
         case 0: IGX_RES1(K, 0, __VA_ARGS__);                         \
         case 1: IGX_RES1(K, 1, __VA_ARGS__);                         \
         case 2: IGX_RES1(K, 2, __VA_ARGS__);                         \
@@ -1891,7 +1907,11 @@ int resident_blocks(K kernel, size_t dyn_lds = 0) {
         case 4: IGX_RES1(K, 4, __VA_ARGS__);                         \
         case 5: IGX_RES1(K, 5, __VA_ARGS__);                         \
         case 6: IGX_RES1(K, 6, __VA_ARGS__);                         \
-        default: IGX_RES1(K, 7, __VA_ARGS__);                        \
+        case 7: IGX_RES1(K, 7, __VA_ARGS__);                         \
+        case 2 | VARIANT_Q4: IGX_RES1(K, 130, __VA_ARGS__);          \
+        case 3 | VARIANT_Q4: IGX_RES1(K, 131, __VA_ARGS__);          \
+        case 6 | VARIANT_Q4: IGX_RES1(K, 134, __VA_ARGS__);          \
+        default: IGX_RES1(K, 135, __VA_ARGS__);                      \
         }                                                            \
     } while (0)
 #define IGX_RESIDENT_G(K) IGX_RESIDENT(K, STATS)
@@ -1905,16 +1925,9 @@ int shadow_blocks_per_cu(int v, size_t lds, bool refill, size_t tree) {
 template <bool STATS>
 int finish_blocks_per_cu(int v, size_t lds, size_t tree, bool pairs) {
     if (!lds && pairs) {
-        switch (v) {
-        case 0: return resident_blocks(k_finish_pairs<0, STATS>, tree);
-        case 1: return resident_blocks(k_finish_pairs<1, STATS>, tree);
-        case 2: return resident_blocks(k_finish_pairs<2, STATS>, tree);
-        case 3: return resident_blocks(k_finish_pairs<3, STATS>, tree);
-        case 4: return resident_blocks(k_finish_pairs<4, STATS>, tree);
-        case 5: return resident_blocks(k_finish_pairs<5, STATS>, tree);
-        case 6: return resident_blocks(k_finish_pairs<6, STATS>, tree);
-        default: return resident_blocks(k_finish_pairs<7, STATS>, tree);
-        }
+#define L_RP(S) return resident_blocks(k_finish_pairs<S, STATS>, tree)
+        IGX_DISPATCH_VARIANT8(v, L_RP);
+#undef L_RP
     }
     IGX_RESIDENT8(k_finish, STATS);
 }
@@ -2188,6 +2201,10 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     else if (k == "treelet_kernels") dev->treelet_kernels = (int)(value & 7);
     else if (k == "shadow_classes") dev->shadow_classes_opt = value != 0;
     else if (k == "overlap_shadow") dev->overlap_shadow_opt = value != 0;
+    else if (k == "bvh_quantize") {
+        if (value < -1 || value > 1) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "bvh_quantize must be -1 (auto), 0 or 1");
+        dev->quantize_opt = (int)value;
+    }
     else if (k == "speculative") dev->spec_opt = value != 0;
     else if (k == "tail_pairs") {
         if (value < -1 || value > 1) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "tail_pairs must be -1 (auto), 0 or 1");
@@ -2271,15 +2288,27 @@ extern "C" igx_status igx_synchronize(igx_device* dev) {
 // nodes keep their relative (depth-first) order.  Every inner-node reference
 // (node children, instance BLAS roots, the TLAS root) is renumbered; the
 // traversal result does not depend on node numbering.
-static void order_hot_nodes(std::vector<float4>& nodes, int nf4, std::vector<float4>& inst, int& tlas_root, size_t front) {
+// `format`: 2 (BVH2, 64 B), 4 (4-wide, 128 B) or 5 (quantised 4-wide, 64 B).
+static void order_hot_nodes(std::vector<float4>& nodes, int format, std::vector<float4>& inst, int& tlas_root, size_t front) {
+    const int nf4 = format == 4 ? 8 : 4;
     const size_t nn = nodes.size() / nf4;
     if (nn == 0 || front == 0) return;
-    const int width = nf4 == 8 ? 4 : 2;
+    const int width = format == 2 ? 2 : 4;
     auto ref = [&](size_t n, int k) -> int32_t& {
-        return reinterpret_cast<int32_t*>(&nodes[n * nf4])[width == 4 ? 24 + k : 12 + k];
+        return reinterpret_cast<int32_t*>(&nodes[n * nf4])[format == 4 ? 24 + k : 12 + k];
     };
     auto box = [&](size_t n, int k, float lo[3], float hi[3]) {
         const float* f = reinterpret_cast<const float*>(&nodes[n * nf4]);
+        if (format == 5) { // origin + code * scale (Bvh4QNode)
+            const uint32_t* u = reinterpret_cast<const uint32_t*>(f);
+            const float sc[3] = {f[3], f[4], f[5]};
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = f[a] + (float)((u[6 + 2 * a] >> (8 * k)) & 255u) * sc[a];
+                hi[a] = f[a] + (float)((u[7 + 2 * a] >> (8 * k)) & 255u) * sc[a];
+            }
+            if (ref(n, k) == igx::kEmptyRef) lo[0] = INFINITY;
+            return;
+        }
         for (int a = 0; a < 3; ++a) {
             lo[a] = width == 4 ? f[8 * a + k] : f[6 * k + 2 * a];
             hi[a] = width == 4 ? f[8 * a + 4 + k] : f[6 * k + 2 * a + 1];
@@ -2474,7 +2503,15 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     const int width = dev->bvh_width_opt == 2 || dev->bvh_width_opt == 4
                           ? dev->bvh_width_opt
                           : (tlas_br.depth + blas_depth2 + 3 <= LDS_STACK ? 2 : 4);
-    const int nf4 = node_f4(width);
+    // 4-wide nodes quantised to 64 B (Bvh4QNode) on the split schedule's
+    // scenes, whose node fetches go to the Infinity Cache / HBM (soup-16M frame
+    // 74.7 -> 70.0, soup-1M 98.2 -> 92.8 ms); where the tables stay on chip the
+    // decode only costs instructions (primitives 8.6 -> 9.4, S-deep 46.7 -> 49.5)
+    size_t est_tri = 0;
+    for (const auto& b : brs) est_tri += b.prim_order.size();
+    const size_t est_bytes = est_tri * 48 + (size_t)desc->num_entities * 64 + (est_tri / 2 + desc->num_entities) * 128;
+    const bool quantize = width == 4 && (dev->quantize_opt == 1 || (dev->quantize_opt < 0 && est_bytes > SPLIT_TABLE_BYTES));
+    const int nf4 = quantize ? 4 : node_f4(width);
 
     // ---- phase 2: node, triangle and instance tables ----------------------
     std::vector<float4> nodes; // nf4 float4s per node
@@ -2509,9 +2546,16 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
                     if (nd.ref[k] >= 0) nd.ref[k] += node_off;
                     else if (nd.ref[k] != igx::kEmptyRef) nd.ref[k] = move_leaf(nd.ref[k]);
                 }
-                float4 f[8];
-                std::memcpy(f, &nd, 128);
-                nodes.insert(nodes.end(), f, f + 8);
+                if (quantize) {
+                    const igx::Bvh4QNode qn = igx::quantize_bvh4(nd);
+                    float4 f[4];
+                    std::memcpy(f, &qn, 64);
+                    nodes.insert(nodes.end(), f, f + 4);
+                } else {
+                    float4 f[8];
+                    std::memcpy(f, &nd, 128);
+                    nodes.insert(nodes.end(), f, f + 8);
+                }
             }
             need = b4.stack_need;
         }
@@ -2820,7 +2864,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     }
 
     // hot nodes first: any prefix of the node array is a treelet (stage_treelet)
-    order_hot_nodes(nodes, nf4, inst, tlas_root, TREELET_FRONT);
+    order_hot_nodes(nodes, quantize ? 5 : width, inst, tlas_root, TREELET_FRONT);
 
     // ---- upload ----------------------------------------------------------
     SceneView sv{};
@@ -2840,6 +2884,8 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     sv.num_nodes = (int)(nodes.size() / nf4);
     sv.node_f4 = nf4;
     dev->bvh_width = width;
+    dev->quantized = quantize;
+    dev->nf4 = nf4;
     sv.num_inst = (int)(inst.size() / 4);
     sv.num_enc = (int)enc_tab.size();
     sv.num_tris = (int)(tris.size() / 3);
@@ -3278,7 +3324,7 @@ extern "C" igx_status igx_get_stats(igx_device* dev, igx_stats* out) {
     out->shadow_wave_node_iters = h[11];
     out->shadow_wave_leaf_iters = h[12];
     out->bvh_width = dev->bvh_width;
-    out->node_bytes = node_f4(dev->bvh_width) * 16;
+    out->node_bytes = dev->nf4 * 16;
     out->lds_scene_bytes = (int32_t)dev->lds_scene_bytes;
     if (dev->has_scene && dev->tree_dirty) configure_treelet(dev);
     out->shadow_blocks_per_cu = dev->has_scene ? shadow_blocks_per_cu<false>(dev->variant, dev->lds_scene_bytes, use_refill(dev),

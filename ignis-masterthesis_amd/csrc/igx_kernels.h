@@ -307,11 +307,58 @@ __device__ __forceinline__ int node_step4(const SceneView& sv, const Trav& t, in
     return ref[0];
 }
 
+// Quantised 4-wide node (64 B, host Bvh4QNode): per axis an origin and a
+// power-of-two scale, child bounds as bytes.  The slab distance of code q on
+// axis a is fma(q, s_a * idir_a, fma(o_a, idir_a, iorg_a)); the boxes carry at
+// least half a quantum of slack (quantize_bvh4), so every ray the exact box
+// accepts is accepted here.  Absent children (kEmptyRef) are masked by ref.
+template <bool STATS, bool SPILL, bool TREE>
+__device__ __forceinline__ int node_step4q(const SceneView& sv, const Trav& t, int node, const TStack& ts, int& sp,
+                                           TraceStats& st) {
+    if (STATS) {
+        st.nodes++;
+        if (first_active_lane()) st.wnodes++;
+    }
+    const float4* np = (TREE && node < sv.tree_n ? sv.tree : sv.nodes) + 4 * node; // see node_step2
+    const float4 A = np[0], B = np[1], C = np[2];
+    const int4 r = *reinterpret_cast<const int4*>(np + 3);
+    const float SX = A.w * t.idir.x, SY = B.x * t.idir.y, SZ = B.y * t.idir.z;
+    const float OX = fmaf(A.x, t.idir.x, t.iorg.x), OY = fmaf(A.y, t.idir.y, t.iorg.y), OZ = fmaf(A.z, t.idir.z, t.iorg.z);
+    const uint32_t qlx = __float_as_uint(B.z), qhx = __float_as_uint(B.w);
+    const uint32_t qly = __float_as_uint(C.x), qhy = __float_as_uint(C.y);
+    const uint32_t qlz = __float_as_uint(C.z), qhz = __float_as_uint(C.w);
+    float d[4];
+    int ref[4] = {r.x, r.y, r.z, r.w};
+    int n = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float ax = fmaf((float)((qlx >> (8 * k)) & 255u), SX, OX), bx = fmaf((float)((qhx >> (8 * k)) & 255u), SX, OX);
+        const float ay = fmaf((float)((qly >> (8 * k)) & 255u), SY, OY), by = fmaf((float)((qhy >> (8 * k)) & 255u), SY, OY);
+        const float az = fmaf((float)((qlz >> (8 * k)) & 255u), SZ, OZ), bz = fmaf((float)((qhz >> (8 * k)) & 255u), SZ, OZ);
+        const float en = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), t.tmin));
+        const float ex = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), t.tmax));
+        const bool h = en <= ex && ref[k] != REF_EMPTY;
+        d[k] = h ? en : INFINITY;
+        n += h ? 1 : 0;
+    }
+    if (n == 0) return tpop<SPILL>(ts, sp);
+    cswap(d[0], ref[0], d[1], ref[1]);
+    cswap(d[2], ref[2], d[3], ref[3]);
+    cswap(d[0], ref[0], d[2], ref[2]);
+    cswap(d[1], ref[1], d[3], ref[3]);
+    cswap(d[1], ref[1], d[2], ref[2]);
+    if (n > 3) tpush<SPILL>(ts, sp, ref[3]);
+    if (n > 2) tpush<SPILL>(ts, sp, ref[2]);
+    if (n > 1) tpush<SPILL>(ts, sp, ref[1]);
+    return ref[0];
+}
+
 template <bool STATS, int V>
 __device__ __forceinline__ int node_step(const SceneView& sv, const Trav& t, int node, const TStack& ts, int& sp,
                                          TraceStats& st) {
     constexpr int PAD = variant_ldspad(V) ? 1 : 0;
-    if constexpr (variant_width(V) == 4) return node_step4<STATS, variant_spill(V), 8 + PAD, variant_tree(V)>(sv, t, node, ts, sp, st);
+    if constexpr (variant_q4(V)) return node_step4q<STATS, variant_spill(V), variant_tree(V)>(sv, t, node, ts, sp, st);
+    else if constexpr (variant_width(V) == 4) return node_step4<STATS, variant_spill(V), 8 + PAD, variant_tree(V)>(sv, t, node, ts, sp, st);
     else return node_step2<STATS, variant_spill(V), 4 + PAD, variant_tree(V)>(sv, t, node, ts, sp, st);
 }
 

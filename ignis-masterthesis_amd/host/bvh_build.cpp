@@ -615,6 +615,65 @@ Bvh4Result collapse_bvh4(const BvhBuildResult& in) {
 }
 
 // ---------------------------------------------------------------------------
+// Quantised 4-wide nodes (Bvh4QNode, bvh_build.h)
+// ---------------------------------------------------------------------------
+Bvh4QNode quantize_bvh4(const Bvh4Node& n) {
+    Bvh4QNode q{};
+    const float* lo[3] = {n.lo_x, n.lo_y, n.lo_z};
+    const float* hi[3] = {n.hi_x, n.hi_y, n.hi_z};
+    bool valid[4];
+    for (int k = 0; k < 4; ++k) {
+        q.ref[k] = n.ref[k];
+        valid[k] = n.ref[k] != kEmptyRef;
+        for (int a = 0; a < 3; ++a)
+            valid[k] = valid[k] && std::isfinite(lo[a][k]) && std::isfinite(hi[a][k]) && lo[a][k] <= hi[a][k];
+    }
+    uint32_t* qlo[3] = {&q.qlo_x, &q.qlo_y, &q.qlo_z};
+    uint32_t* qhi[3] = {&q.qhi_x, &q.qhi_y, &q.qhi_z};
+    float* sc[3] = {&q.sx, &q.sy, &q.sz};
+    for (int a = 0; a < 3; ++a) {
+        double l = INFINITY, h = -INFINITY;
+        for (int k = 0; k < 4; ++k)
+            if (valid[k]) {
+                l = std::min(l, (double)lo[a][k]);
+                h = std::max(h, (double)hi[a][k]);
+            }
+        if (!(l <= h)) l = h = 0; // no valid child (never built, kept total)
+        const double mag = std::max(std::fabs(l), std::fabs(h));
+        // a quantum: the extent over 249 codes (three spare on each side), and at
+        // least 2^-19 of the magnitude so rounding in the slab test stays far below it
+        double s = std::max({(h - l) / 249.0, mag * std::ldexp(1.0, -19), std::ldexp(1.0, -100)});
+        s = std::ldexp(1.0, (int)std::ceil(std::log2(s)));
+        for (;;) {
+            const float o = std::nextafter((float)(l - 2 * s), -INFINITY);
+            bool ok = true;
+            uint32_t wl = 0, wh = 0;
+            for (int k = 0; k < 4; ++k) {
+                long ql = 0, qh = 0;
+                if (valid[k]) {
+                    ql = (long)std::floor(((double)lo[a][k] - o) / s) - 1;
+                    qh = (long)std::ceil(((double)hi[a][k] - o) / s) + 1;
+                    // at least half a quantum of slack on both sides, in exact arithmetic
+                    ok = ok && ql >= 0 && qh <= 255 && (double)o + ql * s <= lo[a][k] - 0.5 * s &&
+                         (double)o + qh * s >= hi[a][k] + 0.5 * s;
+                }
+                wl |= (uint32_t)std::clamp(ql, 0L, 255L) << (8 * k);
+                wh |= (uint32_t)std::clamp(qh, 0L, 255L) << (8 * k);
+            }
+            if (ok) {
+                q.origin[a] = o;
+                *sc[a] = (float)s;
+                *qlo[a] = wl;
+                *qhi[a] = wh;
+                break;
+            }
+            s *= 2;
+        }
+    }
+    return q;
+}
+
+// ---------------------------------------------------------------------------
 // Reference GPU BLAS (Node2 + Tri1 blob) -> BvhBuildResult.
 // Node2 (traversal/mapping_gpu.art:3-7) stores the child boxes in the same
 // interleaving as BvhNode; children are inner index + 1 (> 0), ~first Tri1

@@ -92,6 +92,26 @@ struct Bvh4Result {
 // surface-area collapse of wide-BVH builders).  Leaf codes are kept.
 Bvh4Result collapse_bvh4(const BvhBuildResult& bvh2);
 
+// 4-wide node with quantised child boxes (64 B, half a Bvh4Node; traversed by
+// node_step4q).  Per axis a a node origin o_a and a power-of-two scale s_a;
+// child k's bound on axis a is o_a + q * s_a with q the byte k of the qlo / qhi
+// word of that axis.  Every quantised box contains the child's (padded) box
+// with at least half a quantum to spare on each side, and a quantum is at
+// least 2^-19 of the coordinates' magnitude (16 float ulps), so the slab test
+// accepts every ray the exact box would: the tree visits a superset of the
+// triangles, and closest hits (independent of topology, accept_hit) stay the
+// same.  Absent children keep kEmptyRef and are masked by their ref.
+//   float o_x, o_y, o_z, s_x | float s_y, s_z, u32 qlo_x, qhi_x |
+//   u32 qlo_y, qhi_y, qlo_z, qhi_z | int32 ref[4]
+struct Bvh4QNode {
+    float origin[3];
+    float sx, sy, sz;
+    uint32_t qlo_x, qhi_x, qlo_y, qhi_y, qlo_z, qhi_z;
+    int32_t ref[4];
+};
+static_assert(sizeof(Bvh4QNode) == 64, "Bvh4QNode must be 64 bytes");
+Bvh4QNode quantize_bvh4(const Bvh4Node& n);
+
 // Read the reference's GPU BLAS (one FixTables["trimesh_primbvh"] entry:
 // u32 node_count, tri_count, 0, 0; Node2[]; Tri1[], TriMeshProvider.cpp:307-326)
 // into the device's BVH2 form: same boxes and topology, leaf codes over the

@@ -147,6 +147,30 @@ def test_bvh_width_invariance(device, root, name):
     np.testing.assert_array_equal(imgs[0], imgs[1])
 
 
+def test_quantised_nodes_match(device, root):
+    """Quantised 4-wide nodes (the soups' default, bvh_quantize) against the
+    128-B nodes on soup-1M: conservative boxes visit a superset of the
+    triangles, so closest hits agree (tie rule); a triangle hit inside the
+    Moeller-Trumbore tolerance but outside an exact padded box can appear in
+    rare rays, as with any change of the tree (padded boxes)."""
+    sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", "s_soup_1m.json"))
+    rays = np.concatenate([camera_rays(sc, 200, 200, jitter=0.29), random_rays(sc, 100000, seed=9)])
+    res, imgs = [], []
+    try:
+        for q in (0, 1):
+            device.set_option("bvh_quantize", q)
+            device.upload(sc)
+            assert device.stats()["node_bytes"] == (64 if q else 128)
+            res.append(device.trace_hits(rays, 0x1))
+            imgs.append(render_gpu(device, sc, 128, 128, 4))
+    finally:
+        device.set_option("bvh_quantize", -1)
+    (e0, t0), (e1, t1) = res
+    same = np.all(e0 == e1, axis=1) & (t0[:, 0] == t1[:, 0])
+    assert same.mean() >= 0.99999, same.mean()
+    assert rel_mse(imgs[1], imgs[0]) <= 1e-6
+
+
 @pytest.mark.parametrize("name", ["diamond_scene.json", "s_deep.json"])
 def test_spatial_split_invariance(device, root, name):
     """BLAS built with spatial splits (SBVH: triangles referenced from several
