@@ -961,8 +961,15 @@ __global__ void __launch_bounds__(BLOCK) k_finish(FrameArgs fa, SceneView gsv, P
 // of bounce k, shadow ray of bounce k, emission of bounce k + 1), so the image
 // is bit-identical to k_finish.
 // ---------------------------------------------------------------------------
+// occupancy target of k_finish_pairs (waves per SIMD).  The compiler's own
+// choice is 212-234 VGPRs = 2 waves; 3 waves (168 VGPRs, ~30 spilled) hides
+// more of the long tail's latency: soup-16M frame 70.6 -> 69.4 ms, soup-1M
+// 54.3 -> 53.2 ms (tools/exp_n.sh, round 3)
+#ifndef FINISH_PAIRS_WAVES
+#define FINISH_PAIRS_WAVES 3
+#endif
 template <int V0, bool STATS>
-__global__ void __launch_bounds__(BLOCK) k_finish_pairs(FrameArgs fa, SceneView gsv, PathBuf in, float4* L, const int* cnt,
+__global__ void __launch_bounds__(BLOCK, FINISH_PAIRS_WAVES) k_finish_pairs(FrameArgs fa, SceneView gsv, PathBuf in, float4* L, const int* cnt,
                                                         int tail_threshold, unsigned long long* stats,
                                                         unsigned long long* tail_counts) {
     constexpr int V = kernel_variant(V0, false);
