@@ -130,6 +130,7 @@ struct FrameArgs {
     int classify;        // surviving paths' stream class (see wave_append_paths): 0 all A, 1 B = inside a dielectric (eta != 1), 2 B = after a specular event
     int dynamic;         // k_extend: waves take 64-path groups from per-shard work counters (KernelCounters::work)
     int shadow_classes;  // shadow rays crossing an enclosing entity's box go to the back of their shard (shadow_class_b)
+    float class_shrink;  // > 0: class 3 tests the box's inscribed ellipsoid scaled by this instead of the box
 };
 
 // path slot -> (local pixel, sample, iteration): slots run over the chunk's
@@ -376,11 +377,34 @@ __device__ __forceinline__ bool shadow_class_b(int enabled, const SceneView& sv,
     }
     return hit;
 }
-__device__ __forceinline__ bool path_class_b(int classify, const SceneView& sv, const PathState& ps) {
+// the same question against the ellipsoid inscribed in the box, its semi-axes
+// scaled by `s`: a closer guess of "this ray will shade the dielectric" for
+// gem-like shapes whose box corners are empty (no square root: the line meets
+// the ellipsoid iff the discriminant is >= 0, and the far root is >= 0 iff the
+// origin is inside or the ray points towards the centre)
+__device__ __forceinline__ bool crosses_enclosing_ellipsoid(const SceneView& sv, f3 o, f3 d, float s) {
+    bool hit = false;
+    for (int k = 0; k < sv.num_enc && !hit; ++k) {
+        const float4 lo = sv.enc_box[2 * k], hi = sv.enc_box[2 * k + 1];
+        const float ix = __builtin_amdgcn_rcpf(0.5f * s * (hi.x - lo.x));
+        const float iy = __builtin_amdgcn_rcpf(0.5f * s * (hi.y - lo.y));
+        const float iz = __builtin_amdgcn_rcpf(0.5f * s * (hi.z - lo.z));
+        const float ox = (o.x - 0.5f * (lo.x + hi.x)) * ix, oy = (o.y - 0.5f * (lo.y + hi.y)) * iy,
+                    oz = (o.z - 0.5f * (lo.z + hi.z)) * iz;
+        const float dx = d.x * ix, dy = d.y * iy, dz = d.z * iz;
+        const float a = dx * dx + dy * dy + dz * dz;
+        const float b = ox * dx + oy * dy + oz * dz;
+        const float c = ox * ox + oy * oy + oz * oz - 1.0f;
+        hit = b * b - a * c >= 0.0f && (c <= 0.0f || b <= 0.0f);
+    }
+    return hit;
+}
+__device__ __forceinline__ bool path_class_b(int classify, float shrink, const SceneView& sv, const PathState& ps) {
     switch (classify) {
     case 1: return ps.eta != 1.0f;
     case 2: return ps.inv_pdf == 0.0f;
-    case 3: return ps.eta != 1.0f || crosses_enclosing_box(sv, ps.o, ps.d);
+    case 3: return ps.eta != 1.0f || (shrink > 0.0f ? crosses_enclosing_ellipsoid(sv, ps.o, ps.d, shrink)
+                                                     : crosses_enclosing_box(sv, ps.o, ps.d));
     default: return false;
     }
 }
@@ -570,6 +594,9 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
 // a read of the counter) since the previous mark is added to phase k; marks
 // sit at wave-uniform points.
 __device__ __forceinline__ void phase_mark(TraceStats& st, unsigned long long& last, int k) {
+#ifdef IGX_KIND_PROBE // the four slots count shading-kind mixing instead (k_extend below)
+    return;
+#endif
     const unsigned long long now = __builtin_amdgcn_s_memtime();
     st.cyc[k] += now - last;
     last = now;
@@ -663,6 +690,23 @@ __device__ __forceinline__ int take_group(int* work, int& s, uint64_t& done, int
     }
 }
 
+// path i of a generated chunk at its camera vertex (k_extend's fused bounce 0)
+__device__ __forceinline__ PathState camera_path(const FrameArgs& fa, const SceneView& sv, int i) {
+    const GenPath g = gen_path(fa, sv, i);
+    PathState ps;
+    ps.o = g.o;
+    ps.d = g.d;
+    ps.counter = g.counter;
+    ps.seed = g.seed;
+    ps.depth = g.depth;
+    ps.slot = i;
+    ps.contrib = mk(1, 1, 1); // init_pt_raypayload (technique/pathtracer.art:33-38)
+    ps.inv_pdf = 0;
+    ps.eta = 1.0f;
+    ps.inside = -1;
+    return ps;
+}
+
 // ---------------------------------------------------------------------------
 // extend kernel: one bounce for every live path, compacted outputs.  Each
 // wave walks its shard of the input stream and appends survivors and shadow
@@ -725,18 +769,8 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
         if (pos < ns) {
             if (gen) { // inverse of gen_index
                 const int i = ((pos >> 6) << 12) | (s << 6) | (pos & 63);
-                const GenPath g = gen_path(fa, sv, i);
+                ps = camera_path(fa, sv, i);
                 L[i] = make_float4(0, 0, 0, 0);
-                ps.o = g.o;
-                ps.d = g.d;
-                ps.counter = g.counter;
-                ps.seed = g.seed;
-                ps.depth = g.depth;
-                ps.slot = i;
-                ps.contrib = mk(1, 1, 1); // init_pt_raypayload (technique/pathtracer.art:33-38)
-                ps.inv_pdf = 0;
-                ps.eta = 1.0f;
-                ps.inside = -1;
             } else {
                 ps = load_path(in, stream_index(s, pos, sc.a, in.shard_cap));
             }
@@ -763,6 +797,27 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
                 trace_path_ray<STATS, V>(sv, ps.inside, ps.o, ps.d, tmin, tmax, rflags, ts, hit_ent, hit_prim, hu, hv, st);
                 if (hit_ent >= 0) st.hits++;
             }
+#ifdef IGX_KIND_PROBE
+            {
+                // dev probe: how often a wave shades specular and non-specular
+                // hits together (slots 16-19: waves, mixed waves, lanes of the
+                // minority kind, mixed waves of class B)
+                int kind = 0;
+                if (act && hit_ent >= 0) {
+                    const int mat = reinterpret_cast<const int4*>(sv.ent + ENT_STRIDE * hit_ent + 6)->y;
+                    kind = bsdf_is_specular<variant_full(V)>(sv.mats[mat]) ? 2 : 3;
+                }
+                const uint64_t bsp = __ballot(kind == 2), bdf = __ballot(kind == 3), bact = __ballot(act);
+                if (lane_id() == 0 && bact) {
+                    const int a = __popcll(bsp), b = __popcll(bdf);
+                    const bool mixed = a && b, cls_b = !gen && p0 >= sc.a;
+                    st.cyc[0] += 1;
+                    st.cyc[1] += mixed;
+                    st.cyc[2] += a < b ? a : b;
+                    st.cyc[3] += mixed && cls_b;
+                }
+            }
+#endif
 #ifdef IGX_SHADE_PROBE
             phase_mark(st, t_last, 0);
 #else
@@ -786,7 +841,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
 #endif
         }
         int dst, sdst;
-        wave_append_paths(alive, path_class_b(fa.classify, sv, ps), has_shadow,
+        wave_append_paths(alive, path_class_b(fa.classify, fa.class_shrink, sv, ps), has_shadow,
                           has_shadow && shadow_class_b(fa.shadow_classes, sv, sr.o, sr.d, sr.tmax), c_out, c_sh, out.shard_cap,
                           sh.shard_cap, dst, sdst);
         if (alive) store_path(out, s * out.shard_cap + dst, ps);
@@ -804,6 +859,160 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
 #endif
     }
     if (STATS) flush_stats<STATS>(st, kc.stats, 0, true);
+}
+
+// ---------------------------------------------------------------------------
+// Block-regrouped extend (option "regroup", dynamic distribution only): the
+// shading half of a bounce diverges when one wave holds hits of different
+// kinds -- a dielectric lane idles through the diffuse lanes' NEE sample
+// (light sample, BSDF evaluation) and both BSDF samplers run in turn.  Here
+// the block's four waves first trace their groups, then sort the block's hits
+// by kind (miss / specular / non-specular) with a counting sort through LDS,
+// and lane j shades the j-th hit of that order, so at most two of the four
+// waves shade mixed kinds.  The exchange record (stream index, shard, hit)
+// lives in the traversal stack's LDS, idle between the two halves; the
+// shading lane reloads the path record (just read, so from L2) or rebuilds
+// the camera path.  Survivors and shadow rays still go to the shard their
+// path came from (per distinct shard of the wave, wave_append_paths), so
+// shard capacities hold; the streams' order changes, not the image (each
+// path's arithmetic is the same, radiance is per path slot).
+// ---------------------------------------------------------------------------
+constexpr int RG_KEYS = 4;  // 0 miss, 1 specular, 2 non-specular hit, 3 nothing to shade
+constexpr int RG_FIELDS = 7; // stream (or camera) index, shard, entity, primitive, t, u, v
+static_assert(RG_FIELDS * BLOCK <= LDS_STACK * BLOCK, "the exchange record fits the stack's LDS");
+
+template <int V>
+__device__ __forceinline__ int shading_key(const SceneView& sv, int hit_ent) {
+    if (hit_ent < 0) return 0;
+    const int mat = reinterpret_cast<const int4*>(sv.ent + ENT_STRIDE * hit_ent + 6)->y;
+    return bsdf_is_specular<variant_full(V)>(sv.mats[mat]) ? 1 : 2;
+}
+
+template <int V0, bool LDS>
+__global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(V0) ? EXTEND_WAVES_FULL : EXTEND_WAVES)) k_extend_rg(FrameArgs fa, SceneView gsv, PathBuf in, PathBuf out, ShadowBuf sh,
+                                                  float4* L, KernelCounters kc, int tail_threshold) {
+    constexpr int V = kernel_variant(V0, LDS);
+    __shared__ int stack_mem[LDS_STACK * BLOCK];
+    __shared__ int key_count[WAVES_PER_BLOCK][RG_KEYS];
+    extern __shared__ float4 lds_scene[];
+    const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
+    const bool gen = fa.gen_n > 0;
+    if (!gen && row_total(kc.cnt_in) <= tail_threshold) return; // block-uniform
+    const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : stage_treelet<BLOCK>(gsv, lds_scene);
+    TraceStats st{0, 0, 0, 0, 0, 0, 0};
+    const WaveWork w = wave_work();
+    const int wv = (int)(threadIdx.x >> 6), lane = lane_id();
+    const uint64_t below = (1ull << lane) - 1ull;
+    int* const ex = stack_mem; // ex[f * BLOCK + j]: field f of the j-th hit in kind order
+    int s = w.s;
+    auto count_of = [&](int sh_) {
+        return gen ? ShardCount{gen_shard_count(fa.gen_n, sh_), gen_shard_count(fa.gen_n, sh_)} : shard_count(kc.cnt_in, sh_);
+    };
+    ShardCount sc = count_of(s);
+    uint64_t done = 0;
+    bool drained = false;
+    for (;;) {
+        int g = -1;
+        if (!drained) {
+            g = take_group(kc.work, s, done, sc.n, [&](int sh_) {
+                sc = count_of(sh_);
+                return sc.n;
+            });
+            drained = g < 0;
+        }
+        // every wave of the block runs the same number of rounds (the sort's
+        // barriers); also orders the previous round's exchange reads before
+        // this round's traversal stacks
+        if (!__syncthreads_or(g >= 0)) break;
+        // -- trace --
+        const int pos = g * 64 + lane;
+        int idx = -1, key = 3, hit_ent = -1, hit_prim = -1;
+        float tmax = 0, hu = 0, hv = 0;
+        if (g >= 0 && pos < sc.n) {
+            PathState ps;
+            if (gen) {
+                idx = ((pos >> 6) << 12) | (s << 6) | (pos & 63);
+                ps = camera_path(fa, sv, idx);
+            } else {
+                idx = stream_index(s, pos, sc.a, in.shard_cap);
+                ps = load_path(in, idx);
+            }
+            if (ps.depth > 0) {
+                float tmin;
+                uint32_t rflags;
+                ray_extent(fa, sv, ps.depth, ps.slot, tmin, tmax, rflags);
+                trace_path_ray<false, V>(sv, ps.inside, ps.o, ps.d, tmin, tmax, rflags, ts, hit_ent, hit_prim, hu, hv, st);
+                key = shading_key<V>(sv, hit_ent);
+            } else if (gen) {
+                L[idx] = make_float4(0, 0, 0, 0); // a padding slot: nothing to shade
+            }
+        }
+        // -- counting sort of the block's hits by kind --
+        const uint64_t b0 = __ballot(key == 0), b1 = __ballot(key == 1), b2 = __ballot(key == 2);
+        if (lane == 0) {
+            key_count[wv][0] = __popcll(b0);
+            key_count[wv][1] = __popcll(b1);
+            key_count[wv][2] = __popcll(b2);
+        }
+        __syncthreads(); // every traversal done (the stacks are free), counts visible
+        int total = 0, dst = 0;
+        for (int k = 0; k < RG_KEYS - 1; ++k)
+            for (int v = 0; v < WAVES_PER_BLOCK; ++v) {
+                const int c = key_count[v][k];
+                if (k < key || (k == key && v < wv)) dst += c;
+                total += c;
+            }
+        if (key < 3) {
+            dst += __popcll((key == 0 ? b0 : key == 1 ? b1 : b2) & below);
+            ex[0 * BLOCK + dst] = idx;
+            ex[1 * BLOCK + dst] = s;
+            ex[2 * BLOCK + dst] = hit_ent;
+            ex[3 * BLOCK + dst] = hit_prim;
+            ex[4 * BLOCK + dst] = __float_as_int(tmax);
+            ex[5 * BLOCK + dst] = __float_as_int(hu);
+            ex[6 * BLOCK + dst] = __float_as_int(hv);
+        }
+        __syncthreads();
+        // -- shade the j-th hit of the order --
+        const int j = (int)threadIdx.x;
+        bool alive = false, has_shadow = false;
+        int my_s = -1;
+        PathState ps;
+        ShadowRec sr;
+        if (j < total) {
+            const int i = ex[0 * BLOCK + j];
+            my_s = ex[1 * BLOCK + j];
+            ps = gen ? camera_path(fa, sv, i) : load_path(in, i);
+            f3 Lacc;
+            bool has_l;
+            alive = shade_step<variant_full(V)>(fa, sv, ps, ex[2 * BLOCK + j], ex[3 * BLOCK + j], __int_as_float(ex[4 * BLOCK + j]),
+                                                __int_as_float(ex[5 * BLOCK + j]), __int_as_float(ex[6 * BLOCK + j]), Lacc,
+                                                has_l, has_shadow, sr);
+            if (gen)
+                L[i] = make_float4(0.0f + Lacc.x, 0.0f + Lacc.y, 0.0f + Lacc.z, 0); // add_radiance onto the cleared slot
+            else if (has_l)
+                add_radiance(L, ps.slot, Lacc);
+        }
+        // -- append, once per distinct shard among the wave's lanes --
+        const bool cls_b = alive && path_class_b(fa.classify, fa.class_shrink, sv, ps);
+        const bool sh_b = has_shadow && shadow_class_b(fa.shadow_classes, sv, sr.o, sr.d, sr.tmax);
+        uint64_t pending = __ballot(alive || has_shadow);
+        while (pending) {
+            const int cur = __shfl(my_s, __ffsll((unsigned long long)pending) - 1);
+            const bool mine = (alive || has_shadow) && my_s == cur;
+            int pdst, sdst;
+            wave_append_paths(alive && mine, cls_b, has_shadow && mine, sh_b, kc.cnt_out + cur * CSTRIDE,
+                              kc.cnt_shadow + cur * CSTRIDE, out.shard_cap, sh.shard_cap, pdst, sdst);
+            if (mine && alive) store_path(out, cur * out.shard_cap + pdst, ps);
+            if (mine && has_shadow) {
+                const int e = cur * sh.shard_cap + sdst;
+                sh.s0[e] = make_float4(sr.o.x, sr.o.y, sr.o.z, __int_as_float(ps.slot));
+                sh.s1[e] = make_float4(sr.d.x, sr.d.y, sr.d.z, sr.tmax);
+                sh.s2[e] = make_float4(sr.color.x, sr.color.y, sr.color.z, 0);
+            }
+            pending &= ~__ballot(mine);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -877,7 +1086,7 @@ __global__ void __launch_bounds__(BLOCK) k_shade(FrameArgs fa, SceneView sv, Pat
             }
         }
         int dst, sdst;
-        wave_append_paths(alive, path_class_b(fa.classify, sv, ps), has_shadow,
+        wave_append_paths(alive, path_class_b(fa.classify, fa.class_shrink, sv, ps), has_shadow,
                           has_shadow && shadow_class_b(fa.shadow_classes, sv, sr.o, sr.d, sr.tmax), c_out, c_sh, out.shard_cap,
                           sh.shard_cap, dst, sdst);
         if (alive) store_path(out, w.s * out.shard_cap + dst, ps);
@@ -1515,6 +1724,10 @@ struct igx_device {
     // (diamond frame 132.5 -> 119.3 ms, k_extend 1770 -> 1591 us per launch,
     // bit-identical)
     int classify_opt = 3;
+    float class_shrink = 0.0f;  // option "class_ellipsoid_pct" / 100 (FrameArgs::class_shrink)
+    // option "regroup": k_extend_rg sorts each block's hits by shading kind
+    // before shading (dynamic distribution only)
+    bool regroup_opt = false;
     // option "shadow_classes": shadow rays whose segment crosses an enclosing
     // entity's box apart from the rest (shadow_class_b), 0/1: diamond shadow
     // time 26.9 -> 21.7 ms per frame, frame 121.1 -> 118.4 ms, bit-identical
@@ -1779,6 +1992,22 @@ inline bool use_shadow_ifif(const igx_device* dev) {
 template <bool STATS>
 void launch_extend(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const PathBuf& in, const PathBuf& out,
                    const KernelCounters& kc, int tail) {
+    if constexpr (!STATS) {
+        if (dev->regroup_opt && fa.dynamic) { // block-regrouped shading (k_extend_rg)
+            SceneView tsv = dev->sv;
+            tsv.tree_n = dev->tree_ext;
+#define L_RG(S)                                                                                                          \
+    if (dev->lds_scene_bytes)                                                                                            \
+        hipLaunchKernelGGL((k_extend_rg<S, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->stream, fa, dev->sv, \
+                           in, out, s.sh, s.L, kc, tail);                                                                \
+    else                                                                                                                 \
+        hipLaunchKernelGGL((k_extend_rg<S, false>), dim3(grid), dim3(BLOCK), tree_bytes(dev, tsv.tree_n), dev->stream, fa, \
+                           tsv, in, out, s.sh, s.L, kc, tail)
+            IGX_DISPATCH_VARIANT8(dev->variant, L_RG);
+#undef L_RG
+            return;
+        }
+    }
     if (dev->lds_scene_bytes) {
 #define L_EXTL(S) hipLaunchKernelGGL((k_extend<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->stream, fa, dev->sv, in, out, s.sh, s.L, kc, tail)
         IGX_DISPATCH_VARIANT8(dev->variant, L_EXTL);
@@ -2264,6 +2493,11 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     else if (k == "path_classes") {
         if (value < 0 || value > 3) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "path_classes must be 0, 1, 2 or 3");
         dev->classify_opt = (int)value;
+    }
+    else if (k == "regroup") dev->regroup_opt = value != 0;
+    else if (k == "class_ellipsoid_pct") {
+        if (value < 0 || value > 200) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "class_ellipsoid_pct must be in [0, 200]");
+        dev->class_shrink = (float)value / 100.0f;
     }
     else if (k == "sah_node_cost_pct") {
         if (value < 10 || value > 2000) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "sah_node_cost_pct must be in [10, 2000]");
@@ -2993,6 +3227,7 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
     fa.seed = p->seed;
     fa.inv_spi = 1.0f / (float)p->spi;
     fa.classify = dev->classify_opt;
+    fa.class_shrink = dev->class_shrink;
     fa.shadow_classes = dev->shadow_classes_opt;
     fa.dynamic = dev->dynamic_opt & DYN_EXTEND;
     long long local_pixels;
