@@ -55,9 +55,13 @@ def parse():
 # Tables up to half the 256 MiB Infinity Cache count as on-chip: a table stays resident only while it and
 # everything streamed between two uses of a line fit the cache (MI355X_MICROARCH.md, Infinity Cache)
 MALL_BYTES = 128 << 20
-# N > 1: device memory per handle for its two stream slots (a rank holds two
-# handles); 20 GB bounds a chunk at 51 M paths, 196 B each per slot
-SLOT_BUDGET_MB = int(os.environ.get("IGX_SLOT_BUDGET_MB", "20000"))
+# N > 1: a rank holds two handles, each with ONE stream slot (option
+# stream_slots) sized to the rank's share of a frame, which is one chunk:
+# N = 2: 128 M paths = 25 GB per handle, 8: 6.3 GB.  A budget below the share
+# splits a frame into chunks and costs time (slot_budget_mb 20000 at N = 2:
+# 67.3 vs 55.2 ms per rank frame, profiles/r03_exp_classes_regroup_slots.log);
+# IGX_SLOT_BUDGET_MB caps it anyway (0 = auto)
+SLOT_BUDGET_MB = int(os.environ.get("IGX_SLOT_BUDGET_MB", "0"))
 
 
 def algorithmic_bytes(inst, st):
@@ -334,9 +338,9 @@ def main():
     if n_gpus > 1:
         devs.append(ignis_amd.Device(gpu))
         devs[1].upload(scene)
-        # each handle's stream slots sized to the rank's share: two handles in
-        # 2 x SLOT_BUDGET_MB (the auto size is a quarter of HBM per handle)
+        # one stream slot per handle, sized to the rank's share of a frame
         for d in devs:
+            d.set_option("stream_slots", 1)
             d.set_option("slot_budget_mb", SLOT_BUDGET_MB)
     pending = []
     count = [0]

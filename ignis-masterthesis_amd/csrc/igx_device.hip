@@ -67,7 +67,6 @@ constexpr int SLOT_BITS = 27;
 constexpr uint32_t SLOT_MASK = (1u << SLOT_BITS) - 1;
 [[maybe_unused]] constexpr int MAX_ENCLOSING = 31;
 static_assert(MAX_CHUNK_PATHS <= (1ll << SLOT_BITS), "path slots must fit the slot bits");
-[[maybe_unused]] constexpr long long PATH_SLOT_BYTES = 2 * 56 + 48 + 20 + 16; // two path buffers, shadow ray, hit record, radiance
 // Occupancy target (waves per SIMD) of k_extend, with global and with
 // LDS-staged traversal tables: 4 caps it at 128 VGPRs.  k_finish keeps the
 // compiler's choice (it would spill).
@@ -105,6 +104,7 @@ struct PathBuf {
     float4* p2; // contrib.rgb, inv_pdf
     float2* p3; // eta, RNG seed (uint bits): hashed once by k_generate, not per bounce
     int shard_cap;
+    int c_base; // record index of the class-C region (FrameArgs::classify 4), 0: none
 };
 struct ShadowBuf {
     float4* s0; // org.xyz, slot
@@ -130,7 +130,6 @@ struct FrameArgs {
     int classify;        // surviving paths' stream class (see wave_append_paths): 0 all A, 1 B = inside a dielectric (eta != 1), 2 B = after a specular event
     int dynamic;         // k_extend: waves take 64-path groups from per-shard work counters (KernelCounters::work)
     int shadow_classes;  // shadow rays crossing an enclosing entity's box go to the back of their shard (shadow_class_b)
-    float class_shrink;  // > 0: class 3 tests the box's inscribed ellipsoid scaled by this instead of the box
 };
 
 // path slot -> (local pixel, sample, iteration): slots run over the chunk's
@@ -178,7 +177,7 @@ static_assert(BLOCK == TSTACK_STRIDE, "traversal stacks are laid out for BLOCK t
 // shard, class B from its back, wave_append_paths); other streams leave the
 // second word 0.
 __device__ __forceinline__ int row_total(const int* row) {
-    int v = row[lane_id() * CSTRIDE] + row[lane_id() * CSTRIDE + 1];
+    int v = row[lane_id() * CSTRIDE] + row[lane_id() * CSTRIDE + 1] + row[lane_id() * CSTRIDE + 2];
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
     return __builtin_amdgcn_readfirstlane(v);
 }
@@ -205,40 +204,52 @@ __device__ __forceinline__ int gen_shard_count(int n, int s) {
     return (n >> 12) * 64 + (rem < 0 ? 0 : (rem > 64 ? 64 : rem));
 }
 
-// Records of path-stream shard s: `a` of class A at offsets [0, a) and n - a
-// of class B at offsets shard_cap - 1 down to shard_cap - (n - a); position
-// pos in [0, n) of the shard maps to stream index stream_index(s, pos, ...), so
+// Records of path-stream shard s: `a` of class A at offsets [0, a) and ab - a
+// of class B at offsets shard_cap - 1 down to shard_cap - (ab - a); with a
+// class-C region (PathBuf::c_base, FrameArgs::classify 4) n - ab of class C
+// at its offsets [0, n - ab).  Position pos in [0, n) of the shard maps to
+// stream index path_index(...) (stream_index for two-class streams), so
 // consecutive positions, and so the 64 paths of one wave, share a class.
 struct ShardCount {
-    int a, n;
+    int a, ab, n;
 };
 __device__ __forceinline__ ShardCount shard_count(const int* cnt, int s) {
     const int a = uniform_load(cnt + s * CSTRIDE), b = uniform_load(cnt + s * CSTRIDE + 1);
-    return ShardCount{a, a + b};
+    const int c = uniform_load(cnt + s * CSTRIDE + 2);
+    return ShardCount{a, a + b, a + b + c};
 }
 __device__ __forceinline__ int stream_index(int s, int pos, int a, int shard_cap) {
     return s * shard_cap + (pos < a ? pos : shard_cap - 1 - (pos - a));
 }
+__device__ __forceinline__ int path_index(const PathBuf& b, int s, int pos, const ShardCount& sc) {
+    return pos < sc.ab ? stream_index(s, pos, sc.a, b.shard_cap) : b.c_base + s * b.shard_cap + (pos - sc.ab);
+}
 
 // Wave-level compaction of the surviving paths (class A appended from the
-// front of the wave's shard, class B from its back: the next bounce's waves
-// then trace paths of one class, e.g. all inside a dielectric) and of the
-// shadow rays: one returning 64-bit atomic per stream (a/b counts in the two
-// words), lanes 0 and 1 issue both in one instruction; positions inside the
-// wave by ballot prefix.  Needs every lane of the wave active.
-__device__ __forceinline__ void wave_append_paths(bool alive, bool cls_b, bool shadow, bool sh_b, int* cp, int* cs,
-                                                  int shard_cap, int sh_cap, int& dst, int& sdst) {
+// front of the wave's shard, class B from its back, class C from the front
+// of the shard's class-C region: the next bounce's waves then trace paths of
+// one class, e.g. all inside a dielectric) and of the shadow rays (A front,
+// B back): one returning 64-bit atomic per counter (a/b counts in its two
+// words; the class-C count in word 2), lanes 0-2 issue them in one
+// instruction; positions inside the wave by ballot prefix.  `dst` is the
+// record offset from the start of the shard (c_base added for class C).
+// Needs every lane of the wave active.
+__device__ __forceinline__ void wave_append_paths(bool alive, int cls, bool shadow, bool sh_b, int* cp, int* cs,
+                                                  int shard_cap, int c_base, int sh_cap, int& dst, int& sdst) {
     const int lane = lane_id();
-    const uint64_t ma = __ballot(alive && !cls_b), mb = __ballot(alive && cls_b);
+    const uint64_t ma = __ballot(alive && cls == 0), mb = __ballot(alive && cls == 1), mc = __ballot(alive && cls == 2);
     const uint64_t sa = __ballot(shadow && !sh_b), sb = __ballot(shadow && sh_b);
     const uint64_t below = (1ull << lane) - 1ull;
-    const unsigned long long want = lane == 0 ? ((unsigned long long)__popcll(ma) | ((unsigned long long)__popcll(mb) << 32))
-                                              : ((unsigned long long)__popcll(sa) | ((unsigned long long)__popcll(sb) << 32));
+    const unsigned long long want = lane == 0   ? ((unsigned long long)__popcll(ma) | ((unsigned long long)__popcll(mb) << 32))
+                                    : lane == 1 ? ((unsigned long long)__popcll(sa) | ((unsigned long long)__popcll(sb) << 32))
+                                                : (unsigned long long)__popcll(mc);
     unsigned long long r = 0;
-    if (lane < 2 && want != 0) r = atomicAdd(reinterpret_cast<unsigned long long*>(lane == 0 ? cp : cs), want);
+    if (lane < 3 && want != 0) r = atomicAdd(reinterpret_cast<unsigned long long*>(lane == 0 ? cp : lane == 1 ? cs : cp + 2), want);
     const int lo = (int)(uint32_t)r, hi = (int)(uint32_t)(r >> 32);
-    const int a0 = __shfl(lo, 0), b0 = __shfl(hi, 0), s0 = __shfl(lo, 1), t0 = __shfl(hi, 1);
-    dst = cls_b ? shard_cap - 1 - (b0 + __popcll(mb & below)) : a0 + __popcll(ma & below);
+    const int a0 = __shfl(lo, 0), b0 = __shfl(hi, 0), s0 = __shfl(lo, 1), t0 = __shfl(hi, 1), c0 = __shfl(lo, 2);
+    dst = cls == 1   ? shard_cap - 1 - (b0 + __popcll(mb & below))
+          : cls == 2 ? c_base + c0 + __popcll(mc & below)
+                     : a0 + __popcll(ma & below);
     sdst = sh_b ? sh_cap - 1 - (t0 + __popcll(sb & below)) : s0 + __popcll(sa & below);
 }
 
@@ -377,35 +388,16 @@ __device__ __forceinline__ bool shadow_class_b(int enabled, const SceneView& sv,
     }
     return hit;
 }
-// the same question against the ellipsoid inscribed in the box, its semi-axes
-// scaled by `s`: a closer guess of "this ray will shade the dielectric" for
-// gem-like shapes whose box corners are empty (no square root: the line meets
-// the ellipsoid iff the discriminant is >= 0, and the far root is >= 0 iff the
-// origin is inside or the ray points towards the centre)
-__device__ __forceinline__ bool crosses_enclosing_ellipsoid(const SceneView& sv, f3 o, f3 d, float s) {
-    bool hit = false;
-    for (int k = 0; k < sv.num_enc && !hit; ++k) {
-        const float4 lo = sv.enc_box[2 * k], hi = sv.enc_box[2 * k + 1];
-        const float ix = __builtin_amdgcn_rcpf(0.5f * s * (hi.x - lo.x));
-        const float iy = __builtin_amdgcn_rcpf(0.5f * s * (hi.y - lo.y));
-        const float iz = __builtin_amdgcn_rcpf(0.5f * s * (hi.z - lo.z));
-        const float ox = (o.x - 0.5f * (lo.x + hi.x)) * ix, oy = (o.y - 0.5f * (lo.y + hi.y)) * iy,
-                    oz = (o.z - 0.5f * (lo.z + hi.z)) * iz;
-        const float dx = d.x * ix, dy = d.y * iy, dz = d.z * iz;
-        const float a = dx * dx + dy * dy + dz * dz;
-        const float b = ox * dx + oy * dy + oz * dz;
-        const float c = ox * ox + oy * oy + oz * oz - 1.0f;
-        hit = b * b - a * c >= 0.0f && (c <= 0.0f || b <= 0.0f);
-    }
-    return hit;
-}
-__device__ __forceinline__ bool path_class_b(int classify, float shrink, const SceneView& sv, const PathState& ps) {
+// 4: three classes, C = inside a dielectric, B = its next ray crosses an
+// enclosing entity's world box, A = the rest (the fused schedule only: the
+// split schedule's hit records have no class-C region)
+__device__ __forceinline__ int path_class(int classify, const SceneView& sv, const PathState& ps) {
     switch (classify) {
     case 1: return ps.eta != 1.0f;
     case 2: return ps.inv_pdf == 0.0f;
-    case 3: return ps.eta != 1.0f || (shrink > 0.0f ? crosses_enclosing_ellipsoid(sv, ps.o, ps.d, shrink)
-                                                     : crosses_enclosing_box(sv, ps.o, ps.d));
-    default: return false;
+    case 3: return ps.eta != 1.0f || crosses_enclosing_box(sv, ps.o, ps.d);
+    case 4: return ps.eta != 1.0f ? 2 : crosses_enclosing_box(sv, ps.o, ps.d);
+    default: return 0;
     }
 }
 
@@ -594,9 +586,6 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
 // a read of the counter) since the previous mark is added to phase k; marks
 // sit at wave-uniform points.
 __device__ __forceinline__ void phase_mark(TraceStats& st, unsigned long long& last, int k) {
-#ifdef IGX_KIND_PROBE // the four slots count shading-kind mixing instead (k_extend below)
-    return;
-#endif
     const unsigned long long now = __builtin_amdgcn_s_memtime();
     st.cyc[k] += now - last;
     last = now;
@@ -736,7 +725,11 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
     // to the shard the group came from (its output never exceeds its input).
     int s = w.s;
     auto count_of = [&](int sh_) {
-        return gen ? ShardCount{gen_shard_count(fa.gen_n, sh_), gen_shard_count(fa.gen_n, sh_)} : shard_count(kc.cnt_in, sh_);
+        if (gen) {
+            const int g = gen_shard_count(fa.gen_n, sh_);
+            return ShardCount{g, g, g};
+        }
+        return shard_count(kc.cnt_in, sh_);
     };
     ShardCount sc = count_of(s);
     uint64_t done = 0; // shards this wave knows to be exhausted (dynamic)
@@ -772,7 +765,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
                 ps = camera_path(fa, sv, i);
                 L[i] = make_float4(0, 0, 0, 0);
             } else {
-                ps = load_path(in, stream_index(s, pos, sc.a, in.shard_cap));
+                ps = load_path(in, path_index(in, s, pos, sc));
             }
             if (!STATS && ps.depth > 0) {
                 f3 Lacc;
@@ -797,27 +790,6 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
                 trace_path_ray<STATS, V>(sv, ps.inside, ps.o, ps.d, tmin, tmax, rflags, ts, hit_ent, hit_prim, hu, hv, st);
                 if (hit_ent >= 0) st.hits++;
             }
-#ifdef IGX_KIND_PROBE
-            {
-                // dev probe: how often a wave shades specular and non-specular
-                // hits together (slots 16-19: waves, mixed waves, lanes of the
-                // minority kind, mixed waves of class B)
-                int kind = 0;
-                if (act && hit_ent >= 0) {
-                    const int mat = reinterpret_cast<const int4*>(sv.ent + ENT_STRIDE * hit_ent + 6)->y;
-                    kind = bsdf_is_specular<variant_full(V)>(sv.mats[mat]) ? 2 : 3;
-                }
-                const uint64_t bsp = __ballot(kind == 2), bdf = __ballot(kind == 3), bact = __ballot(act);
-                if (lane_id() == 0 && bact) {
-                    const int a = __popcll(bsp), b = __popcll(bdf);
-                    const bool mixed = a && b, cls_b = !gen && p0 >= sc.a;
-                    st.cyc[0] += 1;
-                    st.cyc[1] += mixed;
-                    st.cyc[2] += a < b ? a : b;
-                    st.cyc[3] += mixed && cls_b;
-                }
-            }
-#endif
 #ifdef IGX_SHADE_PROBE
             phase_mark(st, t_last, 0);
 #else
@@ -841,9 +813,9 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
 #endif
         }
         int dst, sdst;
-        wave_append_paths(alive, path_class_b(fa.classify, fa.class_shrink, sv, ps), has_shadow,
+        wave_append_paths(alive, path_class(fa.classify, sv, ps), has_shadow,
                           has_shadow && shadow_class_b(fa.shadow_classes, sv, sr.o, sr.d, sr.tmax), c_out, c_sh, out.shard_cap,
-                          sh.shard_cap, dst, sdst);
+                          out.c_base, sh.shard_cap, dst, sdst);
         if (alive) store_path(out, s * out.shard_cap + dst, ps);
         if (has_shadow) {
             const int e = s * sh.shard_cap + sdst;
@@ -859,160 +831,6 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
 #endif
     }
     if (STATS) flush_stats<STATS>(st, kc.stats, 0, true);
-}
-
-// ---------------------------------------------------------------------------
-// Block-regrouped extend (option "regroup", dynamic distribution only): the
-// shading half of a bounce diverges when one wave holds hits of different
-// kinds -- a dielectric lane idles through the diffuse lanes' NEE sample
-// (light sample, BSDF evaluation) and both BSDF samplers run in turn.  Here
-// the block's four waves first trace their groups, then sort the block's hits
-// by kind (miss / specular / non-specular) with a counting sort through LDS,
-// and lane j shades the j-th hit of that order, so at most two of the four
-// waves shade mixed kinds.  The exchange record (stream index, shard, hit)
-// lives in the traversal stack's LDS, idle between the two halves; the
-// shading lane reloads the path record (just read, so from L2) or rebuilds
-// the camera path.  Survivors and shadow rays still go to the shard their
-// path came from (per distinct shard of the wave, wave_append_paths), so
-// shard capacities hold; the streams' order changes, not the image (each
-// path's arithmetic is the same, radiance is per path slot).
-// ---------------------------------------------------------------------------
-constexpr int RG_KEYS = 4;  // 0 miss, 1 specular, 2 non-specular hit, 3 nothing to shade
-constexpr int RG_FIELDS = 7; // stream (or camera) index, shard, entity, primitive, t, u, v
-static_assert(RG_FIELDS * BLOCK <= LDS_STACK * BLOCK, "the exchange record fits the stack's LDS");
-
-template <int V>
-__device__ __forceinline__ int shading_key(const SceneView& sv, int hit_ent) {
-    if (hit_ent < 0) return 0;
-    const int mat = reinterpret_cast<const int4*>(sv.ent + ENT_STRIDE * hit_ent + 6)->y;
-    return bsdf_is_specular<variant_full(V)>(sv.mats[mat]) ? 1 : 2;
-}
-
-template <int V0, bool LDS>
-__global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(V0) ? EXTEND_WAVES_FULL : EXTEND_WAVES)) k_extend_rg(FrameArgs fa, SceneView gsv, PathBuf in, PathBuf out, ShadowBuf sh,
-                                                  float4* L, KernelCounters kc, int tail_threshold) {
-    constexpr int V = kernel_variant(V0, LDS);
-    __shared__ int stack_mem[LDS_STACK * BLOCK];
-    __shared__ int key_count[WAVES_PER_BLOCK][RG_KEYS];
-    extern __shared__ float4 lds_scene[];
-    const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
-    const bool gen = fa.gen_n > 0;
-    if (!gen && row_total(kc.cnt_in) <= tail_threshold) return; // block-uniform
-    const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : stage_treelet<BLOCK>(gsv, lds_scene);
-    TraceStats st{0, 0, 0, 0, 0, 0, 0};
-    const WaveWork w = wave_work();
-    const int wv = (int)(threadIdx.x >> 6), lane = lane_id();
-    const uint64_t below = (1ull << lane) - 1ull;
-    int* const ex = stack_mem; // ex[f * BLOCK + j]: field f of the j-th hit in kind order
-    int s = w.s;
-    auto count_of = [&](int sh_) {
-        return gen ? ShardCount{gen_shard_count(fa.gen_n, sh_), gen_shard_count(fa.gen_n, sh_)} : shard_count(kc.cnt_in, sh_);
-    };
-    ShardCount sc = count_of(s);
-    uint64_t done = 0;
-    bool drained = false;
-    for (;;) {
-        int g = -1;
-        if (!drained) {
-            g = take_group(kc.work, s, done, sc.n, [&](int sh_) {
-                sc = count_of(sh_);
-                return sc.n;
-            });
-            drained = g < 0;
-        }
-        // every wave of the block runs the same number of rounds (the sort's
-        // barriers); also orders the previous round's exchange reads before
-        // this round's traversal stacks
-        if (!__syncthreads_or(g >= 0)) break;
-        // -- trace --
-        const int pos = g * 64 + lane;
-        int idx = -1, key = 3, hit_ent = -1, hit_prim = -1;
-        float tmax = 0, hu = 0, hv = 0;
-        if (g >= 0 && pos < sc.n) {
-            PathState ps;
-            if (gen) {
-                idx = ((pos >> 6) << 12) | (s << 6) | (pos & 63);
-                ps = camera_path(fa, sv, idx);
-            } else {
-                idx = stream_index(s, pos, sc.a, in.shard_cap);
-                ps = load_path(in, idx);
-            }
-            if (ps.depth > 0) {
-                float tmin;
-                uint32_t rflags;
-                ray_extent(fa, sv, ps.depth, ps.slot, tmin, tmax, rflags);
-                trace_path_ray<false, V>(sv, ps.inside, ps.o, ps.d, tmin, tmax, rflags, ts, hit_ent, hit_prim, hu, hv, st);
-                key = shading_key<V>(sv, hit_ent);
-            } else if (gen) {
-                L[idx] = make_float4(0, 0, 0, 0); // a padding slot: nothing to shade
-            }
-        }
-        // -- counting sort of the block's hits by kind --
-        const uint64_t b0 = __ballot(key == 0), b1 = __ballot(key == 1), b2 = __ballot(key == 2);
-        if (lane == 0) {
-            key_count[wv][0] = __popcll(b0);
-            key_count[wv][1] = __popcll(b1);
-            key_count[wv][2] = __popcll(b2);
-        }
-        __syncthreads(); // every traversal done (the stacks are free), counts visible
-        int total = 0, dst = 0;
-        for (int k = 0; k < RG_KEYS - 1; ++k)
-            for (int v = 0; v < WAVES_PER_BLOCK; ++v) {
-                const int c = key_count[v][k];
-                if (k < key || (k == key && v < wv)) dst += c;
-                total += c;
-            }
-        if (key < 3) {
-            dst += __popcll((key == 0 ? b0 : key == 1 ? b1 : b2) & below);
-            ex[0 * BLOCK + dst] = idx;
-            ex[1 * BLOCK + dst] = s;
-            ex[2 * BLOCK + dst] = hit_ent;
-            ex[3 * BLOCK + dst] = hit_prim;
-            ex[4 * BLOCK + dst] = __float_as_int(tmax);
-            ex[5 * BLOCK + dst] = __float_as_int(hu);
-            ex[6 * BLOCK + dst] = __float_as_int(hv);
-        }
-        __syncthreads();
-        // -- shade the j-th hit of the order --
-        const int j = (int)threadIdx.x;
-        bool alive = false, has_shadow = false;
-        int my_s = -1;
-        PathState ps;
-        ShadowRec sr;
-        if (j < total) {
-            const int i = ex[0 * BLOCK + j];
-            my_s = ex[1 * BLOCK + j];
-            ps = gen ? camera_path(fa, sv, i) : load_path(in, i);
-            f3 Lacc;
-            bool has_l;
-            alive = shade_step<variant_full(V)>(fa, sv, ps, ex[2 * BLOCK + j], ex[3 * BLOCK + j], __int_as_float(ex[4 * BLOCK + j]),
-                                                __int_as_float(ex[5 * BLOCK + j]), __int_as_float(ex[6 * BLOCK + j]), Lacc,
-                                                has_l, has_shadow, sr);
-            if (gen)
-                L[i] = make_float4(0.0f + Lacc.x, 0.0f + Lacc.y, 0.0f + Lacc.z, 0); // add_radiance onto the cleared slot
-            else if (has_l)
-                add_radiance(L, ps.slot, Lacc);
-        }
-        // -- append, once per distinct shard among the wave's lanes --
-        const bool cls_b = alive && path_class_b(fa.classify, fa.class_shrink, sv, ps);
-        const bool sh_b = has_shadow && shadow_class_b(fa.shadow_classes, sv, sr.o, sr.d, sr.tmax);
-        uint64_t pending = __ballot(alive || has_shadow);
-        while (pending) {
-            const int cur = __shfl(my_s, __ffsll((unsigned long long)pending) - 1);
-            const bool mine = (alive || has_shadow) && my_s == cur;
-            int pdst, sdst;
-            wave_append_paths(alive && mine, cls_b, has_shadow && mine, sh_b, kc.cnt_out + cur * CSTRIDE,
-                              kc.cnt_shadow + cur * CSTRIDE, out.shard_cap, sh.shard_cap, pdst, sdst);
-            if (mine && alive) store_path(out, cur * out.shard_cap + pdst, ps);
-            if (mine && has_shadow) {
-                const int e = cur * sh.shard_cap + sdst;
-                sh.s0[e] = make_float4(sr.o.x, sr.o.y, sr.o.z, __int_as_float(ps.slot));
-                sh.s1[e] = make_float4(sr.d.x, sr.d.y, sr.d.z, sr.tmax);
-                sh.s2[e] = make_float4(sr.color.x, sr.color.y, sr.color.z, 0);
-            }
-            pending &= ~__ballot(mine);
-        }
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1035,7 +853,7 @@ __global__ void __launch_bounds__(BLOCK, WAVES) k_trace(FrameArgs fa, SceneView 
     const ShardCount sc = shard_count(cnt, w.s);
     const int ns = sc.n;
     for (int pos = w.k * 64 + lane_id(); pos < ns; pos += w.K * 64) {
-        const int i = stream_index(w.s, pos, sc.a, in.shard_cap);
+        const int i = path_index(in, w.s, pos, sc);
         float4 p0 = in.p0[i], p1 = in.p1[i];
         int depth = (int)(__float_as_uint(p1.w) >> 24);
         int hit_ent = -1, hit_prim = -1;
@@ -1069,7 +887,7 @@ __global__ void __launch_bounds__(BLOCK) k_shade(FrameArgs fa, SceneView sv, Pat
     int* const c_sh = kc.cnt_shadow + w.s * CSTRIDE;
     for (int p0 = w.k * 64; p0 < ns; p0 += w.K * 64) {
         const int pos = p0 + lane_id();
-        const int i = stream_index(w.s, pos, sc.a, in.shard_cap);
+        const int i = path_index(in, w.s, pos, sc);
         bool alive = false, has_shadow = false;
         PathState ps;
         ShadowRec sr;
@@ -1086,9 +904,9 @@ __global__ void __launch_bounds__(BLOCK) k_shade(FrameArgs fa, SceneView sv, Pat
             }
         }
         int dst, sdst;
-        wave_append_paths(alive, path_class_b(fa.classify, fa.class_shrink, sv, ps), has_shadow,
+        wave_append_paths(alive, path_class(fa.classify, sv, ps), has_shadow,
                           has_shadow && shadow_class_b(fa.shadow_classes, sv, sr.o, sr.d, sr.tmax), c_out, c_sh, out.shard_cap,
-                          sh.shard_cap, dst, sdst);
+                          out.c_base, sh.shard_cap, dst, sdst);
         if (alive) store_path(out, w.s * out.shard_cap + dst, ps);
         if (has_shadow) {
             const int e = w.s * sh.shard_cap + sdst;
@@ -1123,7 +941,7 @@ __global__ void __launch_bounds__(BLOCK) k_finish(FrameArgs fa, SceneView gsv, P
     const ShardCount sc = shard_count(cnt, w.s);
     const int ns = sc.n;
     for (int pos = w.k * 64 + lane_id(); pos < ns; pos += w.K * 64) {
-        PathState ps = load_path(in, stream_index(w.s, pos, sc.a, in.shard_cap));
+        PathState ps = load_path(in, path_index(in, w.s, pos, sc));
         if (ps.depth <= 0) continue;
         for (;;) {
             f3 Lacc;
@@ -1200,7 +1018,7 @@ __global__ void __launch_bounds__(BLOCK, FINISH_PAIRS_WAVES) k_finish_pairs(Fram
         const int pos = pos0 + (lane >> 1);
         PathState ps;
         ps.depth = 0;
-        if (path_lane && pos < ns) ps = load_path(in, stream_index(w.s, pos, sc.a, in.shard_cap));
+        if (path_lane && pos < ns) ps = load_path(in, path_index(in, w.s, pos, sc));
         bool tracing = path_lane && pos < ns && ps.depth > 0; // path lane: its current ray needs a closest hit
         bool sh_trace = false;                                  // odd lane: a shadow ray to trace
         bool had_shadow = false;                                // path lane: its last shadow ray is out
@@ -1382,7 +1200,7 @@ struct GroupSeq {
     __device__ __forceinline__ ShardCount count_of(int sh) const {
         if constexpr (CLASSES) return shard_count(cnt, sh);
         const int n = uniform_load(cnt + sh * CSTRIDE);
-        return ShardCount{n, n};
+        return ShardCount{n, n, n};
     }
     __device__ __forceinline__ void init(const int* cnt_, int* work_, int cap, const WaveWork& w_) {
         cnt = cnt_;
@@ -1669,7 +1487,7 @@ inline long long row_total(const Slot& s, int row) {
     if (row == 0) return s.n0;
     long long t = 0;
     const int* r = s.pinned + (size_t)row * CROW;
-    for (int k = 0; k < NSH; ++k) t += r[k * CSTRIDE] + r[k * CSTRIDE + 1]; // class A + class B (wave_append_paths)
+    for (int k = 0; k < NSH; ++k) t += r[k * CSTRIDE] + r[k * CSTRIDE + 1] + r[k * CSTRIDE + 2]; // classes A, B, C (wave_append_paths)
     return t;
 }
 
@@ -1689,9 +1507,14 @@ struct igx_device {
     bool instrument = false;
     int64_t capacity_opt = 0;
     // option "slot_budget_mb": device memory the two stream slots of this
-    // handle may take (0 = auto: a quarter of the device memory).  A rank of
-    // a multi-GPU render holds two handles (bench.py), each sized to its share
+    // handle may take (0 = auto: a quarter of the device memory)
     int64_t slot_budget_mb = 0;
+    // option "stream_slots": chunks alternate between two slots (chunk k + 1's
+    // bounces overlap chunk k's tail), or use one (half the memory; chunk k + 1
+    // waits for chunk k).  A rank of a multi-GPU render holds two handles that
+    // alternate frames, and a rank's share of a frame is one chunk, so there
+    // one slot per handle loses nothing: bench.py sets 1 at N > 1
+    int stream_slots = 2;
     // LDS treelet (stage_treelet) on global-table scenes: nodes staged per
     // kernel (the largest prefix of the hot order that keeps the kernel's
     // register-bound occupancy), recomputed when the scene or option changes.
@@ -1723,11 +1546,11 @@ struct igx_device {
     // 3: also paths whose next ray crosses an enclosing entity's world box
     // (diamond frame 132.5 -> 119.3 ms, k_extend 1770 -> 1591 us per launch,
     // bit-identical)
-    int classify_opt = 3;
-    float class_shrink = 0.0f;  // option "class_ellipsoid_pct" / 100 (FrameArgs::class_shrink)
-    // option "regroup": k_extend_rg sorts each block's hits by shading kind
-    // before shading (dynamic distribution only)
-    bool regroup_opt = false;
+    // 4: three classes, the paths inside a dielectric in their own region of
+    // the path buffers (class C), apart from those heading for the box (B):
+    // diamond frame 109.6 -> 106.4 ms, bit-identical; the split schedule
+    // falls back to 3 (its hit records have no class-C region)
+    int classify_opt = 4;
     // option "shadow_classes": shadow rays whose segment crosses an enclosing
     // entity's box apart from the rest (shadow_class_b), 0/1: diamond shadow
     // time 26.9 -> 21.7 ms per frame, frame 121.1 -> 118.4 ms, bit-identical
@@ -1873,14 +1696,18 @@ void free_slot_buffers(Slot& s) {
     s.shard_cap = 0;
 }
 
-igx_status ensure_slot(igx_device* dev, Slot& s, size_t cap) {
+// `hits`: the chunk runs the split schedule, whose k_trace writes a hit
+// record per path (20 B) for k_shade; the fused schedule needs none.
+// `region_c`: three path classes (FrameArgs::classify 4), so each path buffer
+// holds a second set of records for class C (PathBuf::c_base)
+igx_status ensure_slot(igx_device* dev, Slot& s, size_t cap, bool hits, bool region_c) {
     if (!s.ctr) {
         HIPCHK(hipMalloc((void**)&s.ctr, CTR_INTS * sizeof(int)));
         HIPCHK(hipHostMalloc((void**)&s.pinned, CTR_INTS * sizeof(int), hipHostMallocDefault));
         HIPCHK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
         std::memset(s.pinned, 0, CTR_INTS * sizeof(int));
     }
-    if (s.cap >= cap) return IGX_OK;
+    if (s.cap >= cap && (!hits || s.hb.h) && (!region_c || s.pa.c_base)) return IGX_OK;
     free_slot_buffers(s);
     // shard capacity: a generated chunk puts at most ceil(cap / (64 NSH)) groups
     // of 64 paths in one shard, and a shard's outputs never exceed its inputs
@@ -1888,14 +1715,18 @@ igx_status ensure_slot(igx_device* dev, Slot& s, size_t cap) {
     const size_t recs = (size_t)shard_cap * NSH;
     auto alloc4 = [&](float4** p, size_t k) -> igx_status { HIPCHK(hipMalloc((void**)p, k * sizeof(float4))); return IGX_OK; };
     igx_status st;
-    if ((st = alloc4(&s.pa.p0, recs)) || (st = alloc4(&s.pa.p1, recs)) || (st = alloc4(&s.pa.p2, recs))) return st;
-    HIPCHK(hipMalloc((void**)&s.pa.p3, recs * sizeof(float2)));
-    if ((st = alloc4(&s.pb.p0, recs)) || (st = alloc4(&s.pb.p1, recs)) || (st = alloc4(&s.pb.p2, recs))) return st;
-    HIPCHK(hipMalloc((void**)&s.pb.p3, recs * sizeof(float2)));
+    const size_t precs = region_c ? 2 * recs : recs;
+    if ((st = alloc4(&s.pa.p0, precs)) || (st = alloc4(&s.pa.p1, precs)) || (st = alloc4(&s.pa.p2, precs))) return st;
+    HIPCHK(hipMalloc((void**)&s.pa.p3, precs * sizeof(float2)));
+    if ((st = alloc4(&s.pb.p0, precs)) || (st = alloc4(&s.pb.p1, precs)) || (st = alloc4(&s.pb.p2, precs))) return st;
+    HIPCHK(hipMalloc((void**)&s.pb.p3, precs * sizeof(float2)));
+    s.pa.c_base = s.pb.c_base = region_c ? (int)recs : 0;
     if ((st = alloc4(&s.sh.s0, recs)) || (st = alloc4(&s.sh.s1, recs)) || (st = alloc4(&s.sh.s2, recs))) return st;
     if ((st = alloc4(&s.L, cap))) return st; // radiance is indexed by path slot, not sharded
-    if ((st = alloc4(&s.hb.h, recs))) return st;
-    HIPCHK(hipMalloc((void**)&s.hb.prim, recs * sizeof(int)));
+    if (hits) {
+        if ((st = alloc4(&s.hb.h, recs))) return st;
+        HIPCHK(hipMalloc((void**)&s.hb.prim, recs * sizeof(int)));
+    }
     s.pa.shard_cap = s.pb.shard_cap = s.sh.shard_cap = shard_cap;
     s.cap = cap;
     s.shard_cap = shard_cap;
@@ -1992,22 +1823,6 @@ inline bool use_shadow_ifif(const igx_device* dev) {
 template <bool STATS>
 void launch_extend(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const PathBuf& in, const PathBuf& out,
                    const KernelCounters& kc, int tail) {
-    if constexpr (!STATS) {
-        if (dev->regroup_opt && fa.dynamic) { // block-regrouped shading (k_extend_rg)
-            SceneView tsv = dev->sv;
-            tsv.tree_n = dev->tree_ext;
-#define L_RG(S)                                                                                                          \
-    if (dev->lds_scene_bytes)                                                                                            \
-        hipLaunchKernelGGL((k_extend_rg<S, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->stream, fa, dev->sv, \
-                           in, out, s.sh, s.L, kc, tail);                                                                \
-    else                                                                                                                 \
-        hipLaunchKernelGGL((k_extend_rg<S, false>), dim3(grid), dim3(BLOCK), tree_bytes(dev, tsv.tree_n), dev->stream, fa, \
-                           tsv, in, out, s.sh, s.L, kc, tail)
-            IGX_DISPATCH_VARIANT8(dev->variant, L_RG);
-#undef L_RG
-            return;
-        }
-    }
     if (dev->lds_scene_bytes) {
 #define L_EXTL(S) hipLaunchKernelGGL((k_extend<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->stream, fa, dev->sv, in, out, s.sh, s.L, kc, tail)
         IGX_DISPATCH_VARIANT8(dev->variant, L_EXTL);
@@ -2446,6 +2261,15 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
         if (value < -1 || value > 1) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "tail_pairs must be -1 (auto), 0 or 1");
         dev->tail_pairs_opt = (int)value;
     }
+    else if (k == "stream_slots") {
+        if (value != 1 && value != 2) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "stream_slots must be 1 or 2");
+        if (value == 1 && dev->slots[1].cap) { // give the second slot's memory back
+            igx_status st = harvest(dev, dev->slots[1]);
+            if (st != IGX_OK) return st;
+            free_slot_buffers(dev->slots[1]);
+        }
+        dev->stream_slots = (int)value;
+    }
     else if (k == "slot_budget_mb") {
         if (value < 0) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "slot_budget_mb must be >= 0 (0 = auto)");
         dev->slot_budget_mb = value;
@@ -2491,13 +2315,8 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
         dev->bvh_bins_tlas = (int)value;
     }
     else if (k == "path_classes") {
-        if (value < 0 || value > 3) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "path_classes must be 0, 1, 2 or 3");
+        if (value < 0 || value > 4) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "path_classes must be 0, 1, 2, 3 or 4");
         dev->classify_opt = (int)value;
-    }
-    else if (k == "regroup") dev->regroup_opt = value != 0;
-    else if (k == "class_ellipsoid_pct") {
-        if (value < 0 || value > 200) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "class_ellipsoid_pct must be in [0, 200]");
-        dev->class_shrink = (float)value / 100.0f;
     }
     else if (k == "sah_node_cost_pct") {
         if (value < 10 || value > 2000) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "sah_node_cost_pct must be in [10, 2000]");
@@ -3227,7 +3046,6 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
     fa.seed = p->seed;
     fa.inv_spi = 1.0f / (float)p->spi;
     fa.classify = dev->classify_opt;
-    fa.class_shrink = dev->class_shrink;
     fa.shadow_classes = dev->shadow_classes_opt;
     fa.dynamic = dev->dynamic_opt & DYN_EXTEND;
     long long local_pixels;
@@ -3264,16 +3082,23 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
         return IGX_OK;
     }
     // default chunk of a multi-iteration render: the largest power of two
-    // whose two stream slots take at most a quarter of the device memory
-    // (MI355X: 128 M paths, 2 x 25 GB).  Fewer, larger chunks leave fewer
-    // tails that overlap nothing: diamond frame 193 -> 179 ms, S-deep 4096^2
-    // 865 -> 823 ms from 32 M to 128 M paths (tools/sweep_frame.py)
-    const long long slot_budget = dev->slot_budget_mb > 0 ? dev->slot_budget_mb * (1ll << 20) : (long long)(dev->mem_total / 4);
+    // whose stream slots take at most 30 % of the device memory (MI355X: 128 M
+    // paths; two slots of 22.5 GB, 36.9 GB with three path classes).  Fewer,
+    // larger chunks leave fewer tails that overlap nothing: diamond frame 193
+    // -> 179 ms, S-deep 4096^2 865 -> 823 ms from 32 M to 128 M paths
+    // (tools/sweep_frame.py).  Per path and slot: two path buffers (56 B a
+    // record; twice that with the class-C region), shadow ray 48 B, hit
+    // record 20 B (split schedule), radiance 16 B.
+    const bool split = use_split(dev);
+    if (split && fa.classify == 4) fa.classify = 3; // hit records have no class-C region
+    const long long path_slot_bytes = 2 * 56 * (fa.classify == 4 ? 2 : 1) + 48 + (split ? 20 : 0) + 16;
+    const long long slot_budget =
+        dev->slot_budget_mb > 0 ? dev->slot_budget_mb * (1ll << 20) : (long long)((double)dev->mem_total * 0.3);
     long long auto_chunk_paths = 1ll << 24;
-    while (auto_chunk_paths < MAX_CHUNK_PATHS && 2 * (2 * auto_chunk_paths) * PATH_SLOT_BYTES <= slot_budget)
+    while (auto_chunk_paths < MAX_CHUNK_PATHS && dev->stream_slots * (2 * auto_chunk_paths) * path_slot_bytes <= slot_budget)
         auto_chunk_paths *= 2;
     if (dev->slot_budget_mb > 0) // an explicit budget also bounds the chunk below 16 M paths
-        auto_chunk_paths = std::max<long long>(1ll << 20, std::min<long long>(auto_chunk_paths, slot_budget / (2 * PATH_SLOT_BYTES)));
+        auto_chunk_paths = std::max<long long>(1ll << 20, std::min<long long>(auto_chunk_paths, slot_budget / (dev->stream_slots * path_slot_bytes)));
     long long cap = dev->capacity_opt > 0 ? dev->capacity_opt
                                           : (count > 1 ? auto_chunk_paths : std::min<long long>({total_paths, 1ll << 24, auto_chunk_paths}));
     cap = std::min<long long>(cap, MAX_CHUNK_PATHS);
@@ -3295,7 +3120,6 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
                             : trace_blocks_per_cu<false>(sd, dev->trace_waves, dev->lds_scene_bytes, refill, tr_tree);
     const bool full = variant_full(sd);
     const int shade_bpc = shade_blocks_per_cu(full);
-    const bool split = use_split(dev);
     const int sh_bpc = inst ? shadow_blocks_per_cu<true>(sd, dev->lds_scene_bytes, refill, tree_bytes(dev, dev->tree_shadow))
                             : shadow_blocks_per_cu<false>(sd, dev->lds_scene_bytes, refill, tree_bytes(dev, dev->tree_shadow));
     const bool pairs = use_tail_pairs(dev);
@@ -3306,11 +3130,11 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
     for (long long px0 = 0; px0 < local_pixels; px0 += chunk_pixels_max) {
         fa.iter = p->iteration + it0;
         fa.chunk_iters = std::min(iters_per_chunk, count - it0);
-        Slot& S = dev->slots[dev->next_slot];
+        Slot& S = dev->slots[dev->stream_slots == 1 ? 0 : dev->next_slot];
         dev->next_slot ^= 1;
-        igx_status st = harvest(dev, S); // waits for the chunk that used this slot two chunks ago
+        igx_status st = harvest(dev, S); // waits for the chunk that used this slot two chunks ago (one, with one slot)
         if (st != IGX_OK) return st;
-        if ((st = ensure_slot(dev, S, slot_cap)) != IGX_OK) return st;
+        if ((st = ensure_slot(dev, S, slot_cap, split, fa.classify == 4)) != IGX_OK) return st;
 
         auto begin_timed = [&](int kind, int bounce, hipStream_t strm) {
             if (!dev->timing) return;
@@ -3578,7 +3402,8 @@ extern "C" igx_status igx_get_stats(igx_device* dev, igx_stats* out) {
     out->table_bytes = dev->table_bytes;
     out->shading_bytes = dev->shading_bytes;
     out->slot_bytes = 0;
-    for (const Slot& s : dev->slots) out->slot_bytes += (uint64_t)s.shard_cap * NSH * (2 * 56 + 48 + 20) + (uint64_t)s.cap * 16;
+    for (const Slot& s : dev->slots)
+        out->slot_bytes += (uint64_t)s.shard_cap * NSH * (2 * 56 * (s.pa.c_base ? 2 : 1) + 48 + (s.hb.h ? 20 : 0)) + (uint64_t)s.cap * 16;
     return IGX_OK;
 }
 

@@ -282,6 +282,40 @@ def test_render_iterations_equals_single_calls(device, diamond_path, tile, capac
         assert sa[k] == sb[k], (k, sa[k], sb[k])
 
 
+@pytest.mark.parametrize("split", [0, 1])
+def test_one_stream_slot_matches_two(diamond_path, split):
+    """stream_slots 1 (every chunk in the same slot: each waits for the one
+    before, bench.py's setting at N > 1) renders the frame of stream_slots 2
+    bit for bit over many chunks, gives the second slot's memory back, and the
+    per-path hit record is only allocated for the split schedule (a fresh
+    handle, so no slot is left over from a larger earlier render)."""
+    sc = ignis_amd.Scene.from_file(diamond_path)
+    p = ignis_amd.RenderParams()
+    p.width, p.height, p.spi = 160, 120, 2
+    d = ignis_amd.Device(0)
+    try:
+        d.upload(sc)
+        d.set_option("split", split)
+        d.set_option("capacity", 20000)  # 10000 pixels x spi 2 per chunk: 4 chunks per iteration
+        imgs, mem = [], []
+        for slots in (2, 1, 2):
+            d.set_option("stream_slots", slots)
+            d.clear()
+            d.render_iterations(p, 3)
+            imgs.append(d.framebuffer(160 * 120 * 3)[0])
+            mem.append(d.stats()["slot_bytes"])
+    finally:
+        d.close()
+    np.testing.assert_array_equal(imgs[0], imgs[1])
+    np.testing.assert_array_equal(imgs[0], imgs[2])
+    assert imgs[0].sum() > 0
+    assert mem[1] * 2 == mem[0] == mem[2], mem
+    cap = 20000
+    per_rec = 2 * 56 + 48 + (20 if split else 0)  # two path buffers, shadow ray, hit record
+    shard_cap = -(-cap // (64 * 64)) * 64
+    assert mem[1] == shard_cap * 64 * per_rec + cap * 16, (mem[1], split)
+
+
 def test_bench_frame_equals_single_iterations(device, diamond_path):
     """At the bench's full size (diamond 1000x1000, 32 iterations of spi 8 =
     256 spp) the batched frame -- 128 M-path chunks, 16 iterations each -- is
@@ -362,14 +396,17 @@ def test_split_and_refill_invariance(device, root, name):
 @pytest.mark.parametrize("name", ["diamond_scene.json", "s_deep.json"])
 def test_path_class_invariance(device, root, name):
     """Surviving paths split into two stream classes (inside a dielectric or
-    not, or after a specular event: front / back of each shard) render the same
-    image bit for bit with the same ray counts as one class, on the fused and
-    the split schedule, and through the tail kernel (tail threshold 0 / all)."""
+    not, or after a specular event: front / back of each shard) or three
+    (inside / heading for an enclosing entity's box / the rest: class C in its
+    own region) render the same image bit for bit with the same ray counts as
+    one class, on the fused and the split schedule (three classes fall back
+    to two there), and through the tail kernel (tail threshold 0 / all)."""
     sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", name))
     imgs, counts = [], []
     try:
         device.upload(sc)
-        for classes, split, tail in [(0, -1, -1), (1, -1, -1), (2, -1, -1), (1, 1, -1), (1, 0, 0), (1, -1, 1 << 30)]:
+        for classes, split, tail in [(0, -1, -1), (1, -1, -1), (2, -1, -1), (1, 1, -1), (1, 0, 0), (1, -1, 1 << 30),
+                                     (3, -1, -1), (4, 0, -1), (4, 0, 0), (4, 1, -1)]:
             device.set_option("path_classes", classes)
             device.set_option("split", split)
             device.set_option("tail_threshold", tail)
@@ -378,7 +415,7 @@ def test_path_class_invariance(device, root, name):
             st = device.stats()
             counts.append((st["camera_rays"], st["bounce_rays"], st["shadow_rays"]))
     finally:
-        device.set_option("path_classes", 1)
+        device.set_option("path_classes", 3)
         device.set_option("split", -1)
         device.set_option("tail_threshold", -1)
     for im, c in zip(imgs[1:], counts[1:]):

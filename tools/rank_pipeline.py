@@ -2,7 +2,7 @@
 simulated on one GPU) over K back-to-back frames, with one device handle
 (each frame drained before the next, as the gather requires) and with two
 handles alternating (bench.py's N > 1 pipelining: frame k+1 queued before
-frame k is drained).  usage: rank_pipeline.py scene N [K]"""
+frame k is drained).  usage: rank_pipeline.py scene N [K] [stream_slots]"""
 import json, os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "ignis-masterthesis_amd"))
@@ -14,8 +14,10 @@ n = int(sys.argv[2])
 K = int(sys.argv[3]) if len(sys.argv) > 3 else 6
 W, H = scene.film_size
 devs = [ignis_amd.Device(0), ignis_amd.Device(0)]
+slots = int(sys.argv[4]) if len(sys.argv) > 4 else 2
 for d in devs:
     d.upload(scene)
+    d.set_option("stream_slots", slots)
 p = ignis_amd.RenderParams()
 p.width, p.height, p.spi = W, H, 8
 if n > 1:
@@ -42,4 +44,5 @@ def run(handles):
 
 for handles in (devs[:1], devs, devs[:1], devs):
     run(handles)
-    print(json.dumps({"n": n, "handles": len(handles), "ms_per_frame": round(run(handles) * 1e3, 2)}), flush=True)
+    print(json.dumps({"n": n, "stream_slots": slots, "handles": len(handles), "ms_per_frame": round(run(handles) * 1e3, 2),
+                      "slot_gb_per_handle": [round(d.stats()["slot_bytes"] / 1e9, 2) for d in handles]}), flush=True)
