@@ -182,7 +182,9 @@ def roofline(dev, st, render_one, n_gpus, scene_key):
         "avg_launch_us": round(avg_launch_s * 1e6, 2),
         "launches": launches,
     }
-    rp = load_rocprof(scene_key, split) if n_gpus == 1 else None
+    # split schedule: the committed profile is of the trace kernel alone
+    # (overlap_shadow 0), compared with roofline["isolated"] (suite_line)
+    rp = load_rocprof(scene_key, split) if n_gpus == 1 and not split else None
     if rp:
         # the same quantities over the committed rocprof average of the same kernel and workload
         t = rp["avg_us"] * 1e-6
@@ -246,6 +248,12 @@ def suite_line(ignis_amd, dev_index, path, spi, iters, size=None):
                          "frac": round(per_launch / t_iso / 1e9 / HBM_PEAK_GBS, 4) if t_iso > 0 else None,
                          "frac_traffic": round(r["traffic"] / t_iso / 1e9 / HBM_PEAK_GBS, 4) if t_iso > 0 and r["traffic"] else None,
                          "note": "k_trace_refill alone (overlap_shadow 0): its own launch duration"}
+        rp = load_rocprof(key, True)
+        if rp:
+            # the committed rocprofv3 profile of the same workload, also with overlap_shadow 0
+            t = rp["avg_us"] * 1e-6
+            r["isolated"]["rocprof"] = dict(rp, frac=round(per_launch / t / 1e9 / HBM_PEAK_GBS, 4),
+                                            frac_traffic=round(r["traffic"] / t / 1e9 / HBM_PEAK_GBS, 4) if r["traffic"] else None)
     dev.close()
     del scene
     return line

@@ -177,7 +177,8 @@ static_assert(BLOCK == TSTACK_STRIDE, "traversal stacks are laid out for BLOCK t
 // shard, class B from its back, wave_append_paths); other streams leave the
 // second word 0.
 __device__ __forceinline__ int row_total(const int* row) {
-    int v = row[lane_id() * CSTRIDE] + row[lane_id() * CSTRIDE + 1] + row[lane_id() * CSTRIDE + 2];
+    const int* r = row + lane_id() * CSTRIDE;
+    int v = r[0] + r[1] + r[2];
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
     return __builtin_amdgcn_readfirstlane(v);
 }
@@ -2315,7 +2316,7 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
         dev->bvh_bins_tlas = (int)value;
     }
     else if (k == "path_classes") {
-        if (value < 0 || value > 4) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "path_classes must be 0, 1, 2, 3 or 4");
+        if (value < 0 || value > 4) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "path_classes must be in [0, 4]");
         dev->classify_opt = (int)value;
     }
     else if (k == "sah_node_cost_pct") {

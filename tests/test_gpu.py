@@ -311,7 +311,9 @@ def test_one_stream_slot_matches_two(diamond_path, split):
     assert imgs[0].sum() > 0
     assert mem[1] * 2 == mem[0] == mem[2], mem
     cap = 20000
-    per_rec = 2 * 56 + 48 + (20 if split else 0)  # two path buffers, shadow ray, hit record
+    # two path buffers (with the class-C region of path_classes 4 on the fused
+    # schedule: twice the records), shadow ray, hit record (split schedule)
+    per_rec = 2 * 56 * (1 if split else 2) + 48 + (20 if split else 0)
     shard_cap = -(-cap // (64 * 64)) * 64
     assert mem[1] == shard_cap * 64 * per_rec + cap * 16, (mem[1], split)
 
