@@ -584,6 +584,18 @@ def cpu_baseline(scene, dev, W, H, spi, target_s):
             runs.append(((st["camera_rays"] + st["bounce_rays"] + st["shadow_rays"]) / st["seconds"] / 1e6, st["seconds"]))
     rates = sorted(r for r, _ in runs)
     med = float(np.median(rates))
+    # the reference's TBB thread count as such (hardware_concurrency, Device.cpp:347),
+    # measured beside the quota-sized run: 1 warm-up + 3 timed runs of the same band
+    at_hc = None
+    if affinity != threads:
+        hc = []
+        for it in range(4):
+            _, st = orc.render(W, H, spi, iteration=it, threads=affinity, window=win)
+            if it >= 1:
+                hc.append((st["camera_rays"] + st["bounce_rays"] + st["shadow_rays"]) / st["seconds"] / 1e6)
+        at_hc = {"threads": affinity, "value": round(float(np.median(hc)), 3),
+                 "note": "same band at the reference CPU device's thread count (TBB hardware_concurrency); "
+                         "more threads than the cgroup CPU quota are throttled"}
     cpu = {
         "value": round(med, 3),
         "unit": "Mrays/s",
@@ -595,6 +607,7 @@ def cpu_baseline(scene, dev, W, H, spi, target_s):
         "machine_logical_cpus": os.cpu_count(),
         "hardware_concurrency": affinity,
         "cgroup_cpu_quota": quota,
+        "at_hardware_concurrency": at_hc,
         "sample": f"oracle/oracle.c (restated reference CPU device, SAH BVH4 + Tri4 leaves), {threads} threads "
                   f"(hardware_concurrency {affinity} on a {cpu_model()} host, cgroup CPU quota "
                   f"{quota if quota else 'none'}: min of the two), rows {y0}-{y0 + rows} of the "

@@ -62,6 +62,12 @@ constexpr int VARIANT_SPEC = 64;
 // tables stay in global memory.  Set by the upload with bit 1 (option
 // "bvh_quantize").
 constexpr int VARIANT_Q4 = 128;
+// Width of the quantised nodes (build knob): 4 (Bvh4QNode, 64 B) or 8
+// (Bvh8QNode, 128 B, node_step8q).
+#ifndef IGX_QWIDTH
+#define IGX_QWIDTH 4
+#endif
+static_assert(IGX_QWIDTH == 4 || IGX_QWIDTH == 8, "IGX_QWIDTH must be 4 or 8");
 __host__ __device__ constexpr bool variant_q4(int v) { return (v & VARIANT_Q4) != 0; }
 constexpr int32_t REF_EMPTY = (int32_t)0x80000002; // absent child of a 4-wide node (host kEmptyRef)
 __host__ __device__ constexpr bool variant_spec(int v) { return (v & VARIANT_SPEC) != 0; }

@@ -1665,7 +1665,7 @@ int max_grid(const igx_device* dev) {
 igx_status configure_stack(igx_device* dev) {
     const int need = dev->scene_depth;
     const int extra = std::max(0, need - LDS_STACK);
-    dev->variant = (dev->bvh_width == 4 ? 2 : 0) | (extra > 0 ? 1 : 0) | (dev->full_shading ? 4 : 0) | (dev->quantized ? VARIANT_Q4 : 0);
+    dev->variant = (dev->bvh_width >= 4 ? 2 : 0) | (extra > 0 ? 1 : 0) | (dev->full_shading ? 4 : 0) | (dev->quantized ? VARIANT_Q4 : 0);
     const size_t threads = (size_t)max_grid(dev) * BLOCK;
     for (int k = 0; k < 3; ++k) {
         int*& old = k == 0 ? dev->spill_main : k == 1 ? dev->spill_tail : dev->spill_shadow;
@@ -2349,17 +2349,28 @@ extern "C" igx_status igx_synchronize(igx_device* dev) {
 // nodes keep their relative (depth-first) order.  Every inner-node reference
 // (node children, instance BLAS roots, the TLAS root) is renumbered; the
 // traversal result does not depend on node numbering.
-// `format`: 2 (BVH2, 64 B), 4 (4-wide, 128 B) or 5 (quantised 4-wide, 64 B).
+// `format`: 2 (BVH2, 64 B), 4 (4-wide, 128 B), 5 (quantised 4-wide, 64 B) or
+// 8 (quantised 8-wide, 128 B).
 static void order_hot_nodes(std::vector<float4>& nodes, int format, std::vector<float4>& inst, int& tlas_root, size_t front) {
-    const int nf4 = format == 4 ? 8 : 4;
+    const int nf4 = format == 4 || format == 8 ? 8 : 4;
     const size_t nn = nodes.size() / nf4;
     if (nn == 0 || front == 0) return;
-    const int width = format == 2 ? 2 : 4;
+    const int width = format == 2 ? 2 : format == 8 ? 8 : 4;
     auto ref = [&](size_t n, int k) -> int32_t& {
-        return reinterpret_cast<int32_t*>(&nodes[n * nf4])[format == 4 ? 24 + k : 12 + k];
+        return reinterpret_cast<int32_t*>(&nodes[n * nf4])[format == 4 ? 24 + k : format == 8 ? 20 + k : 12 + k];
     };
     auto box = [&](size_t n, int k, float lo[3], float hi[3]) {
         const float* f = reinterpret_cast<const float*>(&nodes[n * nf4]);
+        if (format == 8) { // origin + code * scale (Bvh8QNode)
+            const uint32_t* u = reinterpret_cast<const uint32_t*>(f);
+            const float sc[3] = {f[3], f[4], f[5]};
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = f[a] + (float)((u[6 + 4 * a + k / 4] >> (8 * (k % 4))) & 255u) * sc[a];
+                hi[a] = f[a] + (float)((u[8 + 4 * a + k / 4] >> (8 * (k % 4))) & 255u) * sc[a];
+            }
+            if (ref(n, k) == igx::kEmptyRef) lo[0] = INFINITY;
+            return;
+        }
         if (format == 5) { // origin + code * scale (Bvh4QNode)
             const uint32_t* u = reinterpret_cast<const uint32_t*>(f);
             const float sc[3] = {f[3], f[4], f[5]};
@@ -2384,7 +2395,7 @@ static void order_hot_nodes(std::vector<float4>& nodes, int format, std::vector<
     // children of node n with the node's likelihood pn: f(child ref, child likelihood)
     auto children = [&](size_t n, double pn, auto&& f) {
         float ulo[3] = {INFINITY, INFINITY, INFINITY}, uhi[3] = {-INFINITY, -INFINITY, -INFINITY};
-        double ak[4] = {0, 0, 0, 0};
+        double ak[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         for (int k = 0; k < width; ++k) {
             float lo[3], hi[3];
             box(n, k, lo, hi);
@@ -2572,7 +2583,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     for (const auto& b : brs) est_tri += b.prim_order.size();
     const size_t est_bytes = est_tri * 48 + (size_t)desc->num_entities * 64 + (est_tri / 2 + desc->num_entities) * 128;
     const bool quantize = width == 4 && (dev->quantize_opt == 1 || (dev->quantize_opt < 0 && est_bytes > SPLIT_TABLE_BYTES));
-    const int nf4 = quantize ? 4 : node_f4(width);
+    const int nf4 = quantize ? (IGX_QWIDTH == 8 ? 8 : 4) : node_f4(width);
 
     // ---- phase 2: node, triangle and instance tables ----------------------
     std::vector<float4> nodes; // nf4 float4s per node
@@ -2600,6 +2611,19 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
                 nodes.insert(nodes.end(), f, f + 4);
             }
             need = br.depth;
+        } else if (quantize && IGX_QWIDTH == 8) {
+            igx::Bvh8Result b8 = igx::collapse_bvh8(br);
+            for (auto nd : b8.nodes) {
+                for (int k = 0; k < 8; ++k) {
+                    if (nd.ref[k] >= 0) nd.ref[k] += node_off;
+                    else if (nd.ref[k] != igx::kEmptyRef) nd.ref[k] = move_leaf(nd.ref[k]);
+                }
+                const igx::Bvh8QNode qn = igx::quantize_bvh8(nd);
+                float4 f[8];
+                std::memcpy(f, &qn, 128);
+                nodes.insert(nodes.end(), f, f + 8);
+            }
+            need = b8.stack_need;
         } else {
             igx::Bvh4Result b4 = igx::collapse_bvh4(br);
             for (auto nd : b4.nodes) {
@@ -2925,7 +2949,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     }
 
     // hot nodes first: any prefix of the node array is a treelet (stage_treelet)
-    order_hot_nodes(nodes, quantize ? 5 : width, inst, tlas_root, TREELET_FRONT);
+    order_hot_nodes(nodes, quantize ? (IGX_QWIDTH == 8 ? 8 : 5) : width, inst, tlas_root, TREELET_FRONT);
 
     // ---- upload ----------------------------------------------------------
     SceneView sv{};
@@ -2944,7 +2968,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     sv.tlas_root = tlas_root;
     sv.num_nodes = (int)(nodes.size() / nf4);
     sv.node_f4 = nf4;
-    dev->bvh_width = width;
+    dev->bvh_width = quantize && IGX_QWIDTH == 8 ? 8 : width; // reported; the variant's width bit is set for 4 and 8
     dev->quantized = quantize;
     dev->nf4 = nf4;
     sv.num_inst = (int)(inst.size() / 4);

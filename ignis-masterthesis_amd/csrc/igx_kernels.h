@@ -353,11 +353,66 @@ __device__ __forceinline__ int node_step4q(const SceneView& sv, const Trav& t, i
     return ref[0];
 }
 
+// Quantised 8-wide node (128 B, host Bvh8QNode): the decode of node_step4q for
+// eight children (child k's byte is byte k % 4 of word k / 4 of each bound),
+// hit children ordered by entry distance with the 19-exchange sorting network
+// of eight inputs, the nearest returned and the others pushed farthest-first.
+// One visit reads one 128-B line, the line a 64-B quantised 4-wide node costs
+// as well, and covers twice the children.
+__device__ __forceinline__ float qbyte(uint32_t w, int b) { return (float)((w >> (8 * b)) & 255u); }
+template <bool STATS, bool SPILL, bool TREE>
+__device__ __forceinline__ int node_step8q(const SceneView& sv, const Trav& t, int node, const TStack& ts, int& sp,
+                                           TraceStats& st) {
+    if (STATS) {
+        st.nodes++;
+        if (first_active_lane()) st.wnodes++;
+    }
+    const float4* np = (TREE && node < sv.tree_n ? sv.tree : sv.nodes) + 8 * node; // see node_step2
+    const float4 A = np[0], B = np[1], C = np[2], D = np[3], E = np[4];
+    const int4 r0 = *reinterpret_cast<const int4*>(np + 5), r1 = *reinterpret_cast<const int4*>(np + 6);
+    const float SX = A.w * t.idir.x, SY = B.x * t.idir.y, SZ = B.y * t.idir.z;
+    const float OX = fmaf(A.x, t.idir.x, t.iorg.x), OY = fmaf(A.y, t.idir.y, t.iorg.y), OZ = fmaf(A.z, t.idir.z, t.iorg.z);
+    const uint32_t qlx[2] = {__float_as_uint(B.z), __float_as_uint(B.w)}, qhx[2] = {__float_as_uint(C.x), __float_as_uint(C.y)};
+    const uint32_t qly[2] = {__float_as_uint(C.z), __float_as_uint(C.w)}, qhy[2] = {__float_as_uint(D.x), __float_as_uint(D.y)};
+    const uint32_t qlz[2] = {__float_as_uint(D.z), __float_as_uint(D.w)}, qhz[2] = {__float_as_uint(E.x), __float_as_uint(E.y)};
+    float d[8];
+    int ref[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+    int n = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int w = k >> 2, b = k & 3;
+        const float ax = fmaf(qbyte(qlx[w], b), SX, OX), bx = fmaf(qbyte(qhx[w], b), SX, OX);
+        const float ay = fmaf(qbyte(qly[w], b), SY, OY), by = fmaf(qbyte(qhy[w], b), SY, OY);
+        const float az = fmaf(qbyte(qlz[w], b), SZ, OZ), bz = fmaf(qbyte(qhz[w], b), SZ, OZ);
+        const float en = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), t.tmin));
+        const float ex = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), t.tmax));
+        const bool h = en <= ex && ref[k] != REF_EMPTY;
+        d[k] = h ? en : INFINITY;
+        n += h ? 1 : 0;
+    }
+    if (n == 0) return tpop<SPILL>(ts, sp);
+    // optimal 8-input network (19 exchanges, depth 6)
+    cswap(d[0], ref[0], d[2], ref[2]); cswap(d[1], ref[1], d[3], ref[3]);
+    cswap(d[4], ref[4], d[6], ref[6]); cswap(d[5], ref[5], d[7], ref[7]);
+    cswap(d[0], ref[0], d[4], ref[4]); cswap(d[1], ref[1], d[5], ref[5]);
+    cswap(d[2], ref[2], d[6], ref[6]); cswap(d[3], ref[3], d[7], ref[7]);
+    cswap(d[0], ref[0], d[1], ref[1]); cswap(d[2], ref[2], d[3], ref[3]);
+    cswap(d[4], ref[4], d[5], ref[5]); cswap(d[6], ref[6], d[7], ref[7]);
+    cswap(d[2], ref[2], d[4], ref[4]); cswap(d[3], ref[3], d[5], ref[5]);
+    cswap(d[1], ref[1], d[4], ref[4]); cswap(d[3], ref[3], d[6], ref[6]);
+    cswap(d[1], ref[1], d[2], ref[2]); cswap(d[3], ref[3], d[4], ref[4]); cswap(d[5], ref[5], d[6], ref[6]);
+#pragma unroll
+    for (int k = 7; k > 0; --k)
+        if (n > k) tpush<SPILL>(ts, sp, ref[k]);
+    return ref[0];
+}
+
 template <bool STATS, int V>
 __device__ __forceinline__ int node_step(const SceneView& sv, const Trav& t, int node, const TStack& ts, int& sp,
                                          TraceStats& st) {
     constexpr int PAD = variant_ldspad(V) ? 1 : 0;
-    if constexpr (variant_q4(V)) return node_step4q<STATS, variant_spill(V), variant_tree(V)>(sv, t, node, ts, sp, st);
+    if constexpr (variant_q4(V) && IGX_QWIDTH == 8) return node_step8q<STATS, variant_spill(V), variant_tree(V)>(sv, t, node, ts, sp, st);
+    else if constexpr (variant_q4(V)) return node_step4q<STATS, variant_spill(V), variant_tree(V)>(sv, t, node, ts, sp, st);
     else if constexpr (variant_width(V) == 4) return node_step4<STATS, variant_spill(V), 8 + PAD, variant_tree(V)>(sv, t, node, ts, sp, st);
     else return node_step2<STATS, variant_spill(V), 4 + PAD, variant_tree(V)>(sv, t, node, ts, sp, st);
 }

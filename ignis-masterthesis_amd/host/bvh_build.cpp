@@ -538,28 +538,38 @@ float half_area(const Child2& c) {
 
 } // namespace
 
-Bvh4Result collapse_bvh4(const BvhBuildResult& in) {
-    Bvh4Result res;
+namespace {
+
+// Surface-area collapse of a BVH2 into N-wide nodes (N = 4 or 8): every wide
+// node absorbs the largest-area inner grandchildren of its BVH2 node until it
+// has N children; children are laid out after their parent in DFS order.
+template <int N>
+void collapse_wide(const BvhBuildResult& in, std::vector<WideNode<N>>& out, int& depth, int& stack_need) {
     const float inf = std::numeric_limits<float>::infinity();
-    auto set = [&](Bvh4Node& n, int k, const Child2& c, int32_t ref) {
-        n.lo_x[k] = c.lo[0]; n.hi_x[k] = c.hi[0];
-        n.lo_y[k] = c.lo[1]; n.hi_y[k] = c.hi[1];
-        n.lo_z[k] = c.lo[2]; n.hi_z[k] = c.hi[2];
+    auto set = [&](WideNode<N>& n, int k, const Child2& c, int32_t ref) {
+        for (int a = 0; a < 3; ++a) {
+            n.lo[a][k] = c.lo[a];
+            n.hi[a][k] = c.hi[a];
+        }
         n.ref[k] = ref;
     };
-    auto set_empty4 = [&](Bvh4Node& n, int k) {
-        n.lo_x[k] = n.hi_x[k] = n.lo_y[k] = n.hi_y[k] = n.lo_z[k] = n.hi_z[k] = inf;
-        n.ref[k] = kEmptyRef;
+    auto empty_node = [&]() {
+        WideNode<N> n{};
+        for (int k = 0; k < N; ++k) {
+            for (int a = 0; a < 3; ++a) n.lo[a][k] = n.hi[a][k] = inf;
+            n.ref[k] = kEmptyRef;
+        }
+        return n;
     };
-    if (in.nodes.empty()) return res;
-    Bvh4Node root{};
-    for (int k = 0; k < 4; ++k) set_empty4(root, k);
-    res.nodes.push_back(root);
+    out.clear();
+    depth = 0;
+    stack_need = 0;
+    if (in.nodes.empty()) return;
+    out.push_back(empty_node());
     if (in.root_is_leaf || in.prim_order.empty()) {
-        if (in.root_is_leaf) set(res.nodes[0], 0, child_of(in.nodes[0], 0), in.root_leaf_ref);
-        res.depth = 1;
-        res.stack_need = 0;
-        return res;
+        if (in.root_is_leaf) set(out[0], 0, child_of(in.nodes[0], 0), in.root_leaf_ref);
+        depth = 1;
+        return;
     }
     // iterative DFS: (BVH2 inner node, output node, depth)
     struct Item { int32_t src; int32_t out; int depth; };
@@ -568,12 +578,12 @@ Bvh4Result collapse_bvh4(const BvhBuildResult& in) {
     while (!stack.empty()) {
         Item it = stack.back();
         stack.pop_back();
-        res.depth = std::max(res.depth, it.depth);
-        Child2 kids[4];
+        depth = std::max(depth, it.depth);
+        Child2 kids[N];
         int nk = 0;
         for (int k = 0; k < 2; ++k) // an absent BVH2 child (kEmptyRef, bvh2_from_reference) stays absent
             if (in.nodes[it.src].ref[k] != kEmptyRef) kids[nk++] = child_of(in.nodes[it.src], k);
-        while (nk < 4) {
+        while (nk < N) {
             int best = -1;
             float best_area = -1;
             for (int k = 0; k < nk; ++k)
@@ -584,18 +594,16 @@ Bvh4Result collapse_bvh4(const BvhBuildResult& in) {
             kids[nk++] = child_of(e, 1);
         }
         nchild[it.out] = nk;
-        // children in DFS order: inner children laid out after their parent
-        int32_t out_idx[4] = {-1, -1, -1, -1};
+        int32_t out_idx[N];
+        for (int k = 0; k < N; ++k) out_idx[k] = -1;
         for (int k = 0; k < nk; ++k) {
             if (kids[k].ref >= 0) {
-                out_idx[k] = (int32_t)res.nodes.size();
-                Bvh4Node nn{};
-                for (int j = 0; j < 4; ++j) set_empty4(nn, j);
-                res.nodes.push_back(nn);
+                out_idx[k] = (int32_t)out.size();
+                out.push_back(empty_node());
                 nchild.push_back(0);
-                set(res.nodes[it.out], k, kids[k], out_idx[k]);
+                set(out[it.out], k, kids[k], out_idx[k]);
             } else {
-                set(res.nodes[it.out], k, kids[k], kids[k].ref);
+                set(out[it.out], k, kids[k], kids[k].ref);
             }
         }
         for (int k = nk - 1; k >= 0; --k)
@@ -603,73 +611,128 @@ Bvh4Result collapse_bvh4(const BvhBuildResult& in) {
     }
     // stack need: pushes along a path = sum over its nodes of (children - 1);
     // children come after their parent, so one reverse sweep computes it
-    std::vector<int> need(res.nodes.size(), 0);
-    for (size_t i = res.nodes.size(); i-- > 0;) {
+    std::vector<int> need(out.size(), 0);
+    for (size_t i = out.size(); i-- > 0;) {
         int below = 0;
-        for (int k = 0; k < 4; ++k)
-            if (res.nodes[i].ref[k] >= 0) below = std::max(below, need[res.nodes[i].ref[k]]);
+        for (int k = 0; k < N; ++k)
+            if (out[i].ref[k] >= 0) below = std::max(below, need[out[i].ref[k]]);
         need[i] = (nchild[i] - 1) + below;
     }
-    res.stack_need = need[0];
+    stack_need = need[0];
+}
+
+// Quantise axis a of an N-wide node: origin o, power-of-two scale s and the
+// child bytes (packed four to a word, child k in byte k % 4 of word k / 4).
+// Every quantised bound keeps at least half a quantum of slack outside the
+// child's box (exact arithmetic), and a quantum is at least 2^-19 of the
+// coordinates' magnitude.
+template <int N>
+void quantize_axis(const float* lo, const float* hi, const bool* valid, float& origin, float& scale, uint32_t* wlo,
+                   uint32_t* whi) {
+    double l = INFINITY, h = -INFINITY;
+    for (int k = 0; k < N; ++k)
+        if (valid[k]) {
+            l = std::min(l, (double)lo[k]);
+            h = std::max(h, (double)hi[k]);
+        }
+    if (!(l <= h)) l = h = 0; // no valid child (never built, kept total)
+    const double mag = std::max(std::fabs(l), std::fabs(h));
+    // a quantum: the extent over 249 codes (three spare on each side), and at
+    // least 2^-19 of the magnitude so rounding in the slab test stays far below it
+    double s = std::max({(h - l) / 249.0, mag * std::ldexp(1.0, -19), std::ldexp(1.0, -100)});
+    s = std::ldexp(1.0, (int)std::ceil(std::log2(s)));
+    for (;;) {
+        const float o = std::nextafter((float)(l - 2 * s), -INFINITY);
+        bool ok = true;
+        uint32_t wl[N / 4] = {}, wh[N / 4] = {};
+        for (int k = 0; k < N; ++k) {
+            long ql = 0, qh = 0;
+            if (valid[k]) {
+                ql = (long)std::floor(((double)lo[k] - o) / s) - 1;
+                qh = (long)std::ceil(((double)hi[k] - o) / s) + 1;
+                // at least half a quantum of slack on both sides, in exact arithmetic
+                ok = ok && ql >= 0 && qh <= 255 && (double)o + ql * s <= lo[k] - 0.5 * s && (double)o + qh * s >= hi[k] + 0.5 * s;
+            }
+            wl[k / 4] |= (uint32_t)std::clamp(ql, 0L, 255L) << (8 * (k % 4));
+            wh[k / 4] |= (uint32_t)std::clamp(qh, 0L, 255L) << (8 * (k % 4));
+        }
+        if (ok) {
+            origin = o;
+            scale = (float)s;
+            for (int w = 0; w < N / 4; ++w) {
+                wlo[w] = wl[w];
+                whi[w] = wh[w];
+            }
+            return;
+        }
+        s *= 2;
+    }
+}
+
+template <int N>
+void valid_children(const WideNode<N>& n, bool* valid) {
+    for (int k = 0; k < N; ++k) {
+        valid[k] = n.ref[k] != kEmptyRef;
+        for (int a = 0; a < 3; ++a)
+            valid[k] = valid[k] && std::isfinite(n.lo[a][k]) && std::isfinite(n.hi[a][k]) && n.lo[a][k] <= n.hi[a][k];
+    }
+}
+
+} // namespace
+
+Bvh4Result collapse_bvh4(const BvhBuildResult& in) {
+    Bvh4Result res;
+    std::vector<WideNode<4>> w;
+    collapse_wide<4>(in, w, res.depth, res.stack_need);
+    res.nodes.resize(w.size());
+    for (size_t i = 0; i < w.size(); ++i) {
+        Bvh4Node& n = res.nodes[i];
+        std::memset(&n, 0, sizeof(n));
+        for (int k = 0; k < 4; ++k) {
+            n.lo_x[k] = w[i].lo[0][k]; n.hi_x[k] = w[i].hi[0][k];
+            n.lo_y[k] = w[i].lo[1][k]; n.hi_y[k] = w[i].hi[1][k];
+            n.lo_z[k] = w[i].lo[2][k]; n.hi_z[k] = w[i].hi[2][k];
+            n.ref[k] = w[i].ref[k];
+        }
+    }
+    return res;
+}
+
+Bvh8Result collapse_bvh8(const BvhBuildResult& in) {
+    Bvh8Result res;
+    collapse_wide<8>(in, res.nodes, res.depth, res.stack_need);
     return res;
 }
 
 // ---------------------------------------------------------------------------
-// Quantised 4-wide nodes (Bvh4QNode, bvh_build.h)
+// Quantised wide nodes (Bvh4QNode, Bvh8QNode; bvh_build.h)
 // ---------------------------------------------------------------------------
 Bvh4QNode quantize_bvh4(const Bvh4Node& n) {
-    Bvh4QNode q{};
-    const float* lo[3] = {n.lo_x, n.lo_y, n.lo_z};
-    const float* hi[3] = {n.hi_x, n.hi_y, n.hi_z};
-    bool valid[4];
+    WideNode<4> w;
     for (int k = 0; k < 4; ++k) {
-        q.ref[k] = n.ref[k];
-        valid[k] = n.ref[k] != kEmptyRef;
-        for (int a = 0; a < 3; ++a)
-            valid[k] = valid[k] && std::isfinite(lo[a][k]) && std::isfinite(hi[a][k]) && lo[a][k] <= hi[a][k];
+        w.lo[0][k] = n.lo_x[k]; w.hi[0][k] = n.hi_x[k];
+        w.lo[1][k] = n.lo_y[k]; w.hi[1][k] = n.hi_y[k];
+        w.lo[2][k] = n.lo_z[k]; w.hi[2][k] = n.hi_z[k];
+        w.ref[k] = n.ref[k];
     }
+    bool valid[4];
+    valid_children<4>(w, valid);
+    Bvh4QNode q{};
+    for (int k = 0; k < 4; ++k) q.ref[k] = n.ref[k];
+    float* sc[3] = {&q.sx, &q.sy, &q.sz};
     uint32_t* qlo[3] = {&q.qlo_x, &q.qlo_y, &q.qlo_z};
     uint32_t* qhi[3] = {&q.qhi_x, &q.qhi_y, &q.qhi_z};
+    for (int a = 0; a < 3; ++a) quantize_axis<4>(w.lo[a], w.hi[a], valid, q.origin[a], *sc[a], qlo[a], qhi[a]);
+    return q;
+}
+
+Bvh8QNode quantize_bvh8(const Bvh8Node& n) {
+    bool valid[8];
+    valid_children<8>(n, valid);
+    Bvh8QNode q{};
+    for (int k = 0; k < 8; ++k) q.ref[k] = n.ref[k];
     float* sc[3] = {&q.sx, &q.sy, &q.sz};
-    for (int a = 0; a < 3; ++a) {
-        double l = INFINITY, h = -INFINITY;
-        for (int k = 0; k < 4; ++k)
-            if (valid[k]) {
-                l = std::min(l, (double)lo[a][k]);
-                h = std::max(h, (double)hi[a][k]);
-            }
-        if (!(l <= h)) l = h = 0; // no valid child (never built, kept total)
-        const double mag = std::max(std::fabs(l), std::fabs(h));
-        // a quantum: the extent over 249 codes (three spare on each side), and at
-        // least 2^-19 of the magnitude so rounding in the slab test stays far below it
-        double s = std::max({(h - l) / 249.0, mag * std::ldexp(1.0, -19), std::ldexp(1.0, -100)});
-        s = std::ldexp(1.0, (int)std::ceil(std::log2(s)));
-        for (;;) {
-            const float o = std::nextafter((float)(l - 2 * s), -INFINITY);
-            bool ok = true;
-            uint32_t wl = 0, wh = 0;
-            for (int k = 0; k < 4; ++k) {
-                long ql = 0, qh = 0;
-                if (valid[k]) {
-                    ql = (long)std::floor(((double)lo[a][k] - o) / s) - 1;
-                    qh = (long)std::ceil(((double)hi[a][k] - o) / s) + 1;
-                    // at least half a quantum of slack on both sides, in exact arithmetic
-                    ok = ok && ql >= 0 && qh <= 255 && (double)o + ql * s <= lo[a][k] - 0.5 * s &&
-                         (double)o + qh * s >= hi[a][k] + 0.5 * s;
-                }
-                wl |= (uint32_t)std::clamp(ql, 0L, 255L) << (8 * k);
-                wh |= (uint32_t)std::clamp(qh, 0L, 255L) << (8 * k);
-            }
-            if (ok) {
-                q.origin[a] = o;
-                *sc[a] = (float)s;
-                *qlo[a] = wl;
-                *qhi[a] = wh;
-                break;
-            }
-            s *= 2;
-        }
-    }
+    for (int a = 0; a < 3; ++a) quantize_axis<8>(n.lo[a], n.hi[a], valid, q.origin[a], *sc[a], &q.q[4 * a], &q.q[4 * a + 2]);
     return q;
 }
 

@@ -160,7 +160,8 @@ def test_quantised_nodes_match(device, root):
         for q in (0, 1):
             device.set_option("bvh_quantize", q)
             device.upload(sc)
-            assert device.stats()["node_bytes"] == (64 if q else 128)
+            st = device.stats()
+            assert st["node_bytes"] == (16 * st["bvh_width"] if q else 128)  # 64-B 4-wide or 128-B 8-wide (IGX_QWIDTH)
             res.append(device.trace_hits(rays, 0x1))
             imgs.append(render_gpu(device, sc, 128, 128, 4))
     finally:
