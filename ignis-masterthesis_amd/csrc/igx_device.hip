@@ -633,8 +633,11 @@ __device__ __forceinline__ void flush_stats(const TraceStats& st, unsigned long 
         atomicAdd(&stats[9 + (base / 4) * 2], wn);
         atomicAdd(&stats[10 + (base / 4) * 2], wl);
 #ifndef IGX_SHADE_PROBE
-        if (st.cyc[0] | st.cyc[1] | st.cyc[2] | st.cyc[3])
+        if (st.cyc[0] | st.cyc[1] | st.cyc[2] | st.cyc[3]) {
             for (int k = 0; k < 4; ++k) atomicAdd(&stats[16 + k], st.cyc[k]);
+            for (int k = 0; k < 12; ++k)
+                if (st.ccyc[k]) atomicAdd(&stats[20 + k], st.ccyc[k]);
+        }
 #endif
     }
 #ifdef IGX_SHADE_PROBE // per-lane marks: the lanes' sum / 64
@@ -786,6 +789,8 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
 #else
             phase_mark(st, t_last, 0);
 #endif
+            // class of the wave's group (wave-uniform): camera, A, B, C
+            const int bucket = gen ? 0 : (p0 < sc.a ? 1 : p0 < sc.ab ? 2 : 3);
             if (act) {
                 ray_extent(fa, sv, ps.depth, ps.slot, tmin, tmax, rflags);
                 trace_path_ray<STATS, V>(sv, ps.inside, ps.o, ps.d, tmin, tmax, rflags, ts, hit_ent, hit_prim, hu, hv, st);
@@ -794,7 +799,10 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
 #ifdef IGX_SHADE_PROBE
             phase_mark(st, t_last, 0);
 #else
+            const unsigned long long c_tr = st.cyc[1];
             phase_mark(st, t_last, 1);
+            st.ccyc[bucket] += st.cyc[1] - c_tr;
+            st.ccyc[8 + bucket] += 1;
 #endif
             if (act) {
                 f3 Lacc;
@@ -810,7 +818,9 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
 #ifdef IGX_SHADE_PROBE
             phase_mark(st, t_last, 3); // bounce sampling and the rest
 #else
+            const unsigned long long c_sh = st.cyc[2];
             phase_mark(st, t_last, 2);
+            st.ccyc[4 + bucket] += st.cyc[2] - c_sh;
 #endif
         }
         int dst, sdst;
@@ -2200,12 +2210,12 @@ extern "C" igx_status igx_create(int hip_device, igx_device** out) {
         delete dev;
         return IGX_ERR_HIP;
     }
-    if (hipMalloc((void**)&dev->dstats, 20 * sizeof(unsigned long long)) != hipSuccess ||
+    if (hipMalloc((void**)&dev->dstats, 32 * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc((void**)&dev->tail_counts, 2 * sizeof(unsigned long long)) != hipSuccess) {
         delete dev;
         return IGX_ERR_OUT_OF_MEMORY;
     }
-    (void)hipMemset(dev->dstats, 0, 20 * sizeof(unsigned long long));
+    (void)hipMemset(dev->dstats, 0, 32 * sizeof(unsigned long long));
     (void)hipMemset(dev->tail_counts, 0, 2 * sizeof(unsigned long long));
     *out = dev;
     return IGX_OK;
@@ -3395,8 +3405,10 @@ extern "C" igx_status igx_get_stats(igx_device* dev, igx_stats* out) {
     *out = dev->stats;
     out->bvh_depth = dev->scene_depth;
     out->stack_entries = LDS_STACK;
-    unsigned long long h[20] = {0};
+    unsigned long long h[32] = {0};
     HIPCHK(hipMemcpy(h, dev->dstats, sizeof(h), hipMemcpyDeviceToHost));
+    for (int k = 0; k < 8; ++k) out->extend_class_cycles[k] = h[20 + k];
+    for (int k = 0; k < 4; ++k) out->extend_class_groups[k] = h[28 + k];
     out->extend_cycles_load = h[16];
     out->extend_cycles_trace = h[17];
     out->extend_cycles_shade = h[18];
@@ -3438,7 +3450,7 @@ extern "C" igx_status igx_reset_stats(igx_device* dev) {
     igx_status st = drain(dev);
     if (st != IGX_OK) return st;
     dev->stats = igx_stats{};
-    HIPCHK(hipMemset(dev->dstats, 0, 20 * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(dev->dstats, 0, 32 * sizeof(unsigned long long)));
     return IGX_OK;
 }
 

@@ -104,6 +104,9 @@ struct TraceStats {
     uint32_t wnodes, wleaves; // wave-level iterations of the node loop / leaf phase (SIMD efficiency)
     // k_extend phase clocks (wave-level, s_memtime): load, trace, shade, store
     unsigned long long cyc[4] = {0, 0, 0, 0};
+    // k_extend by the class of the wave's group (camera, A, B, C): trace
+    // cycles 0-3, shade cycles 4-7, groups 8-11
+    unsigned long long ccyc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 };
 
 // true on the lowest active lane of the wave (counts one event per wave)

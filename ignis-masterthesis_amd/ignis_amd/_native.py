@@ -127,7 +127,8 @@ class Stats(C.Structure):
                 ("table_bytes", C.c_uint64), ("shading_bytes", C.c_uint64),
                 ("extend_cycles_load", C.c_uint64), ("extend_cycles_trace", C.c_uint64),
                 ("extend_cycles_shade", C.c_uint64), ("extend_cycles_store", C.c_uint64),
-                ("slot_bytes", C.c_uint64), ("treelet_nodes", C.c_int32 * 4)]
+                ("slot_bytes", C.c_uint64), ("treelet_nodes", C.c_int32 * 4),
+                ("extend_class_cycles", C.c_uint64 * 8), ("extend_class_groups", C.c_uint64 * 4)]
 
     def as_dict(self):
         return {name: (list(getattr(self, name)) if isinstance(getattr(self, name), C.Array) else getattr(self, name))

@@ -1,9 +1,16 @@
 #!/bin/bash
-# Full GPU test suite, then the measurement of record (tools/gpu_r03_profile.sh)
+# Measurement of record, part 1: full GPU test suite, bench (headline + suite
+# + CPU baseline), rocprof kernel stats and PMC traffic of the headline
+# workload.  Part 2 (suite profiles, multi-rank rehearsal):
+# tools/gpu_r03_final2.sh.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 900 python3 -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+export TMPDIR=/tmp
+rm -rf gpurun_out/prof gpurun_out/pmc_fetch gpurun_out/pmc_write
+timeout -k 10 400 python3 -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; tail -3 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error" gpurun_out/pytest_gpu.log | head -20; exit $rc; }
-bash tools/gpu_r03_profile.sh
-rc=$?; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 python3 tools/sweep_frame.py scenes/diamond_scene.json '[{"path_classes":4},{"path_classes":5},{"path_classes":4},{"path_classes":5}]' 32 > gpurun_out/exp_q.log 2>&1; cut -c1-200 gpurun_out/exp_q.log
+timeout -k 10 400 python3 bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err && head -c 400 gpurun_out/bench.json && echo && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --suite 0 > gpurun_out/prof_bench.json 2> gpurun_out/prof.err && \
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 tools/pmc_run.py 32 > gpurun_out/pmc_fetch.log 2>&1 && \
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 tools/pmc_run.py 32 > gpurun_out/pmc_write.log 2>&1
+rc=$?; echo "rc=$rc"; exit $rc

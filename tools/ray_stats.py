@@ -34,4 +34,11 @@ cyc = [s["extend_cycles_" + k] for k in ("load", "trace", "shade", "store")]
 if sum(cyc):  # share of k_extend's wave time per phase (instrumented build)
     out.update({"ext_phase_" + k: c / sum(cyc) for k, c in zip(("load", "trace", "shade", "store"), cyc)})
     out["ext_wave_cycles/64rays"] = 64 * sum(cyc) / max(1, s["extend_rays"])
+cc, cg = list(s["extend_class_cycles"]), list(s["extend_class_groups"])
+if sum(cc):  # k_extend wave time by the class of the group: camera, A, B, C (trace / shade share, cycles per group)
+    for i, k in enumerate(("cam", "A", "B", "C")):
+        out[f"ext_{k}_trace_share"] = cc[i] / sum(cc)
+        out[f"ext_{k}_shade_share"] = cc[4 + i] / sum(cc)
+        out[f"ext_{k}_groups"] = cg[i]
+        out[f"ext_{k}_cyc_per_group"] = (cc[i] + cc[4 + i]) / max(1, cg[i])
 print(json.dumps({k: round(v, 3) if isinstance(v, float) else v for k, v in out.items()}))
