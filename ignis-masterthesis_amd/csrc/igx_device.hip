@@ -587,7 +587,11 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
 // a read of the counter) since the previous mark is added to phase k; marks
 // sit at wave-uniform points.
 __device__ __forceinline__ void phase_mark(TraceStats& st, unsigned long long& last, int k) {
+    // the phase's memory operations completed, and no instruction moves across the mark
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_sched_barrier(0);
     const unsigned long long now = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_sched_barrier(0);
     st.cyc[k] += now - last;
     last = now;
 }
@@ -615,7 +619,9 @@ template <bool STATS>
 __device__ __forceinline__ void flush_stats(const TraceStats& st, unsigned long long* stats, int base, bool with_hits) {
     // slots: base+0..3 nodes/leaves/tris/blas, 8 hits, 9+base/4*2 .. wave node / leaf iterations
     unsigned long long a = st.nodes, b = st.leaves, c = st.tris, e = st.blas, h = st.hits, wn = st.wnodes, wl = st.wleaves;
+    unsigned long long cv[4] = {st.ccyc[16], st.ccyc[17], st.ccyc[18], st.ccyc[19]}; // lane node visits per class
     for (int off = 32; off > 0; off >>= 1) {
+        for (int k = 0; k < 4; ++k) cv[k] += __shfl_down(cv[k], off);
         a += __shfl_down(a, off);
         b += __shfl_down(b, off);
         c += __shfl_down(c, off);
@@ -635,8 +641,10 @@ __device__ __forceinline__ void flush_stats(const TraceStats& st, unsigned long 
 #ifndef IGX_SHADE_PROBE
         if (st.cyc[0] | st.cyc[1] | st.cyc[2] | st.cyc[3]) {
             for (int k = 0; k < 4; ++k) atomicAdd(&stats[16 + k], st.cyc[k]);
-            for (int k = 0; k < 12; ++k)
+            for (int k = 0; k < 16; ++k)
                 if (st.ccyc[k]) atomicAdd(&stats[20 + k], st.ccyc[k]);
+            for (int k = 0; k < 4; ++k)
+                if (cv[k]) atomicAdd(&stats[36 + k], cv[k]);
         }
 #endif
     }
@@ -791,6 +799,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
 #endif
             // class of the wave's group (wave-uniform): camera, A, B, C
             const int bucket = gen ? 0 : (p0 < sc.a ? 1 : p0 < sc.ab ? 2 : 3);
+            const unsigned long long wn0 = st.wnodes, ln0 = st.nodes;
             if (act) {
                 ray_extent(fa, sv, ps.depth, ps.slot, tmin, tmax, rflags);
                 trace_path_ray<STATS, V>(sv, ps.inside, ps.o, ps.d, tmin, tmax, rflags, ts, hit_ent, hit_prim, hu, hv, st);
@@ -803,6 +812,8 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
             phase_mark(st, t_last, 1);
             st.ccyc[bucket] += st.cyc[1] - c_tr;
             st.ccyc[8 + bucket] += 1;
+            st.ccyc[12 + bucket] += st.wnodes - wn0;
+            st.ccyc[16 + bucket] += st.nodes - ln0;
 #endif
             if (act) {
                 f3 Lacc;
@@ -2210,12 +2221,12 @@ extern "C" igx_status igx_create(int hip_device, igx_device** out) {
         delete dev;
         return IGX_ERR_HIP;
     }
-    if (hipMalloc((void**)&dev->dstats, 32 * sizeof(unsigned long long)) != hipSuccess ||
+    if (hipMalloc((void**)&dev->dstats, 40 * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc((void**)&dev->tail_counts, 2 * sizeof(unsigned long long)) != hipSuccess) {
         delete dev;
         return IGX_ERR_OUT_OF_MEMORY;
     }
-    (void)hipMemset(dev->dstats, 0, 32 * sizeof(unsigned long long));
+    (void)hipMemset(dev->dstats, 0, 40 * sizeof(unsigned long long));
     (void)hipMemset(dev->tail_counts, 0, 2 * sizeof(unsigned long long));
     *out = dev;
     return IGX_OK;
@@ -3405,10 +3416,14 @@ extern "C" igx_status igx_get_stats(igx_device* dev, igx_stats* out) {
     *out = dev->stats;
     out->bvh_depth = dev->scene_depth;
     out->stack_entries = LDS_STACK;
-    unsigned long long h[32] = {0};
+    unsigned long long h[40] = {0};
     HIPCHK(hipMemcpy(h, dev->dstats, sizeof(h), hipMemcpyDeviceToHost));
     for (int k = 0; k < 8; ++k) out->extend_class_cycles[k] = h[20 + k];
-    for (int k = 0; k < 4; ++k) out->extend_class_groups[k] = h[28 + k];
+    for (int k = 0; k < 4; ++k) {
+        out->extend_class_groups[k] = h[28 + k];
+        out->extend_class_node_iters[k] = h[32 + k];
+        out->extend_class_node_visits[k] = h[36 + k];
+    }
     out->extend_cycles_load = h[16];
     out->extend_cycles_trace = h[17];
     out->extend_cycles_shade = h[18];
@@ -3450,7 +3465,7 @@ extern "C" igx_status igx_reset_stats(igx_device* dev) {
     igx_status st = drain(dev);
     if (st != IGX_OK) return st;
     dev->stats = igx_stats{};
-    HIPCHK(hipMemset(dev->dstats, 0, 32 * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(dev->dstats, 0, 40 * sizeof(unsigned long long)));
     return IGX_OK;
 }
 

@@ -105,8 +105,9 @@ struct TraceStats {
     // k_extend phase clocks (wave-level, s_memtime): load, trace, shade, store
     unsigned long long cyc[4] = {0, 0, 0, 0};
     // k_extend by the class of the wave's group (camera, A, B, C): trace
-    // cycles 0-3, shade cycles 4-7, groups 8-11
-    unsigned long long ccyc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    // cycles 0-3, shade cycles 4-7, groups 8-11, wave-level node iterations
+    // 12-15, lane node visits 16-19
+    unsigned long long ccyc[20] = {};
 };
 
 // true on the lowest active lane of the wave (counts one event per wave)

@@ -41,4 +41,6 @@ if sum(cc):  # k_extend wave time by the class of the group: camera, A, B, C (tr
         out[f"ext_{k}_shade_share"] = cc[4 + i] / sum(cc)
         out[f"ext_{k}_groups"] = cg[i]
         out[f"ext_{k}_cyc_per_group"] = (cc[i] + cc[4 + i]) / max(1, cg[i])
+        out[f"ext_{k}_wave_node_iters_per_group"] = s["extend_class_node_iters"][i] / max(1, cg[i])
+        out[f"ext_{k}_simd_eff"] = s["extend_class_node_visits"][i] / max(1, 64 * s["extend_class_node_iters"][i])
 print(json.dumps({k: round(v, 3) if isinstance(v, float) else v for k, v in out.items()}))
