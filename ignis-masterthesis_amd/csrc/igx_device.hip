@@ -130,6 +130,8 @@ struct FrameArgs {
     int classify;        // surviving paths' stream class (see wave_append_paths): 0 all A, 1 B = inside a dielectric (eta != 1), 2 B = after a specular event
     int dynamic;         // k_extend: waves take 64-path groups from per-shard work counters (KernelCounters::work)
     int shadow_classes;  // shadow rays crossing an enclosing entity's box go to the back of their shard (shadow_class_b)
+    int reverse;         // k_extend: a shard's positions are taken from its end (class C, then B, then A:
+                         // the groups whose paths run longest start first, the short ones fill the launch's end)
 };
 
 // path slot -> (local pixel, sample, iteration): slots run over the chunk's
@@ -766,12 +768,13 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
         const int ns = sc.n;
         int* const c_out = kc.cnt_out + s * CSTRIDE;
         int* const c_sh = kc.cnt_shadow + s * CSTRIDE;
-        const int pos = p0 + lane_id();
+        const int q = p0 + lane_id();
+        const int pos = (fa.reverse && !gen) ? ns - 1 - q : q; // reverse: longest classes first
         bool alive = false, has_shadow = false;
         PathState ps;
         ShadowRec sr;
         ps.depth = 0;
-        if (pos < ns) {
+        if (q < ns) {
             if (gen) { // inverse of gen_index
                 const int i = ((pos >> 6) << 12) | (s << 6) | (pos & 63);
                 ps = camera_path(fa, sv, i);
@@ -788,7 +791,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
         }
         if constexpr (STATS) {
             // instrumented: extend_step's two halves with phase clocks between them
-            const bool act = pos < ns && ps.depth > 0;
+            const bool act = q < ns && ps.depth > 0;
             int hit_ent = -1, hit_prim = -1;
             float hu = 0, hv = 0, tmin = 0, tmax = 0;
             uint32_t rflags = 0;
@@ -798,7 +801,8 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
             phase_mark(st, t_last, 0);
 #endif
             // class of the wave's group (wave-uniform): camera, A, B, C
-            const int bucket = gen ? 0 : (p0 < sc.a ? 1 : p0 < sc.ab ? 2 : 3);
+            const int pg = (fa.reverse && !gen) ? ns - 1 - p0 : p0;
+            const int bucket = gen ? 0 : (pg < sc.a ? 1 : pg < sc.ab ? 2 : 3);
             const unsigned long long wn0 = st.wnodes, ln0 = st.nodes;
             if (act) {
                 ray_extent(fa, sv, ps.depth, ps.slot, tmin, tmax, rflags);
@@ -1587,6 +1591,9 @@ struct igx_device {
     // 452 -> 382 ms (k_shadow_refill 220 -> 164, k_trace_refill 205 -> 193),
     // S-deep 52.7 -> 48.6 ms
     int dynamic_opt = DYN_EXTEND | DYN_REFILL_TRACE | DYN_REFILL_SHADOW;
+    // option "group_order": 1 = k_extend takes a shard's groups from its end
+    // (classes C, B, A: longest paths first), 0 = from its front, -1 = auto
+    int group_order_opt = -1;
     // option "face_normals": precomputed world-space face normals for scenes
     // with at most FACE_NORMAL_TABLE_MAX face instances (next upload)
     int face_normals_opt = 1;
@@ -1787,6 +1794,10 @@ int grid_for(igx_device* dev, long long items, int blocks_per_cu) {
 //    faster (no hit records): S-deep (18 MB of tables) 49.4 -> 46.9 ms per
 //    8-iteration frame fused, soup-1M (104 MB) 382 split vs 451 fused.
 constexpr size_t SPLIT_TABLE_BYTES = 64u << 20;
+// order in which k_extend's dynamic groups take a shard's positions (option "group_order" -1)
+#ifndef GROUP_ORDER_AUTO
+#define GROUP_ORDER_AUTO 0
+#endif
 // tail kernel with lane pairs (k_finish_pairs) on global-table scenes; option "tail_pairs" (-1 auto, 0, 1)
 inline bool use_tail_pairs(const igx_device* dev) {
     return dev->lds_scene_bytes == 0 && (dev->tail_pairs_opt < 0 ? true : dev->tail_pairs_opt != 0);
@@ -2327,6 +2338,10 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     else if (k == "spatial_splits") dev->spatial_splits = value != 0;
     else if (k == "rebuild_bvh") dev->rebuild_bvh = value != 0;
     else if (k == "dynamic") dev->dynamic_opt = (int)(value & 15);
+    else if (k == "group_order") {
+        if (value < -1 || value > 1) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "group_order must be -1 (auto), 0 (A, B, C) or 1 (C, B, A)");
+        dev->group_order_opt = (int)value;
+    }
     else if (k == "face_normals") dev->face_normals_opt = value != 0;
     else if (k == "bvh_bins") {
         if (value < 2 || value > 4096) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "bvh_bins must be in [2, 4096]");
@@ -3094,6 +3109,7 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
     fa.classify = dev->classify_opt;
     fa.shadow_classes = dev->shadow_classes_opt;
     fa.dynamic = dev->dynamic_opt & DYN_EXTEND;
+    fa.reverse = fa.dynamic ? (dev->group_order_opt < 0 ? GROUP_ORDER_AUTO : dev->group_order_opt) : 0;
     long long local_pixels;
     if (list_mode) {
         // the previous ray list may still be read by a queued tail kernel

@@ -476,14 +476,16 @@ def test_dynamic_groups_invariance(device, root, name, film):
     (waves move on to the next open shard once their own is exhausted)
     renders the same image bit for bit, with the same ray counts, as the
     static grid-stride distribution: survivors stay in the shard they came
-    from and every path is taken exactly once."""
+    from and every path is taken exactly once; likewise with a shard's groups
+    taken from its end (group_order 1: classes C, B, A)."""
     sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", name))
     imgs, counts = [], []
     try:
         device.upload(sc)
-        for dynamic, tail in [(0, -1), (1, -1), (15, -1), (2, 0), (15, 0)]:
+        for dynamic, tail, order in [(0, -1, 0), (1, -1, 0), (15, -1, 0), (2, 0, 0), (15, 0, 0), (13, -1, 1), (13, -1, 0)]:
             device.set_option("dynamic", dynamic)
             device.set_option("tail_threshold", tail)
+            device.set_option("group_order", order)
             device.reset_stats()
             imgs.append(render_gpu(device, sc, film[0], film[1], 4))
             st = device.stats()
@@ -491,6 +493,7 @@ def test_dynamic_groups_invariance(device, root, name, film):
     finally:
         device.set_option("dynamic", 13)
         device.set_option("tail_threshold", -1)
+        device.set_option("group_order", -1)
     for im, c in zip(imgs[1:], counts[1:]):
         np.testing.assert_array_equal(imgs[0], im)
         assert c == counts[0]
