@@ -621,9 +621,7 @@ template <bool STATS>
 __device__ __forceinline__ void flush_stats(const TraceStats& st, unsigned long long* stats, int base, bool with_hits) {
     // slots: base+0..3 nodes/leaves/tris/blas, 8 hits, 9+base/4*2 .. wave node / leaf iterations
     unsigned long long a = st.nodes, b = st.leaves, c = st.tris, e = st.blas, h = st.hits, wn = st.wnodes, wl = st.wleaves;
-    unsigned long long cv[4] = {st.ccyc[16], st.ccyc[17], st.ccyc[18], st.ccyc[19]}; // lane node visits per class
     for (int off = 32; off > 0; off >>= 1) {
-        for (int k = 0; k < 4; ++k) cv[k] += __shfl_down(cv[k], off);
         a += __shfl_down(a, off);
         b += __shfl_down(b, off);
         c += __shfl_down(c, off);
@@ -643,10 +641,9 @@ __device__ __forceinline__ void flush_stats(const TraceStats& st, unsigned long 
 #ifndef IGX_SHADE_PROBE
         if (st.cyc[0] | st.cyc[1] | st.cyc[2] | st.cyc[3]) {
             for (int k = 0; k < 4; ++k) atomicAdd(&stats[16 + k], st.cyc[k]);
-            for (int k = 0; k < 16; ++k)
-                if (st.ccyc[k]) atomicAdd(&stats[20 + k], st.ccyc[k]);
-            for (int k = 0; k < 4; ++k)
-                if (cv[k]) atomicAdd(&stats[36 + k], cv[k]);
+            if (st.cls)
+                for (int k = 0; k < 20; ++k)
+                    if (st.cls[k]) atomicAdd(&stats[20 + k], st.cls[k]);
         }
 #endif
     }
@@ -730,6 +727,11 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
     if (!gen && row_total(kc.cnt_in) <= tail_threshold) return; // k_finish takes the remaining paths (block-uniform)
     const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : stage_treelet<BLOCK>(gsv, lds_scene);
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
+    __shared__ unsigned long long cls_mem[STATS ? WAVES_PER_BLOCK * 20 : 1]; // per-class counters (instrumented)
+    if constexpr (STATS) {
+        st.cls = cls_mem + 20 * (threadIdx.x >> 6);
+        if (lane_id() < 20) st.cls[lane_id()] = 0;
+    }
     const WaveWork w = wave_work();
     // Groups of 64 positions of shard s: statically every K-th group from
     // the wave's own (grid-stride), or (fa.dynamic) the next group a shard
@@ -814,10 +816,14 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
 #else
             const unsigned long long c_tr = st.cyc[1];
             phase_mark(st, t_last, 1);
-            st.ccyc[bucket] += st.cyc[1] - c_tr;
-            st.ccyc[8 + bucket] += 1;
-            st.ccyc[12 + bucket] += st.wnodes - wn0;
-            st.ccyc[16 + bucket] += st.nodes - ln0;
+            uint32_t visits = (uint32_t)(st.nodes - ln0);
+            for (int off = 32; off > 0; off >>= 1) visits += __shfl_xor(visits, off);
+            if (lane_id() == 0) {
+                st.cls[bucket] += st.cyc[1] - c_tr;
+                st.cls[8 + bucket] += 1;
+                st.cls[12 + bucket] += st.wnodes - wn0;
+                st.cls[16 + bucket] += visits;
+            }
 #endif
             if (act) {
                 f3 Lacc;
@@ -835,7 +841,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
 #else
             const unsigned long long c_sh = st.cyc[2];
             phase_mark(st, t_last, 2);
-            st.ccyc[4 + bucket] += st.cyc[2] - c_sh;
+            if (lane_id() == 0) st.cls[4 + bucket] += st.cyc[2] - c_sh;
 #endif
         }
         int dst, sdst;

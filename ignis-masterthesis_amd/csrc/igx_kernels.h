@@ -106,8 +106,9 @@ struct TraceStats {
     unsigned long long cyc[4] = {0, 0, 0, 0};
     // k_extend by the class of the wave's group (camera, A, B, C): trace
     // cycles 0-3, shade cycles 4-7, groups 8-11, wave-level node iterations
-    // 12-15, lane node visits 16-19
-    unsigned long long ccyc[20] = {};
+    // 12-15, lane node visits 16-19 -- the wave's 20 counters in LDS (lane 0
+    // updates them), so the instrumentation holds no registers
+    unsigned long long* cls = nullptr;
 };
 
 // true on the lowest active lane of the wave (counts one event per wave)
