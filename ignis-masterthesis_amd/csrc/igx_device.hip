@@ -1190,6 +1190,15 @@ __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, f
 // of wave-level steps.  Each wave walks the positions k, k + K, ... (in
 // groups of 64) of its shard, like the grid-stride kernels.
 // ---------------------------------------------------------------------------
+// k_trace_refill with an LDS treelet (option treelet_kernels bit 2; it loses:
+// the trace kernel's top nodes stay L2 hits anyway).  0 (default) compiles it
+// without one, so its node fetches are global loads instead of the flat loads
+// that serve LDS and global addresses alike: soup-1M 8-iteration frame
+// 315.8 / 313.5 -> 305.6 / 307.2 ms, soup-16M 118.2 -> 117.9 ms
+// (profiles/r03_ab_trace_global.log)
+#ifndef TRACE_TREELET
+#define TRACE_TREELET 0
+#endif
 // occupancy target of the persistent-lane kernels (waves per SIMD): 6 caps
 // them at 80 VGPRs (trace 4.8 -> 4.5 ms per S-deep iteration, soup-16M
 // 45.6 -> 43.3); 7 and 8 spill and run slower
@@ -1301,7 +1310,10 @@ template <int V0, bool STATS, bool LDS>
 __global__ void __launch_bounds__(BLOCK, LDS ? REFILL_WAVES_LDS : (variant_q4(V0) ? REFILL_WAVES_Q4 : REFILL_WAVES)) k_trace_refill(FrameArgs fa, SceneView gsv, PathBuf in, HitBuf hits,
                                                                      const int* cnt, int tail_threshold,
                                                                      unsigned long long* stats, int refill_min, int* work) {
-    constexpr int V = kernel_variant(V0, LDS); // LDS-staged nodes: padded stride; global tables: treelet (device_scene.h)
+    // LDS-staged nodes: padded stride; global tables: treelet (device_scene.h),
+    // unless the trace kernel stages none (TRACE_TREELET 0): then its node
+    // fetches are global loads, not the flat loads that serve both spaces
+    constexpr int V = LDS ? kernel_variant(V0, true) : (TRACE_TREELET ? kernel_variant(V0, false) : V0);
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
@@ -2155,7 +2167,7 @@ void configure_treelet(igx_device* dev) {
         return lo;
     };
     if (dev->treelet_kernels & 1) dev->tree_ext = fit([&](size_t t) { return extend_blocks_per_cu<false>(v, 0, t); });
-    if (refill && (dev->treelet_kernels & 2))
+    if (TRACE_TREELET && refill && (dev->treelet_kernels & 2))
         dev->tree_trace = fit([&](size_t t) { return trace_blocks_per_cu<false>(v, dev->trace_waves, 0, true, t); });
     if (dev->treelet_kernels & 4) dev->tree_shadow = fit([&](size_t t) { return shadow_blocks_per_cu<false>(v, 0, refill, t); });
     // k_finish: none -- the tail kernel overlaps the next chunk's kernels, and

@@ -363,6 +363,35 @@ def test_shading_variant_invariance(device, diamond_path):
     np.testing.assert_array_equal(imgs[0], imgs[1])
 
 
+@pytest.mark.parametrize("name", ["s_deep.json", "s_soup_1m.json"])
+def test_treelet_invariance(device, root, name):
+    """The LDS treelet of the hottest BVH nodes (global-table scenes: k_extend
+    and the shadow kernels read nodes below tree_n from LDS) changes where a
+    node is read from, never what is traced: images bit for bit equal and
+    ray counts equal with the treelet off, automatic and at 32 nodes, and
+    with the speculative trace kernel on and off."""
+    sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", name))
+    imgs, counts, staged = [], [], []
+    try:
+        device.upload(sc)
+        for treelet, spec in [(0, 1), (-1, 1), (32, 1), (-1, 0)]:
+            device.set_option("treelet", treelet)
+            device.set_option("speculative", spec)
+            device.reset_stats()
+            imgs.append(render_gpu(device, sc, 112, 80, 4))
+            st = device.stats()
+            counts.append((st["camera_rays"], st["bounce_rays"], st["shadow_rays"]))
+            staged.append(list(st["treelet_nodes"]))
+    finally:
+        device.set_option("treelet", -1)
+        device.set_option("speculative", 1)
+    assert staged[0] == [0, 0, 0, 0] and max(staged[1]) > 0 and max(staged[2]) <= 32, staged
+    for im, c in zip(imgs[1:], counts[1:]):
+        np.testing.assert_array_equal(imgs[0], im)
+        assert c == counts[0]
+    assert imgs[0].sum() > 0
+
+
 @pytest.mark.parametrize("name", ["diamond_scene.json", "s_deep.json"])
 def test_split_and_refill_invariance(device, root, name):
     """Fused k_extend, split k_trace + k_shade, and the persistent-lane (refill)
