@@ -96,6 +96,23 @@ constexpr int NSH = 64;             // shards per stream (one per lane of the co
 constexpr int CSTRIDE = 16;         // ints between two shard counters: one 64-B atomic line each
 constexpr int CROW = NSH * CSTRIDE; // ints per counter row (one row per stream and bounce)
 constexpr int WAVES_PER_BLOCK = BLOCK / 64;
+// k_trace_refill with an LDS treelet (option treelet_kernels bit 2; it loses:
+// the trace kernel's top nodes stay L2 hits anyway).  0 (default) compiles it
+// without one, so its node fetches are global loads instead of the flat loads
+// that serve LDS and global addresses alike: soup-1M 8-iteration frame
+// 315.8 / 313.5 -> 305.6 / 307.2 ms, soup-16M 118.2 -> 117.9 ms
+// (profiles/r03_ab_trace_global.log)
+#ifndef TRACE_TREELET
+#define TRACE_TREELET 0
+#endif
+// k_extend and the shadow kernels on global-table scenes: LDS treelet (1,
+// option treelet_kernels bits 1 and 4) or none and global node loads (0)
+#ifndef EXTEND_TREELET
+#define EXTEND_TREELET 1
+#endif
+#ifndef SHADOW_TREELET
+#define SHADOW_TREELET 1
+#endif
 [[maybe_unused]] constexpr int GRID_QUANTUM = NSH / WAVES_PER_BLOCK; // grids are multiples of this: every shard gets the same waves
 
 struct PathBuf {
@@ -716,7 +733,7 @@ __device__ __forceinline__ PathState camera_path(const FrameArgs& fa, const Scen
 template <int V0, bool STATS, bool LDS>
 __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(V0) ? EXTEND_WAVES_FULL : EXTEND_WAVES)) k_extend(FrameArgs fa, SceneView gsv, PathBuf in, PathBuf out, ShadowBuf sh,
                                                   float4* L, KernelCounters kc, int tail_threshold) {
-    constexpr int V = kernel_variant(V0, LDS); // LDS-staged nodes: padded stride; global tables: treelet (device_scene.h)
+    constexpr int V = LDS ? kernel_variant(V0, true) : (EXTEND_TREELET ? kernel_variant(V0, false) : V0); // LDS-staged nodes: padded stride; global tables: treelet (device_scene.h) or global node loads
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
@@ -874,7 +891,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
 template <int V0, bool STATS, int WAVES, bool LDS>
 __global__ void __launch_bounds__(BLOCK, WAVES) k_trace(FrameArgs fa, SceneView gsv, PathBuf in, HitBuf hits,
                                                       const int* cnt, int tail_threshold, unsigned long long* stats) {
-    constexpr int V = kernel_variant(V0, LDS); // LDS-staged nodes: padded stride; global tables: treelet (device_scene.h)
+    constexpr int V = LDS ? kernel_variant(V0, true) : V0; // LDS-staged nodes: padded stride; global tables: global node loads (no treelet)
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
@@ -959,7 +976,7 @@ template <int V0, bool STATS, bool LDS>
 __global__ void __launch_bounds__(BLOCK) k_finish(FrameArgs fa, SceneView gsv, PathBuf in, float4* L, const int* cnt,
                                                   int tail_threshold, unsigned long long* stats,
                                                   unsigned long long* tail_counts) {
-    constexpr int V = kernel_variant(V0, LDS); // LDS-staged nodes: padded stride; global tables: treelet (device_scene.h)
+    constexpr int V = LDS ? kernel_variant(V0, true) : V0; // LDS-staged nodes: padded stride; global tables: global node loads (the tail kernel stages no treelet)
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
@@ -1031,7 +1048,7 @@ template <int V0, bool STATS>
 __global__ void __launch_bounds__(BLOCK, FINISH_PAIRS_WAVES) k_finish_pairs(FrameArgs fa, SceneView gsv, PathBuf in, float4* L, const int* cnt,
                                                         int tail_threshold, unsigned long long* stats,
                                                         unsigned long long* tail_counts) {
-    constexpr int V = kernel_variant(V0, false);
+    constexpr int V = V0; // global node loads: the tail kernel stages no treelet
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
@@ -1146,7 +1163,7 @@ __global__ void __launch_bounds__(BLOCK, FINISH_PAIRS_WAVES) k_finish_pairs(Fram
 template <int V0, bool STATS, bool LDS>
 __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, float4* L, const int* cnt,
                                                   unsigned long long* stats, int* work) {
-    constexpr int V = kernel_variant(V0, LDS); // LDS-staged nodes: padded stride; global tables: treelet (device_scene.h)
+    constexpr int V = LDS ? kernel_variant(V0, true) : (SHADOW_TREELET ? kernel_variant(V0, false) : V0); // LDS-staged nodes: padded stride; global tables: treelet or global node loads
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
@@ -1190,15 +1207,6 @@ __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, f
 // of wave-level steps.  Each wave walks the positions k, k + K, ... (in
 // groups of 64) of its shard, like the grid-stride kernels.
 // ---------------------------------------------------------------------------
-// k_trace_refill with an LDS treelet (option treelet_kernels bit 2; it loses:
-// the trace kernel's top nodes stay L2 hits anyway).  0 (default) compiles it
-// without one, so its node fetches are global loads instead of the flat loads
-// that serve LDS and global addresses alike: soup-1M 8-iteration frame
-// 315.8 / 313.5 -> 305.6 / 307.2 ms, soup-16M 118.2 -> 117.9 ms
-// (profiles/r03_ab_trace_global.log)
-#ifndef TRACE_TREELET
-#define TRACE_TREELET 0
-#endif
 // occupancy target of the persistent-lane kernels (waves per SIMD): 6 caps
 // them at 80 VGPRs (trace 4.8 -> 4.5 ms per S-deep iteration, soup-16M
 // 45.6 -> 43.3); 7 and 8 spill and run slower
@@ -1350,7 +1358,11 @@ __global__ void __launch_bounds__(BLOCK, LDS ? REFILL_WAVES_LDS : (variant_q4(V0
 template <int V0, bool STATS, bool LDS>
 __global__ void __launch_bounds__(BLOCK, LDS ? REFILL_WAVES_LDS : (variant_ifif(V0) ? SHADOW_IFIF_WAVES : REFILL_WAVES)) k_shadow_refill(SceneView gsv, ShadowBuf sh, float4* L, const int* cnt,
                                                                       unsigned long long* stats, int refill_min, int* work) {
-    constexpr int V = kernel_variant(V0, LDS); // LDS-staged nodes: padded stride; global tables: treelet (device_scene.h)
+    // LDS-staged nodes: padded stride; global tables: treelet, except with if-if
+    // stepping (the split schedule's scenes), where global node loads beat the
+    // treelet's flat loads: soup-1M 32-iteration frame 1179.6 / 1188.1 ->
+    // 1154.5 / 1153.5 ms (profiles/r03_ab_treelet_global.log)
+    constexpr int V = LDS ? kernel_variant(V0, true) : ((SHADOW_TREELET && !variant_ifif(V0)) ? kernel_variant(V0, false) : V0);
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
@@ -2166,10 +2178,10 @@ void configure_treelet(igx_device* dev) {
         }
         return lo;
     };
-    if (dev->treelet_kernels & 1) dev->tree_ext = fit([&](size_t t) { return extend_blocks_per_cu<false>(v, 0, t); });
+    if (EXTEND_TREELET && (dev->treelet_kernels & 1)) dev->tree_ext = fit([&](size_t t) { return extend_blocks_per_cu<false>(v, 0, t); });
     if (TRACE_TREELET && refill && (dev->treelet_kernels & 2))
         dev->tree_trace = fit([&](size_t t) { return trace_blocks_per_cu<false>(v, dev->trace_waves, 0, true, t); });
-    if (dev->treelet_kernels & 4) dev->tree_shadow = fit([&](size_t t) { return shadow_blocks_per_cu<false>(v, 0, refill, t); });
+    if (SHADOW_TREELET && (dev->treelet_kernels & 4) && !(refill && use_shadow_ifif(dev))) dev->tree_shadow = fit([&](size_t t) { return shadow_blocks_per_cu<false>(v, 0, refill, t); });
     // k_finish: none -- the tail kernel overlaps the next chunk's kernels, and
     // LDS it holds keeps their blocks off the CU (soup-1M frame +4 % with one)
 }
