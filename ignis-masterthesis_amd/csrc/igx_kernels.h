@@ -212,6 +212,45 @@ __device__ __forceinline__ void trav_init(const SceneView& sv, Trav& t, f3 o, f3
     t.node = sv.num_inst > 0 ? sv.tlas_root : REF_EXIT; // the root may be a leaf (one entity)
 }
 
+// The N float4s of node `node` (NS float4s apart): treelet nodes (TREE, node
+// < tree_n) from LDS, the others from global memory.  Default: one generic
+// (flat) load sequence serves both address spaces, so the two sources share
+// registers.  IGX_TREE_SPLIT_LOADS: a branch per source with LDS and global
+// loads (ds_read_b128 / global_load_dwordx4) instead of flat loads.
+#ifndef IGX_TREE_SPLIT_LOADS
+#define IGX_TREE_SPLIT_LOADS 0
+#endif
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const f4v lds_f4v;
+typedef __attribute__((address_space(1))) const f4v global_f4v;
+template <int N, int NS, bool TREE>
+__device__ __forceinline__ void load_node(const SceneView& sv, int node, float4 (&f)[N]) {
+    if constexpr (IGX_TREE_SPLIT_LOADS && TREE) {
+        if (node < sv.tree_n) {
+            lds_f4v* np = (lds_f4v*)(sv.tree + NS * node);
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                const f4v v = np[k];
+                f[k] = make_float4(v.x, v.y, v.z, v.w);
+            }
+        } else {
+            global_f4v* np = (global_f4v*)(sv.nodes + NS * node);
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                const f4v v = np[k];
+                f[k] = make_float4(v.x, v.y, v.z, v.w);
+            }
+        }
+    } else {
+        const float4* np = (TREE && node < sv.tree_n ? sv.tree : sv.nodes) + NS * node;
+#pragma unroll
+        for (int k = 0; k < N; ++k) f[k] = np[k];
+    }
+}
+__device__ __forceinline__ int4 as_int4(float4 v) {
+    return make_int4(__float_as_int(v.x), __float_as_int(v.y), __float_as_int(v.z), __float_as_int(v.w));
+}
+
 // Slab test of both children of BVH2 node `node` (intersect_ray_box,
 // intersection.art:170-181, with ray.tmin folded in).  Returns the next node
 // (nearer child first; the other is pushed) or the popped entry.
@@ -225,9 +264,10 @@ __device__ __forceinline__ int node_step2(const SceneView& sv, const Trav& t, in
     // treelet nodes (TREE, node < tree_n) come from LDS: one generic (flat)
     // load sequence serves both address spaces, so the two sources share
     // registers (a branch per source cost the 80-VGPR persistent-lane kernels spills)
-    const float4* np = (TREE && node < sv.tree_n ? sv.tree : sv.nodes) + NS * node;
-    const float4 a = np[0], b = np[1], c = np[2];
-    const int4 r = *reinterpret_cast<const int4*>(np + 3);
+    float4 f[4];
+    load_node<4, NS, TREE>(sv, node, f);
+    const float4 a = f[0], b = f[1], c = f[2];
+    const int4 r = as_int4(f[3]);
     // child 0 box: lo (a.x, a.z, b.x) hi (a.y, a.w, b.y)
     // slab distances with explicit FMAs (the only contracted arithmetic
     // in the device code, built with -ffp-contract=off)
@@ -279,9 +319,10 @@ __device__ __forceinline__ int node_step4(const SceneView& sv, const Trav& t, in
         st.nodes++;
         if (first_active_lane()) st.wnodes++;
     }
-    const float4* np = (TREE && node < sv.tree_n ? sv.tree : sv.nodes) + NS * node; // see node_step2
-    const float4 lx = np[0], hx = np[1], ly = np[2], hy = np[3], lz = np[4], hz = np[5];
-    const int4 r = *reinterpret_cast<const int4*>(np + 6);
+    float4 f[7];
+    load_node<7, NS, TREE>(sv, node, f); // see node_step2
+    const float4 lx = f[0], hx = f[1], ly = f[2], hy = f[3], lz = f[4], hz = f[5];
+    const int4 r = as_int4(f[6]);
     float d[4];
     int ref[4] = {r.x, r.y, r.z, r.w};
     const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, HX[4] = {hx.x, hx.y, hx.z, hx.w};
@@ -324,9 +365,10 @@ __device__ __forceinline__ int node_step4q(const SceneView& sv, const Trav& t, i
         st.nodes++;
         if (first_active_lane()) st.wnodes++;
     }
-    const float4* np = (TREE && node < sv.tree_n ? sv.tree : sv.nodes) + 4 * node; // see node_step2
-    const float4 A = np[0], B = np[1], C = np[2];
-    const int4 r = *reinterpret_cast<const int4*>(np + 3);
+    float4 f[4];
+    load_node<4, 4, TREE>(sv, node, f); // see node_step2
+    const float4 A = f[0], B = f[1], C = f[2];
+    const int4 r = as_int4(f[3]);
     const float SX = A.w * t.idir.x, SY = B.x * t.idir.y, SZ = B.y * t.idir.z;
     const float OX = fmaf(A.x, t.idir.x, t.iorg.x), OY = fmaf(A.y, t.idir.y, t.iorg.y), OZ = fmaf(A.z, t.idir.z, t.iorg.z);
     const uint32_t qlx = __float_as_uint(B.z), qhx = __float_as_uint(B.w);
@@ -372,9 +414,10 @@ __device__ __forceinline__ int node_step8q(const SceneView& sv, const Trav& t, i
         st.nodes++;
         if (first_active_lane()) st.wnodes++;
     }
-    const float4* np = (TREE && node < sv.tree_n ? sv.tree : sv.nodes) + 8 * node; // see node_step2
-    const float4 A = np[0], B = np[1], C = np[2], D = np[3], E = np[4];
-    const int4 r0 = *reinterpret_cast<const int4*>(np + 5), r1 = *reinterpret_cast<const int4*>(np + 6);
+    float4 f[7];
+    load_node<7, 8, TREE>(sv, node, f); // see node_step2
+    const float4 A = f[0], B = f[1], C = f[2], D = f[3], E = f[4];
+    const int4 r0 = as_int4(f[5]), r1 = as_int4(f[6]);
     const float SX = A.w * t.idir.x, SY = B.x * t.idir.y, SZ = B.y * t.idir.z;
     const float OX = fmaf(A.x, t.idir.x, t.iorg.x), OY = fmaf(A.y, t.idir.y, t.iorg.y), OZ = fmaf(A.z, t.idir.z, t.iorg.z);
     const uint32_t qlx[2] = {__float_as_uint(B.z), __float_as_uint(B.w)}, qhx[2] = {__float_as_uint(C.x), __float_as_uint(C.y)};
