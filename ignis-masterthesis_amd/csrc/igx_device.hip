@@ -113,6 +113,11 @@ constexpr int WAVES_PER_BLOCK = BLOCK / 64;
 #ifndef SHADOW_TREELET
 #define SHADOW_TREELET 1
 #endif
+// the if-if shadow kernel of the split schedule with a treelet too (1) or
+// with global node loads only (0)
+#ifndef SHADOW_IFIF_TREELET
+#define SHADOW_IFIF_TREELET 0
+#endif
 [[maybe_unused]] constexpr int GRID_QUANTUM = NSH / WAVES_PER_BLOCK; // grids are multiples of this: every shard gets the same waves
 
 struct PathBuf {
@@ -1362,7 +1367,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? REFILL_WAVES_LDS : (variant_ifif(
     // stepping (the split schedule's scenes), where global node loads beat the
     // treelet's flat loads: soup-1M 32-iteration frame 1179.6 / 1188.1 ->
     // 1154.5 / 1153.5 ms (profiles/r03_ab_treelet_global.log)
-    constexpr int V = LDS ? kernel_variant(V0, true) : ((SHADOW_TREELET && !variant_ifif(V0)) ? kernel_variant(V0, false) : V0);
+    constexpr int V = LDS ? kernel_variant(V0, true) : ((SHADOW_TREELET && (SHADOW_IFIF_TREELET || !variant_ifif(V0))) ? kernel_variant(V0, false) : V0);
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
@@ -2181,7 +2186,7 @@ void configure_treelet(igx_device* dev) {
     if (EXTEND_TREELET && (dev->treelet_kernels & 1)) dev->tree_ext = fit([&](size_t t) { return extend_blocks_per_cu<false>(v, 0, t); });
     if (TRACE_TREELET && refill && (dev->treelet_kernels & 2))
         dev->tree_trace = fit([&](size_t t) { return trace_blocks_per_cu<false>(v, dev->trace_waves, 0, true, t); });
-    if (SHADOW_TREELET && (dev->treelet_kernels & 4) && !(refill && use_shadow_ifif(dev))) dev->tree_shadow = fit([&](size_t t) { return shadow_blocks_per_cu<false>(v, 0, refill, t); });
+    if (SHADOW_TREELET && (dev->treelet_kernels & 4) && (SHADOW_IFIF_TREELET || !(refill && use_shadow_ifif(dev)))) dev->tree_shadow = fit([&](size_t t) { return shadow_blocks_per_cu<false>(v, 0, refill, t); });
     // k_finish: none -- the tail kernel overlaps the next chunk's kernels, and
     // LDS it holds keeps their blocks off the CU (soup-1M frame +4 % with one)
 }

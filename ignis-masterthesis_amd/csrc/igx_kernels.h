@@ -213,12 +213,13 @@ __device__ __forceinline__ void trav_init(const SceneView& sv, Trav& t, f3 o, f3
 }
 
 // The N float4s of node `node` (NS float4s apart): treelet nodes (TREE, node
-// < tree_n) from LDS, the others from global memory.  Default: one generic
-// (flat) load sequence serves both address spaces, so the two sources share
-// registers.  IGX_TREE_SPLIT_LOADS: a branch per source with LDS and global
-// loads (ds_read_b128 / global_load_dwordx4) instead of flat loads.
+// < tree_n) from LDS, the others from global memory: a branch per source
+// with LDS and global loads (ds_read_b128 / global_load_dwordx4).  Round 3:
+// primitives frame 33.1 / 33.1 -> 31.2 / 31.3 ms, S-deep 177.4 / 173.7 ->
+// 161.8 / 162.1 ms against one generic (flat) load sequence serving both
+// address spaces (IGX_TREE_SPLIT_LOADS 0; profiles/r03_ab_split_loads.log).
 #ifndef IGX_TREE_SPLIT_LOADS
-#define IGX_TREE_SPLIT_LOADS 0
+#define IGX_TREE_SPLIT_LOADS 1
 #endif
 typedef float f4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const f4v lds_f4v;
