@@ -164,16 +164,36 @@ struct TStack {
     int cap;
     int sstride;
 };
+// LDS entries through an LDS pointer, spill entries through a global one: the
+// compiler then emits ds_* and global_* instructions instead of merging the
+// two sources into flat ones (IGX_STACK_SPLIT 0: the plain generic form)
+#ifndef IGX_STACK_SPLIT
+#define IGX_STACK_SPLIT 1
+#endif
+typedef __attribute__((address_space(3))) int lds_int;
+typedef __attribute__((address_space(1))) int global_int;
 template <bool SPILL>
 __device__ __forceinline__ void tpush(const TStack& s, int& sp, int v) {
-    if (!SPILL || sp < s.cap) s.lds[sp * TSTACK_STRIDE] = v;
-    else s.spill[(sp - s.cap) * s.sstride] = v;
+    if constexpr (IGX_STACK_SPLIT && SPILL) {
+        if (sp < s.cap) ((lds_int*)s.lds)[sp * TSTACK_STRIDE] = v;
+        else ((global_int*)s.spill)[(sp - s.cap) * s.sstride] = v;
+    } else {
+        if (!SPILL || sp < s.cap) s.lds[sp * TSTACK_STRIDE] = v;
+        else s.spill[(sp - s.cap) * s.sstride] = v;
+    }
     ++sp;
 }
 template <bool SPILL>
 __device__ __forceinline__ int tpop(const TStack& s, int& sp) {
     --sp;
-    return (!SPILL || sp < s.cap) ? s.lds[sp * TSTACK_STRIDE] : s.spill[(sp - s.cap) * s.sstride];
+    if constexpr (IGX_STACK_SPLIT && SPILL) {
+        int v;
+        if (sp < s.cap) v = ((lds_int*)s.lds)[sp * TSTACK_STRIDE];
+        else v = ((global_int*)s.spill)[(sp - s.cap) * s.sstride];
+        return v;
+    } else {
+        return (!SPILL || sp < s.cap) ? s.lds[sp * TSTACK_STRIDE] : s.spill[(sp - s.cap) * s.sstride];
+    }
 }
 __device__ __forceinline__ TStack make_tstack(int* lds_base, int cap, int* spill) {
     const int g = blockIdx.x * TSTACK_STRIDE + threadIdx.x;
