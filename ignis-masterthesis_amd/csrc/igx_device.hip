@@ -1222,9 +1222,13 @@ __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, f
 #ifndef REFILL_WAVES_Q4
 #define REFILL_WAVES_Q4 6
 #endif
-// the if-if shadow kernel (split-schedule scenes) needs fewer registers
+// the if-if shadow kernel (split-schedule scenes) needs fewer registers: with
+// quantised nodes and global stack / node loads it fits 7 waves per SIMD (72
+// VGPRs, 2 spilled): soup-1M shadow time per 8-iteration frame 102.0 -> 98.2 ms,
+// soup-16M 42.6 -> 42.0 ms (profiles/r03_ab_waves7.log; the trace kernel at 7
+// waves spills 23 registers and runs slower, so it stays at 6)
 #ifndef SHADOW_IFIF_WAVES
-#define SHADOW_IFIF_WAVES 6
+#define SHADOW_IFIF_WAVES 7
 #endif
 // LDS-staged tables (<= 48 KB + the 16 KB stack per block) allow at most
 // 4 blocks per CU: the 6-wave VGPR cap would only force spills
