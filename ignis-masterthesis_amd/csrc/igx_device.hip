@@ -485,22 +485,10 @@ __device__ __forceinline__ void ray_extent(const FrameArgs& fa, const SceneView&
 // advances `ps` by one bounce.  Returns whether the path continues (ps then
 // holds the bounced ray); fills the radiance gathered at this vertex (Lacc,
 // has_l) and the NEE shadow ray (has_shadow, sr).
-#ifdef IGX_SHADE_PROBE
-// dev probe: per-lane shader clock since the lane's previous mark -> slot k
-#define SHADE_MARK(k)                                                                                                 \
-    if (probe) {                                                                                                       \
-        const unsigned long long now_ = __builtin_amdgcn_s_memtime();                                                 \
-        probe->cyc[k] += now_ - *probe_last;                                                                          \
-        *probe_last = now_;                                                                                           \
-    }
-#else
-#define SHADE_MARK(k)
-#endif
 template <bool FULL>
 __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView& sv, PathState& ps, int hit_ent,
                                            int hit_prim, float tmax, float hu, float hv, f3& Lacc, bool& has_l,
-                                           bool& has_shadow, ShadowRec& sr, TraceStats* probe = nullptr,
-                                           unsigned long long* probe_last = nullptr) {
+                                           bool& has_shadow, ShadowRec& sr) {
     Lacc = mk(0, 0, 0);
     has_l = false;
     has_shadow = false;
@@ -522,7 +510,6 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
     int mat_id;
     Surface s = surface_element(sv, hit_ent, hit_prim, tmax, hu, hv, ps.o, rd, mat_id);
     const DevMaterial& m = sv.mats[mat_id];
-    SHADE_MARK(1)
     // on_hit (pathtracer.art:114-134)
     if (m.light >= 0 && s.entering) {
         float dt = -dot(rd, s.local.n);
@@ -571,7 +558,6 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
             has_shadow = true;
         }
     }
-    SHADE_MARK(2)
     // on_bounce (pathtracer.art:165-200)
     if (!(ps.depth + 1 <= sv.max_depth)) return false;
     BsdfSample bs = bsdf_sample<FULL>(m, s, rnd, out_dir);
@@ -639,6 +625,53 @@ __device__ __forceinline__ void add_radiance(float4* L, int slot, f3 c) {
     L[slot] = make_float4(l.x + c.x, l.y + c.y, l.z + c.z, 0);
 }
 
+// extend_step of the instrumented k_extend (STATS): the trace and shade halves
+// with phase clocks between them (load -> 0, trace -> 1, shade -> 2), and the
+// per-class counters of the wave's group (`bucket`: camera, A, B, C; lane 0
+// adds the wave's trace / shade cycles, one group, its wave-level node-loop
+// iterations and its lanes' node visits, both reduced over the wave).
+template <int V>
+__device__ __forceinline__ bool extend_step_instrumented(const FrameArgs& fa, const SceneView& sv, const TStack& ts, float4* L,
+                                                      PathState& ps, bool act, int bucket, bool& has_shadow, ShadowRec& sr,
+                                                      TraceStats& st, unsigned long long& t_last) {
+    int hit_ent = -1, hit_prim = -1;
+    float hu = 0, hv = 0, tmin = 0, tmax = 0;
+    uint32_t rflags = 0;
+    bool alive = false;
+    phase_mark(st, t_last, 0);
+    const unsigned long long wn0 = st.wnodes, ln0 = st.nodes;
+    if (act) {
+        ray_extent(fa, sv, ps.depth, ps.slot, tmin, tmax, rflags);
+        trace_path_ray<true, V>(sv, ps.inside, ps.o, ps.d, tmin, tmax, rflags, ts, hit_ent, hit_prim, hu, hv, st);
+        if (hit_ent >= 0) st.hits++;
+    }
+    const unsigned long long c_tr = st.cyc[1];
+    phase_mark(st, t_last, 1);
+    // wnodes counts on the first active lane of each iteration, so the wave's
+    // iterations are the sum over its lanes (as flush_stats reduces them)
+    uint32_t visits = (uint32_t)(st.nodes - ln0), witers = (uint32_t)(st.wnodes - wn0);
+    for (int off = 32; off > 0; off >>= 1) {
+        visits += __shfl_xor(visits, off);
+        witers += __shfl_xor(witers, off);
+    }
+    if (lane_id() == 0) {
+        st.cls[bucket] += st.cyc[1] - c_tr;
+        st.cls[8 + bucket] += 1;
+        st.cls[12 + bucket] += witers;
+        st.cls[16 + bucket] += visits;
+    }
+    if (act) {
+        f3 Lacc;
+        bool has_l;
+        alive = shade_step<variant_full(V)>(fa, sv, ps, hit_ent, hit_prim, tmax, hu, hv, Lacc, has_l, has_shadow, sr);
+        if (has_l) add_radiance(L, ps.slot, Lacc);
+    }
+    const unsigned long long c_sh = st.cyc[2];
+    phase_mark(st, t_last, 2);
+    if (lane_id() == 0) st.cls[4 + bucket] += st.cyc[2] - c_sh;
+    return alive;
+}
+
 template <bool STATS>
 __device__ __forceinline__ void flush_stats(const TraceStats& st, unsigned long long* stats, int base, bool with_hits) {
     // slots: base+0..3 nodes/leaves/tris/blas, 8 hits, 9+base/4*2 .. wave node / leaf iterations
@@ -660,22 +693,13 @@ __device__ __forceinline__ void flush_stats(const TraceStats& st, unsigned long 
         if (with_hits) atomicAdd(&stats[8], h);
         atomicAdd(&stats[9 + (base / 4) * 2], wn);
         atomicAdd(&stats[10 + (base / 4) * 2], wl);
-#ifndef IGX_SHADE_PROBE
         if (st.cyc[0] | st.cyc[1] | st.cyc[2] | st.cyc[3]) {
             for (int k = 0; k < 4; ++k) atomicAdd(&stats[16 + k], st.cyc[k]);
             if (st.cls)
                 for (int k = 0; k < 20; ++k)
                     if (st.cls[k]) atomicAdd(&stats[20 + k], st.cls[k]);
         }
-#endif
     }
-#ifdef IGX_SHADE_PROBE // per-lane marks: the lanes' sum / 64
-    for (int k = 0; k < 4; ++k) {
-        unsigned long long c = st.cyc[k];
-        for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off);
-        if (lane_id() == 0 && c) atomicAdd(&stats[16 + k], c / 64);
-    }
-#endif
 }
 
 // Dynamic distribution of a launch's groups of 64 stream positions: the
@@ -784,11 +808,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
         } else if (p0 >= sc.n) {
             break;
         }
-#ifdef IGX_SHADE_PROBE
-        if (STATS) phase_mark(st, t_last, 0);
-#else
         if (STATS) phase_mark(st, t_last, 3); // group distribution
-#endif
         const int ns = sc.n;
         int* const c_out = kc.cnt_out + s * CSTRIDE;
         int* const c_sh = kc.cnt_shadow + s * CSTRIDE;
@@ -814,57 +834,10 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
             }
         }
         if constexpr (STATS) {
-            // instrumented: extend_step's two halves with phase clocks between them
-            const bool act = q < ns && ps.depth > 0;
-            int hit_ent = -1, hit_prim = -1;
-            float hu = 0, hv = 0, tmin = 0, tmax = 0;
-            uint32_t rflags = 0;
-#ifdef IGX_SHADE_PROBE
-            phase_mark(st, t_last, 0); // probe: everything outside shade_step -> 0
-#else
-            phase_mark(st, t_last, 0);
-#endif
             // class of the wave's group (wave-uniform): camera, A, B, C
             const int pg = (fa.reverse && !gen) ? ns - 1 - p0 : p0;
             const int bucket = gen ? 0 : (pg < sc.a ? 1 : pg < sc.ab ? 2 : 3);
-            const unsigned long long wn0 = st.wnodes, ln0 = st.nodes;
-            if (act) {
-                ray_extent(fa, sv, ps.depth, ps.slot, tmin, tmax, rflags);
-                trace_path_ray<STATS, V>(sv, ps.inside, ps.o, ps.d, tmin, tmax, rflags, ts, hit_ent, hit_prim, hu, hv, st);
-                if (hit_ent >= 0) st.hits++;
-            }
-#ifdef IGX_SHADE_PROBE
-            phase_mark(st, t_last, 0);
-#else
-            const unsigned long long c_tr = st.cyc[1];
-            phase_mark(st, t_last, 1);
-            uint32_t visits = (uint32_t)(st.nodes - ln0);
-            for (int off = 32; off > 0; off >>= 1) visits += __shfl_xor(visits, off);
-            if (lane_id() == 0) {
-                st.cls[bucket] += st.cyc[1] - c_tr;
-                st.cls[8 + bucket] += 1;
-                st.cls[12 + bucket] += st.wnodes - wn0;
-                st.cls[16 + bucket] += visits;
-            }
-#endif
-            if (act) {
-                f3 Lacc;
-                bool has_l;
-#ifdef IGX_SHADE_PROBE
-                alive = shade_step<variant_full(V)>(fa, sv, ps, hit_ent, hit_prim, tmax, hu, hv, Lacc, has_l, has_shadow, sr,
-                                                    &st, &t_last);
-#else
-                alive = shade_step<variant_full(V)>(fa, sv, ps, hit_ent, hit_prim, tmax, hu, hv, Lacc, has_l, has_shadow, sr);
-#endif
-                if (has_l) add_radiance(L, ps.slot, Lacc);
-            }
-#ifdef IGX_SHADE_PROBE
-            phase_mark(st, t_last, 3); // bounce sampling and the rest
-#else
-            const unsigned long long c_sh = st.cyc[2];
-            phase_mark(st, t_last, 2);
-            if (lane_id() == 0) st.cls[4 + bucket] += st.cyc[2] - c_sh;
-#endif
+            alive = extend_step_instrumented<V>(fa, sv, ts, L, ps, q < ns && ps.depth > 0, bucket, has_shadow, sr, st, t_last);
         }
         int dst, sdst;
         wave_append_paths(alive, path_class(fa.classify, sv, ps), has_shadow,
@@ -878,11 +851,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
             sh.s2[e] = make_float4(sr.color.x, sr.color.y, sr.color.z, 0);
         }
         if (!fa.dynamic) p0 += w.K * 64;
-#ifdef IGX_SHADE_PROBE
-        if (STATS) phase_mark(st, t_last, 0);
-#else
         if (STATS) phase_mark(st, t_last, 3);
-#endif
     }
     if (STATS) flush_stats<STATS>(st, kc.stats, 0, true);
 }

@@ -218,7 +218,7 @@ __device__ __forceinline__ void trav_init(const SceneView& sv, Trav& t, f3 o, f3
     t.idir = mk(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
     t.iorg = mk(-(o.x * t.idir.x), -(o.y * t.idir.y), -(o.z * t.idir.z));
     t.tmin = tmin;
-    t.tmax = tmax;
+    t.tmax = fminf(tmax, FLT_MAX_); // finite: +inf bounds (absent children) then fail every slab test
     t.rflags = rflags;
     t.cur_ent = -1;
     t.hit_ent = -1;
@@ -282,9 +282,8 @@ __device__ __forceinline__ int node_step2(const SceneView& sv, const Trav& t, in
         st.nodes++;
         if (first_active_lane()) st.wnodes++;
     }
-    // treelet nodes (TREE, node < tree_n) come from LDS: one generic (flat)
-    // load sequence serves both address spaces, so the two sources share
-    // registers (a branch per source cost the 80-VGPR persistent-lane kernels spills)
+    // treelet nodes (TREE, node < tree_n) from LDS, the others from global
+    // memory (load_node: a branch per address space)
     float4 f[4];
     load_node<4, NS, TREE>(sv, node, f);
     const float4 a = f[0], b = f[1], c = f[2];
@@ -726,7 +725,7 @@ __device__ __forceinline__ bool trav_init_enclosed(const SceneView& sv, Trav& t,
     t.idir = mk(safe_rcp(t.ld.x), safe_rcp(t.ld.y), safe_rcp(t.ld.z));
     t.iorg = mk(-(t.lo.x * t.idir.x), -(t.lo.y * t.idir.y), -(t.lo.z * t.idir.z));
     t.tmin = tmin;
-    t.tmax = tmax;
+    t.tmax = fminf(tmax, FLT_MAX_); // see trav_init
     t.rflags = rflags;
     t.cur_ent = info.x;
     t.hit_ent = -1;

@@ -1048,7 +1048,9 @@ extern "C" int32_t igx_objscene_add(igx_objscene* sc, int32_t type, const char* 
 extern "C" int32_t igx_objscene_set_property(igx_objscene* sc, int32_t h, const char* key, int32_t type, const void* data,
                                              uint64_t count) {
     Value* obj = find_object(sc, h);
-    if (!obj || !key || (!data && type != IGX_PROP_INTEGER_ARRAY && type != IGX_PROP_NUMBER_ARRAY)) return -1;
+    // an array property may be empty (count 0, data NULL); every other form reads data
+    const bool array = type == IGX_PROP_INTEGER_ARRAY || type == IGX_PROP_NUMBER_ARRAY;
+    if (!obj || !key || (!data && (!array || count > 0))) return -1;
     const std::string k = key;
     if (k == "type" || k == "name" || k == "__base_dir") return -1; // set by igx_objscene_add
     Value v;

@@ -1047,3 +1047,43 @@ def test_database_adapter_renders_bit_identically(device, root, name, max_leaf):
     assert np.array_equal(a, b), f"max |diff| {np.abs(a - b).max()}"
     assert np.array_equal(a, c)
     assert ra["bvh_depth"] > 0
+
+
+def test_imported_one_leaf_blas_with_infinite_tmax(device):
+    """A reference BLAS whose root wraps ONE leaf of more than 16 triangles
+    (BvhNAdapter.h:94-98) is imported with the duplicated sibling absent
+    (kEmptyRef, +inf bounds).  Rays with tmax = +inf and an all-positive
+    direction (the case where an +inf box passes a slab test against an
+    infinite tmax) must not enter it: closest hits equal those over igx's own
+    BVH of the same scene (trav_init keeps tmax finite)."""
+    from refdb import RefDatabase
+
+    doc = {
+        "technique": {"type": "path", "max_depth": 2},
+        "camera": {"type": "perspective", "fov": 60, "near_clip": 0.01, "far_clip": 100,
+                   "transform": [1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, -4]},
+        "film": {"size": [64, 64]},
+        "bsdfs": [{"type": "diffuse", "name": "grey", "reflectance": [0.5, 0.5, 0.5]}],
+        "shapes": [{"type": "icosphere", "name": "Ball", "radius": 1.0, "subdivisions": 1}],
+        "entities": [{"name": "Ball", "shape": "Ball", "bsdf": "grey"}],
+        "lights": [{"type": "env", "name": "sky", "radiance": [1, 1, 1]}],
+    }
+    scene = ignis_amd.Scene.from_string(json.dumps(doc))
+    assert scene.desc.meshes[0].num_faces == 80
+    db, sv, keep = RefDatabase(scene, max_leaf=100).views()  # one leaf of 80 triangles under the root
+    adapted = ignis_amd.Scene.from_database(db, sv)
+    rng = np.random.default_rng(3)
+    n = 20000
+    rays = np.zeros((n, 8), np.float32)
+    rays[:, 0:3] = rng.uniform(-3.0, -1.2, size=(n, 3))
+    d = rng.uniform(0.05, 1.0, size=(n, 3))
+    rays[:, 3:6] = d / np.linalg.norm(d, axis=1, keepdims=True)
+    rays[:, 6], rays[:, 7] = 0.0, np.inf
+    device.upload(scene)
+    own = device.trace_hits(rays, 0x4)
+    device.upload(adapted)
+    imp = device.trace_hits(rays, 0x4)
+    assert (own[0][:, 0] >= 0).mean() > 0.05  # some rays hit the ball, the rest miss
+    np.testing.assert_array_equal(own[0], imp[0])
+    np.testing.assert_array_equal(own[1], imp[1])
+    del keep

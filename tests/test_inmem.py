@@ -108,6 +108,22 @@ def test_object_scene_rules():
         ignis_amd.Scene.from_objects(o)
 
 
+def test_object_scene_array_without_data():
+    """igx_objscene_set_property: an empty array property (count 0) may pass
+    NULL data; NULL data with a count, or for any non-array type, is refused
+    instead of being read."""
+    from ignis_amd._native import lib
+
+    o = ignis_amd.ObjectScene()
+    h = o.add("shapes", "rectangle", "r")
+    L = lib()
+    for ptype in (o.INTEGER_ARRAY, o.NUMBER_ARRAY):
+        assert L.igx_objscene_set_property(o._h, h, b"values", ptype, None, 3) == -1
+        assert L.igx_objscene_set_property(o._h, h, b"values", ptype, None, 0) == 0
+    for ptype in (o.BOOL, o.INTEGER, o.NUMBER, o.STRING, o.TRANSFORM, o.VECTOR2, o.VECTOR3):
+        assert L.igx_objscene_set_property(o._h, h, b"width", ptype, None, 1) == -1
+
+
 def _build_native(tmp_path):
     exe = str(tmp_path / "inmem_kats")
     subprocess.run(["g++", "-O1", "-std=c++17", "-I", os.path.join(ROOT, "include"), "-I", os.path.join(PKG, "host"),
