@@ -13,8 +13,12 @@ Multi-GPU (torchrun, one rank per GPU): the film is cut into square tiles
 dealt round-robin to the ranks (tile t -> rank t % N); every rank renders all 32
 iterations of its tiles, packs them, and an RCCL gather over xGMI brings the
 packed tiles to rank 0, which assembles the frame.  Total work is fixed, so
-scaling is "strong".  `--scene scenes/s_deep.json --size 4096 --spp 64` is the
-config-5 stand-in.
+scaling is "strong".  At every N the line also carries `config5`: BASELINE
+config 5's stand-in (S-deep at 4096x4096, 64 spp) rendered the
+same way, tile-sharded over the N ranks and gathered; at N > 1 both carry a
+per-rank breakdown (`ranks`: frame / pack / gather ms and rays per rank) and
+`frame_equals_single_gpu` (the gathered frame against rank 0's whole-frame
+render, bit for bit).
 
 Output: ONE JSON line on rank 0.
 """
@@ -47,8 +51,12 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample length")
     ap.add_argument("--suite", type=int, default=1, help="also measure the other §8d scenes (N=1 only)")
-    ap.add_argument("--check-frame", action="store_true",
-                    help="N>1: rank 0 also renders the whole frame alone and checks the gathered frame equals it bit for bit")
+    ap.add_argument("--check-frame", action="store_true", help="(default at N > 1; kept for older scripts)")
+    ap.add_argument("--no-check-frame", action="store_true",
+                    help="N>1: skip rank 0's whole-frame render that checks the gathered frame bit for bit")
+    ap.add_argument("--config5", type=int, default=1,
+                    help="also measure BASELINE config 5's stand-in (S-deep 4096x4096, 64 spp) tile-sharded over the N ranks")
+    ap.add_argument("--config5-steps", type=int, default=2, help="timed frames of the config-5 line")
     return ap.parse_args()
 
 
@@ -259,6 +267,206 @@ def suite_line(ignis_amd, dev_index, path, spi, iters, size=None):
     return line
 
 
+class RankFrames:
+    """One rank's frames of an N-GPU tile-sharded render: the
+    film is cut into square tiles dealt round-robin to the ranks; a frame is
+    every iteration of the rank's tiles, then igx_pack_tiles and one gather of
+    the packed tiles to rank 0 (RCCL over xGMI), which assembles the frame.
+    At N = 1 a frame is simply the whole film on one handle.
+
+    N > 1: frames alternate between two device handles on the rank's GPU (own
+    streams, framebuffer and path slots), so frame k+1's wavefront is queued
+    before frame k is packed and gathered: the gather and frame k's tail
+    kernel (its longest paths) overlap the next frame's
+    bounces, as consecutive frames already overlap on one GPU (N = 1 has no
+    per-frame synchronisation).  Every frame is fully rendered and gathered
+    inside the timed region."""
+
+    def __init__(self, ignis_amd, torch, dist, scene, W, H, spi, iters, rank, n, gpu, comm):
+        from ignis_amd import shard
+        self.ig, self.torch, self.dist, self.scene = ignis_amd, torch, dist, scene
+        self.W, self.H, self.spi, self.iters, self.rank, self.n, self.gpu, self.comm = W, H, spi, iters, rank, n, gpu, comm
+        self.tile = shard.balanced_tile(W, n)
+        self.devs = [ignis_amd.Device(gpu)]
+        self.devs[0].upload(scene)
+        self.pending = []
+        self.count = 0
+        if n > 1:
+            max_tiles = shard.max_tiles_per_rank(W, H, self.tile, n)
+            self.pack = torch.zeros(max_tiles * self.tile * self.tile * 3, dtype=torch.float32, device="cuda")
+            self.gather_bufs = [torch.zeros(self.pack.numel(), dtype=torch.float32, device=comm)
+                                for _ in range(n)] if rank == 0 else None
+            self.frame = torch.zeros((W * H, 3), dtype=torch.float32, device="cuda")
+            dst = torch.from_numpy(shard.packed_destinations(W, H, self.tile, n)).cuda()
+            self.valid = dst >= 0
+            self.dst_valid = dst[self.valid]
+            self.devs.append(ignis_amd.Device(gpu))
+            self.devs[1].upload(scene)
+            # one stream slot per handle, sized to the rank's share of a frame
+            for d in self.devs:
+                d.set_option("stream_slots", 1)
+                d.set_option("slot_budget_mb", SLOT_BUDGET_MB)
+
+    def params(self, it=0):
+        p = self.ig.RenderParams()
+        p.width, p.height, p.spi, p.iteration, p.frame, p.seed = self.W, self.H, self.spi, it, 0, 0
+        if self.n > 1:
+            p.tile_size, p.tile_offset, p.tile_stride = self.tile, self.rank, self.n
+        return p
+
+    def _pack(self, d):
+        self.torch.cuda.current_stream().synchronize()  # the previous gather has read `pack`
+        d.pack_tiles(self.params(0), self.pack.data_ptr(), self.pack.numel())  # waits for d's frame
+
+    def _gather(self):
+        # RCCL gather over xGMI to rank 0 (SURVEY.md §8e), assembled there
+        self.dist.gather(self.pack if self.comm == "cuda" else self.pack.cpu(), self.gather_bufs, dst=0)
+        if self.rank == 0:
+            allpix = self.torch.cat(self.gather_bufs).to("cuda").view(-1, 3)
+            self.frame[self.dst_valid] = allpix[self.valid]
+
+    def render_frame(self):
+        d = self.devs[self.count % len(self.devs)]
+        self.count += 1
+        d.clear()
+        # all iterations of the frame in one call: iterations whose paths fit the
+        # capacity are traced as one wavefront
+        d.render_iterations(self.params(0), self.iters)
+        if self.n > 1:
+            if self.pending:
+                e = self.pending.pop()
+                self._pack(e)
+                self._gather()
+            self.pending.append(d)
+
+    def drain(self):
+        if self.pending:
+            e = self.pending.pop()
+            self._pack(e)
+            self._gather()
+        self.torch.cuda.synchronize()
+
+    def measure(self, steps, warmup):
+        """warm-up, then `steps` frames between a barrier + synchronize on both
+        sides; elapsed = the slowest rank's, ray totals summed over ranks"""
+        torch, dist = self.torch, self.dist
+        # every device handle renders (and gathers) at least once before timing:
+        # its framebuffer, path slots and events are allocated outside the timed region
+        for _ in range(max(warmup, len(self.devs))):
+            self.render_frame()
+        self.drain()
+        for d in self.devs:
+            d.reset_stats()
+            d.set_option("timing", 1)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            self.render_frame()
+        self.drain()
+        if dist:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        st = self.devs[0].stats()
+        for d in self.devs[1:]:
+            s2 = d.stats()
+            for key in ("camera_rays", "bounce_rays", "shadow_rays", "ms_trace", "ms_extend", "ms_shadow", "ms_finish",
+                        "ms_generate", "ms_resolve", "launches_extend", "launches_trace", "extend_rays",
+                        "extend_paths_out", "tail_shadow_rays", "tail_bounce_rays"):
+                st[key] += s2[key]
+        for d in self.devs:
+            d.set_option("timing", 0)
+        self.rank_rays = st["camera_rays"] + st["bounce_rays"] + st["shadow_rays"]
+        totals = np.array([self.rank_rays, st["camera_rays"], st["bounce_rays"], st["shadow_rays"]], dtype=np.float64)
+        if dist:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=self.comm)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+            tt = torch.tensor(totals, dtype=torch.float64, device=self.comm)
+            dist.all_reduce(tt, op=dist.ReduceOp.SUM)
+            totals = tt.cpu().numpy()
+        return {"elapsed": elapsed, "stats": st, "totals": totals,
+                "slot_bytes": [int(d.stats()["slot_bytes"]) for d in self.devs]}
+
+    def breakdown(self):
+        """One more frame, untimed for `value`, by phase on every rank: render
+        (all iterations of the rank's tiles, to completion), pack, then -- after
+        a barrier, so no rank's wait for a slower one is counted -- the gather
+        and rank 0's assembly; plus the rays of the rank's share in the timed
+        frames.  Per-rank lists, min / max / mean (shard.rank_summary)."""
+        from ignis_amd import shard
+        torch, dist, d = self.torch, self.dist, self.devs[0]
+        d.clear()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        d.render_iterations(self.params(0), self.iters)
+        d.synchronize()
+        t1 = time.perf_counter()
+        self._pack(d)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        dist.barrier()
+        t3 = time.perf_counter()
+        self._gather()
+        torch.cuda.synchronize()
+        t4 = time.perf_counter()
+        s = shard.rank_summary(dist, {"frame_ms": (t1 - t0) * 1e3, "pack_ms": (t2 - t1) * 1e3,
+                                      "gather_ms": (t4 - t3) * 1e3, "mrays": self.rank_rays / 1e6},
+                               "cpu" if self.comm == "cpu" else "cuda")
+        f = s["frame_ms"]
+        s["imbalance"] = round(f["max"] / f["min"], 4) if f["min"] > 0 else None
+        s["note"] = ("frame_ms: one rank's tiles rendered alone (all iterations, to completion); pack_ms: "
+                     "igx_pack_tiles; gather_ms: the gather to rank 0 after a barrier, plus rank 0's assembly; "
+                     "mrays: the rank's rays over the timed frames")
+        return s
+
+    def check(self):
+        """rank 0 renders the whole frame alone and compares the gathered frame
+        of the last frame with it bit for bit (tile sharding is exact: DESIGN.md §6)"""
+        torch, dist = self.torch, self.dist
+        gathered = self.frame.cpu().numpy()
+        ok = torch.tensor([0.0], dtype=torch.float64, device=self.comm)
+        if self.rank == 0:
+            ref = self.ig.Device(self.gpu)
+            ref.upload(self.scene)
+            p = self.ig.RenderParams()
+            p.width, p.height, p.spi = self.W, self.H, self.spi
+            ref.render_iterations(p, self.iters)
+            full, _ = ref.framebuffer(self.W * self.H * 3)
+            ref.close()
+            ok[0] = float(np.array_equal(full.reshape(-1, 3), gathered))
+        dist.broadcast(ok, 0)
+        return bool(ok.item())
+
+    def close(self):
+        for d in self.devs:
+            d.close()
+        self.devs = []
+
+
+def sharded_line(ignis_amd, torch, dist, path, size, spi, spp, rank, n, gpu, comm, steps, check):
+    """A second multi-GPU line (BASELINE config 5's stand-in): the scene at a
+    size x size film, `spp` samples, tile-sharded over the N ranks exactly as
+    the headline frame, with the per-rank breakdown and the bit-exact check."""
+    scene = ignis_amd.Scene.from_file(path)
+    iters = max(1, math.ceil(spp / spi))
+    rf = RankFrames(ignis_amd, torch, dist, scene, size, size, spi, iters, rank, n, gpu, comm)
+    m = rf.measure(steps, 1)
+    line = {"workload": f"{os.path.basename(path)} {size}x{size}, {iters * spi} spp = {iters} iterations x spi {spi}, "
+                        "path tracer, seed 0 (BASELINE config 5 stand-in, SURVEY.md §8d)",
+            "scene": os.path.basename(path), "width": size, "height": size, "spp": iters * spi, "n_gpus": n,
+            "steps": steps, "value": round(float(m["totals"][0]) / m["elapsed"] / 1e6, 2), "unit": "Mrays/s",
+            "ms_per_step": round(m["elapsed"] / steps * 1e3, 3), "scaling": "strong",
+            "tile": rf.tile if n > 1 else None}
+    if n > 1:
+        line["ranks"] = rf.breakdown()
+        if check:
+            line["frame_equals_single_gpu"] = rf.check()
+    rf.close()
+    return line
+
+
 def launch_ranks(args):
     """`bench.py --gpus N` (N > 1) started without a launcher: run N ranks as a
     child `torch.distributed.run` (one process per GPU, rendezvous on
@@ -312,130 +520,13 @@ def main():
     W, H = (args.size, args.size) if args.size > 0 else scene.film_size
     spi = args.spi
     iters = max(1, math.ceil(args.spp / spi))
-    dev = ignis_amd.Device(gpu)
-    dev.upload(scene)
-
-    from ignis_amd import shard
-    tile = shard.balanced_tile(W, n_gpus)
-
-    def params(it):
-        p = ignis_amd.RenderParams()
-        p.width, p.height, p.spi, p.iteration, p.frame, p.seed = W, H, spi, it, 0, 0
-        if n_gpus > 1:
-            p.tile_size, p.tile_offset, p.tile_stride = tile, rank, n_gpus
-        return p
-
-    gather_bufs = None
-    if n_gpus > 1:
-        max_tiles = shard.max_tiles_per_rank(W, H, tile, n_gpus)
-        pack = torch.zeros(max_tiles * tile * tile * 3, dtype=torch.float32, device="cuda")
-        gather_bufs = [torch.zeros(pack.numel(), dtype=torch.float32, device=comm) for _ in range(n_gpus)] if rank == 0 else None
-        frame = torch.zeros((W * H, 3), dtype=torch.float32, device="cuda")
-        dst = torch.from_numpy(shard.packed_destinations(W, H, tile, n_gpus)).cuda()
-        valid = dst >= 0
-        dst_valid = dst[valid]
-
-    # N > 1: frames alternate between two device handles on the rank's GPU (own
-    # streams, framebuffer and path slots), so frame k+1's wavefront is queued
-    # before frame k is packed and gathered: the gather and frame k's tail
-    # kernel (its longest paths) overlap the next frame's
-    # bounces, as consecutive frames already overlap on one GPU (N = 1 has no
-    # per-frame synchronisation).  Every frame is fully rendered and gathered
-    # inside the timed region.
-    devs = [dev]
-    if n_gpus > 1:
-        devs.append(ignis_amd.Device(gpu))
-        devs[1].upload(scene)
-        # one stream slot per handle, sized to the rank's share of a frame
-        for d in devs:
-            d.set_option("stream_slots", 1)
-            d.set_option("slot_budget_mb", SLOT_BUDGET_MB)
-    pending = []
-    count = [0]
-
-    def gather(d):
-        # pack owned tiles, RCCL gather over xGMI to rank 0, assemble there
-        torch.cuda.current_stream().synchronize()  # the previous gather has read `pack`
-        d.pack_tiles(params(0), pack.data_ptr(), pack.numel())  # waits for d's frame
-        dist.gather(pack if comm == "cuda" else pack.cpu(), gather_bufs, dst=0)
-        if rank == 0:
-            allpix = torch.cat(gather_bufs).to("cuda").view(-1, 3)
-            frame[dst_valid] = allpix[valid]
-
-    def render_frame():
-        d = devs[count[0] % len(devs)]
-        count[0] += 1
-        d.clear()
-        # all iterations of the frame in one call: iterations whose paths fit the
-        # capacity are traced as one wavefront
-        d.render_iterations(params(0), iters)
-        if n_gpus > 1:
-            if pending:
-                gather(pending.pop())
-            pending.append(d)
-
-    def drain_frames():
-        if pending:
-            gather(pending.pop())
-        torch.cuda.synchronize()
-
-    # every device handle renders (and gathers) at least once before timing:
-    # its framebuffer, path slots and events are allocated outside the timed region
-    for _ in range(max(args.warmup, len(devs))):
-        render_frame()
-    drain_frames()
-
-    for d in devs:
-        d.reset_stats()
-        d.set_option("timing", 1)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        render_frame()
-    drain_frames()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    st = dev.stats()
-    for d in devs[1:]:
-        s2 = d.stats()
-        for key in ("camera_rays", "bounce_rays", "shadow_rays", "ms_trace", "ms_extend", "ms_shadow", "ms_finish",
-                    "ms_generate", "ms_resolve", "launches_extend", "launches_trace", "extend_rays", "extend_paths_out",
-                    "tail_shadow_rays", "tail_bounce_rays"):
-            st[key] += s2[key]
-    for d in devs:
-        d.set_option("timing", 0)
-
-    rays_ext = st["camera_rays"] + st["bounce_rays"]
-    rays_local = rays_ext + st["shadow_rays"]
-    totals = np.array([rays_local, st["camera_rays"], st["bounce_rays"], st["shadow_rays"]], dtype=np.float64)
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=comm)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        tt = torch.tensor(totals, dtype=torch.float64, device=comm)
-        dist.all_reduce(tt, op=dist.ReduceOp.SUM)
-        totals = tt.cpu().numpy()
-
-    frame_check = None
-    if n_gpus > 1 and args.check_frame:
-        # the gathered frame of the last timed step against the whole frame
-        # rendered by one device (tile sharding is exact: DESIGN.md §6)
-        gathered = frame.cpu().numpy()
-        ok = torch.tensor([0.0], dtype=torch.float64, device=comm)
-        if rank == 0:
-            ref = ignis_amd.Device(gpu)
-            ref.upload(scene)
-            p = ignis_amd.RenderParams()
-            p.width, p.height, p.spi = W, H, spi
-            ref.render_iterations(p, iters)
-            full, _ = ref.framebuffer(W * H * 3)
-            ref.close()
-            ok[0] = float(np.array_equal(full.reshape(-1, 3), gathered))
-        dist.broadcast(ok, 0)
-        frame_check = bool(ok.item())
+    rf = RankFrames(ignis_amd, torch, dist, scene, W, H, spi, iters, rank, n_gpus, gpu, comm)
+    dev, tile = rf.devs[0], rf.tile
+    params = rf.params
+    m = rf.measure(args.steps, args.warmup)
+    elapsed, st, totals = m["elapsed"], m["stats"], m["totals"]
+    ranks = rf.breakdown() if n_gpus > 1 else None
+    frame_check = rf.check() if n_gpus > 1 and not args.no_check_frame else None
 
     # ---- roofline of the dominant kernel, live HIP-event timing ----
     roof = roofline(dev, st, lambda: dev.render(params(0)), n_gpus, os.path.splitext(os.path.basename(args.scene))[0])
@@ -504,14 +595,27 @@ def main():
         }
         if frame_check is not None:
             result["frame_equals_single_gpu"] = frame_check
-        result["slot_bytes_per_handle"] = [int(d.stats()["slot_bytes"]) for d in devs]
+        if ranks is not None:
+            result["ranks"] = ranks
+        result["slot_bytes_per_handle"] = m["slot_bytes"]
         result["backend"] = ("gloo (rehearsal)" if rehearsal else "nccl (RCCL)") if n_gpus > 1 else None
+    rf.close()
+    if args.config5:
+        # BASELINE config 5 stand-in (S-deep at 4096x4096, 64 spp),
+        # measured the same way at every N: tile-sharded over the ranks, gathered
+        # to rank 0, per-rank breakdown (the headline frame above is config 2)
+        try:
+            c5 = sharded_line(ignis_amd, torch, dist, os.path.join(ROOT, "scenes", "s_deep.json"), 4096, spi, 64, rank,
+                              n_gpus, gpu, comm, args.config5_steps, not args.no_check_frame)
+        except Exception as e:  # the headline line still prints
+            c5 = {"error": f"{type(e).__name__}: {e}"}
+        if result is not None:
+            result["config5"] = c5
+    if result is not None:
         print(json.dumps(result), flush=True)
     if dist:
         dist.barrier()
         dist.destroy_process_group()
-    for d in devs:
-        d.close()
     return result
 
 

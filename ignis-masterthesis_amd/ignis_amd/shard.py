@@ -64,3 +64,27 @@ def assemble(gathered_rgb, dst, frame_rgb):
     valid = dst >= 0
     frame_rgb[dst[valid]] = gathered_rgb[valid]
     return frame_rgb
+
+
+def rank_summary(dist, values, device="cpu"):
+    """Per-rank figures of a sharded frame, collected on every rank: for each
+    key of `values` (this rank's float) the per-rank list in rank order, its
+    min, max and mean.  `dist` is torch.distributed (world > 1) or None (one
+    rank); the all_gather runs on `device` ("cuda" over RCCL, "cpu" over
+    gloo).  bench.py reports the frame, pack and gather times this way, so a
+    sub-linear scaling curve shows whether a slow rank or the gather costs it."""
+    import torch
+
+    keys = sorted(values)
+    mine = torch.tensor([float(values[k]) for k in keys], dtype=torch.float64, device=device)
+    if dist is not None and dist.get_world_size() > 1:
+        parts = [torch.zeros_like(mine) for _ in range(dist.get_world_size())]
+        dist.all_gather(parts, mine)
+        table = torch.stack(parts).cpu().numpy()
+    else:
+        table = mine.cpu().numpy()[None, :]
+    out = {}
+    for j, k in enumerate(keys):
+        col = [round(float(v), 3) for v in table[:, j]]
+        out[k] = {"min": min(col), "max": max(col), "mean": round(float(np.mean(col)), 3), "per_rank": col}
+    return out

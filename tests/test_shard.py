@@ -116,3 +116,35 @@ def test_gloo_world3_gather_assembles_frame():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert all(ok for _, ok, _ in res), res
+
+
+def _summary_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    s = shard.rank_summary(dist, {"frame_ms": 10.0 * (rank + 1), "gather_ms": 0.5 + rank})
+    q.put((rank, s))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_rank_summary():
+    """bench.py's per-rank breakdown (frame / pack / gather ms at N > 1): every
+    rank sees every rank's value, in rank order, with min / max / mean."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_summary_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=120) for _ in range(2)), key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, s in res:
+        assert s["frame_ms"] == {"min": 10.0, "max": 20.0, "mean": 15.0, "per_rank": [10.0, 20.0]}
+        assert s["gather_ms"]["per_rank"] == [0.5, 1.5]
+
+
+def test_rank_summary_single_rank():
+    s = shard.rank_summary(None, {"frame_ms": 3.25})
+    assert s == {"frame_ms": {"min": 3.25, "max": 3.25, "mean": 3.25, "per_rank": [3.25]}}
