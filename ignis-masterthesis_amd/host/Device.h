@@ -36,6 +36,7 @@
 
 #include <array>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -104,6 +105,42 @@ public:
     uint64_t bounceRayCount() const { return mStats.bounce_rays; }
     uint64_t shadowRayCount() const { return mStats.shadow_rays; }
     const igx_stats& raw() const { return mStats; }
+    // Statistics::dump (Statistics.cpp:151-290): kernel times (with the
+    // device's "timing" option, SetupSettings::AcquireStats) in place of the
+    // reference's per-shader timers, then the ray quantities; PrimaryRays =
+    // camera + bounce, TotalRays = camera + bounce + shadow (:286-290)
+    std::string dump(size_t totalMS, size_t iter) const {
+        std::string out = "Statistics:\n  Kernels (summed HIP-event time, ms):\n";
+        auto row = [&](const char* name, double ms, uint64_t launches) {
+            char b[160];
+            std::snprintf(b, sizeof(b), "  |-%-14s %10.3f [%llu]%s", name, ms, (unsigned long long)launches,
+                          iter ? "" : "\n");
+            out += b;
+            if (iter) {
+                std::snprintf(b, sizeof(b), "  %10.3f per Iteration\n", ms / (double)iter);
+                out += b;
+            }
+        };
+        row("Extend", mStats.ms_extend, mStats.launches_extend);
+        row("Trace", mStats.ms_trace, mStats.launches_trace);
+        row("Shadow", mStats.ms_shadow, mStats.launches_shadow);
+        row("Finish", mStats.ms_finish, mStats.launches_finish);
+        row("Generate", mStats.ms_generate, 0);
+        row("Resolve", mStats.ms_resolve, 0);
+        out += "  Quantities:\n";
+        auto qty = [&](const char* name, uint64_t count) {
+            char b[160];
+            std::snprintf(b, sizeof(b), "  |-%-12s %llu per ms [%llu]\n", name,
+                          (unsigned long long)(count / (totalMS ? totalMS : 1)), (unsigned long long)count);
+            out += b;
+        };
+        qty("CameraRays", mStats.camera_rays);
+        qty("ShadowRays", mStats.shadow_rays);
+        qty("BounceRays", mStats.bounce_rays);
+        qty("PrimaryRays", mStats.camera_rays + mStats.bounce_rays);
+        qty("TotalRays", mStats.camera_rays + mStats.bounce_rays + mStats.shadow_rays);
+        return out;
+    }
     igx_stats mStats{};
 };
 

@@ -102,8 +102,53 @@ struct Props {
         }
         return r;
     }
-    // colour: a number is a grey value, an array an RGB triple
-    V3 color(const char* k, V3 def) const { return vec3(k, def); }
+    // colour: a number is a grey value, an array an RGB triple; a string is a
+    // shading expression (ShadingTree::computeColor, PExpr), accepted here in
+    // its constant forms only -- a number, color(v), color(r, g, b) or
+    // color(r, g, b, a) (alpha dropped) -- as Blender exports plain colours
+    V3 color(const char* k, V3 def) const {
+        const Value* p = get(k);
+        if (!p || !p->is_string()) return vec3(k, def);
+        V3 c;
+        if (!constant_color(p->str, c))
+            fail(std::string("property '") + k + "': shading expression '" + p->str +
+                 "' is not a constant colour (shading networks are not supported)");
+        return c;
+    }
+    static bool constant_color(const std::string& e, V3& out) {
+        const char* s = e.c_str();
+        auto ws = [&]() { while (*s == ' ' || *s == '\t') ++s; };
+        auto num = [&](float& v) {
+            ws();
+            char* end = nullptr;
+            v = std::strtof(s, &end);
+            if (end == s) return false;
+            s = end;
+            return true;
+        };
+        ws();
+        float v[4];
+        int n = 0;
+        if (std::strncmp(s, "color", 5) == 0) {
+            s += 5;
+            ws();
+            if (*s++ != '(') return false;
+            for (;;) {
+                if (n == 4 || !num(v[n++])) return false;
+                ws();
+                if (*s == ',') { ++s; continue; }
+                if (*s++ != ')') return false;
+                break;
+            }
+            if (n == 2) return false;
+        } else if (!num(v[n++])) {
+            return false;
+        }
+        ws();
+        if (*s) return false;
+        out = n == 1 ? V3(v[0], v[0], v[0]) : V3(v[0], v[1], v[2]);
+        return true;
+    }
 };
 
 M4 matrix_from_array(const Value& a) {
@@ -767,19 +812,23 @@ static void build_scene(SceneStore& S, const Value& doc, const std::string& base
                 S.materials[ent.material].light = (int)S.lights.size();
             } else if (type == "env" || type == "constant" || type == "uniform") {
                 // EnvironmentLight.cpp:28-78: constant radiance bakes to a 1x1 texture -> make_environment_light
+                // a constant colour expression is accepted (Props::color); an image or
+                // a varying expression is a textured environment (not supported).
+                // The light's transform only rotates the texture lookup: without
+                // effect on a constant environment
                 V3 rad = lp.color("radiance", V3(1, 1, 1));
                 V3 scale = lp.color("scale", V3(1, 1, 1));
-                if (const Value* r = lp.get("radiance"))
-                    if (r->is_string()) fail("env light '" + name + "': textured environments are not supported");
                 L.type = IGX_LIGHT_ENV;
                 for (int i = 0; i < 3; ++i) L.radiance[i] = rad[i] * scale[i];
             } else if (type == "point") {
-                if (lp.has("power")) fail("point light '" + name + "': 'power' is not supported");
                 V3 pos = lp.vec3("position", V3());
-                V3 I = lp.color("intensity", V3(1, 1, 1));
+                // PointLight.cpp:16-30, 61-69: with `power` the intensity is power / (4 pi)
+                // (the embedded SimplePointLight's mColor_Cache / SR), the flux the power
+                const bool power = lp.has("power");
+                const V3 pw = power ? lp.color("power", V3(1, 1, 1)) : lp.color("intensity", V3(1, 1, 1)) * (4 * kPi);
+                const V3 I = power ? pw / (4 * kPi) : lp.color("intensity", V3(1, 1, 1));
                 L.type = IGX_LIGHT_POINT;
                 for (int i = 0; i < 3; ++i) { L.origin[i] = pos[i]; L.radiance[i] = I[i]; L.select_position[i] = pos[i]; }
-                const V3 pw = I * (4 * kPi); // PointLight.cpp:16-30
                 L.select_flux = (pw.x + pw.y + pw.z) / 3;
             } else if (type == "spot") {
                 if (lp.has("power")) fail("spot light '" + name + "': 'power' is not supported");

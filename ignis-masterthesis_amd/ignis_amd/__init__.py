@@ -263,6 +263,12 @@ class Device:
     def render(self, params):
         self._check(self._lib.igx_render(self._h, C.byref(params)))
 
+    def set_camera(self, camera):
+        """Replace the uploaded scene's camera (an N.Camera; igx_set_camera, as
+        Runtime::setCameraOrientationParameter reaches the device through
+        render's ParameterSet, Runtime.cpp:703-708)."""
+        self._check(self._lib.igx_set_camera(self._h, C.byref(camera)))
+
     def render_iterations(self, params, count):
         """`count` consecutive iterations from params.iteration (igx_render_iterations)."""
         self._check(self._lib.igx_render_iterations(self._h, C.byref(params), int(count)))

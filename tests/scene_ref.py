@@ -77,6 +77,15 @@ def _vec(v, default=None):
         return np.array(default, np.float64)
     if isinstance(v, (int, float)):
         return np.array([v, v, v], np.float64)
+    if isinstance(v, str):
+        # a PExpr colour expression (ShadingTree::computeColor) in its constant
+        # forms: a number, color(v), color(r, g, b), color(r, g, b, a)
+        import re
+        m = re.fullmatch(r"\s*color\s*\(([^()]*)\)\s*", v)
+        vals = [float(x) for x in (m.group(1).split(",") if m else [v])]
+        if len(vals) not in (1, 3, 4):
+            raise ValueError(f"not a constant colour: {v!r}")
+        return np.array(vals[:3] if len(vals) > 1 else vals * 3, np.float64)
     return np.array(list(v) + [0] * (3 - len(v)), np.float64)
 
 
@@ -330,9 +339,15 @@ def interpret(path):
         elif typ in ("env", "constant", "uniform"):
             lights.append({"type": "env", "radiance": _vec(l.get("radiance", 1.0)) * _vec(l.get("scale", 1.0))})
         elif typ == "point":
-            I = _vec(l.get("intensity", 1.0))
+            # PointLight.cpp:16-30, 61-69: `power` P gives the intensity P / (4 pi)
+            if "power" in l:
+                P = _vec(l["power"])
+                I = P / (4 * math.pi)
+            else:
+                I = _vec(l.get("intensity", 1.0))
+                P = I * 4 * math.pi
             lights.append({"type": "point", "position": _vec(l.get("position"), [0, 0, 0]), "intensity": I,
-                           "select_flux": float(np.mean(I)) * 4 * math.pi})  # PointLight.cpp:16-30
+                           "select_flux": float(np.mean(P))})
         elif typ == "spot":
             d = _vec(l.get("direction"), [0, 0, 1])
             c_, f_ = math.radians(l.get("cutoff", 30)), math.radians(l.get("falloff", 20))

@@ -588,32 +588,38 @@ def test_full_size_window_parity(device, diamond_path):
     assert np.isfinite(g).all() and (g >= 0).all()
 
 
-def test_config2_diamond_256spp_band_matches_cpu_device(device, diamond_path):
+def test_config2_diamond_256spp_matches_cpu_device(device, diamond_path):
     """BASELINE config 2 at its stated size: diamond 1000x1000, 256 spp = 32
     iterations x spi 8 (the bench's frame), rendered whole on the GPU in one
-    render_iterations call (the bench's chunking); the oracle accumulates the
-    same 32 iterations over a 48-row band.  Diamond contract of SURVEY.md §8c."""
+    render_iterations call (the bench's chunking); the oracle (the restated
+    reference CPU device) accumulates the same 32 iterations over the WHOLE
+    frame (~1.24 G rays, ~20 s on 16 threads).  Diamond contract of
+    SURVEY.md §8c, and the ray counts."""
     sc = ignis_amd.Scene.from_file(diamond_path)
     W = H = 1000
     device.upload(sc)
     device.set_option("capacity", 0)
     device.clear()
+    device.reset_stats()
     p = ignis_amd.RenderParams()
     p.width, p.height, p.spi = W, H, 8
     device.render_iterations(p, 32)
     g, it = device.framebuffer(W * H * 3)
     assert it == 32
-    y0, y1 = 476, 524
+    st = device.stats()
     orc = O.OracleScene(sc)
     o = np.zeros(W * H * 3, np.float32)
+    rays = 0
     for k in range(32):
-        orc.render(W, H, 8, iteration=k, threads=16, window=(0, y0, W, y1), fb=o)
-    gb = g.reshape(H, W, 3)[y0:y1] / 32
-    ob = o.reshape(H, W, 3)[y0:y1] / 32
-    assert rel_mse(gb, ob) <= 5e-3
-    close = np.abs(gb - ob) <= 1e-2 * np.maximum(np.abs(ob), 1e-2)
+        _, ost = orc.render(W, H, 8, iteration=k, threads=16, fb=o)
+        rays += ost["camera_rays"] + ost["bounce_rays"] + ost["shadow_rays"]
+    gi, oi = g.reshape(H, W, 3) / 32, o.reshape(H, W, 3) / 32
+    assert rel_mse(gi, oi) <= 5e-3
+    close = np.abs(gi - oi) <= 1e-2 * np.maximum(np.abs(oi), 1e-2)
     assert close.mean() >= 0.99, close.mean()
     assert np.isfinite(g).all() and (g >= 0).all()
+    gpu_rays = st["camera_rays"] + st["bounce_rays"] + st["shadow_rays"]
+    assert abs(gpu_rays - rays) / rays < 1e-3, (gpu_rays, rays)
 
 
 def test_config3_primitives_256spp_matches_cpu_device(device, primitives_path):
@@ -834,6 +840,42 @@ def test_igcli_writes_exr(tmp_path, diamond_path, root):
     np.testing.assert_array_equal(img, ref)
 
 
+def test_igcli_camera_orientation_matches_api(tmp_path, diamond_path, root):
+    """igcli --eye / --dir / --up (cli/main.cpp:103-107 -> the runtime's
+    __camera_* parameters -> IG::Device::render's ParameterSet) and --width /
+    --height render the same image, bit for bit, as the API with the scene
+    camera replaced by that orientation; --stats dumps the ray quantities."""
+    import subprocess
+    from exr_read import read_exr
+    from ignis_amd import _native as N
+    out = tmp_path / "img.exr"
+    exe = os.path.join(root, "ignis-masterthesis_amd", "igcli")
+    eye, dr, up = (0.4, -0.3, 3.2), (-0.1, 0.08, -1.0), (0.05, 1.0, 0.0)
+    r = subprocess.run([exe, diamond_path, "--spp", "8", "--spi", "4", "--width", "320", "--height", "240",
+                        "--eye", *map(str, eye), "--dir", *map(str, dr), "--up", *map(str, up), "--stats",
+                        "-o", str(out)], check=True, timeout=120, capture_output=True, text=True)
+    for key in ("CameraRays", "BounceRays", "ShadowRays", "PrimaryRays", "TotalRays", "Iterations: 2"):
+        assert key in r.stdout, r.stdout
+    ch, _ = read_exr(out)
+    img = np.stack([ch["R"], ch["G"], ch["B"]], axis=-1).reshape(-1)
+    sc = ignis_amd.Scene.from_file(diamond_path)
+    cam = N.Camera.from_buffer_copy(sc.desc.camera)
+    cam.eye[:], cam.dir[:], cam.up[:] = eye, dr, up
+    dev = ignis_amd.Device(0)
+    dev.upload(sc)
+    dev.set_camera(cam)
+    p = ignis_amd.RenderParams()
+    p.width, p.height, p.spi = 320, 240, 4
+    dev.render_iterations(p, 2)
+    ref, it = dev.framebuffer(320 * 240 * 3)
+    dev.close()
+    assert it == 2
+    np.testing.assert_array_equal(img, ref / np.float32(2))
+    # and the orientation did change the image
+    plain = render_gpu(device=ignis_amd.Device(0), scene=sc, w=320, h=240, spi=4)
+    assert not np.array_equal(plain, ref)
+
+
 def test_image_parity_materials(device, root):
     """§8f wider materials: mirror, smooth / rough conductors (VNDF-GGX, GGX, Beckmann,
     anisotropic), smooth / rough plastic, Oren-Nayar, glass -- GPU vs oracle."""
@@ -1003,8 +1045,51 @@ def test_config4_s_deep_1024spp_full_size(device, root):
     first = halves[0] / 64
     second = (halves[1] - halves[0]) / 64
     assert np.isfinite(full).all() and full.mean() > 0
-    assert rel_mse(second.reshape(h, w, 3), first.reshape(h, w, 3)) < 5e-2
-    assert abs(first.mean() - second.mean()) <= 2e-2 * first.mean()
+    # two independent 512-spp estimates: their RunEvaluations distance is
+    # about twice the per-estimate RelSE (the noise, no bias)
+    halves_err = rel_mse(second.reshape(h, w, 3), first.reshape(h, w, 3))
+    print(f"config 4 halves RelSE {halves_err:.3e}, means {first.mean():.6f} / {second.mean():.6f}")
+    assert halves_err < 1.5e-2, halves_err
+    assert abs(first.mean() - second.mean()) <= 5e-3 * first.mean()
+    # and against the restated reference CPU device: the same 128 iterations
+    # of a 100-row band at the diamond contract of SURVEY.md §8c
+    y0, y1 = 450, 550
+    orc = O.OracleScene(sc)
+    o = np.zeros(w * h * 3, np.float32)
+    for k in range(128):
+        orc.render(w, h, 8, iteration=k, threads=16, window=(0, y0, w, y1), fb=o)
+    gb = full.reshape(h, w, 3)[y0:y1] / 128
+    ob = o.reshape(h, w, 3)[y0:y1] / 128
+    assert rel_mse(gb, ob) <= 5e-3
+    close = np.abs(gb - ob) <= 1e-2 * np.maximum(np.abs(ob), 1e-2)
+    assert close.mean() >= 0.99, close.mean()
+
+
+def test_config5_s_deep_4096_band_matches_cpu_device(device, root):
+    """BASELINE config 5 stand-in at its stated size: S-deep at 4096x4096,
+    64 spp = 8 iterations of spi 8, rendered whole on the GPU in one call (a
+    134 M-path iteration: two chunks per iteration); the oracle accumulates the
+    same 8 iterations over a 64-row band, diamond contract of SURVEY.md §8c."""
+    sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", "s_deep.json"))
+    W = H = 4096
+    device.upload(sc)
+    device.set_option("capacity", 0)
+    device.clear()
+    p = ignis_amd.RenderParams()
+    p.width, p.height, p.spi = W, H, 8
+    device.render_iterations(p, 8)
+    g, it = device.framebuffer(W * H * 3)
+    assert it == 8 and np.isfinite(g).all()
+    y0, y1 = 2016, 2080
+    orc = O.OracleScene(sc)
+    o = np.zeros(W * H * 3, np.float32)
+    for k in range(8):
+        orc.render(W, H, 8, iteration=k, threads=16, window=(0, y0, W, y1), fb=o)
+    gb = g.reshape(H, W, 3)[y0:y1] / 8
+    ob = o.reshape(H, W, 3)[y0:y1] / 8
+    assert rel_mse(gb, ob) <= 5e-3
+    close = np.abs(gb - ob) <= 1e-2 * np.maximum(np.abs(ob), 1e-2)
+    assert close.mean() >= 0.99, close.mean()
 
 
 def test_pack_tiles_rejects_a_film_that_is_not_the_framebuffer(device, diamond_path):
