@@ -122,7 +122,7 @@ def load_pmc(n_gpus, scene="diamond_scene", kernel="extend"):
         return None
 
 
-def load_rocprof(scene_key, split):
+def load_rocprof(scene_key, split, kernel=None):
     """Average duration (us) of the dominant kernel in the newest committed
     rocprofv3 --kernel-trace --stats summary of the same workload:
     profiles/rNN_kernel_stats.csv (headline diamond) or
@@ -135,7 +135,7 @@ def load_rocprof(scene_key, split):
     files = sorted((f for f in os.listdir(d) if pat.match(f)), key=lambda f: int(pat.match(f).group(1)))
     if not files:
         return None
-    want = "k_trace_refill<" if split else "k_extend<"
+    want = kernel or ("k_trace_refill<" if split else "k_extend<")
     with open(os.path.join(d, files[-1])) as f:
         for r in csv.DictReader(f):
             if want in r["Name"]:
@@ -198,10 +198,47 @@ def roofline(dev, st, render_one, n_gpus, scene_key):
         t = rp["avg_us"] * 1e-6
         out["rocprof"] = dict(rp, frac=round(alg_bytes / launches / t / 1e9 / HBM_PEAK_GBS, 4),
                               frac_traffic=round(traffic / t / 1e9 / HBM_PEAK_GBS, 4) if traffic else None)
+    out["_inst"] = inst  # visit counts for shadow_roofline (dropped before the line is printed)
     out["limiter"] = (f"not HBM: tables on chip, node loop at {simd:.0%} SIMD efficiency (divergent per-lane "
                       "traversal; VALU-issue bound, profiles/r01_pmc_diamond.md)" if resident else
                       f"dependent node-fetch latency: {simd:.0%} SIMD efficiency, L2 hit rate ~44% "
                       "(profiles/pmc_trace_s_soup_16m.json)")
+    return out
+
+
+def shadow_roofline(st, inst, si, scene_key):
+    """Roofline object of the split schedule's any-hit kernel (k_shadow_refill):
+    per shadow ray 32 B of ray read, at most 48 B more for an unoccluded one
+    (its colour, and the radiance slot read and written), plus -- tables beyond
+    the Infinity Cache -- node_bytes per node, 64 B per instance and 48 B per
+    triangle the any-hit walk visits (instrumented pass); over the kernel's own
+    launch time (the overlap_shadow 0 run `si`), next to the PMC traffic of the
+    committed profile of the same workload."""
+    ns = max(1, inst["shadow_rays"])
+    resident = st["table_bytes"] + st["shading_bytes"] <= MALL_BYTES
+    tables = (float(st.get("node_bytes", 64)) * inst["shadow_node_visits"] + 64.0 * inst["shadow_leaf_visits"] +
+              48.0 * inst["shadow_tri_tests"]) / ns
+    per_ray = 32 + 48 + (0 if resident else tables)
+    launches = max(1, si["launches_shadow"])
+    t = si["ms_shadow"] / 1e3 / launches
+    per_launch = si["shadow_rays"] * per_ray / launches
+    pmc = load_pmc(1, scene_key, "shadow_refill")
+    traffic = float(pmc["hbm_bytes_per_launch"]) if pmc else None
+    out = {"bound": "hbm", "kernel": "k_shadow_refill (any-hit traversal, persistent lanes)",
+           "achieved": round(per_launch / t / 1e9, 1) if t > 0 else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(per_launch / t / 1e9 / HBM_PEAK_GBS, 4) if t > 0 else None, "traffic": traffic,
+           "frac_traffic": round(traffic / t / 1e9 / HBM_PEAK_GBS, 4) if traffic and t > 0 else None,
+           "algorithmic_bytes_per_launch": round(per_launch, 1), "bytes_per_ray": round(per_ray, 1),
+           "visits_per_ray": {"nodes": round(inst["shadow_node_visits"] / ns, 2),
+                              "instances": round(inst["shadow_leaf_visits"] / ns, 2),
+                              "triangles": round(inst["shadow_tri_tests"] / ns, 2)},
+           "avg_launch_us": round(t * 1e6, 2), "launches": launches,
+           "note": "the kernel's own launches (overlap_shadow 0); 48 B per ray counted as if every shadow ray were unoccluded"}
+    rp = load_rocprof(scene_key, True, "k_shadow_refill<")
+    if rp:
+        tr = rp["avg_us"] * 1e-6
+        out["rocprof"] = dict(rp, frac=round(per_launch / tr / 1e9 / HBM_PEAK_GBS, 4),
+                              frac_traffic=round(traffic / tr / 1e9 / HBM_PEAK_GBS, 4) if traffic else None)
     return out
 
 
@@ -262,6 +299,8 @@ def suite_line(ignis_amd, dev_index, path, spi, iters, size=None):
             t = rp["avg_us"] * 1e-6
             r["isolated"]["rocprof"] = dict(rp, frac=round(per_launch / t / 1e9 / HBM_PEAK_GBS, 4),
                                             frac_traffic=round(r["traffic"] / t / 1e9 / HBM_PEAK_GBS, 4) if r["traffic"] else None)
+        line["roofline_shadow"] = shadow_roofline(st, r["_inst"], si, key)
+    line["roofline"].pop("_inst", None)
     dev.close()
     del scene
     return line
@@ -530,6 +569,7 @@ def main():
 
     # ---- roofline of the dominant kernel, live HIP-event timing ----
     roof = roofline(dev, st, lambda: dev.render(params(0)), n_gpus, os.path.splitext(os.path.basename(args.scene))[0])
+    roof.pop("_inst", None)
     roof["note"] = ("achieved counts the HBM bytes the kernel must move (path / radiance / shadow-ray streams; "
                     "table reads too when the tables exceed the Infinity Cache); traffic is the rocprofv3 PMC "
                     "measurement of the same kernel and workload; memory_system_gbs counts every table read "
@@ -663,25 +703,27 @@ def cpu_model():
 
 def cpu_baseline(scene, dev, W, H, spi, target_s):
     """Oracle (C restatement of the reference CPU device: binned-SAH BVH4 over
-    Tri4 leaves, per-path integration in 16x16 tiles) timed on this host with
-    scripts/benchmark.sh's protocol (lines 13-14, 58-91): 2 warm-up runs, then
-    10 timed runs, min / median / max.  One run renders one iteration (spi
-    samples) of a band of rows of the same frame, the band sized so that the
-    12 runs take about target_s; value = the median run.  Also the per-pixel
-    parity of the GPU band (iteration 0)."""
+    Tri4 leaves, the device's wavefront loop per 16x16 tile -- cpu_trace,
+    driver/mapping_cpu.art:694-836: a stream of spi * 256 rays, closest hits,
+    sort by entity, shading, compaction, any-hit shadow stream) timed on this
+    host with scripts/benchmark.sh's protocol (lines 13-14, 58-91): 2 warm-up
+    runs, then 10 timed runs, min / median / max.  One run renders one
+    iteration (spi samples) of a band of rows of the same frame, the band sized
+    so that the 12 runs take about target_s; value = the median run.  Also the
+    per-pixel parity of the GPU band (iteration 0)."""
     from oracle import oracle_py as O
     threads, affinity, quota = cpu_threads()
     orc = O.OracleScene(scene)
     # calibrate on 8 rows, then size the band for ~target_s / 12 per run
     y0 = H // 2
-    _, st = orc.render(W, H, spi, iteration=0, threads=threads, window=(0, y0, W, y0 + 8))
+    _, st = orc.render(W, H, spi, iteration=0, threads=threads, window=(0, y0, W, y0 + 8), stream=True)
     rows = int(max(8, min(H, 8 * (target_s / 12) / max(st["seconds"], 1e-4))))
     y0 = max(0, H // 2 - rows // 2)
     win = (0, y0, W, y0 + rows)
     fb0 = None
     runs = []
     for it in range(12):
-        fb, st = orc.render(W, H, spi, iteration=it, threads=threads, window=win)
+        fb, st = orc.render(W, H, spi, iteration=it, threads=threads, window=win, stream=True)
         if it == 0:
             fb0 = fb.copy()  # iteration 0, for the parity check below
         if it >= 2:  # 2 warm-up runs
@@ -694,7 +736,7 @@ def cpu_baseline(scene, dev, W, H, spi, target_s):
     if affinity != threads:
         hc = []
         for it in range(4):
-            _, st = orc.render(W, H, spi, iteration=it, threads=affinity, window=win)
+            _, st = orc.render(W, H, spi, iteration=it, threads=affinity, window=win, stream=True)
             if it >= 1:
                 hc.append((st["camera_rays"] + st["bounce_rays"] + st["shadow_rays"]) / st["seconds"] / 1e6)
         at_hc = {"threads": affinity, "value": round(float(np.median(hc)), 3),
@@ -712,7 +754,8 @@ def cpu_baseline(scene, dev, W, H, spi, target_s):
         "hardware_concurrency": affinity,
         "cgroup_cpu_quota": quota,
         "at_hardware_concurrency": at_hc,
-        "sample": f"oracle/oracle.c (restated reference CPU device, SAH BVH4 + Tri4 leaves), {threads} threads "
+        "sample": f"oracle/oracle.c (restated reference CPU device: SAH BVH4 + Tri4 leaves, cpu_trace's wavefront of "
+                  f"spi x 256 rays per 16x16 tile with sort by entity and compaction), {threads} threads "
                   f"(hardware_concurrency {affinity} on a {cpu_model()} host, cgroup CPU quota "
                   f"{quota if quota else 'none'}: min of the two), rows {y0}-{y0 + rows} of the "
                   f"{W}x{H} frame, 2 warm-up + 10 timed runs of one iteration (spi {spi}) each, "

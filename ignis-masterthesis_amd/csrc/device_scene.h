@@ -97,7 +97,8 @@ struct DevMaterial {   // 128 B
     float kt[4];        // specular transmittance; w = n2 (int ior)
     float eta[4];       // conductor eta; w = alpha_u
     float kappa[4];     // conductor k; w = alpha_v
-    float pad[8];
+    float pad[8];       // textured diffuse (igx_material::texture): pad[0] = texture (int bits),
+                        // pad[1] = scale, pad[2..4] = the colour where the checker is 1 (kd elsewhere)
 };
 
 enum : int32_t { LIGHT_PLANE = 1, LIGHT_ENV = 2, LIGHT_POINT = 3, LIGHT_SPOT = 4, LIGHT_DIRECTIONAL = 5, LIGHT_SUN = 6,

@@ -40,6 +40,7 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <type_traits>
 
 using namespace igxd;
 
@@ -154,6 +155,7 @@ struct FrameArgs {
     int shadow_classes;  // shadow rays crossing an enclosing entity's box go to the back of their shard (shadow_class_b)
     int reverse;         // k_extend: a shard's positions are taken from its end (class C, then B, then A:
                          // the groups whose paths run longest start first, the short ones fill the launch's end)
+    int gen_octets;      // > 0: screen-local layout of the generated chunk (gen_slot): octets of 512 slots per iteration
 };
 
 // path slot -> (local pixel, sample, iteration): slots run over the chunk's
@@ -227,6 +229,44 @@ __device__ __forceinline__ int gen_index(int i, int shard_cap) {
 __device__ __forceinline__ int gen_shard_count(int n, int s) {
     const int rem = (n & (64 * NSH - 1)) - s * 64;
     return (n >> 12) * 64 + (rem < 0 ? 0 : (rem > 64 ? 64 : rem));
+}
+
+// Screen-local layout of a generated chunk (FrameArgs::gen_octets = O > 0).
+// Wave g of a launch serves shard g % 64, and block b runs on XCD b % 8
+// (blocks are dealt round-robin over the XCDs), so XCD x serves shards
+// 4x..4x+3 and 4x+32..4x+35.  Each iteration's P = chunk_pixels x spi slots
+// are cut into O = ceil(P / 512) octets of 8 groups of 64 (a group: 8
+// neighbouring pixels x spi 8); region r = the octets o with 8o / O = r, a
+// band of the film, and group k of an octet of region r goes to shard
+// 4r + (k & 3) + 32 (k >> 2).  One XCD thus traces the rays of one band, whose
+// camera and bounce rays walk the same parts of the BVH: its L2 holds them
+// (the round-robin layout spread every shard over the whole film).  A
+// shard's positions run over (iteration, octet of the region, lane); slots
+// past P in the last octet of an iteration are holes (dead paths).  Placement
+// only bears on speed: any block-to-XCD mapping renders the same image.
+__device__ __forceinline__ int oct_start(int O, int r) { return (r * O + 7) >> 3; }
+__device__ __forceinline__ int oct_count(int O, int r) { return oct_start(O, r + 1) - oct_start(O, r); }
+__device__ __forceinline__ int region_shard(int r, int k) { return 4 * r + (k & 3) + 32 * (k >> 2); }
+__device__ __forceinline__ void shard_region(int s, int& r, int& k) {
+    r = (s & 31) >> 2;
+    k = (s & 3) + 4 * (s >> 5);
+}
+// records of shard s in a generated chunk of n paths (holes included)
+__device__ __forceinline__ int gen_count(int gen_octets, int chunk_iters, int n, int s) {
+    if (gen_octets == 0) return gen_shard_count(n, s);
+    int r, k;
+    shard_region(s, r, k);
+    return chunk_iters * oct_count(gen_octets, r) * 64;
+}
+// path slot at position pos of shard s of a generated chunk; -1: a hole
+__device__ __forceinline__ int gen_slot(int gen_octets, int per_iter, int s, int pos) {
+    if (gen_octets == 0) return ((pos >> 6) << 12) | (s << 6) | (pos & 63); // inverse of gen_index
+    int r, k;
+    shard_region(s, r, k);
+    const int oc = oct_count(gen_octets, r);
+    const int q = pos >> 6, it = q / oc;
+    const int j = ((oct_start(gen_octets, r) + q - it * oc) << 9) + (k << 6) + (pos & 63);
+    return j < per_iter ? it * per_iter + j : -1;
 }
 
 // Records of path-stream shard s: `a` of class A at offsets [0, a) and ab - a
@@ -328,12 +368,28 @@ __device__ __forceinline__ GenPath gen_path(const FrameArgs& fa, const SceneView
 
 #if IGX_PART == 0
 __global__ void __launch_bounds__(BLOCK) k_generate(FrameArgs fa, SceneView sv, PathBuf out, float4* L, int* cnt0) {
-    const int n = fa.chunk_pixels * fa.spi * fa.chunk_iters;
-    if (blockIdx.x == 0 && threadIdx.x < NSH) cnt0[threadIdx.x * CSTRIDE] = gen_shard_count(n, threadIdx.x);
-    for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+    const int per_iter = fa.chunk_pixels * fa.spi, n = per_iter * fa.chunk_iters;
+    const int O = fa.gen_octets;
+    if (blockIdx.x == 0 && threadIdx.x < NSH) cnt0[threadIdx.x * CSTRIDE] = gen_count(O, fa.chunk_iters, n, threadIdx.x);
+    // round-robin layout: t = slot; screen-local: t runs over (iteration,
+    // octet, group, lane) of every position, holes included
+    const int total = O ? fa.chunk_iters * O * 512 : n;
+    for (int t = blockIdx.x * BLOCK + threadIdx.x; t < total; t += gridDim.x * BLOCK) {
+        int i = t, e;
+        if (O) {
+            const int it = t / (O * 512), u = t - it * O * 512, o = u >> 9, k = (u >> 6) & 7;
+            const int r = (8 * o) / O;
+            e = region_shard(r, k) * out.shard_cap + ((it * oct_count(O, r) + o - oct_start(O, r)) << 6) + (u & 63);
+            i = u < per_iter ? it * per_iter + u : -1;
+        } else {
+            e = gen_index(i, out.shard_cap);
+        }
+        if (i < 0) { // a hole: a dead path
+            out.p1[e] = make_float4(0, 0, 1, __uint_as_float(0u));
+            continue;
+        }
         L[i] = make_float4(0, 0, 0, 0);
         const GenPath g = gen_path(fa, sv, i);
-        const int e = gen_index(i, out.shard_cap);
         out.p0[e] = make_float4(g.o.x, g.o.y, g.o.z, __int_as_float(i));
         out.p1[e] = make_float4(g.d.x, g.d.y, g.d.z, __uint_as_float(g.counter | ((uint32_t)g.depth << 24)));
         out.p2[e] = make_float4(1, 1, 1, 0); // init_pt_raypayload (technique/pathtracer.art:33-38)
@@ -485,6 +541,32 @@ __device__ __forceinline__ void ray_extent(const FrameArgs& fa, const SceneView&
 // advances `ps` by one bounce.  Returns whether the path continues (ps then
 // holds the bounced ray); fills the radiance gathered at this vertex (Lacc,
 // has_l) and the NEE shadow ray (has_shadow, sr).
+// A textured diffuse reflectance at the hit (DevMaterial::pad): the checker
+// select(checkerboard(uvw * scale) == 1, kd1, kd) of texture/checkerboard.art:2
+// on the texture coordinates (u, v, 0), interpolated with the hit's
+// barycentrics (vec2_lerp2, shapes/trimesh.art:25; core/vector.art:150-153);
+// math::wrap(x, 0, 2) as i32 % 2 per axis (core/math.art:88-91)
+__device__ __forceinline__ int checker_bit(float x) {
+    const float w = x - 2.0f * floorf(x / 2.0f);
+    return ((int)w) % 2;
+}
+__device__ __forceinline__ void apply_texture(const SceneView& sv, DevMaterial& m, int ent_id, int prim, float hu, float hv) {
+    if (__float_as_int(m.pad[0]) != 1) return;
+    const int4 info = *reinterpret_cast<const int4*>(sv.ent + ENT_STRIDE * ent_id + 6); // shape type, material, vtx_off, idx_off
+    if (info.x == 1) return; // analytic sphere: refused at upload
+    const int4 f = sv.idx[info.w + prim];
+    const float2 t0 = sv.uv[info.z + f.x], t1 = sv.uv[info.z + f.y], t2 = sv.uv[info.z + f.z];
+    const float u = lerp2(t0.x, t1.x, t2.x, hu, hv), v = lerp2(t0.y, t1.y, t2.y, hu, hv);
+    const float sc = m.pad[1];
+    // node_checkerboard3(uvw * sc): ((a == b) == (c == 1)) with c of the zero w
+    const int a = checker_bit(u * sc), b = checker_bit(v * sc), c = checker_bit(0.0f * sc);
+    if ((a == b) == (c == 1)) {
+        m.kd[0] = m.pad[2];
+        m.kd[1] = m.pad[3];
+        m.kd[2] = m.pad[4];
+    }
+}
+
 template <bool FULL>
 __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView& sv, PathState& ps, int hit_ent,
                                            int hit_prim, float tmax, float hu, float hv, f3& Lacc, bool& has_l,
@@ -509,7 +591,11 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
     }
     int mat_id;
     Surface s = surface_element(sv, hit_ent, hit_prim, tmax, hu, hv, ps.o, rd, mat_id);
-    const DevMaterial& m = sv.mats[mat_id];
+    // the full variant shades a copy of the material, into which a texture
+    // writes its value at the hit; the basic one reads the table in place
+    std::conditional_t<FULL, DevMaterial, const DevMaterial&> m = sv.mats[mat_id];
+    if constexpr (FULL)
+        if (sv.uv) apply_texture(sv, m, hit_ent, hit_prim, hu, hv);
     // on_hit (pathtracer.art:114-134)
     if (m.light >= 0 && s.entering) {
         float dt = -dot(rd, s.local.n);
@@ -727,8 +813,13 @@ __device__ __forceinline__ int take_group(int* work, int& s, uint64_t& done, int
         if (lane_id() == 0) m = __hip_atomic_load(done_mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         done |= (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)m) |
                 ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(m >> 32)) << 32);
-        const uint64_t open = ~done;
+        uint64_t open = ~done;
         if (!open) return -1;
+        // the shards of this wave's XCD first (4x..4x+3, 4x+32..4x+35 for the
+        // XCD x of shard s: the screen-local layout keeps one film band there)
+        const int x4 = ((s & 31) >> 2) << 2;
+        const uint64_t own = open & ((0xFull << x4) | (0xFull << (x4 + 32)));
+        if (own) open = own;
         const int r = (s + 1) & (NSH - 1);
         const uint64_t rot = (open >> r) | (r ? (open << (NSH - r)) : 0ull);
         s = (r + __ffsll((unsigned long long)rot) - 1) & (NSH - 1);
@@ -788,7 +879,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
     int s = w.s;
     auto count_of = [&](int sh_) {
         if (gen) {
-            const int g = gen_shard_count(fa.gen_n, sh_);
+            const int g = gen_count(fa.gen_octets, fa.chunk_iters, fa.gen_n, sh_);
             return ShardCount{g, g, g};
         }
         return shard_count(kc.cnt_in, sh_);
@@ -819,10 +910,12 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
         ShadowRec sr;
         ps.depth = 0;
         if (q < ns) {
-            if (gen) { // inverse of gen_index
-                const int i = ((pos >> 6) << 12) | (s << 6) | (pos & 63);
-                ps = camera_path(fa, sv, i);
-                L[i] = make_float4(0, 0, 0, 0);
+            if (gen) {
+                const int i = gen_slot(fa.gen_octets, fa.chunk_pixels * fa.spi, s, pos);
+                if (i >= 0) {
+                    ps = camera_path(fa, sv, i);
+                    L[i] = make_float4(0, 0, 0, 0);
+                } // else a hole of the screen-local layout: stays dead (depth 0)
             } else {
                 ps = load_path(in, path_index(in, s, pos, sc));
             }
@@ -1564,6 +1657,9 @@ struct igx_device {
     int64_t tail_opt = -1;   // paths at or below which k_finish takes over (-1 = auto)
     int64_t tail_last_opt = -1; // the same for the last chunk of a render call, whose tail overlaps nothing (-1 = tail_opt)
     bool fuse_generate = true; // bounce 0 of the fused k_extend builds its camera paths (no k_generate pass)
+    // generated chunks of >= 2^18 paths per iteration in the screen-local
+    // layout (gen_slot: one film band per XCD); 0: round-robin groups
+    int gen_layout_opt = 1;
     int split_opt = -1;      // k_trace + k_shade per bounce instead of the fused k_extend (-1: auto = global-table scenes)
     int trace_waves = 5;     // occupancy target of k_trace (5 waves per SIMD, anything else = compiler's choice)
     int refill_opt = -1;     // persistent-lane trace / shadow, refilled once this many lanes idle (0: off, -1: auto = 16)
@@ -1737,18 +1833,19 @@ void free_slot_buffers(Slot& s) {
 // record per path (20 B) for k_shade; the fused schedule needs none.
 // `region_c`: three path classes (FrameArgs::classify 4), so each path buffer
 // holds a second set of records for class C (PathBuf::c_base)
-igx_status ensure_slot(igx_device* dev, Slot& s, size_t cap, bool hits, bool region_c) {
+igx_status ensure_slot(igx_device* dev, Slot& s, size_t cap, bool hits, bool region_c, int min_shard_cap) {
     if (!s.ctr) {
         HIPCHK(hipMalloc((void**)&s.ctr, CTR_INTS * sizeof(int)));
         HIPCHK(hipHostMalloc((void**)&s.pinned, CTR_INTS * sizeof(int), hipHostMallocDefault));
         HIPCHK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
         std::memset(s.pinned, 0, CTR_INTS * sizeof(int));
     }
-    if (s.cap >= cap && (!hits || s.hb.h) && (!region_c || s.pa.c_base)) return IGX_OK;
+    if (s.cap >= cap && s.shard_cap >= min_shard_cap && (!hits || s.hb.h) && (!region_c || s.pa.c_base)) return IGX_OK;
     free_slot_buffers(s);
     // shard capacity: a generated chunk puts at most ceil(cap / (64 NSH)) groups
-    // of 64 paths in one shard, and a shard's outputs never exceed its inputs
-    const int shard_cap = (int)((cap + 64 * NSH - 1) / (64 * NSH)) * 64;
+    // of 64 paths in one shard (round-robin layout; the screen-local layout
+    // asks for min_shard_cap), and a shard's outputs never exceed its inputs
+    const int shard_cap = std::max((int)((cap + 64 * NSH - 1) / (64 * NSH)) * 64, min_shard_cap);
     const size_t recs = (size_t)shard_cap * NSH;
     auto alloc4 = [&](float4** p, size_t k) -> igx_status { HIPCHK(hipMalloc((void**)p, k * sizeof(float4))); return IGX_OK; };
     igx_status st;
@@ -2318,6 +2415,10 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     else if (k == "tail_threshold") dev->tail_opt = value;
     else if (k == "tail_threshold_last") dev->tail_last_opt = value;
     else if (k == "fuse_generate") dev->fuse_generate = value != 0;
+    else if (k == "gen_layout") {
+        if (value < 0 || value > 1) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "gen_layout must be 0 (round-robin) or 1 (screen-local)");
+        dev->gen_layout_opt = (int)value;
+    }
     else if (k == "split") {
         if (value < -1 || value > 1) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "split must be -1 (auto), 0 or 1");
         dev->split_opt = (int)value;
@@ -2632,6 +2733,9 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     // ---- phase 2: node, triangle and instance tables ----------------------
     std::vector<float4> nodes; // nf4 float4s per node
     std::vector<float4> tris, vtx, nrm, spheres;
+    std::vector<float2> uvs; // texture coordinates, only for scenes with a textured material
+    bool textured = false;
+    for (uint32_t i = 0; i < desc->num_materials; ++i) textured = textured || desc->materials[i].texture != IGX_TEXTURE_NONE;
     std::vector<int4> idx;
     // Append a built BVH2 (as Node2, or collapsed to 4-wide nodes) to the
     // unified node array: inner refs move by the array offset, leaf codes by
@@ -2732,6 +2836,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
         for (uint32_t v = 0; v < m.num_vertices; ++v) {
             vtx.push_back(make_float4(m.vertices[3 * v], m.vertices[3 * v + 1], m.vertices[3 * v + 2], 0));
             nrm.push_back(make_float4(m.normals[3 * v], m.normals[3 * v + 1], m.normals[3 * v + 2], 0));
+            if (textured) uvs.push_back(m.texcoords ? make_float2(m.texcoords[2 * v], m.texcoords[2 * v + 1]) : make_float2(0, 0));
         }
         for (uint32_t f = 0; f < m.num_faces; ++f)
             idx.push_back(make_int4((int)m.indices[3 * f], (int)m.indices[3 * f + 1], (int)m.indices[3 * f + 2], 0));
@@ -2966,6 +3071,14 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
         d.kt[3] = m.int_ior;
         d.eta[3] = m.alpha_u;
         d.kappa[3] = m.alpha_v;
+        if (m.texture == IGX_TEXTURE_CHECKER && m.bsdf_type == IGX_BSDF_DIFFUSE) {
+            const int32_t kind = IGX_TEXTURE_CHECKER;
+            std::memcpy(&d.pad[0], &kind, 4);
+            d.pad[1] = m.tex_scale;
+            for (int c = 0; c < 3; ++c) d.pad[2 + c] = m.tex_kd1[c];
+        } else if (m.texture != IGX_TEXTURE_NONE) {
+            return fail(dev, IGX_ERR_UNSUPPORTED, "texture " + std::to_string(m.texture) + " on this bsdf type");
+        }
         if (m.bsdf_type == IGX_BSDF_PRINCIPLED) {
             // packing of the principled closure (igx_kernels.h, principled_of)
             DevMaterial q{};
@@ -3004,11 +3117,12 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
         (st = upload(dev, lights, &sv.lights)) || (st = upload(dev, lsel.cdf, &sv.sel_cdf)) ||
         (st = upload(dev, lsel.hierarchy, &sv.sel_tree)) || (st = upload(dev, ent_enc, &sv.ent_enc)) ||
         (st = upload(dev, enc_tab, &sv.enc)) || (st = upload(dev, enc_box, &sv.enc_box)) || (st = upload(dev, ent_fn, &sv.ent_fn)) ||
-        (st = upload(dev, fn_tab, &sv.fn_tab))) {
+        (st = upload(dev, fn_tab, &sv.fn_tab)) || (st = upload(dev, uvs, &sv.uv))) {
         free_scene(dev);
         return st;
     }
     if (fn_tab.empty()) sv.fn_tab = nullptr; // surface_element computes the normals
+    if (uvs.empty()) sv.uv = nullptr;
     sv.tlas_root = tlas_root;
     sv.num_nodes = (int)(nodes.size() / nf4);
     sv.node_f4 = nf4;
@@ -3062,6 +3176,14 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     }
     for (uint32_t l = 0; l < desc->num_lights; ++l)
         if (desc->lights[l].type == IGX_LIGHT_SPHERE || desc->lights[l].type == IGX_LIGHT_MESH) dev->full_shading = true;
+    if (textured) dev->full_shading = true; // textures are looked up by the full shading variant only
+    for (uint32_t e = 0; textured && e < desc->num_entities; ++e) {
+        const igx_entity& en = desc->entities[e];
+        if (desc->materials[en.material].texture != IGX_TEXTURE_NONE && desc->shapes[en.shape].type == IGX_SHAPE_SPHERE) {
+            free_scene(dev);
+            return fail(dev, IGX_ERR_UNSUPPORTED, "textured material on an analytic sphere (texture coordinates of spheres are not supported)");
+        }
+    }
     if ((st = configure_stack(dev)) != IGX_OK) {
         free_scene(dev);
         return st;
@@ -3176,6 +3298,13 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
     const long long chunk_pixels_max = std::min<long long>(cap, total_paths) / p->spi;
     const int iters_per_chunk = total_paths <= cap ? (int)std::min<long long>(count, cap / total_paths) : 1;
     const size_t slot_cap = (size_t)(chunk_pixels_max * p->spi * iters_per_chunk);
+    // screen-local layout of the generated chunks (gen_slot): octets of 512
+    // slots per iteration, and the largest shard it fills (holes included)
+    auto octets_of = [&](long long per_iter) -> int {
+        return dev->gen_layout_opt && !list_mode && per_iter >= (1ll << 18) ? (int)((per_iter + 511) / 512) : 0;
+    };
+    const int oct_max = octets_of(chunk_pixels_max * p->spi);
+    const int gen_shard_need = oct_max ? iters_per_chunk * ((oct_max + 7) / 8) * 64 : 0;
 
     const int max_bounces = std::min(std::max(dev->sv.max_depth, 1), MAX_BOUNCES - 1);
     const bool inst = dev->instrument;
@@ -3204,7 +3333,7 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
         dev->next_slot ^= 1;
         igx_status st = harvest(dev, S); // waits for the chunk that used this slot two chunks ago (one, with one slot)
         if (st != IGX_OK) return st;
-        if ((st = ensure_slot(dev, S, slot_cap, split, fa.classify == 4)) != IGX_OK) return st;
+        if ((st = ensure_slot(dev, S, slot_cap, split, fa.classify == 4, gen_shard_need)) != IGX_OK) return st;
 
         auto begin_timed = [&](int kind, int bounce, hipStream_t strm) {
             if (!dev->timing) return;
@@ -3220,6 +3349,7 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
         int chunk_pixels = (int)std::min<long long>(chunk_pixels_max, local_pixels - px0);
         fa.chunk_pixel0 = (int)px0;
         fa.chunk_pixels = chunk_pixels;
+        fa.gen_octets = octets_of((long long)chunk_pixels * p->spi);
         long long n = (long long)chunk_pixels * p->spi * fa.chunk_iters;
         // tail threshold (auto): n / 64, but at most what one pass of k_finish
         // holds (one path per resident lane): beyond that the tail kernel's

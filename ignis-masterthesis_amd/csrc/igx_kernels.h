@@ -47,6 +47,9 @@ struct SceneView {
     // for scenes with few face instances (nullptr otherwise): fn_tab[ent_fn[e] + prim]
     const int* ent_fn;
     const float4* fn_tab;
+    // per mesh vertex: texture coordinates (as vtx), uploaded only when a
+    // material carries a texture (DevMaterial::pad, textured_material)
+    const float2* uv;
 };
 
 // Copy the traversal tables (nodes, instances, triangles) of a small scene

@@ -151,6 +151,41 @@ struct Props {
     }
 };
 
+// select(checkerboard(uvw * S) == 1, A, B) with constant colours A and B (the
+// form Blender's exporter writes for a checker texture; PExpr: Transpiler.cpp
+// select / checkerboard / uvw, texture/checkerboard.art:1-2); false for any
+// other expression
+bool checker_expression(const std::string& expr, float& scale, V3& a, V3& b) {
+    std::string e;
+    for (char c : expr)
+        if (c != ' ' && c != '\t' && c != '\n') e += c;
+    const std::string head = "select(checkerboard(uvw*";
+    if (e.compare(0, head.size(), head) != 0) return false;
+    const char* s = e.c_str() + head.size();
+    char* end = nullptr;
+    scale = std::strtof(s, &end);
+    if (end == s) return false;
+    const std::string mid = ")==1,";
+    if (std::strncmp(end, mid.c_str(), mid.size()) != 0) return false;
+    const size_t p0 = (size_t)(end - e.c_str()) + mid.size();
+    // A ends at the comma at parenthesis depth 0; B at the closing parenthesis of select
+    int depth = 0;
+    size_t comma = std::string::npos;
+    for (size_t i = p0; i < e.size(); ++i) {
+        if (e[i] == '(') ++depth;
+        else if (e[i] == ')') {
+            if (depth == 0) break;
+            --depth;
+        } else if (e[i] == ',' && depth == 0) {
+            comma = i;
+            break;
+        }
+    }
+    if (comma == std::string::npos || e.back() != ')') return false;
+    return Props::constant_color(e.substr(p0, comma - p0), a) &&
+           Props::constant_color(e.substr(comma + 1, e.size() - comma - 2), b);
+}
+
 M4 matrix_from_array(const Value& a) {
     size_t n = a.arr.size();
     M4 m;
@@ -526,7 +561,17 @@ static void build_scene(SceneStore& S, const Value& doc, const std::string& base
             for (int i = 0; i < 3; ++i) m.ks[i] = m.kt[i] = 1.0f;
             if (type == "diffuse" || type == "roughdiffuse") {
                 m.bsdf_type = IGX_BSDF_DIFFUSE;
-                V3 kd = bp.color("reflectance", V3(0.8f, 0.8f, 0.8f)); // DiffuseBSDF.cpp:17
+                V3 kd, kd1;
+                float scale = 0;
+                const Value* refl = bp.get("reflectance");
+                if (refl && refl->is_string() && checker_expression(refl->str, scale, kd1, kd)) {
+                    // the Blender exporter's checker texture (igx_material::texture)
+                    m.texture = IGX_TEXTURE_CHECKER;
+                    m.tex_scale = scale;
+                    m.tex_kd1[0] = kd1.x; m.tex_kd1[1] = kd1.y; m.tex_kd1[2] = kd1.z;
+                } else {
+                    kd = bp.color("reflectance", V3(0.8f, 0.8f, 0.8f)); // DiffuseBSDF.cpp:17
+                }
                 m.kd[0] = kd.x; m.kd[1] = kd.y; m.kd[2] = kd.z;
                 m.diffuse_alpha = bp.number(bp.has("alpha") ? "alpha" : "roughness", 0.0f); // Oren-Nayar above flt_eps
             } else if (type == "dielectric" || type == "glass") {

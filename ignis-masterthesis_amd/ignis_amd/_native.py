@@ -42,7 +42,8 @@ class Material(C.Structure):
                 ("ior", C.c_float), ("diffuse_transmission", C.c_float), ("specular_transmission", C.c_float),
                 ("specular_tint", C.c_float), ("flatness", C.c_float), ("metallic", C.c_float), ("sheen", C.c_float),
                 ("sheen_tint", C.c_float), ("clearcoat", C.c_float), ("clearcoat_gloss", C.c_float),
-                ("clearcoat_roughness", C.c_float), ("clearcoat_top_only", C.c_int32)]
+                ("clearcoat_roughness", C.c_float), ("clearcoat_top_only", C.c_int32),
+                ("texture", C.c_int32), ("tex_scale", C.c_float), ("tex_kd1", C.c_float * 3)]
 
 
 # igx_light.type (include/igx_scene.h)

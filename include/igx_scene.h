@@ -103,7 +103,17 @@ typedef struct igx_material {
     float ior, diffuse_transmission, specular_transmission, specular_tint, flatness, metallic;
     float sheen, sheen_tint, clearcoat, clearcoat_gloss, clearcoat_roughness;
     int32_t clearcoat_top_only;
+    /* diffuse reflectance given by a shading expression the loader recognises
+     * (ShadingTree / PExpr): IGX_TEXTURE_CHECKER is
+     * select(checkerboard(uvw * tex_scale) == 1, tex_kd1, kd), the 3D
+     * checkerboard of texture/checkerboard.art:2 on the surface's texture
+     * coordinates (u, v, 0) (shapes/trimesh.art:25); IGX_TEXTURE_NONE: kd */
+    int32_t texture;
+    float tex_scale;
+    float tex_kd1[3];
 } igx_material;
+
+enum { IGX_TEXTURE_NONE = 0, IGX_TEXTURE_CHECKER = 1 };
 
 /* ---- lights ------------------------------------------------------------ */
 enum {

@@ -945,6 +945,7 @@ typedef struct {
     v3 point, face_normal;
     frame_t local;
     int entering;
+    float tu, tv; /* texture coordinates (vec2_lerp2 of the mesh's, shapes/trimesh.art:25) */
 } osurf;
 
 static inline v3 xf_point(const float* m, v3 p) {
@@ -968,6 +969,7 @@ static osurf surface_element(const oracle_scene* s, const ohit* h, const oray* r
         out.entering = 1;
         out.face_normal = n;
         out.local = make_frame(n);
+        out.tu = out.tv = 0;
         return out;
     }
     const igx_mesh* m = &s->desc.meshes[sh->mesh];
@@ -988,7 +990,22 @@ static osurf surface_element(const oracle_scene* s, const ohit* h, const oray* r
     out.entering = vdot(r->dir, fn) <= 0;
     out.face_normal = out.entering ? fn : vneg(fn);
     out.local = make_frame(out.entering ? normal : vneg(normal));
+    out.tu = out.tv = 0;
+    if (m->texcoords) {
+        const float* t = m->texcoords;
+        out.tu = lerp2(t[2 * f[0]], t[2 * f[1]], t[2 * f[2]], h->u, h->v);
+        out.tv = lerp2(t[2 * f[0] + 1], t[2 * f[1] + 1], t[2 * f[2] + 1], h->u, h->v);
+    }
     return out;
+}
+
+/* node_checkerboard3 (texture/checkerboard.art:2) on uvw * scale with
+ * math::wrap(x, 0, 2) as i32 % 2 per axis (core/math.art:88-91); uvw =
+ * (u, v, 0) (driver/shading_context.art:38) */
+static int checker_bit(float x) { return ((int)(x - 2.0f * floorf(x / 2.0f))) % 2; }
+static int checkerboard3(float u, float v, float scale) {
+    const int a = checker_bit(u * scale), b = checker_bit(v * scale), c = checker_bit(0.0f * scale);
+    return (a == b) == (c == 1) ? 1 : 0;
 }
 
 /* compute_sq (light/area.art:127-176) */
@@ -1841,20 +1858,29 @@ typedef struct {
     otstats tr;
 } pstats;
 
-/* One path: technique/pathtracer.art:52-200 driven bounce by bounce */
-static v3 trace_path(const oracle_scene* s, const oracle_params* p, int x, int y, int sample, int list_index, pstats* ps) {
-    const igx_technique* tech = &s->desc.technique;
+/* The state of one path between two bounces: its next ray and the payload of
+ * init_pt_raypayload (technique/pathtracer.art:17-38), plus its RNG and pixel */
+typedef struct {
+    oray ray;
+    uint32_t seed, counter;
+    v3 contrib;
+    float inv_pdf, eta;
+    int depth, x, y;
+} opath;
+
+/* make_camera_emitter + make_perspective_camera (driver/emitter.art:6-16,
+ * camera/perspective.art:29-66), or the ray-list emitter (emitter.art:18-30) */
+static void path_begin(const oracle_scene* s, const oracle_params* p, int x, int y, int sample, int list_index, opath* q,
+                       pstats* ps) {
     const igx_camera* cam = &s->desc.camera;
     int width = p->num_rays > 0 ? p->num_rays : p->width;
     int height = p->num_rays > 0 ? 1 : p->height;
-    uint32_t seed = oracle_random_seed(sample, p->iteration, p->frame, x, y, p->seed);
-    rng_t rnd = {seed, 1};
-    oray ray;
+    q->seed = oracle_random_seed(sample, p->iteration, p->frame, x, y, p->seed);
+    rng_t rnd = {q->seed, 1};
     if (p->num_rays > 0) {
         const float* r = p->rays + 8 * list_index;
-        ray = make_ray(V(r[0], r[1], r[2]), V(r[3], r[4], r[5]), r[6], r[7], 0);
+        q->ray = make_ray(V(r[0], r[1], r[2]), V(r[3], r[4], r[5]), r[6], r[7], 0);
     } else {
-        /* make_camera_emitter + make_perspective_camera */
         float rx = rng_f32(&rnd);
         float ry = rng_f32(&rnd);
         float nx = 2 * ((float)x + rx) / (float)width - 1;
@@ -1869,92 +1895,126 @@ static v3 trace_path(const oracle_scene* s, const oracle_params* p, int x, int y
         v3 v = V(sx * nx, sy * ny, 1);
         v3 w = V(right.x * v.x + up.x * v.y + dir.x * v.z, right.y * v.x + up.y * v.y + dir.y * v.z,
                  right.z * v.x + up.z * v.y + dir.z * v.z);
-        ray = make_ray(V(cam->eye[0], cam->eye[1], cam->eye[2]), vnormalize(w), cam->near_clip, cam->far_clip, RAY_CAMERA);
+        q->ray = make_ray(V(cam->eye[0], cam->eye[1], cam->eye[2]), vnormalize(w), cam->near_clip, cam->far_clip, RAY_CAMERA);
     }
     ps->camera++;
-    uint32_t counter = rnd.counter;
-    /* init_pt_raypayload */
-    float inv_pdf = 0, eta = 1;
-    v3 contrib = V(1, 1, 1);
-    int depth = 1;
-    v3 Lsum = V(0, 0, 0);
+    q->counter = rnd.counter;
+    q->inv_pdf = 0;
+    q->eta = 1;
+    q->contrib = V(1, 1, 1);
+    q->depth = 1;
+    q->x = x;
+    q->y = y;
+}
+
+/* One vertex of technique/pathtracer.art:52-200 for the closest hit `h` of the
+ * path's ray (h->ent < 0: a miss): the radiance gathered there (*Lacc: on_hit
+ * emission with MIS, or on_miss), the NEE shadow ray and its colour
+ * (on_shadow; *has_shadow), and the bounce (on_bounce with Russian roulette):
+ * returns 1 when the path continues with q->ray, 0 when it ends. */
+static int path_shade(const oracle_scene* s, opath* q, const ohit* h, v3* Lacc, int* has_shadow, oray* sray, v3* scol,
+                      pstats* ps) {
+    const igx_technique* tech = &s->desc.technique;
     const float uni_pdf = s->num_lights == 0 ? 1.0f : 1.0f / (float)s->num_lights;
+    const oray* ray = &q->ray;
+    *Lacc = V(0, 0, 0);
+    *has_shadow = 0;
+    if (h->ent < 0) {
+        for (int li = 0; li < s->num_infinite; ++li) {
+            const olight* L = &s->lights[li];
+            if (L->delta) continue;
+            v3 emit = V(L->rad[0], L->rad[1], L->rad[2]);
+            float pdf_s = 1 / (4 * PI_);
+            float sel = s->selector == IGX_SELECT_UNIFORM ? uni_pdf : select_pdf(s, li, ray->org);
+            float mis = tech->nee ? 1 / (1 + q->inv_pdf * sel * pdf_s) : 1.0f;
+            *Lacc = vadd(*Lacc, handle_color(s, vmulf(vmul(q->contrib, emit), mis)));
+        }
+        return 0;
+    }
+    osurf surf = surface_element(s, h, ray);
+    const igx_entity* ent = &s->desc.entities[h->ent];
+    const igx_material* mat = &s->desc.materials[ent->material];
+    int mlight = s->mat_light[ent->material];
+    if (mlight >= 0 && surf.entering) {
+        float dt = -vdot(ray->dir, surf.local.n);
+        if (dt > FLT_EPS_) {
+            const olight* L = &s->lights[mlight];
+            v3 emit = V(L->rad[0], L->rad[1], L->rad[2]);
+            float pdf_s = area_pdf_direct_solid(s, L, ray->org, dt, h->t * h->t, h->u);
+            float sel = s->selector == IGX_SELECT_UNIFORM ? uni_pdf : select_pdf(s, mlight, ray->org);
+            float mis = tech->nee ? 1 / (1 + q->inv_pdf * sel * pdf_s) : 1.0f;
+            *Lacc = vadd(*Lacc, handle_color(s, vmulf(vmul(q->contrib, emit), mis)));
+        }
+    }
+    igx_material textured;
+    if (mat->texture == IGX_TEXTURE_CHECKER) { /* select(checkerboard(uvw * s) == 1, kd1, kd) */
+        textured = *mat;
+        if (checkerboard3(surf.tu, surf.tv, mat->tex_scale) == 1)
+            for (int c = 0; c < 3; ++c) textured.kd[c] = mat->tex_kd1[c];
+        mat = &textured;
+    }
+    rng_t r2 = {q->seed, q->counter};
+    v3 out_dir = vneg(ray->dir);
+    obsdf bs = obsdf_make(mat, &surf);
+    int specular = obsdf_specular(&bs);
+    /* on_shadow */
+    if (tech->nee && !specular && s->num_lights > 0 && q->depth + 1 <= tech->max_depth) {
+        float sel_pdf;
+        int lid = select_light(s, &r2, surf.point, &sel_pdf);
+        const olight* L = &s->lights[lid];
+        odirect ls = light_sample_direct(s, L, &r2, &surf);
+        float pdf_l_s = (ls.pdf_solid ? ls.pdf_value : ls.pdf_value * (ls.dist * ls.dist) / ls.cos) * sel_pdf;
+        if (pdf_l_s > FLT_EPS_ && ls.cos > FLT_EPS_) {
+            float mis = L->delta ? 1.0f : 1 / (1 + obsdf_pdf(&bs, ls.dir, out_dir) / pdf_l_s);
+            float factor = ls.pdf_value / pdf_l_s;
+            v3 ev = obsdf_eval(&bs, ls.dir, out_dir);
+            *scol = handle_color(s, vmulf(vmul(ls.intensity, vmul(q->contrib, ev)), mis * factor));
+            *sray = L->infinite ? make_ray(surf.point, ls.dir, 0.001f, FLT_MAX_, RAY_SHADOW)
+                                : make_ray(surf.point, vsub(ls.pos, surf.point), 0.001f, 1 - 0.001f, RAY_SHADOW);
+            *has_shadow = 1;
+            ps->shadow++;
+        }
+    }
+    /* on_bounce */
+    if (!(q->depth + 1 <= tech->max_depth)) return 0;
+    osample smp = obsdf_sample(&bs, &r2, out_dir);
+    if (!smp.ok) return 0;
+    v3 c2 = vmul(q->contrib, smp.color);
+    float rr = 1.0f;
+    if (q->depth + 1 > tech->min_depth) {
+        v3 e = vmulf(c2, q->eta * q->eta);
+        rr = clampf_(fmaxf(fmaxf(e.x, e.y), e.z), 0.05f, 0.95f);
+    }
+    if (rng_f32(&r2) >= rr) return 0;
+    q->inv_pdf = specular ? 0 : 1 / smp.pdf;
+    q->contrib = vmulf(c2, 1 / rr);
+    q->eta = q->eta * smp.eta;
+    q->depth = q->depth + 1;
+    q->counter = r2.counter;
+    q->ray = make_ray(surf.point, smp.dir, 0.001f, FLT_MAX_, RAY_BOUNCE);
+    ps->bounce++;
+    return 1;
+}
+
+/* One path to its end, bounce by bounce (the per-path form of the loop: the
+ * checker's default, bit-identical per path to the wavefront form below) */
+static v3 trace_path(const oracle_scene* s, const oracle_params* p, int x, int y, int sample, int list_index, pstats* ps) {
+    opath q;
+    path_begin(s, p, x, y, sample, list_index, &q, ps);
+    v3 Lsum = V(0, 0, 0);
     for (;;) {
         ohit h;
-        trace_scene(s, &ray, 0, &h, &ps->tr);
-        v3 Lacc = V(0, 0, 0);
-        if (h.ent < 0) {
-            for (int li = 0; li < s->num_infinite; ++li) {
-                const olight* L = &s->lights[li];
-                if (L->delta) continue;
-                v3 emit = V(L->rad[0], L->rad[1], L->rad[2]);
-                float pdf_s = 1 / (4 * PI_);
-                float sel = s->selector == IGX_SELECT_UNIFORM ? uni_pdf : select_pdf(s, li, ray.org);
-                float mis = tech->nee ? 1 / (1 + inv_pdf * sel * pdf_s) : 1.0f;
-                Lacc = vadd(Lacc, handle_color(s, vmulf(vmul(contrib, emit), mis)));
-            }
-            Lsum = vadd(Lsum, Lacc);
-            break;
-        }
-        osurf surf = surface_element(s, &h, &ray);
-        const igx_entity* ent = &s->desc.entities[h.ent];
-        const igx_material* mat = &s->desc.materials[ent->material];
-        int mlight = s->mat_light[ent->material];
-        if (mlight >= 0 && surf.entering) {
-            float dt = -vdot(ray.dir, surf.local.n);
-            if (dt > FLT_EPS_) {
-                const olight* L = &s->lights[mlight];
-                v3 emit = V(L->rad[0], L->rad[1], L->rad[2]);
-                float pdf_s = area_pdf_direct_solid(s, L, ray.org, dt, h.t * h.t, h.u);
-                float sel = s->selector == IGX_SELECT_UNIFORM ? uni_pdf : select_pdf(s, mlight, ray.org);
-                float mis = tech->nee ? 1 / (1 + inv_pdf * sel * pdf_s) : 1.0f;
-                Lacc = vadd(Lacc, handle_color(s, vmulf(vmul(contrib, emit), mis)));
-            }
-        }
+        trace_scene(s, &q.ray, 0, &h, &ps->tr);
+        v3 Lacc, scol;
+        oray sr;
+        int has_shadow;
+        int alive = path_shade(s, &q, &h, &Lacc, &has_shadow, &sr, &scol, ps);
         Lsum = vadd(Lsum, Lacc);
-        rng_t r2 = {seed, counter};
-        v3 out_dir = vneg(ray.dir);
-        obsdf bs = obsdf_make(mat, &surf);
-        int specular = obsdf_specular(&bs);
-        /* on_shadow */
-        if (tech->nee && !specular && s->num_lights > 0 && depth + 1 <= tech->max_depth) {
-            float sel_pdf;
-            int lid = select_light(s, &r2, surf.point, &sel_pdf);
-            const olight* L = &s->lights[lid];
-            odirect ls = light_sample_direct(s, L, &r2, &surf);
-            float pdf_l_s = (ls.pdf_solid ? ls.pdf_value : ls.pdf_value * (ls.dist * ls.dist) / ls.cos) * sel_pdf;
-            if (pdf_l_s > FLT_EPS_ && ls.cos > FLT_EPS_) {
-                float mis = L->delta ? 1.0f : 1 / (1 + obsdf_pdf(&bs, ls.dir, out_dir) / pdf_l_s);
-                float factor = ls.pdf_value / pdf_l_s;
-                v3 ev = obsdf_eval(&bs, ls.dir, out_dir);
-                v3 scol = handle_color(s, vmulf(vmul(ls.intensity, vmul(contrib, ev)), mis * factor));
-                oray sr = L->infinite ? make_ray(surf.point, ls.dir, 0.001f, FLT_MAX_, RAY_SHADOW)
-                                      : make_ray(surf.point, vsub(ls.pos, surf.point), 0.001f, 1 - 0.001f, RAY_SHADOW);
-                ps->shadow++;
-                ohit sh;
-                if (!trace_scene(s, &sr, 1, &sh, &ps->tr)) Lsum = vadd(Lsum, scol);
-            }
+        if (has_shadow) {
+            ohit sh;
+            if (!trace_scene(s, &sr, 1, &sh, &ps->tr)) Lsum = vadd(Lsum, scol);
         }
-        /* on_bounce */
-        if (!(depth + 1 <= tech->max_depth)) break;
-        osample smp = obsdf_sample(&bs, &r2, out_dir);
-        if (!smp.ok) break;
-        v3 in_dir = smp.dir, bcol = smp.color;
-        float bpdf = smp.pdf, beta = smp.eta;
-        v3 c2 = vmul(contrib, bcol);
-        float rr = 1.0f;
-        if (depth + 1 > tech->min_depth) {
-            v3 e = vmulf(c2, eta * eta);
-            rr = clampf_(fmaxf(fmaxf(e.x, e.y), e.z), 0.05f, 0.95f);
-        }
-        if (rng_f32(&r2) >= rr) break;
-        inv_pdf = specular ? 0 : 1 / bpdf;
-        contrib = vmulf(c2, 1 / rr);
-        eta = eta * beta;
-        depth = depth + 1;
-        counter = r2.counter;
-        ray = make_ray(surf.point, in_dir, 0.001f, FLT_MAX_, RAY_BOUNCE);
-        ps->bounce++;
+        if (!alive) break;
     }
     return Lsum;
 }
@@ -1972,6 +2032,81 @@ typedef struct {
     pstats total;
 } job_t;
 
+/* framebuffer.splat of the CPU accumulator (driver/accumulator.art:23-30): fb[pixel] += colour / spi */
+static inline void splat(float* fb, int width, int x, int y, v3 c, float inv) {
+    size_t o = 3 * ((size_t)y * width + x);
+    fb[o] += c.x * inv;
+    fb[o + 1] += c.y * inv;
+    fb[o + 2] += c.z * inv;
+}
+
+/* cpu_trace's loop for one tile (driver/mapping_cpu.art:694-836; the default
+ * CPU target: vector width 1, no vector compaction): the tile's spi * 256
+ * camera rays form the primary stream (capacity spi * tile_size^2,
+ * cpu_get_stream_capacity, so one generation fills it); then, while rays
+ * remain: closest hits for the stream (on_traverse_primary), a counting sort
+ * by entity with misses last (cpu_sort_primary, :57-97), hit shading entity by
+ * entity and miss shading (on_hit_shade / on_miss_shade: emission splats, NEE
+ * rays into the secondary stream, bounces), compaction of the surviving rays
+ * (cpu_compact_primary, :199-304), and the any-hit secondary stream, whose
+ * unoccluded rays splat their colour (:815-828). */
+typedef struct {
+    opath* q;       /* primary stream */
+    opath* q2;      /* sort / compaction target */
+    ohit* hit;
+    ohit* hit2;
+    oray* sray;     /* secondary stream */
+    v3* scol;
+    int* spix;      /* 2 ints per secondary ray: its pixel */
+    int* count;     /* entities + 2 sort bins */
+    int cap;
+} ostream;
+
+static void stream_tile(const oracle_scene* s, const oracle_params* p, float* fb, int xs, int ys, int xe, int ye, ostream* S,
+                        pstats* ps) {
+    int width = p->num_rays > 0 ? p->num_rays : p->width;
+    const float inv = 1.0f / (float)p->spi;
+    const int N = s->desc.num_entities;
+    int n = 0;
+    for (int y = ys; y < ye; ++y) /* id = pixel * spi + sample (on_generate) */
+        for (int x = xs; x < xe; ++x)
+            for (int smp = 0; smp < p->spi; ++smp) path_begin(s, p, x, y, smp, x, &S->q[n++], ps);
+    int* count = S->count;
+    while (n > 0) {
+        for (int i = 0; i < n; ++i) trace_scene(s, &S->q[i].ray, 0, &S->hit[i], &ps->tr);
+        /* counting sort by entity, misses (entity N) last */
+        memset(count, 0, sizeof(int) * (size_t)(N + 2));
+        for (int i = 0; i < n; ++i) count[(S->hit[i].ent < 0 ? N : S->hit[i].ent) + 1]++;
+        for (int e = 0; e <= N; ++e) count[e + 1] += count[e];
+        for (int i = 0; i < n; ++i) {
+            const int k = count[S->hit[i].ent < 0 ? N : S->hit[i].ent]++;
+            S->q2[k] = S->q[i];
+            S->hit2[k] = S->hit[i];
+        }
+        /* shading in entity order, then misses; survivors compacted in place */
+        int alive_n = 0, ns = 0;
+        for (int i = 0; i < n; ++i) {
+            opath* q = &S->q2[i];
+            v3 Lacc;
+            int has_shadow;
+            const int px = q->x, py = q->y;
+            const int alive = path_shade(s, q, &S->hit2[i], &Lacc, &has_shadow, &S->sray[ns], &S->scol[ns], ps);
+            splat(fb, width, px, py, Lacc, inv);
+            if (has_shadow) {
+                S->spix[2 * ns] = px;
+                S->spix[2 * ns + 1] = py;
+                ++ns;
+            }
+            if (alive) S->q[alive_n++] = *q;
+        }
+        n = alive_n;
+        for (int i = 0; i < ns; ++i) {
+            ohit sh;
+            if (!trace_scene(s, &S->sray[i], 1, &sh, &ps->tr)) splat(fb, width, S->spix[2 * i], S->spix[2 * i + 1], S->scol[i], inv);
+        }
+    }
+}
+
 static void* worker(void* arg) {
     job_t* j = (job_t*)arg;
     pstats ps;
@@ -1979,11 +2114,28 @@ static void* worker(void* arg) {
     const int T = 16;
     int width = j->p->num_rays > 0 ? j->p->num_rays : j->p->width;
     float inv = 1.0f / (float)j->p->spi;
+    ostream S;
+    memset(&S, 0, sizeof(S));
+    if (j->p->stream) { /* the thread's streams (ignis_get_primary_stream / _secondary_stream) */
+        S.cap = j->p->spi * T * T;
+        S.q = (opath*)malloc(sizeof(opath) * S.cap);
+        S.q2 = (opath*)malloc(sizeof(opath) * S.cap);
+        S.hit = (ohit*)malloc(sizeof(ohit) * S.cap);
+        S.hit2 = (ohit*)malloc(sizeof(ohit) * S.cap);
+        S.sray = (oray*)malloc(sizeof(oray) * S.cap);
+        S.scol = (v3*)malloc(sizeof(v3) * S.cap);
+        S.spix = (int*)malloc(sizeof(int) * 2 * S.cap);
+        S.count = (int*)malloc(sizeof(int) * (size_t)(j->s->desc.num_entities + 2));
+    }
     for (;;) {
         int t = atomic_fetch_add(&j->next, 1);
         if (t >= j->num_tiles) break;
         int tx = t % j->tiles_x, ty = t / j->tiles_x;
         int xs = j->x0 + tx * T, ys = j->y0 + ty * T;
+        if (j->p->stream) {
+            stream_tile(j->s, j->p, j->fb, xs, ys, xs + T < j->x1 ? xs + T : j->x1, ys + T < j->y1 ? ys + T : j->y1, &S, &ps);
+            continue;
+        }
         for (int y = ys; y < ys + T && y < j->y1; ++y)
             for (int x = xs; x < xs + T && x < j->x1; ++x) {
                 float r = 0, g = 0, b = 0;
@@ -1999,6 +2151,14 @@ static void* worker(void* arg) {
                 j->fb[o + 2] += b;
             }
     }
+    free(S.q);
+    free(S.q2);
+    free(S.hit);
+    free(S.hit2);
+    free(S.sray);
+    free(S.scol);
+    free(S.spix);
+    free(S.count);
     pthread_mutex_lock(&j->lock);
     j->total.camera += ps.camera;
     j->total.bounce += ps.bounce;

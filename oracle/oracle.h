@@ -49,6 +49,12 @@ typedef struct oracle_params {
     /* ray-list mode: num_rays > 0 (8 floats per ray), film = num_rays x 1 */
     int32_t num_rays;
     const float* rays;
+    /* 1: the reference CPU device's wavefront per 16x16 tile (cpu_trace,
+     * driver/mapping_cpu.art:694-836: a stream of spi * 256 rays, closest
+     * hits, sort by entity, shading in entity order, compaction, any-hit
+     * shadow stream, splats into the film); 0: each path to its end.  Per
+     * path both compute the same radiance; the film sums in another order. */
+    int32_t stream;
 } oracle_params;
 
 typedef struct oracle_stats {

@@ -29,8 +29,9 @@ SCENES = [
     "sphere-light-ico", "sphere-light-ico-nopt", "sphere-light-pure", "sphere-light-uv",
     "three-planes-dielectric", "three-planes-glass", "three-planes-interface",
     "two-planes-mirror", "two-planes-plastic",
-    # Blender Cycles references: principled BSDF + point (power) + constant environment
-    "cycles-box",
+    # Blender Cycles references: principled BSDF + point (power) + constant environment;
+    # principled cone + sun light over a checker-textured diffuse ground
+    "cycles-box", "cycles-sun",
 ]
 
 

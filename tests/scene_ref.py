@@ -458,8 +458,23 @@ def check_desc(path, desc):
         bt = BSDF_TYPES.get(b.get("type"))
         if bt is not None and m.bsdf_type != bt:
             raise AssertionError(f"entity {re_['name']}: bsdf type {m.bsdf_type} vs {b.get('type')}")
-        if b.get("type") == "diffuse" and not isinstance(b.get("reflectance"), str):
-            _close(m.kd[:], _vec(b.get("reflectance", 0.8)), f"bsdf {b['name']} reflectance")
+        refl = b.get("reflectance", 0.8)
+        if b.get("type") == "diffuse" and isinstance(refl, str) and "checkerboard" in refl:
+            # select(checkerboard(uvw * S) == 1, A, B): texture/checkerboard.art, Transpiler.cpp
+            import re
+            mm = re.fullmatch(r"\s*select\(\s*checkerboard\(\s*uvw\s*\*\s*([-+0-9.eE]+)\s*\)\s*==\s*1\s*,"
+                              r"\s*(color\([^()]*\))\s*,\s*(color\([^()]*\))\s*\)\s*", refl)
+            if not mm:
+                raise AssertionError(f"bsdf {b['name']}: unexpected texture expression {refl!r}")
+            if m.texture != 1:
+                raise AssertionError(f"bsdf {b['name']}: texture {m.texture}, expected the checker")
+            _close([m.tex_scale], [float(mm.group(1))], f"bsdf {b['name']} checker scale")
+            _close(m.tex_kd1[:], _vec(mm.group(2)), f"bsdf {b['name']} checker colour 1")
+            _close(m.kd[:], _vec(mm.group(3)), f"bsdf {b['name']} checker colour 0")
+        elif b.get("type") == "diffuse":
+            if m.texture != 0:
+                raise AssertionError(f"bsdf {b['name']}: texture {m.texture} on a plain colour")
+            _close(m.kd[:], _vec(refl), f"bsdf {b['name']} reflectance")
         if b.get("type") in ("dielectric", "glass"):
             if "int_ior" in b:
                 _close([m.int_ior], [b["int_ior"]], f"bsdf {b['name']} int_ior")

@@ -70,6 +70,8 @@ DIRECT = [
     "cbox-d1", "emissive-plane", "emissive-plane-nopt", "emissive-plane-scale", "emissive-plane-scale-nopt",
     "flipped-prim-glass", "plane-d1", "point", "room", "sphere-light-ico", "sphere-light-ico-nopt",
     "sphere-light-pure", "sphere-light-uv", "two-planes-mirror", "two-planes-plastic",
+    # Blender Cycles: sun light (light/sun.art), principled cone, checker-textured ground
+    "cycles-sun",
 ]
 MULTILIGHT = ["multilight", "multilight-uniform", "multilight-simple", "multilight-hierarchy"]
 SPI = 8
@@ -182,7 +184,7 @@ def test_error_image_metric():
 
 @pytest.mark.parametrize("stem", ["cbox-d1", "emissive-plane", "emissive-plane-scale", "flipped-prim-glass",
                                   "plane-d1", "point", "room", "sphere-light-pure", "sphere-light-uv",
-                                  "two-planes-plastic"])
+                                  "two-planes-plastic", "cycles-sun"])
 def test_oracle_matches_reference_image(stem):
     """CPU twin: the oracle (restated reference CPU device) at 128 spp against
     the reference image, eps scaled by 1024/128."""

@@ -135,6 +135,23 @@ def test_oracle_thread_count_invariant(diamond_path):
     np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("name", ["diamond_scene.json", "primitives.json", "s_deep.json", "materials.json"])
+def test_oracle_stream_mode_equals_per_path(root, name):
+    """The reference CPU device's per-tile wavefront (cpu_trace: stream of
+    spi * 256 rays, sort by entity, compaction, secondary stream; the timed
+    CPU baseline) computes every path exactly as the per-path loop: the same
+    ray counts, the film equal up to the order of its float sums."""
+    sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", name))
+    o = O.OracleScene(sc)
+    a, sa = o.render(80, 64, 8, threads=3)
+    b, sb = o.render(80, 64, 8, threads=3, stream=True)
+    for k in ("camera_rays", "bounce_rays", "shadow_rays", "node_visits", "tri_tests"):
+        assert sa[k] == sb[k], k
+    np.testing.assert_allclose(b, a, rtol=2e-6, atol=1e-7)
+    c, _ = o.render(80, 64, 8, threads=1, stream=True)
+    np.testing.assert_array_equal(b, c)  # tiles are independent: thread count does not matter
+
+
 def test_oracle_furnace_sphere():
     """White diffuse closed sphere in a constant environment: every pixel -> 1 (energy conservation)."""
     scene = {

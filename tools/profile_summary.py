@@ -178,10 +178,12 @@ def suite(tag):
         for line in open(os.path.join(out, "suite.log")) if os.path.exists(os.path.join(out, "suite.log")) else []:
             if line.startswith(f"== {key}:"):
                 args = line.split(":", 1)[1].strip()
-        pmc(os.path.join(d, "fetch"), os.path.join(d, "write"), kernel=kernel, scene=key, second_half=True,
-            workload=f"tools/{args or 'pmc_run.py'} (the suite line's scene, film and iterations, spi 8; "
-                     f"the measured render after a warm-up of the same shape); "
-                     f"rocprof kernel stats: profiles/{tag}_{key}_kernel_stats.md")
+        for k in [kernel] + (["k_shadow_refill"] if kernel == "k_trace" else []):
+            # split schedule: the any-hit kernel gets its own roofline too (bench.py shadow_roofline)
+            pmc(os.path.join(d, "fetch"), os.path.join(d, "write"), kernel=k, scene=key, second_half=True,
+                workload=f"tools/{args or 'pmc_run.py'} (the suite line's scene, film and iterations, spi 8; "
+                         f"the measured render after a warm-up of the same shape); "
+                         f"rocprof kernel stats: profiles/{tag}_{key}_kernel_stats.md")
 
 
 if __name__ == "__main__":

@@ -2,7 +2,7 @@
 simulated on one GPU) over K back-to-back frames, with one device handle
 (each frame drained before the next, as the gather requires) and with two
 handles alternating (bench.py's N > 1 pipelining: frame k+1 queued before
-frame k is drained).  usage: rank_pipeline.py scene N [K] [stream_slots]"""
+frame k is drained).  usage: rank_pipeline.py scene N [K] [stream_slots] [iterations] [square film size]"""
 import json, os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "ignis-masterthesis_amd"))
@@ -13,6 +13,9 @@ scene = ignis_amd.Scene.from_file(os.path.join(ROOT, sys.argv[1]))
 n = int(sys.argv[2])
 K = int(sys.argv[3]) if len(sys.argv) > 3 else 6
 W, H = scene.film_size
+ITERS = int(sys.argv[5]) if len(sys.argv) > 5 else 32
+if len(sys.argv) > 6:
+    W = H = int(sys.argv[6])
 devs = [ignis_amd.Device(0), ignis_amd.Device(0)]
 slots = int(sys.argv[4]) if len(sys.argv) > 4 else 2
 for d in devs:
@@ -30,7 +33,7 @@ def run(handles):
     for k in range(K):
         d = handles[k % len(handles)]
         d.clear()
-        d.render_iterations(p, 32)
+        d.render_iterations(p, ITERS)
         if pending is not None:
             pending.synchronize()
         pending = d
