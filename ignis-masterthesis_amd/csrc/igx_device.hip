@@ -155,7 +155,6 @@ struct FrameArgs {
     int shadow_classes;  // shadow rays crossing an enclosing entity's box go to the back of their shard (shadow_class_b)
     int reverse;         // k_extend: a shard's positions are taken from its end (class C, then B, then A:
                          // the groups whose paths run longest start first, the short ones fill the launch's end)
-    int gen_octets;      // > 0: screen-local layout of the generated chunk (gen_slot): octets of 512 slots per iteration
 };
 
 // path slot -> (local pixel, sample, iteration): slots run over the chunk's
@@ -229,44 +228,6 @@ __device__ __forceinline__ int gen_index(int i, int shard_cap) {
 __device__ __forceinline__ int gen_shard_count(int n, int s) {
     const int rem = (n & (64 * NSH - 1)) - s * 64;
     return (n >> 12) * 64 + (rem < 0 ? 0 : (rem > 64 ? 64 : rem));
-}
-
-// Screen-local layout of a generated chunk (FrameArgs::gen_octets = O > 0).
-// Wave g of a launch serves shard g % 64, and block b runs on XCD b % 8
-// (blocks are dealt round-robin over the XCDs), so XCD x serves shards
-// 4x..4x+3 and 4x+32..4x+35.  Each iteration's P = chunk_pixels x spi slots
-// are cut into O = ceil(P / 512) octets of 8 groups of 64 (a group: 8
-// neighbouring pixels x spi 8); region r = the octets o with 8o / O = r, a
-// band of the film, and group k of an octet of region r goes to shard
-// 4r + (k & 3) + 32 (k >> 2).  One XCD thus traces the rays of one band, whose
-// camera and bounce rays walk the same parts of the BVH: its L2 holds them
-// (the round-robin layout spread every shard over the whole film).  A
-// shard's positions run over (iteration, octet of the region, lane); slots
-// past P in the last octet of an iteration are holes (dead paths).  Placement
-// only bears on speed: any block-to-XCD mapping renders the same image.
-__device__ __forceinline__ int oct_start(int O, int r) { return (r * O + 7) >> 3; }
-__device__ __forceinline__ int oct_count(int O, int r) { return oct_start(O, r + 1) - oct_start(O, r); }
-__device__ __forceinline__ int region_shard(int r, int k) { return 4 * r + (k & 3) + 32 * (k >> 2); }
-__device__ __forceinline__ void shard_region(int s, int& r, int& k) {
-    r = (s & 31) >> 2;
-    k = (s & 3) + 4 * (s >> 5);
-}
-// records of shard s in a generated chunk of n paths (holes included)
-__device__ __forceinline__ int gen_count(int gen_octets, int chunk_iters, int n, int s) {
-    if (gen_octets == 0) return gen_shard_count(n, s);
-    int r, k;
-    shard_region(s, r, k);
-    return chunk_iters * oct_count(gen_octets, r) * 64;
-}
-// path slot at position pos of shard s of a generated chunk; -1: a hole
-__device__ __forceinline__ int gen_slot(int gen_octets, int per_iter, int s, int pos) {
-    if (gen_octets == 0) return ((pos >> 6) << 12) | (s << 6) | (pos & 63); // inverse of gen_index
-    int r, k;
-    shard_region(s, r, k);
-    const int oc = oct_count(gen_octets, r);
-    const int q = pos >> 6, it = q / oc;
-    const int j = ((oct_start(gen_octets, r) + q - it * oc) << 9) + (k << 6) + (pos & 63);
-    return j < per_iter ? it * per_iter + j : -1;
 }
 
 // Records of path-stream shard s: `a` of class A at offsets [0, a) and ab - a
@@ -368,28 +329,12 @@ __device__ __forceinline__ GenPath gen_path(const FrameArgs& fa, const SceneView
 
 #if IGX_PART == 0
 __global__ void __launch_bounds__(BLOCK) k_generate(FrameArgs fa, SceneView sv, PathBuf out, float4* L, int* cnt0) {
-    const int per_iter = fa.chunk_pixels * fa.spi, n = per_iter * fa.chunk_iters;
-    const int O = fa.gen_octets;
-    if (blockIdx.x == 0 && threadIdx.x < NSH) cnt0[threadIdx.x * CSTRIDE] = gen_count(O, fa.chunk_iters, n, threadIdx.x);
-    // round-robin layout: t = slot; screen-local: t runs over (iteration,
-    // octet, group, lane) of every position, holes included
-    const int total = O ? fa.chunk_iters * O * 512 : n;
-    for (int t = blockIdx.x * BLOCK + threadIdx.x; t < total; t += gridDim.x * BLOCK) {
-        int i = t, e;
-        if (O) {
-            const int it = t / (O * 512), u = t - it * O * 512, o = u >> 9, k = (u >> 6) & 7;
-            const int r = (8 * o) / O;
-            e = region_shard(r, k) * out.shard_cap + ((it * oct_count(O, r) + o - oct_start(O, r)) << 6) + (u & 63);
-            i = u < per_iter ? it * per_iter + u : -1;
-        } else {
-            e = gen_index(i, out.shard_cap);
-        }
-        if (i < 0) { // a hole: a dead path
-            out.p1[e] = make_float4(0, 0, 1, __uint_as_float(0u));
-            continue;
-        }
+    const int n = fa.chunk_pixels * fa.spi * fa.chunk_iters;
+    if (blockIdx.x == 0 && threadIdx.x < NSH) cnt0[threadIdx.x * CSTRIDE] = gen_shard_count(n, threadIdx.x);
+    for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
         L[i] = make_float4(0, 0, 0, 0);
         const GenPath g = gen_path(fa, sv, i);
+        const int e = gen_index(i, out.shard_cap);
         out.p0[e] = make_float4(g.o.x, g.o.y, g.o.z, __int_as_float(i));
         out.p1[e] = make_float4(g.d.x, g.d.y, g.d.z, __uint_as_float(g.counter | ((uint32_t)g.depth << 24)));
         out.p2[e] = make_float4(1, 1, 1, 0); // init_pt_raypayload (technique/pathtracer.art:33-38)
@@ -813,13 +758,8 @@ __device__ __forceinline__ int take_group(int* work, int& s, uint64_t& done, int
         if (lane_id() == 0) m = __hip_atomic_load(done_mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         done |= (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)m) |
                 ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(m >> 32)) << 32);
-        uint64_t open = ~done;
+        const uint64_t open = ~done;
         if (!open) return -1;
-        // the shards of this wave's XCD first (4x..4x+3, 4x+32..4x+35 for the
-        // XCD x of shard s: the screen-local layout keeps one film band there)
-        const int x4 = ((s & 31) >> 2) << 2;
-        const uint64_t own = open & ((0xFull << x4) | (0xFull << (x4 + 32)));
-        if (own) open = own;
         const int r = (s + 1) & (NSH - 1);
         const uint64_t rot = (open >> r) | (r ? (open << (NSH - r)) : 0ull);
         s = (r + __ffsll((unsigned long long)rot) - 1) & (NSH - 1);
@@ -879,7 +819,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
     int s = w.s;
     auto count_of = [&](int sh_) {
         if (gen) {
-            const int g = gen_count(fa.gen_octets, fa.chunk_iters, fa.gen_n, sh_);
+            const int g = gen_shard_count(fa.gen_n, sh_);
             return ShardCount{g, g, g};
         }
         return shard_count(kc.cnt_in, sh_);
@@ -910,12 +850,10 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
         ShadowRec sr;
         ps.depth = 0;
         if (q < ns) {
-            if (gen) {
-                const int i = gen_slot(fa.gen_octets, fa.chunk_pixels * fa.spi, s, pos);
-                if (i >= 0) {
-                    ps = camera_path(fa, sv, i);
-                    L[i] = make_float4(0, 0, 0, 0);
-                } // else a hole of the screen-local layout: stays dead (depth 0)
+            if (gen) { // inverse of gen_index
+                const int i = ((pos >> 6) << 12) | (s << 6) | (pos & 63);
+                ps = camera_path(fa, sv, i);
+                L[i] = make_float4(0, 0, 0, 0);
             } else {
                 ps = load_path(in, path_index(in, s, pos, sc));
             }
@@ -1657,9 +1595,6 @@ struct igx_device {
     int64_t tail_opt = -1;   // paths at or below which k_finish takes over (-1 = auto)
     int64_t tail_last_opt = -1; // the same for the last chunk of a render call, whose tail overlaps nothing (-1 = tail_opt)
     bool fuse_generate = true; // bounce 0 of the fused k_extend builds its camera paths (no k_generate pass)
-    // generated chunks of >= 2^18 paths per iteration in the screen-local
-    // layout (gen_slot: one film band per XCD); 0: round-robin groups
-    int gen_layout_opt = 1;
     int split_opt = -1;      // k_trace + k_shade per bounce instead of the fused k_extend (-1: auto = global-table scenes)
     int trace_waves = 5;     // occupancy target of k_trace (5 waves per SIMD, anything else = compiler's choice)
     int refill_opt = -1;     // persistent-lane trace / shadow, refilled once this many lanes idle (0: off, -1: auto = 16)
@@ -1833,19 +1768,18 @@ void free_slot_buffers(Slot& s) {
 // record per path (20 B) for k_shade; the fused schedule needs none.
 // `region_c`: three path classes (FrameArgs::classify 4), so each path buffer
 // holds a second set of records for class C (PathBuf::c_base)
-igx_status ensure_slot(igx_device* dev, Slot& s, size_t cap, bool hits, bool region_c, int min_shard_cap) {
+igx_status ensure_slot(igx_device* dev, Slot& s, size_t cap, bool hits, bool region_c) {
     if (!s.ctr) {
         HIPCHK(hipMalloc((void**)&s.ctr, CTR_INTS * sizeof(int)));
         HIPCHK(hipHostMalloc((void**)&s.pinned, CTR_INTS * sizeof(int), hipHostMallocDefault));
         HIPCHK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
         std::memset(s.pinned, 0, CTR_INTS * sizeof(int));
     }
-    if (s.cap >= cap && s.shard_cap >= min_shard_cap && (!hits || s.hb.h) && (!region_c || s.pa.c_base)) return IGX_OK;
+    if (s.cap >= cap && (!hits || s.hb.h) && (!region_c || s.pa.c_base)) return IGX_OK;
     free_slot_buffers(s);
     // shard capacity: a generated chunk puts at most ceil(cap / (64 NSH)) groups
-    // of 64 paths in one shard (round-robin layout; the screen-local layout
-    // asks for min_shard_cap), and a shard's outputs never exceed its inputs
-    const int shard_cap = std::max((int)((cap + 64 * NSH - 1) / (64 * NSH)) * 64, min_shard_cap);
+    // of 64 paths in one shard, and a shard's outputs never exceed its inputs
+    const int shard_cap = (int)((cap + 64 * NSH - 1) / (64 * NSH)) * 64;
     const size_t recs = (size_t)shard_cap * NSH;
     auto alloc4 = [&](float4** p, size_t k) -> igx_status { HIPCHK(hipMalloc((void**)p, k * sizeof(float4))); return IGX_OK; };
     igx_status st;
@@ -2415,10 +2349,6 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     else if (k == "tail_threshold") dev->tail_opt = value;
     else if (k == "tail_threshold_last") dev->tail_last_opt = value;
     else if (k == "fuse_generate") dev->fuse_generate = value != 0;
-    else if (k == "gen_layout") {
-        if (value < 0 || value > 1) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "gen_layout must be 0 (round-robin) or 1 (screen-local)");
-        dev->gen_layout_opt = (int)value;
-    }
     else if (k == "split") {
         if (value < -1 || value > 1) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "split must be -1 (auto), 0 or 1");
         dev->split_opt = (int)value;
@@ -3298,13 +3228,6 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
     const long long chunk_pixels_max = std::min<long long>(cap, total_paths) / p->spi;
     const int iters_per_chunk = total_paths <= cap ? (int)std::min<long long>(count, cap / total_paths) : 1;
     const size_t slot_cap = (size_t)(chunk_pixels_max * p->spi * iters_per_chunk);
-    // screen-local layout of the generated chunks (gen_slot): octets of 512
-    // slots per iteration, and the largest shard it fills (holes included)
-    auto octets_of = [&](long long per_iter) -> int {
-        return dev->gen_layout_opt && !list_mode && per_iter >= (1ll << 18) ? (int)((per_iter + 511) / 512) : 0;
-    };
-    const int oct_max = octets_of(chunk_pixels_max * p->spi);
-    const int gen_shard_need = oct_max ? iters_per_chunk * ((oct_max + 7) / 8) * 64 : 0;
 
     const int max_bounces = std::min(std::max(dev->sv.max_depth, 1), MAX_BOUNCES - 1);
     const bool inst = dev->instrument;
@@ -3333,7 +3256,7 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
         dev->next_slot ^= 1;
         igx_status st = harvest(dev, S); // waits for the chunk that used this slot two chunks ago (one, with one slot)
         if (st != IGX_OK) return st;
-        if ((st = ensure_slot(dev, S, slot_cap, split, fa.classify == 4, gen_shard_need)) != IGX_OK) return st;
+        if ((st = ensure_slot(dev, S, slot_cap, split, fa.classify == 4)) != IGX_OK) return st;
 
         auto begin_timed = [&](int kind, int bounce, hipStream_t strm) {
             if (!dev->timing) return;
@@ -3349,7 +3272,6 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
         int chunk_pixels = (int)std::min<long long>(chunk_pixels_max, local_pixels - px0);
         fa.chunk_pixel0 = (int)px0;
         fa.chunk_pixels = chunk_pixels;
-        fa.gen_octets = octets_of((long long)chunk_pixels * p->spi);
         long long n = (long long)chunk_pixels * p->spi * fa.chunk_iters;
         // tail threshold (auto): n / 64, but at most what one pass of k_finish
         // holds (one path per resident lane): beyond that the tail kernel's

@@ -6,8 +6,8 @@ set -o pipefail
 mkdir -p gpurun_out/r04l
 export TMPDIR=/tmp
 O=gpurun_out/r04l
-timeout -k 10 600 python3 -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread -rA > $O/pytest_gpu.log 2>&1
-rc=$?; tail -3 $O/pytest_gpu.log; grep -E "halves RelSE|FAILED|Error" $O/pytest_gpu.log | head -5; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python3 -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread -rA ${PYTEST_K:+-k "$PYTEST_K"} > $O/pytest_gpu.log 2>&1
+rc=$?; tail -3 $O/pytest_gpu.log; grep -E "halves RelSE|band vs oracle|FAILED|Error" $O/pytest_gpu.log | head -5; [ $rc -eq 0 ] || exit $rc
 for round in 1 2; do
   timeout -k 10 200 python3 tools/sweep_frame.py scenes/s_soup_16m.json '[{"gen_layout":0},{"gen_layout":1}]' 1 >> $O/ab_soup16m.jsonl 2>&1 || exit 1
   timeout -k 10 200 python3 tools/sweep_frame.py scenes/s_soup_1m.json '[{"gen_layout":0},{"gen_layout":1}]' 2 >> $O/ab_soup1m.jsonl 2>&1 || exit 1
