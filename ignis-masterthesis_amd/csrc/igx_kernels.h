@@ -275,6 +275,68 @@ __device__ __forceinline__ int4 as_int4(float4 v) {
     return make_int4(__float_as_int(v.x), __float_as_int(v.y), __float_as_int(v.z), __float_as_int(v.w));
 }
 
+// Octant-ordered slab tests (the reference CPU traversal's `ordered` box test,
+// intersection.art:174-176 with mapping_cpu.art:20-31, 181): per axis the
+// bound the ray meets first is chosen by the sign of its inverse direction,
+// so the entry distance is a max over three near planes and the exit a min
+// over three far planes, without a min / max pair per axis and child.  For a
+// positive inverse direction fma(lo, idir, iorg) <= fma(hi, idir, iorg)
+// (rounding is monotone), so the ordered and the unordered test give the same
+// entry and exit bit for bit; they differ only when a slab distance is NaN
+// (a direction component below 1e-8 with |origin| > 1: inf - inf), where the
+// reference's CPU and GPU tests differ in the same way.
+// Quantised 4-wide nodes (IGX_ORDERED_SLAB_Q, default on): one select per
+// axis and node picks the near and far byte words.  Round 4, same box,
+// identical images: soup-1M 8-iteration frame 290.5 / 287.4 -> 268.8 / 270.8
+// ms (trace 178.0 / 172.9 -> 160.0 / 163.2, shadow 228.7 / 227.1 -> 213.2 /
+// 213.8), S-soup-16M 1-iteration frame 66.3 / 66.7 -> 63.2 / 62.8 ms
+// (profiles/r04_ab_ordered_slab.log).
+// 4-wide float nodes (IGX_ORDERED_SLAB, default off): the near and far float4
+// of each axis come by load address (offset 0 or 16 B by the sign); the same
+// A/B gave S-deep 79.0 / 78.9 -> 78.6 / 78.3 ms but primitives 30.6 / 30.7 ->
+// 31.8 / 31.7 ms (32 iterations), so the float nodes keep min / max.
+#ifndef IGX_ORDERED_SLAB
+#define IGX_ORDERED_SLAB 0
+#endif
+#ifndef IGX_ORDERED_SLAB_Q
+#define IGX_ORDERED_SLAB_Q 1
+#endif
+// Quantised exit widening: the quantised slab distance fma(q, S, O) carries
+// the rounding of O = fma(origin, idir, iorg) on top of its own, up to about
+// 2^-23 of the distance to the node, which the half quantum of slack only
+// covers out to ~1.7e4 node extents.  The exit distance is
+// scaled by 1 + 2^-20 (the exit plane's own distance bounds both roundings,
+// entry <= exit), so the test stays a superset of the exact box test for
+// rays from any distance (tests/native/quantize_check.cpp: origins up to
+// 1e6 node extents away).  Only |exit| matters: a box with exit < tmin is
+// rejected either way.
+constexpr float QSLAB_EXIT_WIDEN = 1.0f + 0x1p-20f;
+// 4-wide node (SoA float4 bounds lx hx ly hy lz hz, then refs): the near and
+// far float4 of each axis come by load address (offset 0 or 16 B by the sign),
+// the select costing one address add instead of four min and four max.
+template <int NS, bool TREE>
+__device__ __forceinline__ void load_node4_ordered(const SceneView& sv, const Trav& t, int node, float4 (&f)[7]) {
+    const int sx = __float_as_int(t.idir.x) < 0, sy = __float_as_int(t.idir.y) < 0, sz = __float_as_int(t.idir.z) < 0;
+    const int ix[7] = {sx, 1 - sx, 2 + sy, 3 - sy, 4 + sz, 5 - sz, 6};
+    if constexpr (TREE) {
+        if (node < sv.tree_n) {
+            lds_f4v* np = (lds_f4v*)(sv.tree + NS * node);
+#pragma unroll
+            for (int k = 0; k < 7; ++k) {
+                const f4v v = np[ix[k]];
+                f[k] = make_float4(v.x, v.y, v.z, v.w);
+            }
+            return;
+        }
+    }
+    global_f4v* np = (global_f4v*)(sv.nodes + NS * node);
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        const f4v v = np[ix[k]];
+        f[k] = make_float4(v.x, v.y, v.z, v.w);
+    }
+}
+
 // Slab test of both children of BVH2 node `node` (intersect_ray_box,
 // intersection.art:170-181, with ray.tmin folded in).  Returns the next node
 // (nearer child first; the other is pushed) or the popped entry.
@@ -343,7 +405,8 @@ __device__ __forceinline__ int node_step4(const SceneView& sv, const Trav& t, in
         if (first_active_lane()) st.wnodes++;
     }
     float4 f[7];
-    load_node<7, NS, TREE>(sv, node, f); // see node_step2
+    if constexpr (IGX_ORDERED_SLAB) load_node4_ordered<NS, TREE>(sv, t, node, f); // near, far per axis
+    else load_node<7, NS, TREE>(sv, node, f); // see node_step2
     const float4 lx = f[0], hx = f[1], ly = f[2], hy = f[3], lz = f[4], hz = f[5];
     const int4 r = as_int4(f[6]);
     float d[4];
@@ -355,9 +418,15 @@ __device__ __forceinline__ int node_step4(const SceneView& sv, const Trav& t, in
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         float nx, fx, ny, fy, nz, fz;
-        slab4(LX[k], HX[k], t.idir.x, t.iorg.x, nx, fx);
-        slab4(LY[k], HY[k], t.idir.y, t.iorg.y, ny, fy);
-        slab4(LZ[k], HZ[k], t.idir.z, t.iorg.z, nz, fz);
+        if constexpr (IGX_ORDERED_SLAB) { // LX .. are the near, HX .. the far bounds
+            nx = fmaf(LX[k], t.idir.x, t.iorg.x), fx = fmaf(HX[k], t.idir.x, t.iorg.x);
+            ny = fmaf(LY[k], t.idir.y, t.iorg.y), fy = fmaf(HY[k], t.idir.y, t.iorg.y);
+            nz = fmaf(LZ[k], t.idir.z, t.iorg.z), fz = fmaf(HZ[k], t.idir.z, t.iorg.z);
+        } else {
+            slab4(LX[k], HX[k], t.idir.x, t.iorg.x, nx, fx);
+            slab4(LY[k], HY[k], t.idir.y, t.iorg.y, ny, fy);
+            slab4(LZ[k], HZ[k], t.idir.z, t.iorg.z, nz, fz);
+        }
         float en = fmaxf(fmaxf(nx, ny), fmaxf(nz, t.tmin));
         float ex = fminf(fminf(fx, fy), fminf(fz, t.tmax));
         bool h = en <= ex;
@@ -379,8 +448,9 @@ __device__ __forceinline__ int node_step4(const SceneView& sv, const Trav& t, in
 // Quantised 4-wide node (64 B, host Bvh4QNode): per axis an origin and a
 // power-of-two scale, child bounds as bytes.  The slab distance of code q on
 // axis a is fma(q, s_a * idir_a, fma(o_a, idir_a, iorg_a)); the boxes carry at
-// least half a quantum of slack (quantize_bvh4), so every ray the exact box
-// accepts is accepted here.  Absent children (kEmptyRef) are masked by ref.
+// least half a quantum of slack (quantize_bvh4) and the exit distance is
+// widened by QSLAB_EXIT_WIDEN, so every ray the exact box accepts is accepted
+// here.  Absent children (kEmptyRef) are masked by ref.
 template <bool STATS, bool SPILL, bool TREE>
 __device__ __forceinline__ int node_step4q(const SceneView& sv, const Trav& t, int node, const TStack& ts, int& sp,
                                            TraceStats& st) {
@@ -394,9 +464,16 @@ __device__ __forceinline__ int node_step4q(const SceneView& sv, const Trav& t, i
     const int4 r = as_int4(f[3]);
     const float SX = A.w * t.idir.x, SY = B.x * t.idir.y, SZ = B.y * t.idir.z;
     const float OX = fmaf(A.x, t.idir.x, t.iorg.x), OY = fmaf(A.y, t.idir.y, t.iorg.y), OZ = fmaf(A.z, t.idir.z, t.iorg.z);
-    const uint32_t qlx = __float_as_uint(B.z), qhx = __float_as_uint(B.w);
-    const uint32_t qly = __float_as_uint(C.x), qhy = __float_as_uint(C.y);
-    const uint32_t qlz = __float_as_uint(C.z), qhz = __float_as_uint(C.w);
+    uint32_t qlx = __float_as_uint(B.z), qhx = __float_as_uint(B.w);
+    uint32_t qly = __float_as_uint(C.x), qhy = __float_as_uint(C.y);
+    uint32_t qlz = __float_as_uint(C.z), qhz = __float_as_uint(C.w);
+    if constexpr (IGX_ORDERED_SLAB_Q) { // near / far byte words by the sign of idir (= the sign of S*)
+        const bool sx = __float_as_int(t.idir.x) < 0, sy = __float_as_int(t.idir.y) < 0, sz = __float_as_int(t.idir.z) < 0;
+        const uint32_t nx = sx ? qhx : qlx, fx = sx ? qlx : qhx;
+        const uint32_t ny = sy ? qhy : qly, fy = sy ? qly : qhy;
+        const uint32_t nz = sz ? qhz : qlz, fz = sz ? qlz : qhz;
+        qlx = nx, qhx = fx, qly = ny, qhy = fy, qlz = nz, qhz = fz;
+    }
     float d[4];
     int ref[4] = {r.x, r.y, r.z, r.w};
     int n = 0;
@@ -405,8 +482,14 @@ __device__ __forceinline__ int node_step4q(const SceneView& sv, const Trav& t, i
         const float ax = fmaf((float)((qlx >> (8 * k)) & 255u), SX, OX), bx = fmaf((float)((qhx >> (8 * k)) & 255u), SX, OX);
         const float ay = fmaf((float)((qly >> (8 * k)) & 255u), SY, OY), by = fmaf((float)((qhy >> (8 * k)) & 255u), SY, OY);
         const float az = fmaf((float)((qlz >> (8 * k)) & 255u), SZ, OZ), bz = fmaf((float)((qhz >> (8 * k)) & 255u), SZ, OZ);
-        const float en = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), t.tmin));
-        const float ex = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), t.tmax));
+        float en, ex;
+        if constexpr (IGX_ORDERED_SLAB_Q) { // a* near, b* far
+            en = fmaxf(fmaxf(ax, ay), fmaxf(az, t.tmin));
+            ex = fminf(fminf(fminf(bx, by), bz) * QSLAB_EXIT_WIDEN, t.tmax);
+        } else {
+            en = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), t.tmin));
+            ex = fminf(fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz)) * QSLAB_EXIT_WIDEN, t.tmax);
+        }
         const bool h = en <= ex && ref[k] != REF_EMPTY;
         d[k] = h ? en : INFINITY;
         n += h ? 1 : 0;
@@ -456,7 +539,7 @@ __device__ __forceinline__ int node_step8q(const SceneView& sv, const Trav& t, i
         const float ay = fmaf(qbyte(qly[w], b), SY, OY), by = fmaf(qbyte(qhy[w], b), SY, OY);
         const float az = fmaf(qbyte(qlz[w], b), SZ, OZ), bz = fmaf(qbyte(qhz[w], b), SZ, OZ);
         const float en = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), t.tmin));
-        const float ex = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), t.tmax));
+        const float ex = fminf(fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz)) * QSLAB_EXIT_WIDEN, t.tmax);
         const bool h = en <= ex && ref[k] != REF_EMPTY;
         d[k] = h ? en : INFINITY;
         n += h ? 1 : 0;

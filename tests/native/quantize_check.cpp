@@ -3,7 +3,12 @@
 // (1) the decoded box o + q * s contains the child box with at least half a
 // quantum to spare, and (2) every random ray whose slab test accepts the exact
 // box (node_step4's float formula) is accepted by the quantised slab test
-// (node_step4q's formula), with the same tmin / tmax clamps.
+// (node_step4q's formula, both the octant-ordered form the device uses and the
+// min / max form, each with the exit widening QSLAB_EXIT_WIDEN), with the same
+// tmin / tmax clamps, for ray origins up to 1e6 node extents away and rays
+// aimed at points on the child boxes' faces; and (3) the ordered and min / max
+// forms give the same entry and exit distances.  Without the widening, rays
+// from far away are rejected now and then (counted and printed, not failed).
 #include "bvh_build.h"
 
 #include <cmath>
@@ -19,8 +24,9 @@ static float safe_rcp(float x) {
 int main() {
     std::mt19937 rng(7);
     std::uniform_real_distribution<float> u(0.f, 1.f);
-    long bad_box = 0, bad_ray = 0, rays = 0, accepted = 0;
-    for (int it = 0; it < 20000; ++it) {
+    const float widen = 1.0f + 0x1p-20f; // igx_kernels.h QSLAB_EXIT_WIDEN
+    long bad_box = 0, bad_ray = 0, bad_ordered = 0, unwidened_rejects = 0, rays = 0, accepted = 0;
+    for (int it = 0; it < 100000; ++it) {
         const float mag = std::pow(10.f, -3.f + 6.f * u(rng));     // coordinates 1e-3 .. 1e3
         const float ext = mag * std::pow(10.f, -7.f + 7.f * u(rng)); // node extent down to 1e-7 of them
         const float c[3] = {mag * (2 * u(rng) - 1), mag * (2 * u(rng) - 1), mag * (2 * u(rng) - 1)};
@@ -54,11 +60,22 @@ int main() {
         // rays: from around the node towards it, the device formulas
         for (int r = 0; r < 20; ++r) {
             float o[3], d[3];
-            const float far = ext * std::pow(10.f, 3.f * u(rng));
+            const float far = ext * std::pow(10.f, 6.f * u(rng));
+            // half the rays aim at a point on a face of a present child's box
+            float aim[3];
+            const int kc = (int)(u(rng) * 3.999f), fa = (int)(u(rng) * 2.999f);
+            const bool on_face = (r & 1) && n.ref[kc] != igx::kEmptyRef;
+            for (int a = 0; a < 3; ++a) {
+                const float* lo = a == 0 ? n.lo_x : a == 1 ? n.lo_y : n.lo_z;
+                const float* hi = a == 0 ? n.hi_x : a == 1 ? n.hi_y : n.hi_z;
+                if (!on_face) aim[a] = c[a] + ext * (u(rng) - 0.5f);
+                else if (a == fa) aim[a] = u(rng) < 0.5f ? lo[kc] : hi[kc];
+                else aim[a] = lo[kc] + (hi[kc] - lo[kc]) * u(rng);
+            }
             float dn = 0;
             for (int a = 0; a < 3; ++a) {
                 o[a] = c[a] + far * (2 * u(rng) - 1);
-                d[a] = c[a] + ext * (u(rng) - 0.5f) - o[a];
+                d[a] = aim[a] - o[a];
                 dn += d[a] * d[a];
             }
             dn = std::sqrt(dn);
@@ -78,26 +95,37 @@ int main() {
                 if (n.ref[k] == igx::kEmptyRef) continue;
                 const float* lo[3] = {n.lo_x, n.lo_y, n.lo_z};
                 const float* hi[3] = {n.hi_x, n.hi_y, n.hi_z};
-                float en = tmin, ex = tmax, qe = tmin, qx = tmax;
+                float en = tmin, ex = tmax, qe = tmin, qx = INFINITY, oe = tmin, ox = INFINITY;
                 for (int a = 0; a < 3; ++a) {
                     const float t0 = std::fmaf(lo[a][k], idir[a], iorg[a]), t1 = std::fmaf(hi[a][k], idir[a], iorg[a]);
                     en = std::fmax(en, std::fmin(t0, t1));
                     ex = std::fmin(ex, std::fmax(t0, t1));
-                    const float q0 = std::fmaf((float)((ql[a] >> (8 * k)) & 255u), S[a], O[a]);
-                    const float q1 = std::fmaf((float)((qh[a] >> (8 * k)) & 255u), S[a], O[a]);
+                    const uint32_t bl = (ql[a] >> (8 * k)) & 255u, bh = (qh[a] >> (8 * k)) & 255u;
+                    const float q0 = std::fmaf((float)bl, S[a], O[a]);
+                    const float q1 = std::fmaf((float)bh, S[a], O[a]);
                     qe = std::fmax(qe, std::fmin(q0, q1));
                     qx = std::fmin(qx, std::fmax(q0, q1));
+                    // octant-ordered: near / far byte by the sign of idir
+                    const bool neg = std::signbit(idir[a]);
+                    oe = std::fmax(oe, std::fmaf((float)(neg ? bh : bl), S[a], O[a]));
+                    ox = std::fmin(ox, std::fmaf((float)(neg ? bl : bh), S[a], O[a]));
                 }
+                if (oe != qe || ox != qx) ++bad_ordered;
+                const float qx_raw = std::fmin(qx, tmax);
+                qx = std::fmin(qx * widen, tmax);
                 ++rays;
                 if (en <= ex) {
                     ++accepted;
                     if (!(qe <= qx)) ++bad_ray;
+                    if (!(qe <= qx_raw)) ++unwidened_rejects;
                 }
             }
         }
     }
-    std::printf("boxes with < half a quantum of slack: %ld; rays accepted by the exact box %ld of %ld, rejected by the quantised one: %ld\n",
-                bad_box, accepted, rays, bad_ray);
-    std::printf(bad_box || bad_ray ? "failed\n" : "ok\n");
-    return bad_box || bad_ray ? 1 : 0;
+    std::printf("boxes with < half a quantum of slack: %ld; rays accepted by the exact box %ld of %ld, rejected by the quantised one: %ld "
+                "(without the exit widening: %ld); ordered != min/max distances: %ld\n",
+                bad_box, accepted, rays, bad_ray, unwidened_rejects, bad_ordered);
+    const bool fail = bad_box || bad_ray || bad_ordered;
+    std::printf(fail ? "failed\n" : "ok\n");
+    return fail ? 1 : 0;
 }
