@@ -178,6 +178,9 @@ def roofline(dev, st, render_one, n_gpus, scene_key):
         "frac_traffic": round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4) if traffic and avg_launch_s > 0 else None,
         "traffic_raw": {k: pmc[k] for k in ("fetch_size_kib_per_launch", "write_size_kib_per_launch")} if pmc else None,
         "algorithmic_bytes_per_launch": round(alg_bytes / launches, 1),
+        # > 1: bytes the counters see beyond the algorithmic count (table fetches
+        # that miss L2, counted as on chip when the tables fit the Infinity Cache)
+        "traffic_over_algorithmic": round(traffic / (alg_bytes / launches), 2) if traffic and alg_bytes > 0 else None,
         "bytes_per_ray": round(bytes_per_ray, 1),
         "tables_on_chip": bool(resident),
         "table_bytes": int(st["table_bytes"] + st["shading_bytes"]),
@@ -229,6 +232,7 @@ def shadow_roofline(st, inst, si, scene_key):
            "frac": round(per_launch / t / 1e9 / HBM_PEAK_GBS, 4) if t > 0 else None, "traffic": traffic,
            "frac_traffic": round(traffic / t / 1e9 / HBM_PEAK_GBS, 4) if traffic and t > 0 else None,
            "algorithmic_bytes_per_launch": round(per_launch, 1), "bytes_per_ray": round(per_ray, 1),
+           "traffic_over_algorithmic": round(traffic / per_launch, 2) if traffic and per_launch > 0 else None,
            "visits_per_ray": {"nodes": round(inst["shadow_node_visits"] / ns, 2),
                               "instances": round(inst["shadow_leaf_visits"] / ns, 2),
                               "triangles": round(inst["shadow_tri_tests"] / ns, 2)},
