@@ -64,12 +64,29 @@ def parse():
 # everything streamed between two uses of a line fit the cache (MI355X_MICROARCH.md, Infinity Cache)
 MALL_BYTES = 128 << 20
 # N > 1: a rank holds two handles, each with ONE stream slot (option
-# stream_slots) sized to the rank's share of a frame, which is one chunk:
-# N = 2: 128 M paths = 25 GB per handle, 8: 6.3 GB.  A budget below the share
+# stream_slots) sized to the rank's share of a frame when that is one chunk
+# (the diamond: N = 2: 128 M paths = 25 GB per handle, 8: 6.3 GB), two
+# otherwise (rank_stream_slots).  A budget below the share
 # splits a frame into chunks and costs time (slot_budget_mb 20000 at N = 2:
 # 67.3 vs 55.2 ms per rank frame, profiles/r03_exp_classes_regroup_slots.log);
 # IGX_SLOT_BUDGET_MB caps it anyway (0 = auto)
 SLOT_BUDGET_MB = int(os.environ.get("IGX_SLOT_BUDGET_MB", "0"))
+
+
+# paths of one chunk (igx_device.hip MAX_CHUNK_PATHS)
+MAX_CHUNK_PATHS = 1 << 27
+
+
+def rank_stream_slots(W, H, tile, n, spi, iters):
+    """Stream slots per device handle of a rank at N > 1: 1 when the rank's
+    share of a frame (its tiles, all iterations) fits one chunk, else 2.  With
+    one slot per handle the chunks of a multi-chunk share run back to back and
+    each chunk's tail is exposed: S-deep 4096^2, 8 iterations, N = 2: a rank
+    frame of 391.5 ms against 309.1 ms for the same path count as a 2896^2
+    film with two slots (profiles/r04_probe_chunks_tiles.log)."""
+    from ignis_amd import shard
+    share = shard.max_tiles_per_rank(W, H, tile, n) * tile * tile * spi * iters
+    return 1 if share <= MAX_CHUNK_PATHS else 2
 
 
 def algorithmic_bytes(inst, st):
@@ -345,9 +362,11 @@ class RankFrames:
             self.dst_valid = dst[self.valid]
             self.devs.append(ignis_amd.Device(gpu))
             self.devs[1].upload(scene)
-            # one stream slot per handle, sized to the rank's share of a frame
+            # one stream slot per handle when the rank's share of a frame is one
+            # chunk (the other handle overlaps the next frame); a share of several
+            # chunks keeps two, so consecutive chunks of a frame overlap as at N = 1
             for d in self.devs:
-                d.set_option("stream_slots", 1)
+                d.set_option("stream_slots", rank_stream_slots(W, H, self.tile, n, spi, iters))
                 d.set_option("slot_budget_mb", SLOT_BUDGET_MB)
 
     def params(self, it=0):

@@ -198,6 +198,34 @@ __device__ __forceinline__ int tpop(const TStack& s, int& sp) {
         return (!SPILL || sp < s.cap) ? s.lds[sp * TSTACK_STRIDE] : s.spill[(sp - s.cap) * s.sstride];
     }
 }
+// Push the farther hit children of a 4-wide node: r1 .. r(n-1) of the
+// children sorted nearest first (n hit children, r(n-1) the deepest entry,
+// r1 on top).  When all of them fit the LDS column with a slot to spare, the
+// three stores are unconditional: an entry that is not pushed (n < 4, n < 3)
+// is written to the dead slot just above the new top, so the step has no
+// per-push branch (IGX_PUSH_SELECT; otherwise one guarded push each).
+#ifndef IGX_PUSH_SELECT
+#define IGX_PUSH_SELECT 1
+#endif
+template <bool SPILL>
+__device__ __forceinline__ void tpush_hits3(const TStack& s, int& sp, int n, int r1, int r2, int r3) {
+    if constexpr (IGX_PUSH_SELECT) {
+        if (n < 2) return;
+        const int top = sp + n - 2;
+        if (top + 1 < s.cap) {
+            const int dead = top + 1;
+            lds_int* col = (lds_int*)s.lds;
+            col[top * TSTACK_STRIDE] = r1;
+            col[(n > 2 ? top - 1 : dead) * TSTACK_STRIDE] = r2;
+            col[(n > 3 ? top - 2 : dead) * TSTACK_STRIDE] = r3;
+            sp = top + 1;
+            return;
+        }
+    }
+    if (n > 3) tpush<SPILL>(s, sp, r3);
+    if (n > 2) tpush<SPILL>(s, sp, r2);
+    if (n > 1) tpush<SPILL>(s, sp, r1);
+}
 __device__ __forceinline__ TStack make_tstack(int* lds_base, int cap, int* spill) {
     const int g = blockIdx.x * TSTACK_STRIDE + threadIdx.x;
     return TStack{lds_base + threadIdx.x, spill + g, cap, (int)(gridDim.x * TSTACK_STRIDE)};
@@ -439,9 +467,7 @@ __device__ __forceinline__ int node_step4(const SceneView& sv, const Trav& t, in
     cswap(d[0], ref[0], d[2], ref[2]);
     cswap(d[1], ref[1], d[3], ref[3]);
     cswap(d[1], ref[1], d[2], ref[2]);
-    if (n > 3) tpush<SPILL>(ts, sp, ref[3]);
-    if (n > 2) tpush<SPILL>(ts, sp, ref[2]);
-    if (n > 1) tpush<SPILL>(ts, sp, ref[1]);
+    tpush_hits3<SPILL>(ts, sp, n, ref[1], ref[2], ref[3]);
     return ref[0];
 }
 
@@ -500,9 +526,7 @@ __device__ __forceinline__ int node_step4q(const SceneView& sv, const Trav& t, i
     cswap(d[0], ref[0], d[2], ref[2]);
     cswap(d[1], ref[1], d[3], ref[3]);
     cswap(d[1], ref[1], d[2], ref[2]);
-    if (n > 3) tpush<SPILL>(ts, sp, ref[3]);
-    if (n > 2) tpush<SPILL>(ts, sp, ref[2]);
-    if (n > 1) tpush<SPILL>(ts, sp, ref[1]);
+    tpush_hits3<SPILL>(ts, sp, n, ref[1], ref[2], ref[3]);
     return ref[0];
 }
 

@@ -148,3 +148,21 @@ def test_gloo_world2_rank_summary():
 def test_rank_summary_single_rank():
     s = shard.rank_summary(None, {"frame_ms": 3.25})
     assert s == {"frame_ms": {"min": 3.25, "max": 3.25, "mean": 3.25, "per_rank": [3.25]}}
+
+
+def test_rank_stream_slots_by_share():
+    """bench.py keeps one stream slot per device handle when a rank's share of
+    a frame is one chunk (the diamond at any N), two when it spans several
+    (config 5 at N = 2 / 4 / 8), so consecutive chunks of a frame overlap."""
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    from ignis_amd import shard
+    for n in (2, 4, 8):
+        assert bench.rank_stream_slots(1000, 1000, shard.balanced_tile(1000, n), n, 8, 32) == 1
+        assert bench.rank_stream_slots(4096, 4096, shard.balanced_tile(4096, n), n, 8, 8) == 2
+    # exactly one chunk: 2^27 paths
+    assert bench.rank_stream_slots(4096, 4096, 4096, 1, 8, 1) == 1
+    assert bench.rank_stream_slots(4096, 4096, 4096, 1, 8, 2) == 2
