@@ -2195,21 +2195,25 @@ void configure_treelet(igx_device* dev) {
     // LDS it holds keeps their blocks off the CU (soup-1M frame +4 % with one)
 }
 
+// Film pixels among the chunk's local pixels (tiles at the film's right and
+// bottom edges hang over it): per tile in closed form, the valid pixels among
+// a tile's first m row-major pixels being min(m / T, h) * w + (m / T < h ?
+// min(m % T, w) : 0).  (A per-pixel loop cost 8 ms of host time per 67 M-path
+// config-5 chunk, during which the GPU idled: profiles/r04_timeline_gaps.log.)
 long long valid_pixels_in_chunk(const FrameArgs& fa) {
     if (fa.num_rays > 0 || fa.tile_size <= 0) return fa.chunk_pixels;
     long long v = 0;
-    const int T = fa.tile_size;
-    for (int lp0 = fa.chunk_pixel0; lp0 < fa.chunk_pixel0 + fa.chunk_pixels;) {
-        int k = lp0 / (T * T);
-        int t = fa.tile_offset + k * fa.tile_stride;
-        int ty = t / fa.tiles_x, tx = t - ty * fa.tiles_x;
-        int w = std::max(0, std::min(T, fa.width - tx * T)), h = std::max(0, std::min(T, fa.height - ty * T));
-        int end = std::min((k + 1) * T * T, fa.chunk_pixel0 + fa.chunk_pixels);
-        for (int lp = lp0; lp < end; ++lp) {
-            int r = lp - k * T * T;
-            if (r / T < h && r % T < w) ++v;
-        }
-        lp0 = end;
+    const long long T = fa.tile_size, TT = T * T;
+    const long long c0 = fa.chunk_pixel0, c1 = c0 + fa.chunk_pixels;
+    for (long long k = c0 / TT; k * TT < c1; ++k) {
+        const long long t = fa.tile_offset + k * fa.tile_stride;
+        const long long ty = t / fa.tiles_x, tx = t - ty * fa.tiles_x;
+        const long long w = std::max(0ll, std::min(T, fa.width - tx * T)), h = std::max(0ll, std::min(T, fa.height - ty * T));
+        auto valid_first = [&](long long m) { // valid pixels among the tile's first m
+            const long long rows = m / T;
+            return std::min(rows, h) * w + (rows < h ? std::min(m % T, w) : 0);
+        };
+        v += valid_first(std::min(TT, c1 - k * TT)) - valid_first(std::max(0ll, c0 - k * TT));
     }
     return v;
 }
