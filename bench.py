@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--config5", type=int, default=1,
                     help="also measure BASELINE config 5's stand-in (S-deep 4096x4096, 64 spp) tile-sharded over the N ranks")
     ap.add_argument("--config5-steps", type=int, default=2, help="timed frames of the config-5 line")
+    ap.add_argument("--isolated", type=int, default=1,
+                    help="after the timed frames, one more frame with concurrent_chunks 0 for the dominant kernel's own "
+                         "launch duration (roofline.isolated); 0 for rocprofv3 runs whose average should be the timed frames'")
     return ap.parse_args()
 
 
@@ -226,6 +229,29 @@ def roofline(dev, st, render_one, n_gpus, scene_key):
     return out
 
 
+def isolated_extend(dev, render_frame, roof):
+    """Fused schedule with concurrent chunks: the timed frames run two chunks'
+    bounces at once (igx_device.hip render_chunks_concurrent), so a k_extend
+    launch's HIP-event duration includes time shared with the other chunk's
+    kernels.  One more frame with concurrent_chunks 0 (untimed for `value`)
+    gives the kernel's own launch duration, reported next to the timed one."""
+    dev.reset_stats()
+    dev.set_option("timing", 1)
+    dev.set_option("concurrent_chunks", 0)
+    render_frame()
+    dev.synchronize()
+    si = dev.stats()
+    dev.set_option("concurrent_chunks", 1)
+    dev.set_option("timing", 0)
+    t_iso = si["ms_extend"] / 1e3 / max(1, si["launches_extend"])
+    per_launch = roof["algorithmic_bytes_per_launch"]
+    roof["isolated"] = {"avg_launch_us": round(t_iso * 1e6, 2),
+                        "frac": round(per_launch / t_iso / 1e9 / HBM_PEAK_GBS, 4) if t_iso > 0 else None,
+                        "frac_traffic": round(roof["traffic"] / t_iso / 1e9 / HBM_PEAK_GBS, 4) if t_iso > 0 and roof["traffic"] else None,
+                        "note": "k_extend with concurrent_chunks 0 (each chunk's bounces alone on the chip): the kernel's own "
+                                "launch duration; the timed frames overlap one chunk's last bounces with the next chunk's first"}
+
+
 def shadow_roofline(st, inst, si, scene_key):
     """Roofline object of the split schedule's any-hit kernel (k_shadow_refill):
     per shadow ray 32 B of ray read, at most 48 B more for an unoccluded one
@@ -263,7 +289,7 @@ def shadow_roofline(st, inst, si, scene_key):
     return out
 
 
-def suite_line(ignis_amd, dev_index, path, spi, iters, size=None):
+def suite_line(ignis_amd, dev_index, path, spi, iters, size=None, isolated=True):
     """Short single-GPU measurement of another scene of SURVEY.md §8d (load and
     BVH build excluded): Mrays/s over `iters` iterations after one warm-up,
     plus the dominant kernel's roofline on that scene.  `size` overrides the
@@ -321,6 +347,11 @@ def suite_line(ignis_amd, dev_index, path, spi, iters, size=None):
             r["isolated"]["rocprof"] = dict(rp, frac=round(per_launch / t / 1e9 / HBM_PEAK_GBS, 4),
                                             frac_traffic=round(r["traffic"] / t / 1e9 / HBM_PEAK_GBS, 4) if r["traffic"] else None)
         line["roofline_shadow"] = shadow_roofline(st, r["_inst"], si, key)
+    elif isolated:
+        def frame():
+            dev.clear()
+            dev.render_iterations(p, iters)
+        isolated_extend(dev, frame, line["roofline"])
     line["roofline"].pop("_inst", None)
     dev.close()
     del scene
@@ -593,6 +624,11 @@ def main():
     # ---- roofline of the dominant kernel, live HIP-event timing ----
     roof = roofline(dev, st, lambda: dev.render(params(0)), n_gpus, os.path.splitext(os.path.basename(args.scene))[0])
     roof.pop("_inst", None)
+    if args.isolated and st["launches_trace"] == 0:
+        def frame():
+            dev.clear()
+            dev.render_iterations(params(0), iters)
+        isolated_extend(dev, frame, roof)
     roof["note"] = ("achieved counts the HBM bytes the kernel must move (path / radiance / shadow-ray streams; "
                     "table reads too when the tables exceed the Infinity Cache); traffic is the rocprofv3 PMC "
                     "measurement of the same kernel and workload; memory_system_gbs counts every table read "
@@ -610,7 +646,7 @@ def main():
         suite = None
         if n_gpus == 1 and args.suite:
             # other scenes of SURVEY.md §8d, incl. the HBM roofline scene of record (S-soup-16M)
-            suite = [suite_line(ignis_amd, 0, os.path.join(ROOT, "scenes", f), spi, n, size)
+            suite = [suite_line(ignis_amd, 0, os.path.join(ROOT, "scenes", f), spi, n, size, bool(args.isolated))
                      for f, n, size in (("primitives.json", 8, None),
                                         # config 4 stand-in at its stated 1024 spp (128 iterations x spi 8)
                                         ("s_deep.json", 128, None), ("s_soup_1m.json", 2, None),

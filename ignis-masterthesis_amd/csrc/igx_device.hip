@@ -38,7 +38,9 @@
 #include <map>
 #include <cmath>
 #include <cstring>
+#include <deque>
 #include <string>
+#include <thread>
 #include <vector>
 #include <type_traits>
 
@@ -1563,6 +1565,7 @@ using namespace igxh;
 struct igx_device {
     int hip_device = 0;
     hipStream_t stream = nullptr;  // main (wavefront) stream
+    hipStream_t stream2 = nullptr; // slot 1's wavefront stream under concurrent chunks
     hipStream_t tail_stream = nullptr;
     std::string last_error;
     int num_cus = 256;
@@ -1580,6 +1583,10 @@ struct igx_device {
     // alternate frames, and a rank's share of a frame is one chunk, so there
     // one slot per handle loses nothing: bench.py sets 1 at N > 1
     int stream_slots = 2;
+    // option "concurrent_chunks" (0/1): the two slots' chunks run their
+    // bounces concurrently, each on its own stream (render_chunks_concurrent)
+    int concurrent_opt = 1;
+    int concurrent_start_pct = 10; // option "concurrent_start_pct": a chunk starts once the running one is down to this share of its paths
     // LDS treelet (stage_treelet) on global-table scenes: nodes staged per
     // kernel (the largest prefix of the hot order that keeps the kernel's
     // register-bound occupancy), recomputed when the scene or option changes.
@@ -1663,9 +1670,10 @@ struct igx_device {
     // only its BLAS (trace_enclosed); applies at the next upload
     bool enclosing_opt = true;
     int scene_depth = 0;   // worst-case stack entries of the scene
-    int* spill_main = nullptr; // spill columns of the main, tail and shadow streams
+    int* spill_main = nullptr; // spill columns of the main, tail and shadow streams (and of slot 1's stream)
     int* spill_tail = nullptr;
     int* spill_shadow = nullptr;
+    int* spill_main2 = nullptr;
     hipStream_t shadow_stream = nullptr; // split schedule: shadow rays of bounce b overlap the trace of bounce b + 1
     int overlap_shadow_opt = 1;           // option "overlap_shadow" (0/1)
     // option "speculative": k_trace_refill with speculative while-while (VARIANT_SPEC):
@@ -1717,7 +1725,7 @@ igx_status upload(igx_device* dev, const std::vector<T>& v, const T** out) {
 void free_scene(igx_device* dev) {
     for (void* p : dev->scene_allocs) (void)hipFree(p);
     dev->scene_allocs.clear();
-    dev->spill_main = dev->spill_tail = dev->spill_shadow = nullptr;
+    dev->spill_main = dev->spill_tail = dev->spill_shadow = dev->spill_main2 = nullptr;
     dev->has_scene = false;
 }
 
@@ -1734,8 +1742,8 @@ igx_status configure_stack(igx_device* dev) {
     const int extra = std::max(0, need - LDS_STACK);
     dev->variant = (dev->bvh_width >= 4 ? 2 : 0) | (extra > 0 ? 1 : 0) | (dev->full_shading ? 4 : 0) | (dev->quantized ? VARIANT_Q4 : 0);
     const size_t threads = (size_t)max_grid(dev) * BLOCK;
-    for (int k = 0; k < 3; ++k) {
-        int*& old = k == 0 ? dev->spill_main : k == 1 ? dev->spill_tail : dev->spill_shadow;
+    for (int k = 0; k < 4; ++k) {
+        int*& old = k == 0 ? dev->spill_main : k == 1 ? dev->spill_tail : k == 2 ? dev->spill_shadow : dev->spill_main2;
         if (old) {
             auto it = std::find(dev->scene_allocs.begin(), dev->scene_allocs.end(), (void*)old);
             if (it != dev->scene_allocs.end()) dev->scene_allocs.erase(it);
@@ -1745,7 +1753,7 @@ igx_status configure_stack(igx_device* dev) {
         void* p = nullptr;
         HIPCHK(hipMalloc(&p, std::max<size_t>(16, (size_t)extra * threads * sizeof(int))));
         dev->scene_allocs.push_back(p);
-        (k == 0 ? dev->spill_main : k == 1 ? dev->spill_tail : dev->spill_shadow) = static_cast<int*>(p);
+        (k == 0 ? dev->spill_main : k == 1 ? dev->spill_tail : k == 2 ? dev->spill_shadow : dev->spill_main2) = static_cast<int*>(p);
     }
     dev->sv.spill = dev->spill_main;
     return IGX_OK;
@@ -2153,6 +2161,7 @@ igx_status drain(igx_device* dev) {
     igx_status st;
     if ((st = harvest(dev, dev->slots[0])) || (st = harvest(dev, dev->slots[1]))) return st;
     HIPCHK(hipStreamSynchronize(dev->stream));
+    HIPCHK(hipStreamSynchronize(dev->stream2));
     HIPCHK(hipStreamSynchronize(dev->shadow_stream));
     HIPCHK(hipStreamSynchronize(dev->tail_stream));
     unsigned long long tc[2] = {0, 0};
@@ -2270,6 +2279,7 @@ extern "C" igx_status igx_create(int hip_device, igx_device** out) {
         dev->mem_total = prop.totalGlobalMem;
     }
     if (hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&dev->stream2, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&dev->tail_stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&dev->shadow_stream, hipStreamNonBlocking) != hipSuccess) {
         delete dev;
@@ -2290,6 +2300,7 @@ extern "C" igx_status igx_destroy(igx_device* dev) {
     if (!dev) return IGX_ERR_INVALID_ARGUMENT;
     (void)hipSetDevice(dev->hip_device);
     if (dev->stream) (void)hipStreamSynchronize(dev->stream);
+    if (dev->stream2) (void)hipStreamSynchronize(dev->stream2);
     if (dev->tail_stream) (void)hipStreamSynchronize(dev->tail_stream);
     if (dev->shadow_stream) (void)hipStreamSynchronize(dev->shadow_stream);
     free_scene(dev);
@@ -2305,6 +2316,7 @@ extern "C" igx_status igx_destroy(igx_device* dev) {
     if (dev->tail_counts) (void)hipFree(dev->tail_counts);
     if (dev->ray_list) (void)hipFree(dev->ray_list);
     if (dev->stream) (void)hipStreamDestroy(dev->stream);
+    if (dev->stream2) (void)hipStreamDestroy(dev->stream2);
     if (dev->tail_stream) (void)hipStreamDestroy(dev->tail_stream);
     if (dev->shadow_stream) (void)hipStreamDestroy(dev->shadow_stream);
     delete dev;
@@ -2349,6 +2361,11 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     else if (k == "slot_budget_mb") {
         if (value < 0) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "slot_budget_mb must be >= 0 (0 = auto)");
         dev->slot_budget_mb = value;
+    }
+    else if (k == "concurrent_chunks") dev->concurrent_opt = value != 0 ? 1 : 0;
+    else if (k == "concurrent_start_pct") {
+        if (value < 0 || value > 100) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "concurrent_start_pct must be 0..100");
+        dev->concurrent_start_pct = (int)value;
     }
     else if (k == "tail_threshold") dev->tail_opt = value;
     else if (k == "tail_threshold_last") dev->tail_last_opt = value;
@@ -3127,6 +3144,245 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     return IGX_OK;
 }
 
+// Concurrent chunks (option "concurrent_chunks", fused schedule with two
+// stream slots).  The sequential schedule runs every chunk's bounces on the
+// one main stream: chunk k + 1 starts only when chunk k's bounce loop has
+// reached its tail threshold, so each chunk's last bounces -- a few hundred K
+// long paths, a few hundred microseconds each at low occupancy -- run alone.
+// Here slot k's chunk runs on its own stream (dev->stream / dev->stream2,
+// spill columns spill_main / spill_main2), and one host thread advances both
+// chunks' bounce loops as their lagged counts arrive (hipEventQuery, no
+// blocking wait), so one chunk's late bounces share the GPU with the other's
+// early ones.  The tail kernel runs on the chunk's own stream after its
+// bounces; the resolves go to the tail stream strictly in chunk order, so the
+// framebuffer sums every pixel's iterations in the same order as the
+// sequential schedule: bit-identical images.
+static igx_status render_chunks_concurrent(igx_device* dev, const igx_render_params* p, FrameArgs fa, int count,
+                                           long long local_pixels, int iters_per_chunk, long long chunk_pixels_max,
+                                           size_t slot_cap, int max_bounces, int ext_bpc, int sh_bpc, int fin_bpc,
+                                           bool pairs, std::chrono::steady_clock::time_point t_start) {
+    struct Run {
+        int slot = 0;
+        FrameArgs fa{};
+        long long n = 0;
+        int tail = 0, chunk_pixels = 0, ext_grid = 0, sh_grid = 0, fin_grid = 0;
+        bool fuse_gen = false;
+        int b = 0, switch_b = -1;
+        long long live = 0; // paths entering the last bounce whose count arrived
+        bool loop_done = false, tail_queued = false;
+        hipEvent_t fin_ev = nullptr;
+    };
+    const bool inst = dev->instrument;
+    const int width = fa.width;
+    hipStream_t const main0 = dev->stream, tail0 = dev->tail_stream;
+    int* const spill0 = dev->spill_main;
+    int* const spill_tail0 = dev->spill_tail;
+    hipStream_t const slot_stream[2] = {dev->stream, dev->stream2};
+    int* const slot_spill[2] = {dev->spill_main, dev->spill_main2};
+    // the launch helpers read dev->stream, dev->tail_stream and the spill
+    // columns: point them at slot k while its work is queued
+    auto use_slot = [&](int k) {
+        dev->stream = dev->tail_stream = slot_stream[k];
+        dev->sv.spill = dev->spill_tail = slot_spill[k];
+    };
+    auto restore = [&]() {
+        dev->stream = main0;
+        dev->tail_stream = tail0;
+        dev->sv.spill = spill0;
+        dev->spill_tail = spill_tail0;
+    };
+    auto begin_timed = [&](Slot& S, int kind, int bounce, hipStream_t strm) {
+        if (!dev->timing) return;
+        TimedLaunch t{slot_event(S), slot_event(S), kind, bounce};
+        (void)hipEventRecord(t.a, strm);
+        S.timed.push_back(t);
+    };
+    auto end_timed = [&](Slot& S, hipStream_t strm) {
+        if (!dev->timing) return;
+        (void)hipEventRecord(S.timed.back().b, strm);
+    };
+    std::vector<std::pair<int, long long>> chunks; // (first iteration, first local pixel), in order
+    for (int it0 = 0; it0 < count; it0 += iters_per_chunk)
+        for (long long px0 = 0; px0 < local_pixels; px0 += chunk_pixels_max) chunks.push_back({it0, px0});
+    std::deque<Run> inflight; // chunk order
+    size_t next = 0;
+    igx_status st = IGX_OK;
+#define IGX_CC(expr)                                                                                   \
+    do {                                                                                               \
+        hipError_t e_ = (expr);                                                                        \
+        if (e_ != hipSuccess) {                                                                        \
+            restore();                                                                                 \
+            return fail(dev, IGX_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));         \
+        }                                                                                              \
+    } while (0)
+    while (next < chunks.size() || !inflight.empty()) {
+        bool progress = false;
+        // start the next chunk once its slot's previous chunk has resolved
+        if (next < chunks.size()) {
+            const int k = dev->next_slot;
+            Slot& S = dev->slots[k];
+            bool busy = false;
+            // and once every running chunk is in its late bounces (live paths at
+            // most concurrent_start_pct % of its own): two chunks started together
+            // contend for the chip in their heavy early bounces
+            for (const Run& r : inflight)
+                busy = busy || r.slot == k || (!r.loop_done && r.live * 100 > (long long)dev->concurrent_start_pct * r.n);
+            if (!busy && S.pending) {
+                const hipError_t q = hipEventQuery(S.done);
+                if (q == hipErrorNotReady) busy = true;
+                else IGX_CC(q);
+            }
+            if (!busy) {
+                if ((st = harvest(dev, S)) != IGX_OK || (st = ensure_slot(dev, S, slot_cap, false, fa.classify == 4)) != IGX_OK) {
+                    restore();
+                    return st;
+                }
+                dev->next_slot ^= 1;
+                Run r;
+                r.slot = k;
+                r.fa = fa;
+                const int it0 = chunks[next].first;
+                const long long px0 = chunks[next].second;
+                r.fa.iter = p->iteration + it0;
+                r.fa.chunk_iters = std::min(iters_per_chunk, count - it0);
+                r.chunk_pixels = (int)std::min<long long>(chunk_pixels_max, local_pixels - px0);
+                r.fa.chunk_pixel0 = (int)px0;
+                r.fa.chunk_pixels = r.chunk_pixels;
+                r.n = (long long)r.chunk_pixels * p->spi * r.fa.chunk_iters;
+                r.live = r.n;
+                // tail threshold: as the sequential schedule (render_impl)
+                const long long fin_lanes = (long long)fin_bpc * dev->num_cus * BLOCK / (pairs ? 2 : 1);
+                const bool last_chunk = next + 1 == chunks.size();
+                const int64_t topt = last_chunk && dev->tail_last_opt >= 0 ? dev->tail_last_opt : dev->tail_opt;
+                r.tail = topt >= 0 ? (int)std::min<int64_t>(topt, 1 << 30) : (int)std::max<long long>(32768, std::min(r.n / 64, fin_lanes));
+                S.tail = r.tail;
+                S.camera = valid_pixels_in_chunk(r.fa) * p->spi * r.fa.chunk_iters;
+                S.n0 = r.n;
+                S.split = false;
+                S.bounce_ev.clear();
+                S.launched = 0;
+                r.ext_grid = grid_for(dev, r.n, ext_bpc);
+                r.sh_grid = grid_for(dev, r.n, sh_bpc);
+                r.fin_grid = grid_for(dev, std::min<long long>(r.n, r.tail) * (pairs ? 2 : 1), fin_bpc);
+                r.fuse_gen = dev->fuse_generate && r.n > r.tail;
+                use_slot(k);
+                IGX_CC(hipMemsetAsync(S.ctr, 0, (size_t)(2 * max_bounces + 4) * CROW * sizeof(int), dev->stream));
+                if (dev->dynamic_opt)
+                    IGX_CC(hipMemsetAsync(S.ctr + (size_t)WORK_ROW0 * CROW, 0, (size_t)4 * max_bounces * CROW * sizeof(int), dev->stream));
+                if (!r.fuse_gen) {
+                    begin_timed(S, 2, -1, dev->stream);
+                    hipLaunchKernelGGL(k_generate, dim3(grid_for(dev, r.n, 8)), dim3(BLOCK), 0, dev->stream, r.fa, dev->sv, S.pa, S.L, S.ctr);
+                    end_timed(S, dev->stream);
+                    IGX_CC(hipGetLastError());
+                }
+                restore();
+                if (r.n <= r.tail) { // the whole chunk is one tail pass
+                    r.switch_b = 0;
+                    r.loop_done = true;
+                }
+                inflight.push_back(r);
+                ++next;
+                progress = true;
+            }
+        }
+        // advance every chunk's bounce loop as far as its lagged counts allow
+        for (Run& r : inflight) {
+            Slot& S = dev->slots[r.slot];
+            int* const cnt = S.ctr;
+            auto row = [&](int rr) { return cnt + (size_t)rr * CROW; };
+            use_slot(r.slot);
+            while (!r.loop_done) {
+                if (r.b < max_bounces) {
+                    if (r.b >= 2) {
+                        const hipError_t q = hipEventQuery(S.bounce_ev[r.b - 2]);
+                        if (q == hipErrorNotReady) break;
+                        IGX_CC(q);
+                        r.live = row_total(S, 2 * (r.b - 1));
+                        if (r.live <= r.tail) {
+                            r.switch_b = r.b - 1;
+                            r.loop_done = true;
+                            break;
+                        }
+                    }
+                    const int b = r.b;
+                    PathBuf in = (b & 1) ? S.pb : S.pa, out = (b & 1) ? S.pa : S.pb;
+                    KernelCounters kc{row(2 * b), row(2 * (b + 1)), row(2 * b + 1), dev->dstats, row(WORK_ROW0 + 4 * b)};
+                    begin_timed(S, 0, b, dev->stream);
+                    FrameArgs fb = r.fa;
+                    fb.gen_n = r.fuse_gen && b == 0 ? (int)r.n : 0;
+                    if (inst) launch_extend<true>(dev, S, r.ext_grid, fb, in, out, kc, r.tail);
+                    else launch_extend<false>(dev, S, r.ext_grid, fb, in, out, kc, r.tail);
+                    end_timed(S, dev->stream);
+                    begin_timed(S, 1, b, dev->stream);
+                    int* const sh_work =
+                        (dev->dynamic_opt & (use_refill(dev) ? DYN_REFILL_SHADOW : DYN_SHADOW)) ? row(WORK_ROW0 + 4 * b + 2) : nullptr;
+                    if (inst) launch_shadow<true>(dev, S, r.sh_grid, row(2 * b + 1), sh_work, dev->stream);
+                    else launch_shadow<false>(dev, S, r.sh_grid, row(2 * b + 1), sh_work, dev->stream);
+                    end_timed(S, dev->stream);
+                    IGX_CC(hipGetLastError());
+                    IGX_CC(hipMemcpyAsync(S.pinned + (size_t)(2 * b + 1) * CROW, row(2 * b + 1), 2 * CROW * sizeof(int),
+                                          hipMemcpyDeviceToHost, dev->stream));
+                    hipEvent_t e = slot_event(S);
+                    IGX_CC(hipEventRecord(e, dev->stream));
+                    S.bounce_ev.push_back(e);
+                    ++S.launched;
+                    ++r.b;
+                    progress = true;
+                } else {
+                    // every bounce queued: the counts are known once the last one completed
+                    const hipError_t q = hipEventQuery(S.bounce_ev.back());
+                    if (q == hipErrorNotReady) break;
+                    IGX_CC(q);
+                    r.switch_b = max_bounces;
+                    for (int b = 1; b <= max_bounces; ++b)
+                        if (row_total(S, 2 * b) <= r.tail) {
+                            r.switch_b = b;
+                            break;
+                        }
+                    r.loop_done = true;
+                }
+            }
+            if (r.loop_done && !r.tail_queued) {
+                S.switch_bounce = r.switch_b;
+                if (r.switch_b < MAX_BOUNCES) {
+                    PathBuf in = (r.switch_b & 1) ? S.pb : S.pa;
+                    begin_timed(S, 4, r.switch_b, dev->stream);
+                    if (inst) launch_finish<true>(dev, S, r.fin_grid, r.fa, in, row(2 * r.switch_b), r.tail);
+                    else launch_finish<false>(dev, S, r.fin_grid, r.fa, in, row(2 * r.switch_b), r.tail);
+                    end_timed(S, dev->stream);
+                    IGX_CC(hipGetLastError());
+                }
+                r.fin_ev = slot_event(S);
+                IGX_CC(hipEventRecord(r.fin_ev, dev->stream));
+                r.tail_queued = true;
+                progress = true;
+            }
+            restore();
+        }
+        // resolves strictly in chunk order on the tail stream
+        while (!inflight.empty() && inflight.front().tail_queued) {
+            Run& r = inflight.front();
+            Slot& S = dev->slots[r.slot];
+            IGX_CC(hipStreamWaitEvent(tail0, r.fin_ev, 0));
+            begin_timed(S, 3, -1, tail0);
+            hipLaunchKernelGGL(k_resolve, dim3((r.chunk_pixels + 63) / 64), dim3(64 * RES_G), 0, tail0, r.fa, S.L, dev->fb, width);
+            end_timed(S, tail0);
+            IGX_CC(hipGetLastError());
+            IGX_CC(hipEventRecord(S.done, tail0));
+            S.pending = true;
+            inflight.pop_front();
+            progress = true;
+        }
+        if (!progress) std::this_thread::yield();
+    }
+#undef IGX_CC
+    restore();
+    dev->iteration_count += count;
+    dev->stats.iterations += count;
+    dev->stats.ms_render += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    return IGX_OK;
+}
+
 // Render `count` consecutive iterations (p->iteration, p->iteration + 1, ...).
 // Small iterations are batched: one chunk then holds several iterations'
 // paths (up to the path capacity), so a shard with few pixels (multi-GPU
@@ -3251,6 +3507,10 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
     const bool pairs = use_tail_pairs(dev);
     const int fin_bpc = inst ? finish_blocks_per_cu<true>(sd, ldsb, tree_bytes(dev, dev->tree_fin), pairs)
                              : finish_blocks_per_cu<false>(sd, ldsb, tree_bytes(dev, dev->tree_fin), pairs);
+
+    if (dev->concurrent_opt && !split && dev->stream_slots == 2)
+        return render_chunks_concurrent(dev, p, fa, count, local_pixels, iters_per_chunk, chunk_pixels_max, slot_cap,
+                                        max_bounces, ext_bpc, sh_bpc, fin_bpc, pairs, t_start);
 
     for (int it0 = 0; it0 < count; it0 += iters_per_chunk)
     for (long long px0 = 0; px0 < local_pixels; px0 += chunk_pixels_max) {

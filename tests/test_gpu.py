@@ -713,6 +713,41 @@ def test_bitwise_reproducible_and_spi_dependent(device):
     assert not np.allclose(a, c)
 
 
+@pytest.mark.parametrize("start_pct", [10, 100])
+def test_concurrent_chunks_bit_identical(root, diamond_path, start_pct):
+    """Concurrent chunks (render_chunks_concurrent: the two stream slots' chunks
+    run their bounces at once, resolves in chunk order) give the sequential
+    schedule's film bit for bit; small chunks (option capacity) force many
+    chunks per call, over iterations and over pixel ranges of one iteration,
+    with and without tiles."""
+    sc = ignis_amd.Scene.from_file(diamond_path)
+    w, h, spi, iters = 160, 120, 4, 6
+    films = []
+    for conc in (0, 1):
+        for tile in (None, (40, 1, 3)):
+            d = ignis_amd.Device(0)
+            d.upload(sc)
+            # chunks of at most 65536 paths: a tile share's two iterations, or part
+            # of one iteration of the whole film; a low tail threshold keeps each
+            # chunk in its wavefront bounce loop for several bounces
+            d.set_option("capacity", 65536)
+            d.set_option("tail_threshold", 4096)
+            d.set_option("concurrent_chunks", conc)
+            d.set_option("concurrent_start_pct", start_pct)
+            p = ignis_amd.RenderParams()
+            p.width, p.height, p.spi = w, h, spi
+            if tile:
+                p.tile_size, p.tile_offset, p.tile_stride = tile
+            d.render_iterations(p, iters)
+            fb, n = d.framebuffer(w * h * 3)
+            assert n == iters
+            films.append(fb)
+            d.close()
+    np.testing.assert_array_equal(films[0], films[2])
+    np.testing.assert_array_equal(films[1], films[3])
+    assert films[0].sum() > 0
+
+
 def test_tile_sharding_equals_full_render(device, diamond_path):
     """Multi-GPU decomposition: tiles rendered by 3 shards sum to the full render bit for bit."""
     sc = ignis_amd.Scene.from_file(diamond_path)
