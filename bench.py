@@ -437,6 +437,10 @@ class RankFrames:
             e = self.pending.pop()
             self._pack(e)
             self._gather()
+        # igx_synchronize: the handle's worker thread (async_render) has queued
+        # every frame and the GPU has finished them
+        for d in self.devs:
+            d.synchronize()
         self.torch.cuda.synchronize()
 
     def measure(self, steps, warmup):

@@ -38,7 +38,10 @@
 #include <map>
 #include <cmath>
 #include <cstring>
+#include <condition_variable>
 #include <deque>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -1693,7 +1696,14 @@ struct igx_device {
     uint64_t iteration_count = 0;
     // stats
     igx_stats stats{};
+    // asynchronous rendering (option "async_render"): the worker thread and
+    // its queue (render_impl, igx_clear); nullptr until the first queued render
+    int async_opt = 1;
+    struct AsyncRender* async = nullptr;
 };
+// the worker has queued everything submitted; its first error (part 0)
+igx_status wait_idle(igx_device* dev);
+void stop_async(igx_device* dev);
 
 namespace igxh {
 
@@ -2159,7 +2169,7 @@ igx_status harvest(igx_device* dev, Slot& s) {
 
 igx_status drain(igx_device* dev) {
     igx_status st;
-    if ((st = harvest(dev, dev->slots[0])) || (st = harvest(dev, dev->slots[1]))) return st;
+    if ((st = ::wait_idle(dev)) || (st = harvest(dev, dev->slots[0])) || (st = harvest(dev, dev->slots[1]))) return st;
     HIPCHK(hipStreamSynchronize(dev->stream));
     HIPCHK(hipStreamSynchronize(dev->stream2));
     HIPCHK(hipStreamSynchronize(dev->shadow_stream));
@@ -2227,10 +2237,10 @@ long long valid_pixels_in_chunk(const FrameArgs& fa) {
     return v;
 }
 
-void setup_camera(igx_device* dev, int width, int height) {
+DevCamera make_camera(const igx_device* dev, int width, int height) {
     // make_perspective_camera (camera/perspective.art:29-42), compute_scale_from_{h,v}fov (:2-14)
     const igx_camera& c = dev->cam_desc;
-    DevCamera& k = dev->sv.cam;
+    DevCamera k{};
     float aspect = c.aspect > 0 ? c.aspect : (float)width / (float)height;
     if (c.vertical_fov) {
         k.scale_y = std::tan(c.fov / 2);
@@ -2251,6 +2261,7 @@ void setup_camera(igx_device* dev, int width, int height) {
     }
     k.tmin = c.near_clip;
     k.tmax = c.far_clip;
+    return k;
 }
 
 #endif // IGX_PART == 0
@@ -2299,6 +2310,8 @@ extern "C" igx_status igx_create(int hip_device, igx_device** out) {
 extern "C" igx_status igx_destroy(igx_device* dev) {
     if (!dev) return IGX_ERR_INVALID_ARGUMENT;
     (void)hipSetDevice(dev->hip_device);
+    (void)wait_idle(dev);
+    stop_async(dev);
     if (dev->stream) (void)hipStreamSynchronize(dev->stream);
     if (dev->stream2) (void)hipStreamSynchronize(dev->stream2);
     if (dev->tail_stream) (void)hipStreamSynchronize(dev->tail_stream);
@@ -2327,6 +2340,8 @@ extern "C" const char* igx_last_error(const igx_device* dev) { return dev ? dev-
 
 extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t value) {
     if (!dev || !key) return IGX_ERR_INVALID_ARGUMENT;
+    // options change what queued work reads: let the worker drain first
+    if (igx_status w = wait_idle(dev); w != IGX_OK) return w;
     std::string k(key);
     dev->tree_dirty = true; // schedule options change which kernels run, and so their treelets
     if (k == "timing") dev->timing = value != 0;
@@ -2363,6 +2378,7 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
         dev->slot_budget_mb = value;
     }
     else if (k == "concurrent_chunks") dev->concurrent_opt = value != 0 ? 1 : 0;
+    else if (k == "async_render") dev->async_opt = value != 0 ? 1 : 0;
     else if (k == "concurrent_start_pct") {
         if (value < 0 || value > 100) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "concurrent_start_pct must be 0..100");
         dev->concurrent_start_pct = (int)value;
@@ -3152,38 +3168,93 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
 // Here slot k's chunk runs on its own stream (dev->stream / dev->stream2,
 // spill columns spill_main / spill_main2), and one host thread advances both
 // chunks' bounce loops as their lagged counts arrive (hipEventQuery, no
-// blocking wait), so one chunk's late bounces share the GPU with the other's
-// early ones.  The tail kernel runs on the chunk's own stream after its
-// bounces; the resolves go to the tail stream strictly in chunk order, so the
-// framebuffer sums every pixel's iterations in the same order as the
-// sequential schedule: bit-identical images.
-static igx_status render_chunks_concurrent(igx_device* dev, const igx_render_params* p, FrameArgs fa, int count,
-                                           long long local_pixels, int iters_per_chunk, long long chunk_pixels_max,
-                                           size_t slot_cap, int max_bounces, int ext_bpc, int sh_bpc, int fin_bpc,
-                                           bool pairs, std::chrono::steady_clock::time_point t_start) {
-    struct Run {
-        int slot = 0;
-        FrameArgs fa{};
-        long long n = 0;
-        int tail = 0, chunk_pixels = 0, ext_grid = 0, sh_grid = 0, fin_grid = 0;
-        bool fuse_gen = false;
-        int b = 0, switch_b = -1;
-        long long live = 0; // paths entering the last bounce whose count arrived
-        bool loop_done = false, tail_queued = false;
-        hipEvent_t fin_ev = nullptr;
-    };
-    const bool inst = dev->instrument;
-    const int width = fa.width;
+// blocking wait).  The next chunk starts once the running one is down to
+// concurrent_start_pct % of its paths, so one chunk's late bounces share the
+// GPU with the other's early ones.  The tail kernel runs on the chunk's own
+// stream after its bounces; resolves (and framebuffer clears) go to the tail
+// stream strictly in submission order, so the framebuffer sums every pixel's
+// iterations in the sequential order: bit-identical images.
+//
+// Asynchronous rendering (option "async_render", on top of concurrent
+// chunks): render and clear calls only queue their work for a per-handle
+// worker thread that runs the same scheduler over consecutive calls, so the
+// last chunk of frame k overlaps the first of frame k + 1 too (one chunk per
+// frame on an 8-rank diamond share).  Every other call waits until the queue
+// has drained (wait_idle).
+struct ChunkPlan { // one render call's chunking (render_impl)
+    FrameArgs fa{};
+    DevCamera cam{};
+    int iteration = 0, spi = 1, count = 1, width = 1;
+    long long local_pixels = 0, chunk_pixels_max = 0;
+    int iters_per_chunk = 1;
+    size_t slot_cap = 0;
+    int max_bounces = 1, ext_bpc = 1, sh_bpc = 1, fin_bpc = 1;
+    bool pairs = false;
+};
+struct SchedItem {
+    bool clear = false;
+    std::shared_ptr<const ChunkPlan> plan;
+    int it0 = 0;
+    long long px0 = 0;
+    bool last_of_plan = false;
+    bool started = false;
+    int slot = 0;
+    FrameArgs fa{};
+    long long n = 0;
+    int tail = 0, chunk_pixels = 0, ext_grid = 0, sh_grid = 0, fin_grid = 0;
+    bool fuse_gen = false;
+    int b = 0, switch_b = -1;
+    long long live = 0; // paths entering the last bounce whose count arrived
+    bool loop_done = false, tail_queued = false;
+    hipEvent_t fin_ev = nullptr;
+};
+struct ChunkScheduler {
+    std::deque<SchedItem> items; // submission order
+    bool empty() const { return items.empty(); }
+    void add(const std::shared_ptr<const ChunkPlan>& plan) {
+        const ChunkPlan& pl = *plan;
+        const size_t first = items.size();
+        for (int it0 = 0; it0 < pl.count; it0 += pl.iters_per_chunk)
+            for (long long px0 = 0; px0 < pl.local_pixels; px0 += pl.chunk_pixels_max) {
+                SchedItem s;
+                s.plan = plan;
+                s.it0 = it0;
+                s.px0 = px0;
+                items.push_back(s);
+            }
+        if (items.size() > first) items.back().last_of_plan = true;
+    }
+    void add_clear() {
+        SchedItem s;
+        s.clear = true;
+        items.push_back(s);
+    }
+    igx_status step(igx_device* dev, bool& progress);
+};
+struct AsyncRender {
+    std::thread th;
+    std::mutex m;
+    std::condition_variable cv, cv_idle;
+    std::deque<std::pair<bool, std::shared_ptr<const ChunkPlan>>> jobs; // (clear, plan)
+    bool stop = false, idle = true;
+    igx_status err = IGX_OK;
+    ChunkScheduler sched; // the worker's
+};
+
+igx_status ChunkScheduler::step(igx_device* dev, bool& progress) {
     hipStream_t const main0 = dev->stream, tail0 = dev->tail_stream;
     int* const spill0 = dev->spill_main;
     int* const spill_tail0 = dev->spill_tail;
     hipStream_t const slot_stream[2] = {dev->stream, dev->stream2};
     int* const slot_spill[2] = {dev->spill_main, dev->spill_main2};
-    // the launch helpers read dev->stream, dev->tail_stream and the spill
-    // columns: point them at slot k while its work is queued
-    auto use_slot = [&](int k) {
-        dev->stream = dev->tail_stream = slot_stream[k];
-        dev->sv.spill = dev->spill_tail = slot_spill[k];
+    const bool inst = dev->instrument;
+    // the launch helpers read dev->stream, dev->tail_stream, dev->sv (camera,
+    // spill columns): point them at slot k and the item's camera while its
+    // work is queued
+    auto use_slot = [&](const SchedItem& r) {
+        dev->stream = dev->tail_stream = slot_stream[r.slot];
+        dev->sv.spill = dev->spill_tail = slot_spill[r.slot];
+        dev->sv.cam = r.plan->cam;
     };
     auto restore = [&]() {
         dev->stream = main0;
@@ -3201,12 +3272,6 @@ static igx_status render_chunks_concurrent(igx_device* dev, const igx_render_par
         if (!dev->timing) return;
         (void)hipEventRecord(S.timed.back().b, strm);
     };
-    std::vector<std::pair<int, long long>> chunks; // (first iteration, first local pixel), in order
-    for (int it0 = 0; it0 < count; it0 += iters_per_chunk)
-        for (long long px0 = 0; px0 < local_pixels; px0 += chunk_pixels_max) chunks.push_back({it0, px0});
-    std::deque<Run> inflight; // chunk order
-    size_t next = 0;
-    igx_status st = IGX_OK;
 #define IGX_CC(expr)                                                                                   \
     do {                                                                                               \
         hipError_t e_ = (expr);                                                                        \
@@ -3215,172 +3280,264 @@ static igx_status render_chunks_concurrent(igx_device* dev, const igx_render_par
             return fail(dev, IGX_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));         \
         }                                                                                              \
     } while (0)
-    while (next < chunks.size() || !inflight.empty()) {
-        bool progress = false;
-        // start the next chunk once its slot's previous chunk has resolved
-        if (next < chunks.size()) {
-            const int k = dev->next_slot;
-            Slot& S = dev->slots[k];
-            bool busy = false;
-            // and once every running chunk is in its late bounces (live paths at
-            // most concurrent_start_pct % of its own): two chunks started together
-            // contend for the chip in their heavy early bounces
-            for (const Run& r : inflight)
-                busy = busy || r.slot == k || (!r.loop_done && r.live * 100 > (long long)dev->concurrent_start_pct * r.n);
-            if (!busy && S.pending) {
-                const hipError_t q = hipEventQuery(S.done);
-                if (q == hipErrorNotReady) busy = true;
-                else IGX_CC(q);
-            }
-            if (!busy) {
-                if ((st = harvest(dev, S)) != IGX_OK || (st = ensure_slot(dev, S, slot_cap, false, fa.classify == 4)) != IGX_OK) {
-                    restore();
-                    return st;
-                }
-                dev->next_slot ^= 1;
-                Run r;
-                r.slot = k;
-                r.fa = fa;
-                const int it0 = chunks[next].first;
-                const long long px0 = chunks[next].second;
-                r.fa.iter = p->iteration + it0;
-                r.fa.chunk_iters = std::min(iters_per_chunk, count - it0);
-                r.chunk_pixels = (int)std::min<long long>(chunk_pixels_max, local_pixels - px0);
-                r.fa.chunk_pixel0 = (int)px0;
-                r.fa.chunk_pixels = r.chunk_pixels;
-                r.n = (long long)r.chunk_pixels * p->spi * r.fa.chunk_iters;
-                r.live = r.n;
-                // tail threshold: as the sequential schedule (render_impl)
-                const long long fin_lanes = (long long)fin_bpc * dev->num_cus * BLOCK / (pairs ? 2 : 1);
-                const bool last_chunk = next + 1 == chunks.size();
-                const int64_t topt = last_chunk && dev->tail_last_opt >= 0 ? dev->tail_last_opt : dev->tail_opt;
-                r.tail = topt >= 0 ? (int)std::min<int64_t>(topt, 1 << 30) : (int)std::max<long long>(32768, std::min(r.n / 64, fin_lanes));
-                S.tail = r.tail;
-                S.camera = valid_pixels_in_chunk(r.fa) * p->spi * r.fa.chunk_iters;
-                S.n0 = r.n;
-                S.split = false;
-                S.bounce_ev.clear();
-                S.launched = 0;
-                r.ext_grid = grid_for(dev, r.n, ext_bpc);
-                r.sh_grid = grid_for(dev, r.n, sh_bpc);
-                r.fin_grid = grid_for(dev, std::min<long long>(r.n, r.tail) * (pairs ? 2 : 1), fin_bpc);
-                r.fuse_gen = dev->fuse_generate && r.n > r.tail;
-                use_slot(k);
-                IGX_CC(hipMemsetAsync(S.ctr, 0, (size_t)(2 * max_bounces + 4) * CROW * sizeof(int), dev->stream));
-                if (dev->dynamic_opt)
-                    IGX_CC(hipMemsetAsync(S.ctr + (size_t)WORK_ROW0 * CROW, 0, (size_t)4 * max_bounces * CROW * sizeof(int), dev->stream));
-                if (!r.fuse_gen) {
-                    begin_timed(S, 2, -1, dev->stream);
-                    hipLaunchKernelGGL(k_generate, dim3(grid_for(dev, r.n, 8)), dim3(BLOCK), 0, dev->stream, r.fa, dev->sv, S.pa, S.L, S.ctr);
-                    end_timed(S, dev->stream);
-                    IGX_CC(hipGetLastError());
-                }
-                restore();
-                if (r.n <= r.tail) { // the whole chunk is one tail pass
-                    r.switch_b = 0;
-                    r.loop_done = true;
-                }
-                inflight.push_back(r);
-                ++next;
-                progress = true;
-            }
+    // start the next chunk once its slot's previous chunk has resolved and
+    // every running chunk is in its late bounces (live paths at most
+    // concurrent_start_pct % of its own): two chunks started together only
+    // contend for the chip in their heavy early bounces
+    SchedItem* nx = nullptr;
+    bool late = true;
+    for (SchedItem& r : items) {
+        if (r.clear) continue;
+        if (!r.started) {
+            nx = &r;
+            break;
         }
-        // advance every chunk's bounce loop as far as its lagged counts allow
-        for (Run& r : inflight) {
-            Slot& S = dev->slots[r.slot];
-            int* const cnt = S.ctr;
-            auto row = [&](int rr) { return cnt + (size_t)rr * CROW; };
-            use_slot(r.slot);
-            while (!r.loop_done) {
-                if (r.b < max_bounces) {
-                    if (r.b >= 2) {
-                        const hipError_t q = hipEventQuery(S.bounce_ev[r.b - 2]);
-                        if (q == hipErrorNotReady) break;
-                        IGX_CC(q);
-                        r.live = row_total(S, 2 * (r.b - 1));
-                        if (r.live <= r.tail) {
-                            r.switch_b = r.b - 1;
-                            r.loop_done = true;
-                            break;
-                        }
-                    }
-                    const int b = r.b;
-                    PathBuf in = (b & 1) ? S.pb : S.pa, out = (b & 1) ? S.pa : S.pb;
-                    KernelCounters kc{row(2 * b), row(2 * (b + 1)), row(2 * b + 1), dev->dstats, row(WORK_ROW0 + 4 * b)};
-                    begin_timed(S, 0, b, dev->stream);
-                    FrameArgs fb = r.fa;
-                    fb.gen_n = r.fuse_gen && b == 0 ? (int)r.n : 0;
-                    if (inst) launch_extend<true>(dev, S, r.ext_grid, fb, in, out, kc, r.tail);
-                    else launch_extend<false>(dev, S, r.ext_grid, fb, in, out, kc, r.tail);
-                    end_timed(S, dev->stream);
-                    begin_timed(S, 1, b, dev->stream);
-                    int* const sh_work =
-                        (dev->dynamic_opt & (use_refill(dev) ? DYN_REFILL_SHADOW : DYN_SHADOW)) ? row(WORK_ROW0 + 4 * b + 2) : nullptr;
-                    if (inst) launch_shadow<true>(dev, S, r.sh_grid, row(2 * b + 1), sh_work, dev->stream);
-                    else launch_shadow<false>(dev, S, r.sh_grid, row(2 * b + 1), sh_work, dev->stream);
-                    end_timed(S, dev->stream);
-                    IGX_CC(hipGetLastError());
-                    IGX_CC(hipMemcpyAsync(S.pinned + (size_t)(2 * b + 1) * CROW, row(2 * b + 1), 2 * CROW * sizeof(int),
-                                          hipMemcpyDeviceToHost, dev->stream));
-                    hipEvent_t e = slot_event(S);
-                    IGX_CC(hipEventRecord(e, dev->stream));
-                    S.bounce_ev.push_back(e);
-                    ++S.launched;
-                    ++r.b;
-                    progress = true;
-                } else {
-                    // every bounce queued: the counts are known once the last one completed
-                    const hipError_t q = hipEventQuery(S.bounce_ev.back());
-                    if (q == hipErrorNotReady) break;
-                    IGX_CC(q);
-                    r.switch_b = max_bounces;
-                    for (int b = 1; b <= max_bounces; ++b)
-                        if (row_total(S, 2 * b) <= r.tail) {
-                            r.switch_b = b;
-                            break;
-                        }
-                    r.loop_done = true;
-                }
+        if (!r.loop_done && r.live * 100 > (long long)dev->concurrent_start_pct * r.n) late = false;
+    }
+    if (nx && late) {
+        const int k = dev->next_slot;
+        Slot& S = dev->slots[k];
+        bool busy = false;
+        for (const SchedItem& r : items) busy = busy || (!r.clear && r.started && r.slot == k);
+        if (!busy && S.pending) {
+            const hipError_t q = hipEventQuery(S.done);
+            if (q == hipErrorNotReady) busy = true;
+            else IGX_CC(q);
+        }
+        if (!busy) {
+            SchedItem& r = *nx;
+            const ChunkPlan& pl = *r.plan;
+            igx_status st;
+            if ((st = harvest(dev, S)) != IGX_OK || (st = ensure_slot(dev, S, pl.slot_cap, false, pl.fa.classify == 4)) != IGX_OK) {
+                restore();
+                return st;
             }
-            if (r.loop_done && !r.tail_queued) {
-                S.switch_bounce = r.switch_b;
-                if (r.switch_b < MAX_BOUNCES) {
-                    PathBuf in = (r.switch_b & 1) ? S.pb : S.pa;
-                    begin_timed(S, 4, r.switch_b, dev->stream);
-                    if (inst) launch_finish<true>(dev, S, r.fin_grid, r.fa, in, row(2 * r.switch_b), r.tail);
-                    else launch_finish<false>(dev, S, r.fin_grid, r.fa, in, row(2 * r.switch_b), r.tail);
-                    end_timed(S, dev->stream);
-                    IGX_CC(hipGetLastError());
-                }
-                r.fin_ev = slot_event(S);
-                IGX_CC(hipEventRecord(r.fin_ev, dev->stream));
-                r.tail_queued = true;
-                progress = true;
+            dev->next_slot ^= 1;
+            r.started = true;
+            r.slot = k;
+            r.fa = pl.fa;
+            r.fa.iter = pl.iteration + r.it0;
+            r.fa.chunk_iters = std::min(pl.iters_per_chunk, pl.count - r.it0);
+            r.chunk_pixels = (int)std::min<long long>(pl.chunk_pixels_max, pl.local_pixels - r.px0);
+            r.fa.chunk_pixel0 = (int)r.px0;
+            r.fa.chunk_pixels = r.chunk_pixels;
+            r.n = (long long)r.chunk_pixels * pl.spi * r.fa.chunk_iters;
+            r.live = r.n;
+            // tail threshold: as the sequential schedule (render_impl)
+            const long long fin_lanes = (long long)pl.fin_bpc * dev->num_cus * BLOCK / (pl.pairs ? 2 : 1);
+            const int64_t topt = r.last_of_plan && dev->tail_last_opt >= 0 ? dev->tail_last_opt : dev->tail_opt;
+            r.tail = topt >= 0 ? (int)std::min<int64_t>(topt, 1 << 30) : (int)std::max<long long>(32768, std::min(r.n / 64, fin_lanes));
+            S.tail = r.tail;
+            S.camera = valid_pixels_in_chunk(r.fa) * pl.spi * r.fa.chunk_iters;
+            S.n0 = r.n;
+            S.split = false;
+            S.bounce_ev.clear();
+            S.launched = 0;
+            r.ext_grid = grid_for(dev, r.n, pl.ext_bpc);
+            r.sh_grid = grid_for(dev, r.n, pl.sh_bpc);
+            r.fin_grid = grid_for(dev, std::min<long long>(r.n, r.tail) * (pl.pairs ? 2 : 1), pl.fin_bpc);
+            r.fuse_gen = dev->fuse_generate && r.n > r.tail;
+            use_slot(r);
+            IGX_CC(hipMemsetAsync(S.ctr, 0, (size_t)(2 * pl.max_bounces + 4) * CROW * sizeof(int), dev->stream));
+            if (dev->dynamic_opt)
+                IGX_CC(hipMemsetAsync(S.ctr + (size_t)WORK_ROW0 * CROW, 0, (size_t)4 * pl.max_bounces * CROW * sizeof(int), dev->stream));
+            if (!r.fuse_gen) {
+                begin_timed(S, 2, -1, dev->stream);
+                hipLaunchKernelGGL(k_generate, dim3(grid_for(dev, r.n, 8)), dim3(BLOCK), 0, dev->stream, r.fa, dev->sv, S.pa, S.L, S.ctr);
+                end_timed(S, dev->stream);
+                IGX_CC(hipGetLastError());
             }
             restore();
+            if (r.n <= r.tail) { // the whole chunk is one tail pass
+                r.switch_b = 0;
+                r.loop_done = true;
+            }
+            progress = true;
         }
-        // resolves strictly in chunk order on the tail stream
-        while (!inflight.empty() && inflight.front().tail_queued) {
-            Run& r = inflight.front();
+    }
+    // advance every chunk's bounce loop as far as its lagged counts allow
+    for (SchedItem& r : items) {
+        if (r.clear || !r.started || r.tail_queued) continue;
+        Slot& S = dev->slots[r.slot];
+        const ChunkPlan& pl = *r.plan;
+        const int max_bounces = pl.max_bounces;
+        int* const cnt = S.ctr;
+        auto row = [&](int rr) { return cnt + (size_t)rr * CROW; };
+        use_slot(r);
+        while (!r.loop_done) {
+            if (r.b < max_bounces) {
+                if (r.b >= 2) {
+                    const hipError_t q = hipEventQuery(S.bounce_ev[r.b - 2]);
+                    if (q == hipErrorNotReady) break;
+                    IGX_CC(q);
+                    r.live = row_total(S, 2 * (r.b - 1));
+                    if (r.live <= r.tail) {
+                        r.switch_b = r.b - 1;
+                        r.loop_done = true;
+                        break;
+                    }
+                }
+                const int b = r.b;
+                PathBuf in = (b & 1) ? S.pb : S.pa, out = (b & 1) ? S.pa : S.pb;
+                KernelCounters kc{row(2 * b), row(2 * (b + 1)), row(2 * b + 1), dev->dstats, row(WORK_ROW0 + 4 * b)};
+                begin_timed(S, 0, b, dev->stream);
+                FrameArgs fb = r.fa;
+                fb.gen_n = r.fuse_gen && b == 0 ? (int)r.n : 0;
+                if (inst) launch_extend<true>(dev, S, r.ext_grid, fb, in, out, kc, r.tail);
+                else launch_extend<false>(dev, S, r.ext_grid, fb, in, out, kc, r.tail);
+                end_timed(S, dev->stream);
+                begin_timed(S, 1, b, dev->stream);
+                int* const sh_work =
+                    (dev->dynamic_opt & (use_refill(dev) ? DYN_REFILL_SHADOW : DYN_SHADOW)) ? row(WORK_ROW0 + 4 * b + 2) : nullptr;
+                if (inst) launch_shadow<true>(dev, S, r.sh_grid, row(2 * b + 1), sh_work, dev->stream);
+                else launch_shadow<false>(dev, S, r.sh_grid, row(2 * b + 1), sh_work, dev->stream);
+                end_timed(S, dev->stream);
+                IGX_CC(hipGetLastError());
+                IGX_CC(hipMemcpyAsync(S.pinned + (size_t)(2 * b + 1) * CROW, row(2 * b + 1), 2 * CROW * sizeof(int),
+                                      hipMemcpyDeviceToHost, dev->stream));
+                hipEvent_t e = slot_event(S);
+                IGX_CC(hipEventRecord(e, dev->stream));
+                S.bounce_ev.push_back(e);
+                ++S.launched;
+                ++r.b;
+                progress = true;
+            } else {
+                // every bounce queued: the counts are known once the last one completed
+                const hipError_t q = hipEventQuery(S.bounce_ev.back());
+                if (q == hipErrorNotReady) break;
+                IGX_CC(q);
+                r.switch_b = max_bounces;
+                for (int b = 1; b <= max_bounces; ++b)
+                    if (row_total(S, 2 * b) <= r.tail) {
+                        r.switch_b = b;
+                        break;
+                    }
+                r.loop_done = true;
+            }
+        }
+        if (r.loop_done && !r.tail_queued) {
+            S.switch_bounce = r.switch_b;
+            if (r.switch_b < MAX_BOUNCES) {
+                PathBuf in = (r.switch_b & 1) ? S.pb : S.pa;
+                begin_timed(S, 4, r.switch_b, dev->stream);
+                if (inst) launch_finish<true>(dev, S, r.fin_grid, r.fa, in, row(2 * r.switch_b), r.tail);
+                else launch_finish<false>(dev, S, r.fin_grid, r.fa, in, row(2 * r.switch_b), r.tail);
+                end_timed(S, dev->stream);
+                IGX_CC(hipGetLastError());
+            }
+            r.fin_ev = slot_event(S);
+            IGX_CC(hipEventRecord(r.fin_ev, dev->stream));
+            r.tail_queued = true;
+            progress = true;
+        }
+        restore();
+    }
+    // resolves and framebuffer clears strictly in submission order on the tail stream
+    while (!items.empty() && (items.front().clear || items.front().tail_queued)) {
+        SchedItem& r = items.front();
+        if (r.clear) {
+            IGX_CC(hipMemsetAsync(dev->fb, 0, dev->fb_count * sizeof(float), tail0));
+        } else {
             Slot& S = dev->slots[r.slot];
             IGX_CC(hipStreamWaitEvent(tail0, r.fin_ev, 0));
             begin_timed(S, 3, -1, tail0);
-            hipLaunchKernelGGL(k_resolve, dim3((r.chunk_pixels + 63) / 64), dim3(64 * RES_G), 0, tail0, r.fa, S.L, dev->fb, width);
+            hipLaunchKernelGGL(k_resolve, dim3((r.chunk_pixels + 63) / 64), dim3(64 * RES_G), 0, tail0, r.fa, S.L, dev->fb, r.plan->width);
             end_timed(S, tail0);
             IGX_CC(hipGetLastError());
             IGX_CC(hipEventRecord(S.done, tail0));
             S.pending = true;
-            inflight.pop_front();
-            progress = true;
         }
-        if (!progress) std::this_thread::yield();
+        items.pop_front();
+        progress = true;
     }
 #undef IGX_CC
     restore();
-    dev->iteration_count += count;
-    dev->stats.iterations += count;
-    dev->stats.ms_render += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     return IGX_OK;
+}
+
+// Runs the scheduler in the calling thread until everything queued is resolved.
+static igx_status run_scheduler(igx_device* dev, ChunkScheduler& sched) {
+    while (!sched.empty()) {
+        bool progress = false;
+        igx_status st = sched.step(dev, progress);
+        if (st != IGX_OK) {
+            sched.items.clear();
+            return st;
+        }
+        if (!progress) std::this_thread::yield();
+    }
+    return IGX_OK;
+}
+
+static void async_worker(igx_device* dev) {
+    AsyncRender& a = *dev->async;
+    (void)hipSetDevice(dev->hip_device);
+    for (;;) {
+        {
+            std::unique_lock<std::mutex> lk(a.m);
+            while (!a.jobs.empty()) {
+                if (a.jobs.front().first) a.sched.add_clear();
+                else a.sched.add(a.jobs.front().second);
+                a.jobs.pop_front();
+            }
+            if (a.sched.empty()) {
+                a.idle = true;
+                a.cv_idle.notify_all();
+                if (a.stop) return;
+                a.cv.wait(lk, [&] { return a.stop || !a.jobs.empty(); });
+                if (a.jobs.empty() && a.stop) return;
+                a.idle = false;
+                continue;
+            }
+        }
+        bool progress = false;
+        igx_status st = a.sched.step(dev, progress);
+        if (st != IGX_OK) {
+            std::lock_guard<std::mutex> lk(a.m);
+            a.sched.items.clear();
+            a.jobs.clear();
+            if (a.err == IGX_OK) a.err = st;
+            continue;
+        }
+        if (!progress) std::this_thread::yield();
+    }
+}
+
+// Waits until the worker has queued (on the GPU) everything submitted and
+// returns its first error, if any.  No-op without a worker.
+igx_status wait_idle(igx_device* dev) {
+    if (!dev->async) return IGX_OK;
+    AsyncRender& a = *dev->async;
+    std::unique_lock<std::mutex> lk(a.m);
+    a.cv_idle.wait(lk, [&] { return a.idle && a.jobs.empty(); });
+    igx_status st = a.err;
+    a.err = IGX_OK;
+    return st;
+}
+
+void stop_async(igx_device* dev) {
+    if (!dev->async) return;
+    {
+        std::lock_guard<std::mutex> lk(dev->async->m);
+        dev->async->stop = true;
+    }
+    dev->async->cv.notify_all();
+    if (dev->async->th.joinable()) dev->async->th.join();
+    delete dev->async;
+    dev->async = nullptr;
+}
+
+static void submit_async(igx_device* dev, bool clear, std::shared_ptr<const ChunkPlan> plan) {
+    if (!dev->async) {
+        dev->async = new AsyncRender();
+        dev->async->th = std::thread(async_worker, dev);
+    }
+    {
+        std::lock_guard<std::mutex> lk(dev->async->m);
+        dev->async->jobs.push_back({clear, std::move(plan)});
+        dev->async->idle = false;
+    }
+    dev->async->cv.notify_all();
 }
 
 // Render `count` consecutive iterations (p->iteration, p->iteration + 1, ...).
@@ -3401,6 +3558,16 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
     if (p->tile_size > 0 && (p->tile_stride < 1 || p->tile_offset < 0 || p->tile_offset >= p->tile_stride))
         return fail(dev, IGX_ERR_INVALID_ARGUMENT, "invalid tile sharding parameters");
     if (list_mode && p->tile_size > 0) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "ray-list mode cannot be tile-sharded");
+    // schedule: concurrent chunks on the fused schedule with two slots, queued
+    // for the handle's worker thread when async_render is on; anything else
+    // runs here once the worker has drained
+    const bool split = use_split(dev);
+    const bool conc = !list_mode && !split && dev->stream_slots == 2 && dev->concurrent_opt;
+    const bool async = conc && dev->async_opt;
+    if (!async) {
+        igx_status w = wait_idle(dev);
+        if (w != IGX_OK) return w;
+    }
 
     // framebuffer (resize clears, as Device::resize)
     size_t fbc = (size_t)width * height * 3;
@@ -3416,7 +3583,8 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
         dev->fb_count = fbc;
         dev->iteration_count = 0;
     }
-    setup_camera(dev, width, height);
+    const DevCamera cam = make_camera(dev, width, height);
+    if (!async) dev->sv.cam = cam; // the worker sets each chunk's camera itself
 
     FrameArgs fa{};
     fa.width = width;
@@ -3471,7 +3639,6 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
     // (tools/sweep_frame.py).  Per path and slot: two path buffers (56 B a
     // record; twice that with the class-C region), shadow ray 48 B, hit
     // record 20 B (split schedule), radiance 16 B.
-    const bool split = use_split(dev);
     if (split && fa.classify == 4) fa.classify = 3; // hit records have no class-C region
     const long long path_slot_bytes = 2 * 56 * (fa.classify == 4 ? 2 : 1) + 48 + (split ? 20 : 0) + 16;
     const long long slot_budget =
@@ -3508,9 +3675,36 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
     const int fin_bpc = inst ? finish_blocks_per_cu<true>(sd, ldsb, tree_bytes(dev, dev->tree_fin), pairs)
                              : finish_blocks_per_cu<false>(sd, ldsb, tree_bytes(dev, dev->tree_fin), pairs);
 
-    if (dev->concurrent_opt && !split && dev->stream_slots == 2)
-        return render_chunks_concurrent(dev, p, fa, count, local_pixels, iters_per_chunk, chunk_pixels_max, slot_cap,
-                                        max_bounces, ext_bpc, sh_bpc, fin_bpc, pairs, t_start);
+    if (conc) {
+        auto plan = std::make_shared<ChunkPlan>();
+        plan->fa = fa;
+        plan->cam = cam;
+        plan->iteration = p->iteration;
+        plan->spi = p->spi;
+        plan->count = count;
+        plan->width = width;
+        plan->local_pixels = local_pixels;
+        plan->chunk_pixels_max = chunk_pixels_max;
+        plan->iters_per_chunk = iters_per_chunk;
+        plan->slot_cap = slot_cap;
+        plan->max_bounces = max_bounces;
+        plan->ext_bpc = ext_bpc;
+        plan->sh_bpc = sh_bpc;
+        plan->fin_bpc = fin_bpc;
+        plan->pairs = pairs;
+        dev->iteration_count += count;
+        dev->stats.iterations += count;
+        if (async) {
+            submit_async(dev, false, std::move(plan));
+        } else {
+            ChunkScheduler sched;
+            sched.add(plan);
+            igx_status st = run_scheduler(dev, sched);
+            if (st != IGX_OK) return st;
+        }
+        dev->stats.ms_render += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+        return IGX_OK;
+    }
 
     for (int it0 = 0; it0 < count; it0 += iters_per_chunk)
     for (long long px0 = 0; px0 < local_pixels; px0 += chunk_pixels_max) {
@@ -3739,6 +3933,11 @@ extern "C" igx_status igx_pack_tiles(igx_device* dev, const igx_render_params* p
 
 extern "C" igx_status igx_clear(igx_device* dev) {
     if (!dev) return IGX_ERR_INVALID_ARGUMENT;
+    if (dev->async) { // ordered behind the queued renders' resolves by the worker
+        submit_async(dev, true, nullptr);
+        dev->iteration_count = 0;
+        return IGX_OK;
+    }
     if (dev->fb) {
         HIPCHK(hipSetDevice(dev->hip_device));
         // resolves of queued chunks land on the tail stream; clear behind them

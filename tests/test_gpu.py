@@ -723,10 +723,11 @@ def test_concurrent_chunks_bit_identical(root, diamond_path, start_pct):
     sc = ignis_amd.Scene.from_file(diamond_path)
     w, h, spi, iters = 160, 120, 4, 6
     films = []
-    for conc in (0, 1):
+    for conc, asy in ((0, 0), (1, 0), (1, 1)):
         for tile in (None, (40, 1, 3)):
             d = ignis_amd.Device(0)
             d.upload(sc)
+            d.set_option("async_render", asy)
             # chunks of at most 65536 paths: a tile share's two iterations, or part
             # of one iteration of the whole film; a low tail threshold keeps each
             # chunk in its wavefront bounce loop for several bounces
@@ -743,9 +744,44 @@ def test_concurrent_chunks_bit_identical(root, diamond_path, start_pct):
             assert n == iters
             films.append(fb)
             d.close()
-    np.testing.assert_array_equal(films[0], films[2])
-    np.testing.assert_array_equal(films[1], films[3])
+    for k in (2, 4):
+        np.testing.assert_array_equal(films[0], films[k])
+        np.testing.assert_array_equal(films[1], films[k + 1])
     assert films[0].sum() > 0
+
+
+def test_async_render_queue_matches_synchronous(diamond_path):
+    """async_render: clear / render calls only queue work for the handle's
+    worker thread, which overlaps consecutive frames; the frame left in the
+    framebuffer after several queued clear + render pairs, and the statistics,
+    equal a synchronous render of that frame."""
+    sc = ignis_amd.Scene.from_file(diamond_path)
+    w, h, spi = 200, 150, 8
+    p = ignis_amd.RenderParams()
+    p.width, p.height, p.spi = w, h, spi
+    films, rays = [], []
+    for asy in (0, 1):
+        d = ignis_amd.Device(0)
+        d.upload(sc)
+        d.set_option("async_render", asy)
+        d.set_option("capacity", 65536)
+        d.set_option("tail_threshold", 4096)
+        for it in range(3):  # three frames back to back; the last one stays
+            d.clear()
+            p.iteration = it * 4
+            d.render_iterations(p, 4)
+        d.reset_stats()
+        d.clear()
+        p.iteration = 12
+        d.render_iterations(p, 4)
+        fb, n = d.framebuffer(w * h * 3)
+        st = d.stats()
+        assert n == 4
+        films.append(fb)
+        rays.append((st["camera_rays"], st["bounce_rays"], st["shadow_rays"]))
+        d.close()
+    np.testing.assert_array_equal(films[0], films[1])
+    assert rays[0] == rays[1]
 
 
 def test_tile_sharding_equals_full_render(device, diamond_path):
