@@ -68,7 +68,7 @@ def parse():
 MALL_BYTES = 128 << 20
 # N > 1: a rank holds two handles, each with ONE stream slot (option
 # stream_slots) sized to the rank's share of a frame when that is one chunk
-# (the diamond: N = 2: 128 M paths = 25 GB per handle, 8: 6.3 GB), two
+# (the diamond: N = 2: 128 M paths = 37 GB per handle, 8: 9.3 GB), two
 # otherwise (rank_stream_slots).  A budget below the share
 # splits a frame into chunks and costs time (slot_budget_mb 20000 at N = 2:
 # 67.3 vs 55.2 ms per rank frame, profiles/r03_exp_classes_regroup_slots.log);
@@ -426,6 +426,9 @@ class RankFrames:
         # capacity are traced as one wavefront
         d.render_iterations(self.params(0), self.iters)
         if self.n > 1:
+            # async_render: return once this frame's chunks are in their late
+            # bounces, so the next frame (the other handle) overlaps only those
+            d.wait_ready()
             if self.pending:
                 e = self.pending.pop()
                 self._pack(e)

@@ -1586,8 +1586,9 @@ struct igx_device {
     // alternate frames, and a rank's share of a frame is one chunk, so there
     // one slot per handle loses nothing: bench.py sets 1 at N > 1
     int stream_slots = 2;
-    // option "concurrent_chunks" (0/1): the two slots' chunks run their
-    // bounces concurrently, each on its own stream (render_chunks_concurrent)
+    // option "concurrent_chunks" (0/1): the fused schedule's chunks run
+    // through ChunkScheduler, the two slots' chunks concurrently, each on its
+    // own stream (one slot: a chunk still waits for the slot's previous one)
     int concurrent_opt = 1;
     int concurrent_start_pct = 10; // option "concurrent_start_pct": a chunk starts once the running one is down to this share of its paths
     // LDS treelet (stage_treelet) on global-table scenes: nodes staged per
@@ -1703,6 +1704,7 @@ struct igx_device {
 };
 // the worker has queued everything submitted; its first error (part 0)
 igx_status wait_idle(igx_device* dev);
+igx_status wait_ready(igx_device* dev);
 void stop_async(igx_device* dev);
 
 namespace igxh {
@@ -2440,6 +2442,11 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
         dev->leaf_size = (int)value;
     } else return fail(dev, IGX_ERR_INVALID_ARGUMENT, "unknown option '" + k + "'");
     return IGX_OK;
+}
+
+extern "C" igx_status igx_wait_ready(igx_device* dev) {
+    if (!dev) return IGX_ERR_INVALID_ARGUMENT;
+    return wait_ready(dev);
 }
 
 extern "C" igx_status igx_synchronize(igx_device* dev) {
@@ -3230,6 +3237,15 @@ struct ChunkScheduler {
         items.push_back(s);
     }
     igx_status step(igx_device* dev, bool& progress);
+    // every chunk has started and is down to concurrent_start_pct % of its paths (or done)
+    bool all_late(int pct) const {
+        for (const SchedItem& r : items) {
+            if (r.clear) continue;
+            if (!r.started) return false;
+            if (!r.loop_done && r.live * 100 > (long long)pct * r.n) return false;
+        }
+        return true;
+    }
 };
 struct AsyncRender {
     std::thread th;
@@ -3237,6 +3253,7 @@ struct AsyncRender {
     std::condition_variable cv, cv_idle;
     std::deque<std::pair<bool, std::shared_ptr<const ChunkPlan>>> jobs; // (clear, plan)
     bool stop = false, idle = true;
+    bool late = true; // every chunk submitted has started and is in its late bounces (igx_wait_ready)
     igx_status err = IGX_OK;
     ChunkScheduler sched; // the worker's
 };
@@ -3295,7 +3312,7 @@ igx_status ChunkScheduler::step(igx_device* dev, bool& progress) {
         if (!r.loop_done && r.live * 100 > (long long)dev->concurrent_start_pct * r.n) late = false;
     }
     if (nx && late) {
-        const int k = dev->next_slot;
+        const int k = dev->stream_slots == 1 ? 0 : dev->next_slot;
         Slot& S = dev->slots[k];
         bool busy = false;
         for (const SchedItem& r : items) busy = busy || (!r.clear && r.started && r.slot == k);
@@ -3312,7 +3329,7 @@ igx_status ChunkScheduler::step(igx_device* dev, bool& progress) {
                 restore();
                 return st;
             }
-            dev->next_slot ^= 1;
+            if (dev->stream_slots == 2) dev->next_slot ^= 1;
             r.started = true;
             r.slot = k;
             r.fa = pl.fa;
@@ -3499,8 +3516,28 @@ static void async_worker(igx_device* dev) {
             if (a.err == IGX_OK) a.err = st;
             continue;
         }
-        if (!progress) std::this_thread::yield();
+        if (progress) {
+            const bool late = a.sched.all_late(dev->concurrent_start_pct);
+            std::lock_guard<std::mutex> lk(a.m);
+            a.late = late && a.jobs.empty();
+            if (a.late) a.cv_idle.notify_all();
+        } else {
+            std::this_thread::yield();
+        }
     }
+}
+
+// Waits until every chunk submitted has started and is in its late bounces
+// (down to concurrent_start_pct % of its paths), the point from which work on
+// another handle of the same GPU overlaps it without slowing its heavy
+// bounces (bench.py: frame k + 1 on the other handle); or until the queue has
+// drained.  No-op without a worker.
+igx_status wait_ready(igx_device* dev) {
+    if (!dev->async) return IGX_OK;
+    AsyncRender& a = *dev->async;
+    std::unique_lock<std::mutex> lk(a.m);
+    a.cv_idle.wait(lk, [&] { return (a.idle && a.jobs.empty()) || (a.late && a.jobs.empty()); });
+    return a.err;
 }
 
 // Waits until the worker has queued (on the GPU) everything submitted and
@@ -3536,6 +3573,7 @@ static void submit_async(igx_device* dev, bool clear, std::shared_ptr<const Chun
         std::lock_guard<std::mutex> lk(dev->async->m);
         dev->async->jobs.push_back({clear, std::move(plan)});
         dev->async->idle = false;
+        dev->async->late = false;
     }
     dev->async->cv.notify_all();
 }
@@ -3562,7 +3600,7 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
     // for the handle's worker thread when async_render is on; anything else
     // runs here once the worker has drained
     const bool split = use_split(dev);
-    const bool conc = !list_mode && !split && dev->stream_slots == 2 && dev->concurrent_opt;
+    const bool conc = !list_mode && !split && dev->concurrent_opt;
     const bool async = conc && dev->async_opt;
     if (!async) {
         igx_status w = wait_idle(dev);

@@ -294,6 +294,10 @@ class Device:
     def synchronize(self):
         self._check(self._lib.igx_synchronize(self._h))
 
+    def wait_ready(self):
+        """igx_wait_ready: the handle's queued chunks are in their late bounces."""
+        self._check(self._lib.igx_wait_ready(self._h))
+
     def stats(self):
         s = Stats()
         self._check(self._lib.igx_get_stats(self._h, C.byref(s)))

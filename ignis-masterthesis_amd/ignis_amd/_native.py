@@ -143,7 +143,7 @@ EXPORTED_SYMBOLS = [
     "igx_scene_from_database", "igx_scene_find_material", "igx_scene_entity_name",
     "igx_create", "igx_destroy", "igx_last_error", "igx_version", "igx_set_option", "igx_upload_scene",
     "igx_render", "igx_get_framebuffer", "igx_framebuffer_device_ptr", "igx_pack_tiles", "igx_clear",
-    "igx_get_stats", "igx_reset_stats", "igx_trace_hits", "igx_trace_occlusion", "igx_synchronize",
+    "igx_get_stats", "igx_reset_stats", "igx_trace_hits", "igx_trace_occlusion", "igx_synchronize", "igx_wait_ready",
     "igx_render_iterations", "igx_objscene_create", "igx_objscene_free", "igx_objscene_add",
     "igx_objscene_set_property", "igx_scene_from_objects", "igx_set_camera",
 ]
@@ -202,6 +202,7 @@ def lib():
     L.igx_pack_tiles.argtypes = [vp, C.POINTER(RenderParams), C.c_void_p, C.c_size_t]
     L.igx_clear.argtypes = [vp]
     L.igx_synchronize.argtypes = [vp]
+    L.igx_wait_ready.argtypes = [vp]
     L.igx_get_stats.argtypes = [vp, C.POINTER(Stats)]
     L.igx_reset_stats.argtypes = [vp]
     L.igx_trace_hits.argtypes = [vp, C.POINTER(C.c_float), C.c_int32, C.c_uint32, C.POINTER(C.c_int32),
@@ -209,7 +210,7 @@ def lib():
     L.igx_trace_occlusion.argtypes = [vp, C.POINTER(C.c_float), C.c_int32, C.c_uint32, C.POINTER(C.c_int32)]
     for name in ["igx_create", "igx_destroy", "igx_set_option", "igx_upload_scene", "igx_render", "igx_render_iterations",
                  "igx_get_framebuffer", "igx_framebuffer_device_ptr", "igx_pack_tiles", "igx_clear",
-                 "igx_synchronize", "igx_get_stats", "igx_reset_stats", "igx_trace_hits", "igx_trace_occlusion"]:
+                 "igx_synchronize", "igx_wait_ready", "igx_get_stats", "igx_reset_stats", "igx_trace_hits", "igx_trace_occlusion"]:
         getattr(L, name).restype = C.c_int
     _lib = L
     return L

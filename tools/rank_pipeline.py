@@ -21,6 +21,7 @@ if len(sys.argv) > 6:
 devs = [ignis_amd.Device(0), ignis_amd.Device(0)]
 slots = int(sys.argv[4]) if len(sys.argv) > 4 else 2
 extra = json.loads(os.environ.get("IGX_PIPE_OPTS", "{}"))
+READY = os.environ.get("IGX_PIPE_READY") == "1"
 for d in devs:
     d.upload(scene)
     d.set_option("stream_slots", slots)
@@ -39,6 +40,8 @@ def run(handles):
         d = handles[k % len(handles)]
         d.clear()
         d.render_iterations(p, ITERS)
+        if READY and len(handles) > 1:
+            d.wait_ready()  # bench.py's N > 1 order: the next frame starts in this one's late bounces
         if pending is not None:
             pending.synchronize()
         pending = d
@@ -80,5 +83,5 @@ if os.environ.get("IGX_PIPE_THREADS"):
 
 for handles in (devs[:1], devs, devs[:1], devs):
     run(handles)
-    print(json.dumps({"n": n, "stream_slots": slots, "opts": extra, "handles": len(handles), "ms_per_frame": round(run(handles) * 1e3, 2),
+    print(json.dumps({"n": n, "stream_slots": slots, "opts": extra, "ready": READY, "handles": len(handles), "ms_per_frame": round(run(handles) * 1e3, 2),
                       "slot_gb_per_handle": [round(d.stats()["slot_bytes"] / 1e9, 2) for d in handles]}), flush=True)
