@@ -3,7 +3,7 @@
 # diamond N = 8 rank share (one 32 M-path chunk) at capacity 16 M / 8 M with
 # two slots; diamond and S-deep frames at N = 1 with smaller chunks.
 set -o pipefail
-mkdir -p gpurun_out/r04f
+mkdir -p gpurun_out/r04f; rm -f gpurun_out/r04f/*
 export TMPDIR=/tmp
 O=gpurun_out/r04f
 for c in 0 16000000 8000000; do
