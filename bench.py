@@ -74,6 +74,10 @@ MALL_BYTES = 128 << 20
 # 67.3 vs 55.2 ms per rank frame, profiles/r03_exp_classes_regroup_slots.log);
 # IGX_SLOT_BUDGET_MB caps it anyway (0 = auto)
 SLOT_BUDGET_MB = int(os.environ.get("IGX_SLOT_BUDGET_MB", "0"))
+# the rehearsal puts every rank on GPU 0: each rank's two handles then get an
+# equal share of half the device memory for their stream slots
+def rehearsal_slot_budget_mb(torch, n):
+    return max(256, int(torch.cuda.get_device_properties(0).total_memory * 0.5 / (2 * n) / 2**20))
 
 
 # paths of one chunk (igx_device.hip MAX_CHUNK_PATHS)
@@ -398,7 +402,8 @@ class RankFrames:
             # chunks keeps two, so consecutive chunks of a frame overlap as at N = 1
             for d in self.devs:
                 d.set_option("stream_slots", rank_stream_slots(W, H, self.tile, n, spi, iters))
-                d.set_option("slot_budget_mb", SLOT_BUDGET_MB)
+                d.set_option("slot_budget_mb", SLOT_BUDGET_MB if SLOT_BUDGET_MB or comm != "cpu"
+                             else rehearsal_slot_budget_mb(torch, n))
 
     def params(self, it=0):
         p = self.ig.RenderParams()
@@ -551,7 +556,29 @@ def sharded_line(ignis_amd, torch, dist, path, size, spi, spp, rank, n, gpu, com
     the headline frame, with the per-rank breakdown and the bit-exact check."""
     scene = ignis_amd.Scene.from_file(path)
     iters = max(1, math.ceil(spp / spi))
-    rf = RankFrames(ignis_amd, torch, dist, scene, size, size, spi, iters, rank, n, gpu, comm)
+    # pre-flight before any collective of the line: every handle of every rank
+    # renders its share once (allocating its buffers), and the ranks agree that
+    # all did -- a rank failing here (e.g. out of memory) must not leave the
+    # others waiting in a gather or barrier it never reaches
+    rf, err = None, None
+    try:
+        rf = RankFrames(ignis_amd, torch, dist, scene, size, size, spi, iters, rank, n, gpu, comm)
+        for d in rf.devs:
+            d.clear()
+            d.render_iterations(rf.params(0), iters)
+            d.synchronize()
+    except Exception as e:
+        err = f"rank {rank}: {type(e).__name__}: {e}"
+    if dist:
+        flag = torch.tensor([1.0 if err else 0.0], dtype=torch.float64, device=comm)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        failed = flag.item() > 0
+    else:
+        failed = err is not None
+    if failed:
+        if rf is not None:
+            rf.close()
+        return {"error": err or "another rank failed its pre-flight frame"}
     m = rf.measure(steps, 1)
     line = {"workload": f"{os.path.basename(path)} {size}x{size}, {iters * spi} spp = {iters} iterations x spi {spi}, "
                         "path tracer, seed 0 (BASELINE config 5 stand-in, SURVEY.md §8d)",

@@ -166,3 +166,69 @@ def test_rank_stream_slots_by_share():
     # exactly one chunk: 2^27 paths
     assert bench.rank_stream_slots(4096, 4096, 4096, 1, 8, 1) == 1
     assert bench.rank_stream_slots(4096, 4096, 4096, 1, 8, 2) == 2
+
+
+def _load_bench():
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    return bench
+
+
+def _preflight_worker(rank, world, port, fail_rank, q):
+    """bench.sharded_line with stand-ins for the device: rank `fail_rank`
+    fails while rendering its pre-flight frame (as an out-of-memory render
+    does); every rank must return the error line instead of entering the
+    line's gathers and barriers."""
+    import types
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    bench = _load_bench()
+
+    class Dev:
+        def clear(self):
+            pass
+
+        def render_iterations(self, p, n):
+            if rank == fail_rank:
+                raise RuntimeError("hipMalloc: out of memory")
+
+        def synchronize(self):
+            pass
+
+    class Frames:
+        def __init__(self, *a):
+            self.devs = [Dev(), Dev()]
+
+        def params(self, it=0):
+            return None
+
+        def measure(self, steps, warmup):
+            raise AssertionError("measure reached after a failed pre-flight")
+
+        def close(self):
+            self.devs = []
+
+    bench.RankFrames = Frames
+    ig = types.SimpleNamespace(Scene=types.SimpleNamespace(from_file=lambda path: None))
+    line = bench.sharded_line(ig, torch, dist, "s_deep.json", 64, 8, 64, rank, world, 0, "cpu", 1, True)
+    q.put((rank, line))
+    dist.barrier()  # the ranks still agree on the next collective
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_config5_preflight_failure_does_not_hang():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_preflight_worker, args=(r, 2, port, 1, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[1]["error"].startswith("rank 1: RuntimeError")
+    assert res[0]["error"] == "another rank failed its pre-flight frame"
