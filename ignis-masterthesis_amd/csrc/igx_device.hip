@@ -2836,7 +2836,10 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
             const ShapeDev& sd = sdev[en.shape];
             for (int r = 0; r < 3; ++r)
                 inst.push_back(make_float4(en.to_local[r * 4 + 0], en.to_local[r * 4 + 1], en.to_local[r * 4 + 2], en.to_local[r * 4 + 3]));
-            int4 info = make_int4((int)e, sd.type, sd.type == 1 ? sd.idx_off_or_sphere : sd.root, (int)en.flags);
+            static const float kIdentity[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+            const bool identity = sd.type == 0 && std::equal(en.to_local, en.to_local + 12, kIdentity);
+            int4 info = make_int4((int)e, sd.type, sd.type == 1 ? sd.idx_off_or_sphere : sd.root,
+                                  (int)((en.flags & ~INST_IDENTITY) | (identity ? INST_IDENTITY : 0u)));
             float4 fi;
             std::memcpy(&fi, &info, 16);
             inst.push_back(fi);

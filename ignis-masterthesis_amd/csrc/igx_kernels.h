@@ -121,6 +121,13 @@ __device__ __forceinline__ bool first_active_lane() {
 
 // Ray flags (traversal/ray.art:19-23)
 constexpr uint32_t RAY_CAMERA = 0x1, RAY_LIGHT = 0x2, RAY_BOUNCE = 0x4, RAY_SHADOW = 0x8, RAY_TYPE_MASK = 0xF;
+#ifndef IGX_IDENTITY_INSTANCES
+#define IGX_IDENTITY_INSTANCES 1
+#endif
+// instance record flag (info.w, next to the visibility bits): the trimesh
+// instance's to_local is the identity, so its entity-space ray is the world
+// ray (instance_test skips the transform; set by igx_upload_scene)
+constexpr uint32_t INST_IDENTITY = 1u << 30;
 
 // ---------------------------------------------------------------------------
 // Two-level traversal: TLAS (entities) -> BLAS (triangles) or analytic sphere.
@@ -614,6 +621,15 @@ __device__ __forceinline__ bool instance_test(const SceneView& sv, Trav& t, int 
     int4 info = *reinterpret_cast<const int4*>(ip + 3);
     uint32_t ef = (uint32_t)info.w;
     if ((t.rflags & RAY_TYPE_MASK) != ((t.rflags & ef) & RAY_TYPE_MASK)) return false; // check_ray_visibility
+    if (IGX_IDENTITY_INSTANCES && (ef & INST_IDENTITY)) {
+        // identity to_local: t.lo / t.ld / t.idir / t.iorg already hold the
+        // world ray of the TLAS walk
+        if (STATS) st.blas++;
+        t.cur_ent = info.x;
+        t.in_blas = true;
+        blas_root = info.z;
+        return true;
+    }
     float4 m0 = ip[0], m1 = ip[1], m2 = ip[2];
     const f3 o = t.o, d = t.d;
     // transform_ray (ray.art:53-59): point and direction, no renormalisation
@@ -828,10 +844,15 @@ __device__ __forceinline__ bool trav_init_enclosed(const SceneView& sv, Trav& t,
     if ((rflags & RAY_TYPE_MASK) != ((rflags & (uint32_t)info.w) & RAY_TYPE_MASK)) return false;
     t.o = o;
     t.d = d;
-    const float4 m0 = ip[0], m1 = ip[1], m2 = ip[2];
-    t.lo = mk(m0.x * o.x + m0.y * o.y + m0.z * o.z + m0.w, m1.x * o.x + m1.y * o.y + m1.z * o.z + m1.w,
-              m2.x * o.x + m2.y * o.y + m2.z * o.z + m2.w);
-    t.ld = mk(m0.x * d.x + m0.y * d.y + m0.z * d.z, m1.x * d.x + m1.y * d.y + m1.z * d.z, m2.x * d.x + m2.y * d.y + m2.z * d.z);
+    if (IGX_IDENTITY_INSTANCES && ((uint32_t)info.w & INST_IDENTITY)) { // as instance_test
+        t.lo = o;
+        t.ld = d;
+    } else {
+        const float4 m0 = ip[0], m1 = ip[1], m2 = ip[2];
+        t.lo = mk(m0.x * o.x + m0.y * o.y + m0.z * o.z + m0.w, m1.x * o.x + m1.y * o.y + m1.z * o.z + m1.w,
+                  m2.x * o.x + m2.y * o.y + m2.z * o.z + m2.w);
+        t.ld = mk(m0.x * d.x + m0.y * d.y + m0.z * d.z, m1.x * d.x + m1.y * d.y + m1.z * d.z, m2.x * d.x + m2.y * d.y + m2.z * d.z);
+    }
     t.idir = mk(safe_rcp(t.ld.x), safe_rcp(t.ld.y), safe_rcp(t.ld.z));
     t.iorg = mk(-(t.lo.x * t.idir.x), -(t.lo.y * t.idir.y), -(t.lo.z * t.idir.z));
     t.tmin = tmin;
