@@ -2837,9 +2837,15 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
             for (int r = 0; r < 3; ++r)
                 inst.push_back(make_float4(en.to_local[r * 4 + 0], en.to_local[r * 4 + 1], en.to_local[r * 4 + 2], en.to_local[r * 4 + 3]));
             static const float kIdentity[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
-            const bool identity = sd.type == 0 && std::equal(en.to_local, en.to_local + 12, kIdentity);
-            int4 info = make_int4((int)e, sd.type, sd.type == 1 ? sd.idx_off_or_sphere : sd.root,
-                                  (int)((en.flags & ~INST_IDENTITY) | (identity ? INST_IDENTITY : 0u)));
+            const float* m = en.to_local;
+            const bool linear_identity = m[0] == 1 && m[1] == 0 && m[2] == 0 && m[4] == 0 && m[5] == 1 && m[6] == 0 &&
+                                         m[8] == 0 && m[9] == 0 && m[10] == 1 && std::isfinite(m[3]) &&
+                                         std::isfinite(m[7]) && std::isfinite(m[11]);
+            const bool identity = sd.type == 0 && std::equal(m, m + 12, kIdentity);
+            const bool translate = sd.type == 0 && !identity && linear_identity;
+            const uint32_t iflags = (en.flags & ~(INST_IDENTITY | INST_TRANSLATE)) | (identity ? INST_IDENTITY : 0u) |
+                                    (translate ? INST_TRANSLATE : 0u);
+            int4 info = make_int4((int)e, sd.type, sd.type == 1 ? sd.idx_off_or_sphere : sd.root, (int)iflags);
             float4 fi;
             std::memcpy(&fi, &info, 16);
             inst.push_back(fi);

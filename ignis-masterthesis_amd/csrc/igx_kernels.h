@@ -128,6 +128,13 @@ constexpr uint32_t RAY_CAMERA = 0x1, RAY_LIGHT = 0x2, RAY_BOUNCE = 0x4, RAY_SHAD
 // instance's to_local is the identity, so its entity-space ray is the world
 // ray (instance_test skips the transform; set by igx_upload_scene)
 constexpr uint32_t INST_IDENTITY = 1u << 30;
+// ... or a pure translation (rows (1 0 0 tx), (0 1 0 ty), (0 0 1 tz)): the
+// entity-space ray is (o + t, d), so its reciprocal direction is the world
+// ray's (IGX_TRANSLATE_INSTANCES)
+#ifndef IGX_TRANSLATE_INSTANCES
+#define IGX_TRANSLATE_INSTANCES 1
+#endif
+constexpr uint32_t INST_TRANSLATE = 1u << 29;
 
 // ---------------------------------------------------------------------------
 // Two-level traversal: TLAS (entities) -> BLAS (triangles) or analytic sphere.
@@ -630,6 +637,16 @@ __device__ __forceinline__ bool instance_test(const SceneView& sv, Trav& t, int 
         blas_root = info.z;
         return true;
     }
+    if (IGX_TRANSLATE_INSTANCES && (ef & INST_TRANSLATE)) {
+        // transform_ray with a translation: ((1*o.x + 0*o.y) + 0*o.z) + tx is o.x + tx
+        if (STATS) st.blas++;
+        t.lo = mk(t.o.x + ip[0].w, t.o.y + ip[1].w, t.o.z + ip[2].w);
+        t.iorg = mk(-(t.lo.x * t.idir.x), -(t.lo.y * t.idir.y), -(t.lo.z * t.idir.z));
+        t.cur_ent = info.x;
+        t.in_blas = true;
+        blas_root = info.z;
+        return true;
+    }
     float4 m0 = ip[0], m1 = ip[1], m2 = ip[2];
     const f3 o = t.o, d = t.d;
     // transform_ray (ray.art:53-59): point and direction, no renormalisation
@@ -846,6 +863,9 @@ __device__ __forceinline__ bool trav_init_enclosed(const SceneView& sv, Trav& t,
     t.d = d;
     if (IGX_IDENTITY_INSTANCES && ((uint32_t)info.w & INST_IDENTITY)) { // as instance_test
         t.lo = o;
+        t.ld = d;
+    } else if (IGX_TRANSLATE_INSTANCES && ((uint32_t)info.w & INST_TRANSLATE)) {
+        t.lo = mk(o.x + ip[0].w, o.y + ip[1].w, o.z + ip[2].w);
         t.ld = d;
     } else {
         const float4 m0 = ip[0], m1 = ip[1], m2 = ip[2];
