@@ -622,7 +622,11 @@ def main():
                          f"(torch.distributed.run --nproc-per-node {args.gpus}) or drop the launcher")
     if os.environ.get("IGX_BENCH_LAUNCH_PROBE") == "1":
         # launcher test hook (tests/test_bench_launch.py): report the rank layout, touch no GPU
-        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "world": world, "gpus": args.gpus}), flush=True)
+        # one write(2) of the whole line: the ranks share the pipe, and a line
+        # written in pieces can interleave with another rank's
+        sys.stdout.flush()
+        os.write(sys.stdout.fileno(), (json.dumps({"rank": int(os.environ.get("RANK", "0")), "world": world,
+                                                   "gpus": args.gpus}) + "\n").encode())
         return None
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -121,6 +121,14 @@ constexpr int WAVES_PER_BLOCK = BLOCK / 64;
 #endif
 // the if-if shadow kernel of the split schedule with a treelet too (1) or
 // with global node loads only (0)
+#ifndef IGX_KO_SHADOW
+#define IGX_KO_SHADOW 0
+#endif
+// k_shadow loads the colour and the radiance slot of a shadow ray before its
+// any-hit walk (1) or after it, for unoccluded rays only (0)
+#ifndef IGX_SHADOW_PREFETCH
+#define IGX_SHADOW_PREFETCH 1
+#endif
 #ifndef SHADOW_IFIF_TREELET
 #define SHADOW_IFIF_TREELET 0
 #endif
@@ -517,10 +525,26 @@ __device__ __forceinline__ void apply_texture(const SceneView& sv, DevMaterial& 
     }
 }
 
-template <bool FULL>
+// Shading sub-phase clock of the instrumented k_extend (CLK): the wave's
+// shader clock since the previous mark goes to sub-phase k of its group's
+// class (cls[20 + 4 * bucket + k]); marks sit in the hit path, executed by
+// the wave for its active lanes.
+template <bool CLK>
+__device__ __forceinline__ void sub_mark(TraceStats* st, int k) {
+    if constexpr (CLK) {
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_sched_barrier(0);
+        const unsigned long long now = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
+        if (first_active_lane()) st->cls[20 + 4 * st->bucket + k] += now - st->t_sub;
+        st->t_sub = now;
+    }
+}
+
+template <bool FULL, bool CLK = false>
 __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView& sv, PathState& ps, int hit_ent,
                                            int hit_prim, float tmax, float hu, float hv, f3& Lacc, bool& has_l,
-                                           bool& has_shadow, ShadowRec& sr) {
+                                           bool& has_shadow, ShadowRec& sr, TraceStats* clk = nullptr) {
     Lacc = mk(0, 0, 0);
     has_l = false;
     has_shadow = false;
@@ -546,6 +570,7 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
     std::conditional_t<FULL, DevMaterial, const DevMaterial&> m = sv.mats[mat_id];
     if constexpr (FULL)
         if (sv.uv) apply_texture(sv, m, hit_ent, hit_prim, hu, hv);
+    sub_mark<CLK>(clk, 0); // surface element + material
     // on_hit (pathtracer.art:114-134)
     if (m.light >= 0 && s.entering) {
         float dt = -dot(rd, s.local.n);
@@ -559,6 +584,7 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
             has_l = true;
         }
     }
+    sub_mark<CLK>(clk, 1); // emission
     // seed of the path's (sample, iteration, frame, pixel, user seed),
     // create_random_seed (core/random.art:34-43), carried in the path state
     Rng rnd{ps.seed, ps.counter};
@@ -594,6 +620,7 @@ __device__ __forceinline__ bool shade_step(const FrameArgs& fa, const SceneView&
             has_shadow = true;
         }
     }
+    sub_mark<CLK>(clk, 2); // NEE (light sample, BSDF eval / pdf)
     // on_bounce (pathtracer.art:165-200)
     if (!(ps.depth + 1 <= sv.max_depth)) return false;
     BsdfSample bs = bsdf_sample<FULL>(m, s, rnd, out_dir);
@@ -696,15 +723,25 @@ __device__ __forceinline__ bool extend_step_instrumented(const FrameArgs& fa, co
         st.cls[12 + bucket] += witers;
         st.cls[16 + bucket] += visits;
     }
+    st.bucket = bucket;
+    st.t_sub = t_last;
+    unsigned long long sub0 = 0;
+    for (int k = 0; k < 3; ++k) sub0 += st.cls[20 + 4 * bucket + k];
     if (act) {
         f3 Lacc;
         bool has_l;
-        alive = shade_step<variant_full(V)>(fa, sv, ps, hit_ent, hit_prim, tmax, hu, hv, Lacc, has_l, has_shadow, sr);
+        alive = shade_step<variant_full(V), true>(fa, sv, ps, hit_ent, hit_prim, tmax, hu, hv, Lacc, has_l, has_shadow, sr, &st);
         if (has_l) add_radiance(L, ps.slot, Lacc);
     }
     const unsigned long long c_sh = st.cyc[2];
     phase_mark(st, t_last, 2);
-    if (lane_id() == 0) st.cls[4 + bucket] += st.cyc[2] - c_sh;
+    if (lane_id() == 0) {
+        st.cls[4 + bucket] += st.cyc[2] - c_sh;
+        // sub-phase 3: the rest of the shade phase (BSDF sample, roulette, misses)
+        unsigned long long sub1 = 0;
+        for (int k = 0; k < 3; ++k) sub1 += st.cls[20 + 4 * bucket + k];
+        st.cls[20 + 4 * bucket + 3] += (st.cyc[2] - c_sh) - (sub1 - sub0);
+    }
     return alive;
 }
 
@@ -712,6 +749,7 @@ template <bool STATS>
 __device__ __forceinline__ void flush_stats(const TraceStats& st, unsigned long long* stats, int base, bool with_hits) {
     // slots: base+0..3 nodes/leaves/tris/blas, 8 hits, 9+base/4*2 .. wave node / leaf iterations
     unsigned long long a = st.nodes, b = st.leaves, c = st.tris, e = st.blas, h = st.hits, wn = st.wnodes, wl = st.wleaves;
+    unsigned long long tl = st.tlas_nodes, h0 = st.hot[0], h1 = st.hot[1], h2 = st.hot[2];
     for (int off = 32; off > 0; off >>= 1) {
         a += __shfl_down(a, off);
         b += __shfl_down(b, off);
@@ -720,6 +758,10 @@ __device__ __forceinline__ void flush_stats(const TraceStats& st, unsigned long 
         h += __shfl_down(h, off);
         wn += __shfl_down(wn, off);
         wl += __shfl_down(wl, off);
+        tl += __shfl_down(tl, off);
+        h0 += __shfl_down(h0, off);
+        h1 += __shfl_down(h1, off);
+        h2 += __shfl_down(h2, off);
     }
     if (lane_id() == 0) {
         atomicAdd(&stats[base + 0], a);
@@ -729,11 +771,20 @@ __device__ __forceinline__ void flush_stats(const TraceStats& st, unsigned long 
         if (with_hits) atomicAdd(&stats[8], h);
         atomicAdd(&stats[9 + (base / 4) * 2], wn);
         atomicAdd(&stats[10 + (base / 4) * 2], wl);
+        if (base == 0) { // closest-hit node visits: in the TLAS, at hot-order ranks < 256 / 512 / 1280
+            atomicAdd(&stats[50], tl);
+            atomicAdd(&stats[51], h0);
+            atomicAdd(&stats[52], h1);
+            atomicAdd(&stats[53], h2);
+        }
         if (st.cyc[0] | st.cyc[1] | st.cyc[2] | st.cyc[3]) {
             for (int k = 0; k < 4; ++k) atomicAdd(&stats[16 + k], st.cyc[k]);
             if (st.cls)
                 for (int k = 0; k < 20; ++k)
                     if (st.cls[k]) atomicAdd(&stats[20 + k], st.cls[k]);
+            if (st.cls) // shading sub-phase clocks by class (surface, emission, NEE, rest)
+                for (int k = 0; k < 16; ++k)
+                    if (st.cls[20 + k]) atomicAdd(&stats[54 + k], st.cls[20 + k]);
         }
     }
 }
@@ -809,10 +860,10 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
     if (!gen && row_total(kc.cnt_in) <= tail_threshold) return; // k_finish takes the remaining paths (block-uniform)
     const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : stage_treelet<BLOCK>(gsv, lds_scene);
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
-    __shared__ unsigned long long cls_mem[STATS ? WAVES_PER_BLOCK * 20 : 1]; // per-class counters (instrumented)
+    __shared__ unsigned long long cls_mem[STATS ? WAVES_PER_BLOCK * 36 : 1]; // per-class counters (instrumented)
     if constexpr (STATS) {
-        st.cls = cls_mem + 20 * (threadIdx.x >> 6);
-        if (lane_id() < 20) st.cls[lane_id()] = 0;
+        st.cls = cls_mem + 36 * (threadIdx.x >> 6);
+        if (lane_id() < 36) st.cls[lane_id()] = 0;
     }
     const WaveWork w = wave_work();
     // Groups of 64 positions of shard s: statically every K-th group from
@@ -1180,6 +1231,7 @@ __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, f
     if (row_total(cnt) == 0) return;
     const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : stage_treelet<BLOCK>(gsv, lds_scene);
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
+    unsigned long long cls_acc[2][5] = {}; // instrumented: per shadow class groups, wave iterations, visits, cycles, occluded
     const WaveWork w = wave_work();
     // groups of 64 shadow rays: grid-stride over the wave's own shard, or
     // (work != nullptr) handed out by take_group
@@ -1198,14 +1250,67 @@ __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, f
             break;
         }
         const int pos = p0 + lane_id();
-        if (pos >= sc.n) continue;
-        const int i = stream_index(s, pos, sc.a, sh.shard_cap);
-        float4 s0 = sh.s0[i], s1 = sh.s1[i];
-        float tmax = s1.w;
-        int e, p;
-        float u, v;
-        if (!trace_ray<true, STATS, V>(sv, f3of(s0), f3of(s1), 0.001f, tmax, RAY_SHADOW, ts, e, p, u, v, st))
-            add_radiance(L, __float_as_int(s0.w), f3of(sh.s2[i]));
+        // instrumented: the class of the group (wave-uniform), its wave cycles and visits
+        const int cls = p0 < sc.a ? 0 : 1;
+        unsigned long long c0 = 0;
+        uint32_t wn0 = 0, ln0 = 0;
+        if constexpr (STATS) {
+            c0 = __builtin_amdgcn_s_memtime();
+            wn0 = st.wnodes;
+            ln0 = st.nodes;
+        }
+        bool occl = false;
+        if (pos < sc.n) {
+            const int i = stream_index(s, pos, sc.a, sh.shard_cap);
+            const float4 s0 = sh.s0[i], s1 = sh.s1[i];
+            const int slot = __float_as_int(s0.w);
+            float tmax = s1.w;
+            int e, p;
+            float u, v;
+            // the ray's colour and its radiance slot are loaded before the walk
+            // (IGX_SHADOW_PREFETCH): their latency (the slot is a scattered read)
+            // overlaps the any-hit traversal instead of following it
+            float4 col = make_float4(0, 0, 0, 0), l = make_float4(0, 0, 0, 0);
+            if constexpr (IGX_SHADOW_PREFETCH && !(IGX_KO_SHADOW & 2)) {
+                col = sh.s2[i];
+                l = L[slot];
+            }
+            // IGX_KO_SHADOW (experiment builds only, wrong images): bit 1 skips the
+            // any-hit walk, bit 2 the radiance update -- what each part costs
+            if (!(IGX_KO_SHADOW & 1)) occl = trace_ray<true, STATS, V>(sv, f3of(s0), f3of(s1), 0.001f, tmax, RAY_SHADOW, ts, e, p, u, v, st);
+            if (!(IGX_KO_SHADOW & 2) && !occl) {
+                if constexpr (!IGX_SHADOW_PREFETCH) {
+                    col = sh.s2[i];
+                    l = L[slot];
+                }
+                L[slot] = make_float4(l.x + col.x, l.y + col.y, l.z + col.z, 0); // add_radiance
+            }
+            if ((IGX_KO_SHADOW & 2) && !occl && s0.x == 1.2345f) L[0].x = s1.x; // keep the loads live
+        }
+        if constexpr (STATS) {
+            __builtin_amdgcn_s_waitcnt(0);
+            const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+            uint32_t visits = st.nodes - ln0, witers = st.wnodes - wn0, occ = occl ? 1 : 0;
+            for (int off = 32; off > 0; off >>= 1) {
+                visits += __shfl_xor(visits, off);
+                witers += __shfl_xor(witers, off);
+                occ += __shfl_xor(occ, off);
+            }
+            // accumulated per wave (lane 0), flushed once at the end: no atomics in the timed region
+            if (lane_id() == 0) {
+                cls_acc[cls][0] += 1;
+                cls_acc[cls][1] += witers;
+                cls_acc[cls][2] += visits;
+                cls_acc[cls][3] += c1 - c0;
+                cls_acc[cls][4] += occ;
+            }
+        }
+    }
+    if constexpr (STATS) {
+        if (lane_id() == 0)
+            for (int c = 0; c < 2; ++c)
+                for (int k = 0; k < 5; ++k)
+                    if (cls_acc[c][k]) atomicAdd(&stats[40 + 2 * k + c], cls_acc[c][k]);
     }
     if (STATS) flush_stats<STATS>(st, stats, 4, false);
 }
@@ -1540,6 +1645,11 @@ enum { DYN_EXTEND = 1, DYN_SHADOW = 2, DYN_REFILL_TRACE = 4, DYN_REFILL_SHADOW =
 // rows WORK_ROW0 + 4b: k_extend (or k_trace_refill) group counters of bounce b (take_group),
 // + 1: its mask of exhausted shards, + 2 / + 3: the same for k_shadow
 constexpr int WORK_ROW0 = 2 * MAX_BOUNCES + 4;
+// instrumentation counters (igx_get_stats): 0-12 visit counts, 16-19 k_extend
+// phase clocks, 20-39 k_extend by group class, 40-49 k_shadow by class, 50-53
+// closest-hit node visits in the TLAS and by hot-order rank, 54-69 k_extend
+// shading sub-phase clocks by class
+[[maybe_unused]] constexpr int DSTATS = 80;
 constexpr int CTR_ROWS = WORK_ROW0 + 4 * MAX_BOUNCES;
 // BLAS with more triangles build without spatial splits (load time; their
 // triangles are small next to the scene in the suite's soups)
@@ -1701,17 +1811,29 @@ struct igx_device {
     // its queue (render_impl, igx_clear); nullptr until the first queued render
     int async_opt = 1;
     struct AsyncRender* async = nullptr;
+    // option "host_wait_us": the chunk scheduler's host thread sleeps this long
+    // between polls that found no progress (after a few yields); 0 = yield only
+    int host_wait_us = 0;
+    // option "fail_chunk" (test hook): the n-th chunk the chunk scheduler
+    // starts from now on fails with IGX_ERR_HIP instead
+    int64_t fail_chunk_opt = 0;
 };
 // the worker has queued everything submitted; its first error (part 0)
 igx_status wait_idle(igx_device* dev);
 igx_status wait_ready(igx_device* dev);
+bool reset_async_failure(igx_device* dev);
 void stop_async(igx_device* dev);
 
 namespace igxh {
 
 #if IGX_PART == 0
+// Set on a handle's async worker thread (async_worker): errors raised there
+// go to the worker's own message, which the host thread copies into
+// last_error (wait_idle / wait_ready); the host thread alone writes last_error.
+thread_local std::string* t_error_sink = nullptr;
 igx_status fail(igx_device* d, igx_status s, const std::string& msg) {
-    if (d) d->last_error = msg;
+    if (t_error_sink) *t_error_sink = msg;
+    else if (d) d->last_error = msg;
     return s;
 }
 
@@ -2298,12 +2420,12 @@ extern "C" igx_status igx_create(int hip_device, igx_device** out) {
         delete dev;
         return IGX_ERR_HIP;
     }
-    if (hipMalloc((void**)&dev->dstats, 40 * sizeof(unsigned long long)) != hipSuccess ||
+    if (hipMalloc((void**)&dev->dstats, DSTATS * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc((void**)&dev->tail_counts, 2 * sizeof(unsigned long long)) != hipSuccess) {
         delete dev;
         return IGX_ERR_OUT_OF_MEMORY;
     }
-    (void)hipMemset(dev->dstats, 0, 40 * sizeof(unsigned long long));
+    (void)hipMemset(dev->dstats, 0, DSTATS * sizeof(unsigned long long));
     (void)hipMemset(dev->tail_counts, 0, 2 * sizeof(unsigned long long));
     *out = dev;
     return IGX_OK;
@@ -2381,6 +2503,8 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     }
     else if (k == "concurrent_chunks") dev->concurrent_opt = value != 0 ? 1 : 0;
     else if (k == "async_render") dev->async_opt = value != 0 ? 1 : 0;
+    else if (k == "fail_chunk") dev->fail_chunk_opt = std::max<int64_t>(0, value);
+    else if (k == "host_wait_us") dev->host_wait_us = (int)std::max<int64_t>(0, std::min<int64_t>(value, 10000));
     else if (k == "concurrent_start_pct") {
         if (value < 0 || value > 100) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "concurrent_start_pct must be 0..100");
         dev->concurrent_start_pct = (int)value;
@@ -2615,6 +2739,7 @@ static bool closed_mesh(const igx_mesh& m) {
 extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* desc) {
     if (!dev || !desc) return IGX_ERR_INVALID_ARGUMENT;
     HIPCHK(hipSetDevice(dev->hip_device));
+    reset_async_failure(dev); // a new scene starts the handle afresh
     igx_status dst = drain(dev);
     if (dst != IGX_OK) return dst;
     free_scene(dev);
@@ -3263,7 +3388,12 @@ struct AsyncRender {
     std::deque<std::pair<bool, std::shared_ptr<const ChunkPlan>>> jobs; // (clear, plan)
     bool stop = false, idle = true;
     bool late = true; // every chunk submitted has started and is in its late bounces (igx_wait_ready)
+    // a step failed on the worker: everything queued was dropped, so the film
+    // and the iteration count no longer agree.  The handle stays failed --
+    // every call that waits for the queue returns `err` with `msg` as its last
+    // error -- until igx_clear or igx_upload_scene (reset_async_failure)
     igx_status err = IGX_OK;
+    std::string msg;
     ChunkScheduler sched; // the worker's
 };
 
@@ -3333,6 +3463,10 @@ igx_status ChunkScheduler::step(igx_device* dev, bool& progress) {
         if (!busy) {
             SchedItem& r = *nx;
             const ChunkPlan& pl = *r.plan;
+            if (dev->fail_chunk_opt > 0 && --dev->fail_chunk_opt == 0) { // test hook (option "fail_chunk")
+                restore();
+                return fail(dev, IGX_ERR_HIP, "injected failure (option fail_chunk)");
+            }
             igx_status st;
             if ((st = harvest(dev, S)) != IGX_OK || (st = ensure_slot(dev, S, pl.slot_cap, false, pl.fa.classify == 4)) != IGX_OK) {
                 restore();
@@ -3481,8 +3615,24 @@ igx_status ChunkScheduler::step(igx_device* dev, bool& progress) {
     return IGX_OK;
 }
 
+// The scheduler's host thread between steps that made no progress (every
+// chunk waits on a lagged count): a few yields, then sleeps of host_wait_us,
+// so a busy handle does not hold a CPU core at 100 % polling events (ADVICE
+// r4).  The lag of two bounces keeps the GPU fed across one sleep.
+// host_wait_us 0: yield only (the round-4 behaviour).
+struct Backoff {
+    int idle = 0;
+    void wait(const igx_device* dev) {
+        if (dev->host_wait_us <= 0 || idle < 8) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(dev->host_wait_us));
+        ++idle;
+    }
+    void reset() { idle = 0; }
+};
+
 // Runs the scheduler in the calling thread until everything queued is resolved.
 static igx_status run_scheduler(igx_device* dev, ChunkScheduler& sched) {
+    Backoff bo;
     while (!sched.empty()) {
         bool progress = false;
         igx_status st = sched.step(dev, progress);
@@ -3490,7 +3640,8 @@ static igx_status run_scheduler(igx_device* dev, ChunkScheduler& sched) {
             sched.items.clear();
             return st;
         }
-        if (!progress) std::this_thread::yield();
+        if (progress) bo.reset();
+        else bo.wait(dev);
     }
     return IGX_OK;
 }
@@ -3498,6 +3649,9 @@ static igx_status run_scheduler(igx_device* dev, ChunkScheduler& sched) {
 static void async_worker(igx_device* dev) {
     AsyncRender& a = *dev->async;
     (void)hipSetDevice(dev->hip_device);
+    std::string worker_msg;
+    t_error_sink = &worker_msg; // fail() on this thread: the handle's last_error is the host thread's
+    Backoff bo;
     for (;;) {
         {
             std::unique_lock<std::mutex> lk(a.m);
@@ -3519,19 +3673,25 @@ static void async_worker(igx_device* dev) {
         bool progress = false;
         igx_status st = a.sched.step(dev, progress);
         if (st != IGX_OK) {
+            // drop everything queued (a chunk may be half rendered into the
+            // film) and mark the handle failed until a clear or upload
             std::lock_guard<std::mutex> lk(a.m);
             a.sched.items.clear();
             a.jobs.clear();
-            if (a.err == IGX_OK) a.err = st;
+            if (a.err == IGX_OK) {
+                a.err = st;
+                a.msg = "async render: " + worker_msg;
+            }
             continue;
         }
         if (progress) {
+            bo.reset();
             const bool late = a.sched.all_late(dev->concurrent_start_pct);
             std::lock_guard<std::mutex> lk(a.m);
             a.late = late && a.jobs.empty();
             if (a.late) a.cv_idle.notify_all();
         } else {
-            std::this_thread::yield();
+            bo.wait(dev);
         }
     }
 }
@@ -3546,19 +3706,34 @@ igx_status wait_ready(igx_device* dev) {
     AsyncRender& a = *dev->async;
     std::unique_lock<std::mutex> lk(a.m);
     a.cv_idle.wait(lk, [&] { return (a.idle && a.jobs.empty()) || (a.late && a.jobs.empty()); });
+    if (a.err != IGX_OK) dev->last_error = a.msg;
     return a.err;
 }
 
 // Waits until the worker has queued (on the GPU) everything submitted and
-// returns its first error, if any.  No-op without a worker.
+// returns its error, if it failed: the failure stays until igx_clear or
+// igx_upload_scene.  No-op without a worker.
 igx_status wait_idle(igx_device* dev) {
     if (!dev->async) return IGX_OK;
     AsyncRender& a = *dev->async;
     std::unique_lock<std::mutex> lk(a.m);
     a.cv_idle.wait(lk, [&] { return a.idle && a.jobs.empty(); });
-    igx_status st = a.err;
+    if (a.err != IGX_OK) dev->last_error = a.msg;
+    return a.err;
+}
+
+// igx_clear / igx_upload_scene on a failed handle: wait until the worker is
+// idle and lift the failure (the caller then resets the film or the scene).
+// Returns whether the handle had failed.
+bool reset_async_failure(igx_device* dev) {
+    if (!dev->async) return false;
+    AsyncRender& a = *dev->async;
+    std::unique_lock<std::mutex> lk(a.m);
+    a.cv_idle.wait(lk, [&] { return a.idle && a.jobs.empty(); });
+    const bool failed = a.err != IGX_OK;
     a.err = IGX_OK;
-    return st;
+    a.msg.clear();
+    return failed;
 }
 
 void stop_async(igx_device* dev) {
@@ -3614,6 +3789,12 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
     if (!async) {
         igx_status w = wait_idle(dev);
         if (w != IGX_OK) return w;
+    } else if (dev->async) { // a failed handle takes no more work until a clear or upload
+        std::lock_guard<std::mutex> lk(dev->async->m);
+        if (dev->async->err != IGX_OK) {
+            dev->last_error = dev->async->msg;
+            return dev->async->err;
+        }
     }
 
     // framebuffer (resize clears, as Device::resize)
@@ -3980,10 +4161,21 @@ extern "C" igx_status igx_pack_tiles(igx_device* dev, const igx_render_params* p
 
 extern "C" igx_status igx_clear(igx_device* dev) {
     if (!dev) return IGX_ERR_INVALID_ARGUMENT;
-    if (dev->async) { // ordered behind the queued renders' resolves by the worker
-        submit_async(dev, true, nullptr);
-        dev->iteration_count = 0;
-        return IGX_OK;
+    bool failed = false;
+    if (dev->async) {
+        {
+            std::lock_guard<std::mutex> lk(dev->async->m);
+            failed = dev->async->err != IGX_OK;
+        }
+        if (!failed) { // ordered behind the queued renders' resolves by the worker
+            submit_async(dev, true, nullptr);
+            dev->iteration_count = 0;
+            return IGX_OK;
+        }
+        // a failed handle: the worker dropped its queue; clear here and lift the failure
+        reset_async_failure(dev);
+        igx_status st = drain(dev);
+        if (st != IGX_OK) return st;
     }
     if (dev->fb) {
         HIPCHK(hipSetDevice(dev->hip_device));
@@ -4002,8 +4194,18 @@ extern "C" igx_status igx_get_stats(igx_device* dev, igx_stats* out) {
     *out = dev->stats;
     out->bvh_depth = dev->scene_depth;
     out->stack_entries = LDS_STACK;
-    unsigned long long h[40] = {0};
+    unsigned long long h[DSTATS] = {0};
     HIPCHK(hipMemcpy(h, dev->dstats, sizeof(h), hipMemcpyDeviceToHost));
+    for (int k = 0; k < 2; ++k) {
+        out->shadow_class_groups[k] = h[40 + k];
+        out->shadow_class_node_iters[k] = h[42 + k];
+        out->shadow_class_node_visits[k] = h[44 + k];
+        out->shadow_class_cycles[k] = h[46 + k];
+        out->shadow_class_occluded[k] = h[48 + k];
+    }
+    for (int k = 0; k < 16; ++k) out->extend_class_shade_cycles[k] = h[54 + k];
+    out->tlas_node_visits = h[50];
+    for (int k = 0; k < 3; ++k) out->hot_node_visits[k] = h[51 + k];
     for (int k = 0; k < 8; ++k) out->extend_class_cycles[k] = h[20 + k];
     for (int k = 0; k < 4; ++k) {
         out->extend_class_groups[k] = h[28 + k];
@@ -4051,7 +4253,7 @@ extern "C" igx_status igx_reset_stats(igx_device* dev) {
     igx_status st = drain(dev);
     if (st != IGX_OK) return st;
     dev->stats = igx_stats{};
-    HIPCHK(hipMemset(dev->dstats, 0, 40 * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(dev->dstats, 0, DSTATS * sizeof(unsigned long long)));
     return IGX_OK;
 }
 

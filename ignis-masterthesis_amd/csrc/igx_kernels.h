@@ -105,6 +105,9 @@ __device__ __forceinline__ SceneView stage_treelet(const SceneView& sv, float4* 
 struct TraceStats {
     uint32_t nodes, leaves, tris, blas, hits;
     uint32_t wnodes, wleaves; // wave-level iterations of the node loop / leaf phase (SIMD efficiency)
+    // node visits in the TLAS, and at nodes of hot-order rank < 256 / 512 /
+    // 1280 (order_hot_nodes: the prefixes a treelet can stage)
+    uint32_t tlas_nodes = 0, hot[3] = {0, 0, 0};
     // k_extend phase clocks (wave-level, s_memtime): load, trace, shade, store
     unsigned long long cyc[4] = {0, 0, 0, 0};
     // k_extend by the class of the wave's group (camera, A, B, C): trace
@@ -112,11 +115,25 @@ struct TraceStats {
     // 12-15, lane node visits 16-19 -- the wave's 20 counters in LDS (lane 0
     // updates them), so the instrumentation holds no registers
     unsigned long long* cls = nullptr;
+    // shading sub-phase clocks of the instrumented k_extend (shade_step<.., true>):
+    // class bucket of the wave's group and the last mark
+    int bucket = 0;
+    unsigned long long t_sub = 0;
 };
 
 // true on the lowest active lane of the wave (counts one event per wave)
 __device__ __forceinline__ bool first_active_lane() {
     return (int)__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1;
+}
+
+// one node visit of the instrumented traversal
+__device__ __forceinline__ void count_node(TraceStats& st, bool in_blas, int node) {
+    st.nodes++;
+    if (first_active_lane()) st.wnodes++;
+    st.tlas_nodes += in_blas ? 0 : 1;
+    st.hot[0] += node < 256 ? 1 : 0;
+    st.hot[1] += node < 512 ? 1 : 0;
+    st.hot[2] += node < 1280 ? 1 : 0;
 }
 
 // Ray flags (traversal/ray.art:19-23)
@@ -135,6 +152,9 @@ constexpr uint32_t INST_IDENTITY = 1u << 30;
 #define IGX_TRANSLATE_INSTANCES 1
 #endif
 constexpr uint32_t INST_TRANSLATE = 1u << 29;
+// the identity / translation shortcuts give transform_ray's direction bit for
+// bit when no component is zero (with x != 0: 1*x + 0*y + 0*z == x)
+__device__ __forceinline__ bool shortcut_dir_ok(f3 d) { return d.x != 0.0f && d.y != 0.0f && d.z != 0.0f; }
 
 // ---------------------------------------------------------------------------
 // Two-level traversal: TLAS (entities) -> BLAS (triangles) or analytic sphere.
@@ -385,10 +405,7 @@ __device__ __forceinline__ void load_node4_ordered(const SceneView& sv, const Tr
 template <bool STATS, bool SPILL, int NS, bool TREE>
 __device__ __forceinline__ int node_step2(const SceneView& sv, const Trav& t, int node, const TStack& ts, int& sp,
                                          TraceStats& st) {
-    if (STATS) {
-        st.nodes++;
-        if (first_active_lane()) st.wnodes++;
-    }
+    if (STATS) count_node(st, t.in_blas, node);
     // treelet nodes (TREE, node < tree_n) from LDS, the others from global
     // memory (load_node: a branch per address space)
     float4 f[4];
@@ -442,10 +459,7 @@ __device__ __forceinline__ void cswap(float& da, int& ra, float& db, int& rb) {
 template <bool STATS, bool SPILL, int NS, bool TREE>
 __device__ __forceinline__ int node_step4(const SceneView& sv, const Trav& t, int node, const TStack& ts, int& sp,
                                           TraceStats& st) {
-    if (STATS) {
-        st.nodes++;
-        if (first_active_lane()) st.wnodes++;
-    }
+    if (STATS) count_node(st, t.in_blas, node);
     float4 f[7];
     if constexpr (IGX_ORDERED_SLAB) load_node4_ordered<NS, TREE>(sv, t, node, f); // near, far per axis
     else load_node<7, NS, TREE>(sv, node, f); // see node_step2
@@ -494,10 +508,7 @@ __device__ __forceinline__ int node_step4(const SceneView& sv, const Trav& t, in
 template <bool STATS, bool SPILL, bool TREE>
 __device__ __forceinline__ int node_step4q(const SceneView& sv, const Trav& t, int node, const TStack& ts, int& sp,
                                            TraceStats& st) {
-    if (STATS) {
-        st.nodes++;
-        if (first_active_lane()) st.wnodes++;
-    }
+    if (STATS) count_node(st, t.in_blas, node);
     float4 f[4];
     load_node<4, 4, TREE>(sv, node, f); // see node_step2
     const float4 A = f[0], B = f[1], C = f[2];
@@ -554,10 +565,7 @@ __device__ __forceinline__ float qbyte(uint32_t w, int b) { return (float)((w >>
 template <bool STATS, bool SPILL, bool TREE>
 __device__ __forceinline__ int node_step8q(const SceneView& sv, const Trav& t, int node, const TStack& ts, int& sp,
                                            TraceStats& st) {
-    if (STATS) {
-        st.nodes++;
-        if (first_active_lane()) st.wnodes++;
-    }
+    if (STATS) count_node(st, t.in_blas, node);
     float4 f[7];
     load_node<7, 8, TREE>(sv, node, f); // see node_step2
     const float4 A = f[0], B = f[1], C = f[2], D = f[3], E = f[4];
@@ -628,7 +636,12 @@ __device__ __forceinline__ bool instance_test(const SceneView& sv, Trav& t, int 
     int4 info = *reinterpret_cast<const int4*>(ip + 3);
     uint32_t ef = (uint32_t)info.w;
     if ((t.rflags & RAY_TYPE_MASK) != ((t.rflags & ef) & RAY_TYPE_MASK)) return false; // check_ray_visibility
-    if (IGX_IDENTITY_INSTANCES && (ef & INST_IDENTITY)) {
+    // the shortcuts take the world direction as the entity-space one; a zero
+    // component keeps its sign there, while transform_ray's 1*d + 0*d' + 0*d''
+    // may turn -0 into +0 (and safe_rcp then gives +FLT_MAX, not -FLT_MAX):
+    // such rays take the general transform
+    const bool exact_dir = shortcut_dir_ok(t.d);
+    if (IGX_IDENTITY_INSTANCES && (ef & INST_IDENTITY) && exact_dir) {
         // identity to_local: t.lo / t.ld / t.idir / t.iorg already hold the
         // world ray of the TLAS walk
         if (STATS) st.blas++;
@@ -637,7 +650,7 @@ __device__ __forceinline__ bool instance_test(const SceneView& sv, Trav& t, int 
         blas_root = info.z;
         return true;
     }
-    if (IGX_TRANSLATE_INSTANCES && (ef & INST_TRANSLATE)) {
+    if (IGX_TRANSLATE_INSTANCES && (ef & INST_TRANSLATE) && exact_dir) {
         // transform_ray with a translation: ((1*o.x + 0*o.y) + 0*o.z) + tx is o.x + tx
         if (STATS) st.blas++;
         t.lo = mk(t.o.x + ip[0].w, t.o.y + ip[1].w, t.o.z + ip[2].w);
@@ -861,10 +874,11 @@ __device__ __forceinline__ bool trav_init_enclosed(const SceneView& sv, Trav& t,
     if ((rflags & RAY_TYPE_MASK) != ((rflags & (uint32_t)info.w) & RAY_TYPE_MASK)) return false;
     t.o = o;
     t.d = d;
-    if (IGX_IDENTITY_INSTANCES && ((uint32_t)info.w & INST_IDENTITY)) { // as instance_test
+    const bool exact_dir = shortcut_dir_ok(d); // see instance_test
+    if (IGX_IDENTITY_INSTANCES && ((uint32_t)info.w & INST_IDENTITY) && exact_dir) { // as instance_test
         t.lo = o;
         t.ld = d;
-    } else if (IGX_TRANSLATE_INSTANCES && ((uint32_t)info.w & INST_TRANSLATE)) {
+    } else if (IGX_TRANSLATE_INSTANCES && ((uint32_t)info.w & INST_TRANSLATE) && exact_dir) {
         t.lo = mk(o.x + ip[0].w, o.y + ip[1].w, o.z + ip[2].w);
         t.ld = d;
     } else {

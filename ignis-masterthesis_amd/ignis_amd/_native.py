@@ -130,7 +130,11 @@ class Stats(C.Structure):
                 ("extend_cycles_shade", C.c_uint64), ("extend_cycles_store", C.c_uint64),
                 ("slot_bytes", C.c_uint64), ("treelet_nodes", C.c_int32 * 4),
                 ("extend_class_cycles", C.c_uint64 * 8), ("extend_class_groups", C.c_uint64 * 4),
-                ("extend_class_node_iters", C.c_uint64 * 4), ("extend_class_node_visits", C.c_uint64 * 4)]
+                ("extend_class_node_iters", C.c_uint64 * 4), ("extend_class_node_visits", C.c_uint64 * 4),
+                ("shadow_class_groups", C.c_uint64 * 2), ("shadow_class_node_iters", C.c_uint64 * 2),
+                ("shadow_class_node_visits", C.c_uint64 * 2), ("shadow_class_cycles", C.c_uint64 * 2),
+                ("shadow_class_occluded", C.c_uint64 * 2), ("tlas_node_visits", C.c_uint64),
+                ("hot_node_visits", C.c_uint64 * 3), ("extend_class_shade_cycles", C.c_uint64 * 16)]
 
     def as_dict(self):
         return {name: (list(getattr(self, name)) if isinstance(getattr(self, name), C.Array) else getattr(self, name))

@@ -12,6 +12,19 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BENCH = os.path.join(ROOT, "bench.py")
 
 
+def _objects(text):
+    """Every JSON object printed on stdout.  The ranks share one pipe, so two
+    ranks' lines may interleave without a newline between them: decode the
+    objects one after the other instead of line by line."""
+    dec, out, i = json.JSONDecoder(), [], 0
+    while True:
+        i = text.find("{", i)
+        if i < 0:
+            return out
+        obj, i = dec.raw_decode(text, i)
+        out.append(obj)
+
+
 def _env(**kw):
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
     env["IGX_BENCH_LAUNCH_PROBE"] = "1"
@@ -23,7 +36,7 @@ def test_gpus_n_launches_n_ranks():
     r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--steps", "1"], env=_env(), capture_output=True, text=True,
                        timeout=180)
     assert r.returncode == 0, r.stderr[-2000:]
-    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    lines = _objects(r.stdout)
     assert sorted(x["rank"] for x in lines) == [0, 1]
     assert all(x["world"] == 2 and x["gpus"] == 2 for x in lines)
 
@@ -31,7 +44,7 @@ def test_gpus_n_launches_n_ranks():
 def test_single_gpu_needs_no_launcher():
     r = subprocess.run([sys.executable, BENCH], env=_env(), capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
-    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    lines = _objects(r.stdout)
     assert lines == [{"rank": 0, "world": 1, "gpus": 1}]
 
 

@@ -784,6 +784,68 @@ def test_async_render_queue_matches_synchronous(diamond_path):
     assert rays[0] == rays[1]
 
 
+def test_async_worker_failure_is_sticky_until_clear(diamond_path):
+    """A chunk that fails on the async worker (test hook "fail_chunk") drops the
+    queue, so film and iteration count no longer agree: every later call that
+    waits for the queue reports the failure (with its message) until igx_clear,
+    after which the handle renders the synchronous frame again."""
+    sc = ignis_amd.Scene.from_file(diamond_path)
+    w, h, spi = 160, 120, 4
+    p = ignis_amd.RenderParams()
+    p.width, p.height, p.spi = w, h, spi
+    ref = ignis_amd.Device(0)
+    ref.upload(sc)
+    ref.set_option("async_render", 0)
+    ref.set_option("capacity", 32768)
+    ref.render_iterations(p, 4)
+    want, _ = ref.framebuffer(w * h * 3)
+    ref.close()
+    d = ignis_amd.Device(0)
+    d.upload(sc)
+    d.set_option("async_render", 1)
+    d.set_option("capacity", 32768)  # several chunks per call
+    d.set_option("fail_chunk", 3)
+    d.render_iterations(p, 4)  # queued; the third chunk fails on the worker
+    for call in (lambda: d.framebuffer(w * h * 3), d.stats, lambda: d.set_option("timing", 0),
+                 lambda: d.render_iterations(p, 1)):
+        with pytest.raises(ignis_amd.IgxError, match="injected failure"):
+            call()
+    d.clear()  # lifts the failure
+    d.render_iterations(p, 4)
+    got, n = d.framebuffer(w * h * 3)
+    assert n == 4
+    np.testing.assert_array_equal(got, want)
+    d.close()
+
+
+def test_signed_zero_directions_hit_alike(device, root):
+    """Axis-aligned rays through the diamond scene (identity and translated
+    instances, whose BLAS entry skips the transform): +0 and -0 direction
+    components give bit-identical closest hits, and the hits agree with the
+    oracle's general transform_ray (ray.art:53-59).  A -0 component would give
+    safe_rcp's -FLT_MAX where the transform gives +FLT_MAX; such rays take the
+    general transform."""
+    sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", "diamond_scene.json"))
+    device.upload(sc)
+    lo = np.array(sc.desc.scene_bbox_min[:]) - 0.05
+    hi = np.array(sc.desc.scene_bbox_max[:]) + 0.05
+    rng = np.random.default_rng(5)
+    n = 6 * 4096
+    org = rng.uniform(lo, hi, size=(n, 3)).astype(np.float32)
+    axes = np.repeat(np.array([[1, 0, 0], [-1, 0, 0], [0, 1, 0], [0, -1, 0], [0, 0, 1], [0, 0, -1]], np.float32), n // 6, 0)
+    pos = np.zeros((n, 8), np.float32)
+    pos[:, 0:3], pos[:, 3:6], pos[:, 6], pos[:, 7] = org, axes, 1e-3, 3.4e38
+    neg = pos.copy()
+    neg[:, 3:6] = np.where(axes == 0, np.float32(-0.0), axes)  # the zero components negative
+    assert np.signbit(neg[:, 3:6]).sum() > n
+    hp, hn = device.trace_hits(pos, 0x4), device.trace_hits(neg, 0x4)
+    np.testing.assert_array_equal(hp[0], hn[0])
+    np.testing.assert_array_equal(hp[1].view(np.uint32), hn[1].view(np.uint32))
+    assert (hp[0][:, 0] >= 0).mean() > 0.2
+    orc = O.OracleScene(sc)
+    assert_hit_parity(hn, orc.trace_hits(neg, 0x4), neg, 0x4)
+
+
 def test_tile_sharding_equals_full_render(device, diamond_path):
     """Multi-GPU decomposition: tiles rendered by 3 shards sum to the full render bit for bit."""
     sc = ignis_amd.Scene.from_file(diamond_path)

@@ -43,4 +43,23 @@ if sum(cc):  # k_extend wave time by the class of the group: camera, A, B, C (tr
         out[f"ext_{k}_cyc_per_group"] = (cc[i] + cc[4 + i]) / max(1, cg[i])
         out[f"ext_{k}_wave_node_iters_per_group"] = s["extend_class_node_iters"][i] / max(1, cg[i])
         out[f"ext_{k}_simd_eff"] = s["extend_class_node_visits"][i] / max(1, 64 * s["extend_class_node_iters"][i])
+sc = list(s["extend_class_shade_cycles"])
+if sum(sc):  # shading sub-phases per class: surface + material, emission, NEE, rest (share of the class's shade cycles)
+    for i, k in enumerate(("cam", "A", "B", "C")):
+        tot = max(1, sum(sc[4 * i:4 * i + 4]))
+        out[f"ext_{k}_shade_split"] = [round(v / tot, 3) for v in sc[4 * i:4 * i + 4]]
+        out[f"ext_{k}_shade_cyc_per_group"] = tot / max(1, cg[i])
+g, it, vi, cy, oc = (list(s["shadow_class_" + k]) for k in ("groups", "node_iters", "node_visits", "cycles", "occluded"))
+if sum(g):  # k_shadow by the shadow stream class of a group (A / B): share of wave time, cycles per group, occlusion
+    for i, k in enumerate(("A", "B")):
+        out[f"sh_{k}_groups"] = g[i]
+        out[f"sh_{k}_cycle_share"] = cy[i] / max(1, sum(cy))
+        out[f"sh_{k}_cyc_per_group"] = cy[i] / max(1, g[i])
+        out[f"sh_{k}_wave_node_iters_per_group"] = it[i] / max(1, g[i])
+        out[f"sh_{k}_simd_eff"] = vi[i] / max(1, 64 * it[i])
+        out[f"sh_{k}_occluded_per_group"] = oc[i] / max(1, g[i])
+if s["node_visits"]:  # closest-hit node visits in the TLAS and at hot-order ranks < 256 / 512 / 1280
+    out["tlas_node_share"] = s["tlas_node_visits"] / s["node_visits"]
+    for k, r in enumerate((256, 512, 1280)):
+        out[f"node_rank_lt_{r}_share"] = s["hot_node_visits"][k] / s["node_visits"]
 print(json.dumps({k: round(v, 3) if isinstance(v, float) else v for k, v in out.items()}))
