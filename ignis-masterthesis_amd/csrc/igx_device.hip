@@ -1657,6 +1657,9 @@ constexpr int CTR_ROWS = WORK_ROW0 + 4 * MAX_BOUNCES;
 // face instances (faces x entities using them) up to which the upload
 // precomputes world-space face normals (16 B each: at most 64 MB)
 [[maybe_unused]] constexpr size_t FACE_NORMAL_TABLE_MAX = 4u << 20;
+// mesh faces (over all shapes) up to which the upload writes the per-face
+// shading records SceneView::fsh (48 B each: at most 192 MB)
+[[maybe_unused]] constexpr size_t FACE_SHADE_MAX = 4u << 20;
 [[maybe_unused]] constexpr size_t CTR_INTS = (size_t)CTR_ROWS * CROW;
 // nodes moved to the front of the node array in hot order at upload (the
 // largest treelet a kernel may stage: 160 KB of LDS / 128-B nodes)
@@ -1757,6 +1760,9 @@ struct igx_device {
     // option "face_normals": precomputed world-space face normals for scenes
     // with at most FACE_NORMAL_TABLE_MAX face instances (next upload)
     int face_normals_opt = 1;
+    // option "face_shade": per-face shading records (SceneView::fsh) for
+    // scenes with at most FACE_SHADE_MAX faces (next upload)
+    int face_shade_opt = 1;
     float sah_node_cost = 1.0f;    // option "sah_node_cost_pct" (percent of one triangle test)
     int bvh_bins = 32;             // option "bvh_bins": SAH bins per axis of the BLAS builds (next upload)
     int bvh_bins_tlas = 32;        // option "bvh_bins_tlas": the same for the TLAS
@@ -2504,6 +2510,7 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     else if (k == "concurrent_chunks") dev->concurrent_opt = value != 0 ? 1 : 0;
     else if (k == "async_render") dev->async_opt = value != 0 ? 1 : 0;
     else if (k == "fail_chunk") dev->fail_chunk_opt = std::max<int64_t>(0, value);
+    else if (k == "face_shade") dev->face_shade_opt = value != 0 ? 1 : 0;
     else if (k == "host_wait_us") dev->host_wait_us = (int)std::max<int64_t>(0, std::min<int64_t>(value, 10000));
     else if (k == "concurrent_start_pct") {
         if (value < 0 || value > 100) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "concurrent_start_pct must be 0..100");
@@ -2836,6 +2843,13 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     bool textured = false;
     for (uint32_t i = 0; i < desc->num_materials; ++i) textured = textured || desc->materials[i].texture != IGX_TEXTURE_NONE;
     std::vector<int4> idx;
+    // per face: vertex normals and indices in one record (SceneView::fsh),
+    // for scenes with at most FACE_SHADE_MAX faces over all meshes (48 B each)
+    std::vector<float4> fsh;
+    size_t total_faces = 0;
+    for (uint32_t i = 0; i < desc->num_shapes; ++i)
+        if (desc->shapes[i].type != IGX_SHAPE_SPHERE && desc->shapes[i].mesh >= 0) total_faces += desc->meshes[desc->shapes[i].mesh].num_faces;
+    const bool with_fsh = dev->face_shade_opt && total_faces <= FACE_SHADE_MAX;
     // Append a built BVH2 (as Node2, or collapsed to 4-wide nodes) to the
     // unified node array: inner refs move by the array offset, leaf codes by
     // `leaf_off` slots.  Returns the node offset; `need` = stack entries the
@@ -2939,6 +2953,15 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
         }
         for (uint32_t f = 0; f < m.num_faces; ++f)
             idx.push_back(make_int4((int)m.indices[3 * f], (int)m.indices[3 * f + 1], (int)m.indices[3 * f + 2], 0));
+        if (with_fsh)
+            for (uint32_t f = 0; f < m.num_faces; ++f)
+                for (int k = 0; k < 3; ++k) {
+                    const uint32_t v = m.indices[3 * f + k];
+                    float4 r = make_float4(m.normals[3 * v], m.normals[3 * v + 1], m.normals[3 * v + 2], 0);
+                    const int vi = (int)v;
+                    std::memcpy(&r.w, &vi, 4);
+                    fsh.push_back(r);
+                }
         brs[s] = igx::BvhBuildResult{}; // release the host copy
     }
 
@@ -3064,6 +3087,12 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
                     fn_tab.push_back(make_float4(n[0] * inv, n[1] * inv, n[2] * inv, 0));
                 }
             }
+        }
+        // the entity's face-normal offset in row 3 .w of its record, read
+        // with the normal matrix by surface_element's fsh path (-1: none)
+        for (uint32_t e = 0; e < desc->num_entities; ++e) {
+            const int off = ent_fn.empty() ? -1 : ent_fn[e];
+            std::memcpy(&ent[ENT_STRIDE * e + 3].w, &off, 4);
         }
     }
 
@@ -3225,11 +3254,12 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
         (st = upload(dev, lights, &sv.lights)) || (st = upload(dev, lsel.cdf, &sv.sel_cdf)) ||
         (st = upload(dev, lsel.hierarchy, &sv.sel_tree)) || (st = upload(dev, ent_enc, &sv.ent_enc)) ||
         (st = upload(dev, enc_tab, &sv.enc)) || (st = upload(dev, enc_box, &sv.enc_box)) || (st = upload(dev, ent_fn, &sv.ent_fn)) ||
-        (st = upload(dev, fn_tab, &sv.fn_tab)) || (st = upload(dev, uvs, &sv.uv))) {
+        (st = upload(dev, fn_tab, &sv.fn_tab)) || (st = upload(dev, uvs, &sv.uv)) || (st = upload(dev, fsh, &sv.fsh))) {
         free_scene(dev);
         return st;
     }
     if (fn_tab.empty()) sv.fn_tab = nullptr; // surface_element computes the normals
+    if (fsh.empty()) sv.fsh = nullptr;       // ... reads the index and normal tables
     if (uvs.empty()) sv.uv = nullptr;
     sv.tlas_root = tlas_root;
     sv.num_nodes = (int)(nodes.size() / nf4);
@@ -3247,7 +3277,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
         dev->table_bytes = b;
         dev->shading_bytes = ent.size() * sizeof(ent[0]) + vtx.size() * sizeof(vtx[0]) + nrm.size() * sizeof(nrm[0]) +
                              idx.size() * sizeof(idx[0]) + mats.size() * sizeof(DevMaterial) + lights.size() * sizeof(lights[0]) +
-                             fn_tab.size() * sizeof(fn_tab[0]);
+                             fn_tab.size() * sizeof(fn_tab[0]) + fsh.size() * sizeof(fsh[0]);
     }
     sv.num_lights = (int)lights.size();
     sv.num_infinite = num_infinite;

@@ -47,6 +47,12 @@ struct SceneView {
     // for scenes with few face instances (nullptr otherwise): fn_tab[ent_fn[e] + prim]
     const int* ent_fn;
     const float4* fn_tab;
+    // per mesh face (shape level, at idx_off + prim): the three object-space
+    // vertex normals with the vertex indices in .w (int bits), uploaded for
+    // scenes with few faces (nullptr otherwise): one record per hit instead
+    // of the face's index record and three scattered normal loads behind it;
+    // with it, row 3 .w of the entity record holds ent_fn (int bits)
+    const float4* fsh;
     // per mesh vertex: texture coordinates (as vtx), uploaded only when a
     // material carries a texture (DevMaterial::pad, textured_material)
     const float2* uv;
@@ -1027,6 +1033,31 @@ __device__ __forceinline__ Surface surface_element(const SceneView& sv, int ent_
         s.local = make_frame(nrm);
         return s;
     }
+    if (sv.fsh) {
+        // the face's shading record: vertex normals and indices (fsh), the
+        // entity's face-normal offset in row 3 .w; the same values as the
+        // index / normal tables give, so the same bits
+        const float4* fr = sv.fsh + 3 * (info.w + prim);
+        const float4 r0 = fr[0], r1 = fr[1], r2 = fr[2];
+        f3 fn;
+        if (sv.fn_tab) {
+            fn = f3of(sv.fn_tab[__float_as_int(n0.w) + prim]);
+        } else {
+            f3 v0 = xform_point_rows(g0, g1, g2, f3of(sv.vtx[info.z + __float_as_int(r0.w)]));
+            f3 v1 = xform_point_rows(g0, g1, g2, f3of(sv.vtx[info.z + __float_as_int(r1.w)]));
+            f3 v2 = xform_point_rows(g0, g1, g2, f3of(sv.vtx[info.z + __float_as_int(r2.w)]));
+            f3 e1 = sub(v1, v0), e2 = sub(v2, v0);
+            f3 n = cross(e1, e2);
+            float nn = len(n);
+            fn = mulf(n, 1 / nn);
+        }
+        f3 ln = lerp2(f3of(r0), f3of(r1), f3of(r2), hu, hv);
+        f3 normal = normalize(xform_dir_rows(n0, n1, n2, ln));
+        s.entering = dot(rd, fn) <= 0;
+        s.face_normal = s.entering ? fn : neg(fn);
+        s.local = make_frame(s.entering ? normal : neg(normal));
+        return s;
+    }
     int4 f = sv.idx[info.w + prim];
     f3 fn;
     if (sv.fn_tab) {
@@ -1042,8 +1073,17 @@ __device__ __forceinline__ Surface surface_element(const SceneView& sv, int ent_
         float nn = len(n);
         fn = mulf(n, 1 / nn);
     }
-    f3 ln = lerp2(f3of(sv.nrm[info.z + f.x]), f3of(sv.nrm[info.z + f.y]), f3of(sv.nrm[info.z + f.z]), hu, hv);
-    f3 normal = normalize(xform_dir_rows(n0, n1, n2, ln));
+#ifndef IGX_KO_SURF
+#define IGX_KO_SURF 0
+#endif
+    // IGX_KO_SURF (experiment builds only, wrong images): shading normal = face normal
+    f3 normal;
+    if (IGX_KO_SURF) {
+        normal = fn;
+    } else {
+        f3 ln = lerp2(f3of(sv.nrm[info.z + f.x]), f3of(sv.nrm[info.z + f.y]), f3of(sv.nrm[info.z + f.z]), hu, hv);
+        normal = normalize(xform_dir_rows(n0, n1, n2, ln));
+    }
     s.entering = dot(rd, fn) <= 0;
     s.face_normal = s.entering ? fn : neg(fn);
     s.local = make_frame(s.entering ? normal : neg(normal));

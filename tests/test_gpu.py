@@ -483,18 +483,24 @@ def test_enclosing_shortcut_invariance(device, root, name):
 @pytest.mark.parametrize("name", ["diamond_scene.json", "materials.json"])
 def test_face_normal_table_invariance(device, root, name):
     """World-space face normals precomputed at upload (the host restates
-    make_triangle in float with the device's operation order) render the
-    same image bit for bit as normals computed per hit."""
+    make_triangle in float with the device's operation order) and the per-face
+    shading records (vertex normals and indices in one record, option
+    face_shade) render the same image bit for bit as normals computed per hit
+    from the index and normal tables."""
     sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", name))
     imgs = []
     try:
-        for fnt in (0, 1):
+        for fnt, fsh in ((0, 0), (1, 0), (0, 1), (1, 1)):
             device.set_option("face_normals", fnt)
+            device.set_option("face_shade", fsh)
             device.upload(sc)
             imgs.append(render_gpu(device, sc, 160, 120, 4))
     finally:
         device.set_option("face_normals", 1)
-    np.testing.assert_array_equal(imgs[0], imgs[1])
+        device.set_option("face_shade", 1)
+        device.upload(sc)
+    for img in imgs[1:]:
+        np.testing.assert_array_equal(imgs[0], img)
     assert imgs[0].sum() > 0
 
 

@@ -17,7 +17,7 @@ p.width, p.height, p.spi = W, H, 8
 for o in opts:
     for k, v in o.items():
         dev.set_option(k, v)
-    if any(k in ("bvh_width", "bvh_leaf_size", "spatial_splits", "sah_node_cost_pct", "rebuild_bvh", "enclosing", "bvh_bins", "face_normals", "bvh_quantize") for k in o):
+    if any(k in ("bvh_width", "bvh_leaf_size", "spatial_splits", "sah_node_cost_pct", "rebuild_bvh", "enclosing", "bvh_bins", "face_normals", "face_shade", "bvh_quantize") for k in o):
         dev.upload(scene)
     dev.clear()
     dev.render_iterations(p, iters)  # warm-up, buffers sized
