@@ -168,6 +168,7 @@ struct FrameArgs {
     int shadow_classes;  // shadow rays crossing an enclosing entity's box go to the back of their shard (shadow_class_b)
     int reverse;         // k_extend: a shard's positions are taken from its end (class C, then B, then A:
                          // the groups whose paths run longest start first, the short ones fill the launch's end)
+    int probe_sample;    // test hook (option "probe_sample"): 0 = k_resolve adds every sample; s + 1 = sample s only
 };
 
 // path slot -> (local pixel, sample, iteration): slots run over the chunk's
@@ -1536,6 +1537,7 @@ __global__ void __launch_bounds__(64 * RES_G) k_resolve(FrameArgs fa, const floa
             float r = 0, g = 0, b = 0;
 #pragma unroll 8
             for (int s = 0; s < fa.spi; ++s) {
+                if (fa.probe_sample && s != fa.probe_sample - 1) continue; // per-path probes (tests)
                 float4 l = Li[s];
                 r += l.x * fa.inv_spi;
                 g += l.y * fa.inv_spi;
@@ -1823,6 +1825,9 @@ struct igx_device {
     // option "fail_chunk" (test hook): the n-th chunk the chunk scheduler
     // starts from now on fails with IGX_ERR_HIP instead
     int64_t fail_chunk_opt = 0;
+    // option "probe_sample" (test hook): s + 1 = the film receives sample s of
+    // each pixel only (the other paths are traced as usual), 0 = every sample
+    int64_t probe_sample_opt = 0;
 };
 // the worker has queued everything submitted; its first error (part 0)
 igx_status wait_idle(igx_device* dev);
@@ -2509,6 +2514,7 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     }
     else if (k == "concurrent_chunks") dev->concurrent_opt = value != 0 ? 1 : 0;
     else if (k == "async_render") dev->async_opt = value != 0 ? 1 : 0;
+    else if (k == "probe_sample") dev->probe_sample_opt = std::max<int64_t>(0, value);
     else if (k == "fail_chunk") dev->fail_chunk_opt = std::max<int64_t>(0, value);
     else if (k == "face_shade") dev->face_shade_opt = value != 0 ? 1 : 0;
     else if (k == "host_wait_us") dev->host_wait_us = (int)std::max<int64_t>(0, std::min<int64_t>(value, 10000));
@@ -3856,6 +3862,7 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
     fa.shadow_classes = dev->shadow_classes_opt;
     fa.dynamic = dev->dynamic_opt & DYN_EXTEND;
     fa.reverse = fa.dynamic ? (dev->group_order_opt < 0 ? GROUP_ORDER_AUTO : dev->group_order_opt) : 0;
+    fa.probe_sample = dev->probe_sample_opt > 0 && dev->probe_sample_opt <= p->spi ? (int)dev->probe_sample_opt : 0;
     long long local_pixels;
     if (list_mode) {
         // the previous ray list may still be read by a queued tail kernel

@@ -1607,6 +1607,10 @@ static float jac_refr(float eta, float ci, float co) {
 static float prin_g(const oprin* p, v3 wi, v3 wo) {
     return g1_smith_f(&PRIN_IDENTITY, wi, p->ru, p->rv) * g1_smith_f(&PRIN_IDENTITY, wo, p->ru, p->rv);
 }
+/* diffuse lobe of prin_eval_local: 0 the reference's (evalDiffuseTerm,
+ * bsdf/principled.art:117-129); 1 and 2 are what-if models of another
+ * renderer, used ONLY by oracle_principled_eval (tests/golden/cycles_box_model.py) */
+static int prin_diffuse_model = 0;
 static v3 prin_eval_local(const oprin* p, v3 wo, v3 wi) {
     int trans = !hemi_same(wi, wo);
     v3 h = hemi_like(wo, trans ? vnormalize(vadd(wi, vmulf(wo, p->eta))) : vnormalize(vadd(wi, wo)));
@@ -1623,6 +1627,21 @@ static v3 prin_eval_local(const oprin* p, v3 wo, v3 wi) {
             float base_d = (1 - 0.5f * lk) * (1 - 0.5f * vk);
             float rr = (fabsf(vdot(wi, wo)) + 1) * (p->ru + p->rv) / 2;
             float retro = rr * (lk + vk + lk * vk * (rr - 1));
+            if (prin_diffuse_model == 1) {
+                /* Disney 2015's split with R = roughness * (1 + L.V) on the
+                 * roughness input itself (alpha = roughness^2 here) */
+                float rg = sqrtf(0.5f * (p->ru + p->rv));
+                rr = rg * (1 + vdot(wi, wo));
+                retro = rr * (lk + vk + lk * vk * (rr - 1));
+            } else if (prin_diffuse_model == 2) {
+                /* Burley 2012: (1 + (F_D90 - 1) F_L)(1 + (F_D90 - 1) F_V), F_D90 = 0.5 + 2 r cos^2(theta_d) */
+                float rg = sqrtf(0.5f * (p->ru + p->rv));
+                v3 hh = vnormalize(vadd(wi, wo));
+                float cd = vdot(wi, hh);
+                float fd90 = 0.5f + 2 * rg * cd * cd;
+                base_d = (1 + (fd90 - 1) * lk) * (1 + (fd90 - 1) * vk);
+                retro = 0;
+            }
             float ss = 1;
             if (p->thin) {
                 float hl = vdot(wi, h);
@@ -2140,6 +2159,7 @@ static void* worker(void* arg) {
             for (int x = xs; x < xs + T && x < j->x1; ++x) {
                 float r = 0, g = 0, b = 0;
                 for (int smp = 0; smp < j->p->spi; ++smp) {
+                    if (j->p->probe_sample && smp != j->p->probe_sample - 1) continue; /* per-path probe */
                     v3 L = trace_path(j->s, j->p, x, y, smp, x, &ps);
                     r += L.x * inv;
                     g += L.y * inv;
@@ -2250,4 +2270,25 @@ int oracle_intersect_box(const float* bmin3, const float* bmax3, const float* ra
         return 1;
     }
     return 0;
+}
+
+/* Test hook (TEST INFRASTRUCTURE, tests/golden/cycles_box_model.py): the
+ * principled BSDF of material m times the cosine of wi, in the local frame of
+ * a front-facing hit (normal +z), for n direction pairs; `model` selects the
+ * diffuse lobe (prin_diffuse_model): 0 the reference's, 1 Disney 2015's split
+ * on the roughness input, 2 Burley 2012.  out: 3 floats per pair. */
+void oracle_principled_eval(const igx_material* m, int n, const float* wo, const float* wi, int model, float* out) {
+    osurf sf;
+    memset(&sf, 0, sizeof(sf));
+    sf.entering = 1;
+    const oprin p = oprin_make(m, &sf);
+    const int saved = prin_diffuse_model;
+    prin_diffuse_model = model;
+    for (int k = 0; k < n; ++k) {
+        const v3 c = prin_eval_local(&p, V(wo[3 * k], wo[3 * k + 1], wo[3 * k + 2]), V(wi[3 * k], wi[3 * k + 1], wi[3 * k + 2]));
+        out[3 * k] = c.x;
+        out[3 * k + 1] = c.y;
+        out[3 * k + 2] = c.z;
+    }
+    prin_diffuse_model = saved;
 }

@@ -55,6 +55,9 @@ typedef struct oracle_params {
      * shadow stream, splats into the film); 0: each path to its end.  Per
      * path both compute the same radiance; the film sums in another order. */
     int32_t stream;
+    /* per-path probes (tests): 0 = every sample; s + 1 = only sample s of
+     * each pixel enters the film (scaled by 1 / spi as usual; per-path mode) */
+    int32_t probe_sample;
 } oracle_params;
 
 typedef struct oracle_stats {
@@ -86,6 +89,10 @@ int oracle_intersect_box(const float* bmin3, const float* bmax3, const float* ra
 /* RNG helpers exposed for tests (core/random.art). */
 uint32_t oracle_random_seed(int32_t sample, int32_t iter, int32_t frame, int32_t x, int32_t y, int32_t user);
 float oracle_next_f32(uint32_t seed, uint32_t* counter);
+/* principled BSDF * cos(wi) in a front-facing local frame (normal +z), n pairs,
+ * diffuse lobe `model` (0 the reference's, 1 Disney 2015 split on the
+ * roughness input, 2 Burley 2012; tests/golden/cycles_box_model.py) */
+void oracle_principled_eval(const igx_material* m, int n, const float* wo, const float* wi, int model, float* out);
 
 #ifdef __cplusplus
 }

@@ -16,7 +16,8 @@ class Params(C.Structure):
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("spi", C.c_int32), ("iteration", C.c_int32),
                 ("frame", C.c_int32), ("seed", C.c_int32), ("threads", C.c_int32),
                 ("x0", C.c_int32), ("y0", C.c_int32), ("x1", C.c_int32), ("y1", C.c_int32),
-                ("num_rays", C.c_int32), ("rays", C.POINTER(C.c_float)), ("stream", C.c_int32)]
+                ("num_rays", C.c_int32), ("rays", C.POINTER(C.c_float)), ("stream", C.c_int32),
+                ("probe_sample", C.c_int32)]
 
 
 class OStats(C.Structure):
@@ -70,12 +71,16 @@ class OracleScene:
             raise RuntimeError("oracle_scene_create failed")
 
     def render(self, width, height, spi, iteration=0, frame=0, seed=0, threads=0, window=None, fb=None,
-               rays=None, stream=False):
+               rays=None, stream=False, probe_sample=None):
         """One iteration added to fb; stream=True runs the reference CPU
-        device's per-tile wavefront (cpu_trace) instead of one path at a time."""
+        device's per-tile wavefront (cpu_trace) instead of one path at a time;
+        probe_sample=s adds only sample s of each pixel (a per-path probe)."""
         p = Params()
         p.width, p.height, p.spi = width, height, spi
         p.stream = 1 if stream else 0
+        if probe_sample is not None:
+            assert not stream
+            p.probe_sample = probe_sample + 1
         p.iteration, p.frame, p.seed, p.threads = iteration, frame, seed, threads
         if window is not None:
             p.x0, p.y0, p.x1, p.y1 = window
