@@ -837,6 +837,14 @@ static inline void push_children(const onode4* n, const oray* r, sentry* stack, 
     for (int j = 0; j < m; ++j) stack[(*sp)++] = (sentry){ref[j], en[j]};
 }
 
+/* Tie rule at equal distance: 0 the larger (entity, primitive) wins, as on
+ * the device (order-independent); 1 the later-visited hit wins, the
+ * reference's rule (intersection.art:97, traversal/mapping_gpu.art:208:
+ * distance <= hit.distance), which depends on BVH topology and visiting
+ * order.  Test hook: tests/test_oracle.py measures what the rule changes. */
+static int tie_rule_reference = 0;
+void oracle_set_tie_rule(int reference) { tie_rule_reference = reference != 0; }
+
 /* BLAS traversal in entity space (cpu_traverse_helper_prim) */
 static int traverse_blas(const oshape* sh, oray* r, int any, ohit* h, otstats* st) {
     sentry stack[OSTACK];
@@ -859,7 +867,7 @@ static int traverse_blas(const oshape* sh, oray* r, int any, ohit* h, otstats* s
                     /* ties at equal distance: the larger primitive id wins (order-independent
                        rule shared with the device; the reference keeps the later-visited
                        triangle, intersection.art:97, which depends on BVH topology) */
-                    if (t == r->tmax && !((int)sh->bvh.order[first + k] > h->prim)) continue;
+                    if (!tie_rule_reference && t == r->tmax && !((int)sh->bvh.order[first + k] > h->prim)) continue;
                     r->tmax = t;
                     h->t = t;
                     h->u = u;
@@ -924,7 +932,7 @@ static int trace_scene(const oracle_scene* s, const oray* ray_in, int any, ohit*
             } else {
                 got = traverse_blas(sh, &lr, any, &lh, st);
             }
-            if (got && lh.prim != -1 && (lh.t < hit->t || (lh.t == hit->t && eid > hit->ent))) {
+            if (got && lh.prim != -1 && (lh.t < hit->t || (lh.t == hit->t && (tie_rule_reference || eid > hit->ent)))) {
                 hit->ent = eid;
                 hit->prim = lh.prim;
                 hit->t = lh.t;

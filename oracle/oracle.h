@@ -92,6 +92,9 @@ float oracle_next_f32(uint32_t seed, uint32_t* counter);
 /* principled BSDF * cos(wi) in a front-facing local frame (normal +z), n pairs,
  * diffuse lobe `model` (0 the reference's, 1 Disney 2015 split on the
  * roughness input, 2 Burley 2012; tests/golden/cycles_box_model.py) */
+/* tie rule at equal distance: 0 larger (entity, primitive) wins (the
+ * device's), 1 the later-visited hit wins (the reference's); process-wide */
+void oracle_set_tie_rule(int reference);
 void oracle_principled_eval(const igx_material* m, int n, const float* wo, const float* wi, int model, float* out);
 
 #ifdef __cplusplus
