@@ -1798,9 +1798,11 @@ struct igx_device {
     int* spill_main2 = nullptr;
     hipStream_t shadow_stream = nullptr; // split schedule: shadow rays of bounce b overlap the trace of bounce b + 1
     int overlap_shadow_opt = 1;           // option "overlap_shadow" (0/1)
-    // option "speculative": k_trace_refill with speculative while-while (VARIANT_SPEC):
-    // soup-16M 1-iteration frame 76.4 -> 75.6, soup-1M 100.2 -> 98.2 ms, bit-identical
-    int spec_opt = 1;
+    // option "speculative": k_trace_refill with speculative while-while (VARIANT_SPEC).
+    // Round 3 measured soup-16M 76.4 -> 75.6 ms; with the round-5 kernels it is
+    // slower (soup-16M 61.6 -> 62.7 ms) and it changed 2-3 of 10^6 S-deep pixels
+    // (by <= 3.6e-5) from run to run, so it is off (DESIGN_EXPERIMENTS.md)
+    int spec_opt = 0;
     // streams
     Slot slots[2];
     int next_slot = 0;
@@ -1821,7 +1823,7 @@ struct igx_device {
     struct AsyncRender* async = nullptr;
     // option "host_wait_us": the chunk scheduler's host thread sleeps this long
     // between polls that found no progress (after a few yields); 0 = yield only
-    int host_wait_us = 0;
+    int host_wait_us = 20;
     // option "fail_chunk" (test hook): the n-th chunk the chunk scheduler
     // starts from now on fails with IGX_ERR_HIP instead
     int64_t fail_chunk_opt = 0;
@@ -3304,7 +3306,10 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     dev->cam_desc = desc->camera;
     dev->sv = sv;
     // stack: TLAS pushes + BLAS pushes (the depth for BVH2) + marker + resume entry + exit sentinel
-    dev->scene_depth = tlas_depth + blas_depth + 3;
+#ifndef IGX_STACK_SLACK
+#define IGX_STACK_SLACK 0
+#endif
+    dev->scene_depth = tlas_depth + blas_depth + 3 + IGX_STACK_SLACK;
     if (dev->scene_depth > MAX_STACK) {
         free_scene(dev);
         return fail(dev, IGX_ERR_UNSUPPORTED, "BVH too deep for the traversal stack (" + std::to_string(dev->scene_depth) + " entries)");
