@@ -441,8 +441,7 @@ __device__ __forceinline__ int path_class(int classify, const SceneView& sv, con
     }
 }
 
-__device__ __forceinline__ PathState load_path(const PathBuf& in, int i) {
-    float4 p0 = in.p0[i], p1 = in.p1[i], p2 = in.p2[i];
+__device__ __forceinline__ PathState path_from_records(float4 p0, float4 p1, float4 p2, float2 p3) {
     PathState s;
     s.o = f3of(p0);
     s.d = f3of(p1);
@@ -454,10 +453,12 @@ __device__ __forceinline__ PathState load_path(const PathBuf& in, int i) {
     s.counter = cd & 0xFFFFFFu;
     s.contrib = f3of(p2);
     s.inv_pdf = p2.w;
-    const float2 p3 = in.p3[i];
     s.eta = p3.x;
     s.seed = __float_as_uint(p3.y);
     return s;
+}
+__device__ __forceinline__ PathState load_path(const PathBuf& in, int i) {
+    return path_from_records(in.p0[i], in.p1[i], in.p2[i], in.p3[i]);
 }
 
 __device__ __forceinline__ void store_path(const PathBuf& out, int i, const PathState& s) {
