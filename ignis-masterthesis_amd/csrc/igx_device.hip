@@ -1536,13 +1536,19 @@ __global__ void __launch_bounds__(64 * RES_G) k_resolve(FrameArgs fa, const floa
         if (in && it < fa.chunk_iters) {
             const float4* Li = L + ((size_t)it * fa.chunk_pixels + p) * fa.spi;
             float r = 0, g = 0, b = 0;
+            if (fa.probe_sample) { // per-path probes (tests): sample probe_sample - 1 only
+                const float4 l = Li[fa.probe_sample - 1];
+                r = l.x * fa.inv_spi;
+                g = l.y * fa.inv_spi;
+                b = l.z * fa.inv_spi;
+            } else {
 #pragma unroll 8
-            for (int s = 0; s < fa.spi; ++s) {
-                if (fa.probe_sample && s != fa.probe_sample - 1) continue; // per-path probes (tests)
-                float4 l = Li[s];
-                r += l.x * fa.inv_spi;
-                g += l.y * fa.inv_spi;
-                b += l.z * fa.inv_spi;
+                for (int s = 0; s < fa.spi; ++s) {
+                    float4 l = Li[s];
+                    r += l.x * fa.inv_spi;
+                    g += l.y * fa.inv_spi;
+                    b += l.z * fa.inv_spi;
+                }
             }
             part[w][0][lane] = r;
             part[w][1][lane] = g;
