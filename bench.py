@@ -248,6 +248,7 @@ def isolated_extend(dev, render_frame, roof):
     dev.set_option("concurrent_chunks", 1)
     dev.set_option("timing", 0)
     t_iso = si["ms_extend"] / 1e3 / max(1, si["launches_extend"])
+    roof["_si"] = si  # the same run's k_shadow launches (fused_shadow_roofline; dropped before printing)
     per_launch = roof["algorithmic_bytes_per_launch"]
     roof["isolated"] = {"avg_launch_us": round(t_iso * 1e6, 2),
                         "frac": round(per_launch / t_iso / 1e9 / HBM_PEAK_GBS, 4) if t_iso > 0 else None,
@@ -286,6 +287,52 @@ def shadow_roofline(st, inst, si, scene_key):
            "avg_launch_us": round(t * 1e6, 2), "launches": launches,
            "note": "the kernel's own launches (overlap_shadow 0); 48 B per ray counted as if every shadow ray were unoccluded"}
     rp = load_rocprof(scene_key, True, "k_shadow_refill<")
+    if rp:
+        tr = rp["avg_us"] * 1e-6
+        out["rocprof"] = dict(rp, frac=round(per_launch / tr / 1e9 / HBM_PEAK_GBS, 4),
+                              frac_traffic=round(traffic / tr / 1e9 / HBM_PEAK_GBS, 4) if traffic else None)
+    return out
+
+
+def fused_shadow_roofline(st, inst, si, scene_key):
+    """Roofline object of the fused schedule's any-hit kernel (k_shadow): per
+    shadow ray the 32 B ray read, and for an unoccluded one its 16 B colour plus
+    the 16 B radiance slot read and written (tables: LDS-staged or on chip, no
+    per-ray HBM bytes on the scenes that run fused), over the kernel's own
+    launch time (the concurrent_chunks 0 run `si` of isolated_extend), next to
+    the PMC traffic of the committed profile (profiles/pmc_shadow.json).  The
+    per-class split (stream class A: rays that cross no enclosing entity's box,
+    B: the rest, shadow_class_b) comes from the instrumented pass."""
+    rays = max(1, si["shadow_rays"] - si["tail_shadow_rays"])
+    launches = max(1, si["launches_shadow"])
+    t = si["ms_shadow"] / 1e3 / launches
+    g, it, vi, cy, oc = (list(inst["shadow_class_" + k]) for k in ("groups", "node_iters", "node_visits", "cycles", "occluded"))
+    occl = sum(oc) / max(1, 64 * sum(g))  # occluded share of the k_shadow rays (instrumented pass)
+    per_ray = 32 + 48 * (1 - occl)
+    per_launch = rays * per_ray / launches
+    pmc = load_pmc(1, scene_key, "shadow")
+    traffic = float(pmc["hbm_bytes_per_launch"]) if pmc else None
+    classes = {}
+    for k, name in enumerate(("A", "B")):
+        if g[k] == 0:
+            continue
+        classes[name] = {"groups": g[k], "cycle_share": round(cy[k] / max(1, sum(cy)), 3),
+                         "wave_node_iters_per_group": round(it[k] / g[k], 2),
+                         "simd_efficiency": round(vi[k] / max(1, 64 * it[k]), 3),
+                         "occluded_share": round(oc[k] / (64.0 * g[k]), 3)}
+    out = {"bound": "hbm", "kernel": "k_shadow (any-hit traversal of the fused schedule's shadow rays)",
+           "achieved": round(per_launch / t / 1e9, 1) if t > 0 else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(per_launch / t / 1e9 / HBM_PEAK_GBS, 4) if t > 0 else None, "traffic": traffic,
+           "frac_traffic": round(traffic / t / 1e9 / HBM_PEAK_GBS, 4) if traffic and t > 0 else None,
+           "algorithmic_bytes_per_launch": round(per_launch, 1), "bytes_per_ray": round(per_ray, 1),
+           "traffic_over_algorithmic": round(traffic / per_launch, 2) if traffic and per_launch > 0 else None,
+           "visits_per_ray": {"nodes": round(inst["shadow_node_visits"] / max(1, inst["shadow_rays"]), 2),
+                              "triangles": round(inst["shadow_tri_tests"] / max(1, inst["shadow_rays"]), 2)},
+           "avg_launch_us": round(t * 1e6, 2), "launches": launches, "ms_per_frame": round(si["ms_shadow"], 3),
+           "classes": classes,
+           "note": "the kernel's own launches (concurrent_chunks 0); tables LDS-staged, so the bound is the "
+                   "divergent any-hit walk, not HBM (classes: per shadow stream class, instrumented pass)"}
+    rp = load_rocprof(scene_key, False, "k_shadow<")
     if rp:
         tr = rp["avg_us"] * 1e-6
         out["rocprof"] = dict(rp, frac=round(per_launch / tr / 1e9 / HBM_PEAK_GBS, 4),
@@ -357,6 +404,7 @@ def suite_line(ignis_amd, dev_index, path, spi, iters, size=None, isolated=True)
             dev.render_iterations(p, iters)
         isolated_extend(dev, frame, line["roofline"])
     line["roofline"].pop("_inst", None)
+    line["roofline"].pop("_si", None)
     dev.close()
     del scene
     return line
@@ -660,13 +708,18 @@ def main():
     frame_check = rf.check() if n_gpus > 1 and not args.no_check_frame else None
 
     # ---- roofline of the dominant kernel, live HIP-event timing ----
-    roof = roofline(dev, st, lambda: dev.render(params(0)), n_gpus, os.path.splitext(os.path.basename(args.scene))[0])
-    roof.pop("_inst", None)
+    scene_key = os.path.splitext(os.path.basename(args.scene))[0]
+    roof = roofline(dev, st, lambda: dev.render(params(0)), n_gpus, scene_key)
+    inst = roof.pop("_inst", None)
+    roof_shadow = None
     if args.isolated and st["launches_trace"] == 0:
         def frame():
             dev.clear()
             dev.render_iterations(params(0), iters)
         isolated_extend(dev, frame, roof)
+        si = roof.pop("_si")
+        if n_gpus == 1 and si["launches_shadow"] > 0:
+            roof_shadow = fused_shadow_roofline(st, inst, si, scene_key)
     roof["note"] = ("achieved counts the HBM bytes the kernel must move (path / radiance / shadow-ray streams; "
                     "table reads too when the tables exceed the Infinity Cache); traffic is the rocprofv3 PMC "
                     "measurement of the same kernel and workload; memory_system_gbs counts every table read "
@@ -726,6 +779,7 @@ def main():
                           "finish": round(st["ms_finish"], 3),
                           "generate": round(st["ms_generate"], 3), "resolve": round(st["ms_resolve"], 3)},
             "roofline": roof,
+            "roofline_shadow": roof_shadow,
             "cpu_baseline": cpu,
             "parity": parity,
             "suite": suite,

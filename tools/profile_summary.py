@@ -80,6 +80,7 @@ def kernel_stats(src_dir, tag, second_half=False):
 def pmc_file(kernel, scene):
     """profiles/pmc_<kernel>[_<scene>].json (bench.py's load_pmc reads the same name)."""
     k = kernel[2:] if kernel.startswith("k_") else kernel
+    k = k.rstrip("<")
     return f"pmc_{k}.json" if scene == "diamond_scene" else f"pmc_{k}_{scene}.json"
 
 
@@ -198,7 +199,13 @@ if __name__ == "__main__":
     if os.path.isdir(os.path.join(out, "cal_fetch")):
         calibration(os.path.join(out, "cal_fetch"), os.path.join(out, "cal_write"), os.path.join(out, "cal_trace"),
                     os.path.join(out, "cal_fetch.log"), tag)
-    pmc(os.path.join(out, "pmc_fetch"), os.path.join(out, "pmc_write"))
+    # the headline's counter passes (tools/gpu_lib.sh gpu_pmc, tag headline)
+    pf, pw = (os.path.join(out, f"pmc_headline_{k}") for k in ("fetch", "write"))
+    if not os.path.isdir(pf):
+        pf, pw = os.path.join(out, "pmc_fetch"), os.path.join(out, "pmc_write")
+    pmc(pf, pw)
+    # the fused schedule's any-hit kernel from the same counter passes (bench.py fused_shadow_roofline)
+    pmc(pf, pw, kernel="k_shadow<")
     if os.path.isdir(os.path.join(out, "pmc_fetch_soup")):
         # global-table scenes run split: k_trace (persistent-lane k_trace_refill) is the dominant kernel
         pmc(os.path.join(out, "pmc_fetch_soup"), os.path.join(out, "pmc_write_soup"), kernel="k_trace", scene="s_soup_16m")
