@@ -147,12 +147,16 @@ struct ShadowBuf {
     float4* s1; // dir.xyz, tmax
     float4* s2; // colour.rgb, -
     int shard_cap;
+    float4* aov_nee; // "NEE Weights" per path slot (technique aov_mis), nullptr: off
 };
 struct HitBuf {
     float4* h;  // t, u, v, entity (int bits; -1 = miss)
     int* prim;  // primitive id
 };
 
+#ifndef IGX_AOV
+#define IGX_AOV 1 // 0: experiment builds without the AOV code (its cost on the default path)
+#endif
 struct FrameArgs {
     int width, height, spi, iter, frame, seed;
     int tile_size, tile_offset, tile_stride, tiles_x;
@@ -169,6 +173,12 @@ struct FrameArgs {
     int reverse;         // k_extend: a shard's positions are taken from its end (class C, then B, then A:
                          // the groups whose paths run longest start first, the short ones fill the launch's end)
     int probe_sample;    // test hook (option "probe_sample"): 0 = k_resolve adds every sample; s + 1 = sample s only
+    // the path tracer's MIS AOVs (technique aov_mis, PathTechnique.cpp:16-25):
+    // per path slot beside L, "Direct Weights" = emission hits and misses
+    // (pathtracer.art:128,158), "NEE Weights" = unoccluded shadow rays (:206);
+    // nullptr: off (the default path pays one scalar branch per add)
+    float4* aov_di;
+    float4* aov_nee;
 };
 
 // path slot -> (local pixel, sample, iteration): slots run over the chunk's
@@ -347,6 +357,7 @@ __global__ void __launch_bounds__(BLOCK) k_generate(FrameArgs fa, SceneView sv, 
     if (blockIdx.x == 0 && threadIdx.x < NSH) cnt0[threadIdx.x * CSTRIDE] = gen_shard_count(n, threadIdx.x);
     for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
         L[i] = make_float4(0, 0, 0, 0);
+        if (IGX_AOV && fa.aov_di) fa.aov_di[i] = fa.aov_nee[i] = make_float4(0, 0, 0, 0);
         const GenPath g = gen_path(fa, sv, i);
         const int e = gen_index(i, out.shard_cap);
         out.p0[e] = make_float4(g.o.x, g.o.y, g.o.z, __int_as_float(i));
@@ -689,6 +700,10 @@ __device__ __forceinline__ void add_radiance(float4* L, int slot, f3 c) {
     float4 l = L[slot];
     L[slot] = make_float4(l.x + c.x, l.y + c.y, l.z + c.z, 0);
 }
+// an AOV's per-path slot (FrameArgs::aov_di / aov_nee; kernel-argument pointer: a scalar branch)
+__device__ __forceinline__ void add_aov(float4* A, int slot, f3 c) {
+    if (IGX_AOV && A) add_radiance(A, slot, c);
+}
 
 // extend_step of the instrumented k_extend (STATS): the trace and shade halves
 // with phase clocks between them (load -> 0, trace -> 1, shade -> 2), and the
@@ -733,7 +748,10 @@ __device__ __forceinline__ bool extend_step_instrumented(const FrameArgs& fa, co
         f3 Lacc;
         bool has_l;
         alive = shade_step<variant_full(V), true>(fa, sv, ps, hit_ent, hit_prim, tmax, hu, hv, Lacc, has_l, has_shadow, sr, &st);
-        if (has_l) add_radiance(L, ps.slot, Lacc);
+        if (has_l) {
+            add_radiance(L, ps.slot, Lacc);
+            add_aov(fa.aov_di, ps.slot, Lacc);
+        }
     }
     const unsigned long long c_sh = st.cyc[2];
     phase_mark(st, t_last, 2);
@@ -912,6 +930,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
                 const int i = ((pos >> 6) << 12) | (s << 6) | (pos & 63);
                 ps = camera_path(fa, sv, i);
                 L[i] = make_float4(0, 0, 0, 0);
+                if (IGX_AOV && fa.aov_di) fa.aov_di[i] = fa.aov_nee[i] = make_float4(0, 0, 0, 0);
             } else {
                 ps = load_path(in, path_index(in, s, pos, sc));
             }
@@ -919,7 +938,10 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
                 f3 Lacc;
                 bool has_l;
                 alive = extend_step<STATS, V>(fa, sv, ts, ps, Lacc, has_l, has_shadow, sr, st);
-                if (has_l) add_radiance(L, ps.slot, Lacc);
+                if (has_l) {
+                    add_radiance(L, ps.slot, Lacc);
+                    add_aov(fa.aov_di, ps.slot, Lacc);
+                }
             }
         }
         if constexpr (STATS) {
@@ -1012,7 +1034,10 @@ __global__ void __launch_bounds__(BLOCK) k_shade(FrameArgs fa, SceneView sv, Pat
                 f3 Lacc;
                 bool has_l;
                 alive = shade_step<FULL>(fa, sv, ps, __float_as_int(h.w), prim, h.x, h.y, h.z, Lacc, has_l, has_shadow, sr);
-                if (has_l) add_radiance(L, ps.slot, Lacc);
+                if (has_l) {
+                    add_radiance(L, ps.slot, Lacc);
+                    add_aov(fa.aov_di, ps.slot, Lacc);
+                }
             }
         }
         int dst, sdst;
@@ -1060,14 +1085,19 @@ __global__ void __launch_bounds__(BLOCK) k_finish(FrameArgs fa, SceneView gsv, P
             bool has_l, has_shadow;
             ShadowRec sr;
             bool alive = extend_step<STATS, V>(fa, sv, ts, ps, Lacc, has_l, has_shadow, sr, st);
-            if (has_l) add_radiance(L, ps.slot, Lacc);
+            if (has_l) {
+                add_radiance(L, ps.slot, Lacc);
+                add_aov(fa.aov_di, ps.slot, Lacc);
+            }
             if (has_shadow) {
                 ++shadows;
                 float tm = sr.tmax;
                 int e, p;
                 float u, v;
-                if (!trace_ray<true, STATS, V>(sv, sr.o, sr.d, 0.001f, tm, RAY_SHADOW, ts, e, p, u, v, sst))
+                if (!trace_ray<true, STATS, V>(sv, sr.o, sr.d, 0.001f, tm, RAY_SHADOW, ts, e, p, u, v, sst)) {
                     add_radiance(L, ps.slot, sr.color);
+                    add_aov(fa.aov_nee, ps.slot, sr.color);
+                }
             }
             if (!alive) break;
             ++bounces;
@@ -1178,7 +1208,10 @@ __global__ void __launch_bounds__(BLOCK, FINISH_PAIRS_WAVES) k_finish_pairs(Fram
             }
             // ---- the shadow ray's verdict back to its path lane ----
             const bool occluded = __shfl(sh_trace && t.found, partner) != 0;
-            if (path_lane && had_shadow && !occluded) add_radiance(L, ps.slot, sr.color);
+            if (path_lane && had_shadow && !occluded) {
+                add_radiance(L, ps.slot, sr.color);
+                add_aov(fa.aov_nee, ps.slot, sr.color);
+            }
             if (!__ballot(tracing)) break;
             // ---- shade the hits (path lanes) ----
             bool cont = false, has_shadow = false;
@@ -1186,7 +1219,10 @@ __global__ void __launch_bounds__(BLOCK, FINISH_PAIRS_WAVES) k_finish_pairs(Fram
                 f3 Lacc;
                 bool has_l;
                 cont = shade_step<variant_full(V)>(fa, sv, ps, hit_ent, hit_prim, htmax, hu, hv, Lacc, has_l, has_shadow, sr);
-                if (has_l) add_radiance(L, ps.slot, Lacc);
+                if (has_l) {
+                    add_radiance(L, ps.slot, Lacc);
+                    add_aov(fa.aov_di, ps.slot, Lacc);
+                }
                 if (has_shadow) ++shadows;
                 if (cont) ++bounces;
             }
@@ -1286,6 +1322,7 @@ __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, f
                     l = L[slot];
                 }
                 L[slot] = make_float4(l.x + col.x, l.y + col.y, l.z + col.z, 0); // add_radiance
+                add_aov(sh.aov_nee, slot, f3of(col));
             }
             if ((IGX_KO_SHADOW & 2) && !occl && s0.x == 1.2345f) L[0].x = s1.x; // keep the loads live
         }
@@ -1501,7 +1538,10 @@ __global__ void __launch_bounds__(BLOCK, LDS ? REFILL_WAVES_LDS : (variant_ifif(
         },
         [&](int i, const Trav& t) {
             if (t.found) return;
-            add_radiance(L, __float_as_int(sh.s0[i].w), f3of(sh.s2[i]));
+            const int slot = __float_as_int(sh.s0[i].w);
+            const f3 col = f3of(sh.s2[i]);
+            add_radiance(L, slot, col);
+            add_aov(sh.aov_nee, slot, col);
         },
         st);
     if (STATS) flush_stats<STATS>(st, stats, 4, false);
@@ -1633,6 +1673,8 @@ struct Slot {
     ShadowBuf sh{};
     HitBuf hb{};
     float4* L = nullptr;
+    float4* aov_di = nullptr;  // MIS AOV slots beside L (technique aov_mis): "Direct Weights",
+    float4* aov_nee = nullptr; // "NEE Weights" (FrameArgs::aov_di / aov_nee)
     int* ctr = nullptr;        // device shard counters: row 2b = paths entering bounce b, row 2b+1 = shadow rays of bounce b (CROW ints per row)
     int* pinned = nullptr;     // host mirror
     long long n0 = 0;          // paths generated for the chunk (row 0)
@@ -1820,6 +1862,9 @@ struct igx_device {
     // framebuffer
     float* fb = nullptr;
     size_t fb_count = 0;
+    // MIS AOV films ("Direct Weights", "NEE Weights"; technique aov_mis), fb_count floats each
+    bool aov_on = false;
+    float* aov_fb[2] = {nullptr, nullptr};
     int fb_w = 0, fb_h = 0;
     uint64_t iteration_count = 0;
     // stats
@@ -1914,7 +1959,8 @@ igx_status configure_stack(igx_device* dev) {
 }
 
 void free_slot_buffers(Slot& s) {
-    void* ptrs[] = {s.pa.p0, s.pa.p1, s.pa.p2, s.pa.p3, s.pb.p0, s.pb.p1, s.pb.p2, s.pb.p3, s.sh.s0, s.sh.s1, s.sh.s2, s.L, s.hb.h, s.hb.prim};
+    void* ptrs[] = {s.pa.p0, s.pa.p1, s.pa.p2, s.pa.p3, s.pb.p0, s.pb.p1, s.pb.p2, s.pb.p3, s.sh.s0, s.sh.s1, s.sh.s2, s.L, s.hb.h, s.hb.prim,
+                    s.aov_di, s.aov_nee};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     s.pa = PathBuf{};
@@ -1922,6 +1968,7 @@ void free_slot_buffers(Slot& s) {
     s.sh = ShadowBuf{};
     s.hb = HitBuf{};
     s.L = nullptr;
+    s.aov_di = s.aov_nee = nullptr;
     s.cap = 0;
     s.shard_cap = 0;
 }
@@ -1929,15 +1976,16 @@ void free_slot_buffers(Slot& s) {
 // `hits`: the chunk runs the split schedule, whose k_trace writes a hit
 // record per path (20 B) for k_shade; the fused schedule needs none.
 // `region_c`: three path classes (FrameArgs::classify 4), so each path buffer
-// holds a second set of records for class C (PathBuf::c_base)
-igx_status ensure_slot(igx_device* dev, Slot& s, size_t cap, bool hits, bool region_c) {
+// holds a second set of records for class C (PathBuf::c_base); `aov`: the
+// MIS AOV slots (technique aov_mis)
+igx_status ensure_slot(igx_device* dev, Slot& s, size_t cap, bool hits, bool region_c, bool aov) {
     if (!s.ctr) {
         HIPCHK(hipMalloc((void**)&s.ctr, CTR_INTS * sizeof(int)));
         HIPCHK(hipHostMalloc((void**)&s.pinned, CTR_INTS * sizeof(int), hipHostMallocDefault));
         HIPCHK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
         std::memset(s.pinned, 0, CTR_INTS * sizeof(int));
     }
-    if (s.cap >= cap && (!hits || s.hb.h) && (!region_c || s.pa.c_base)) return IGX_OK;
+    if (s.cap >= cap && (!hits || s.hb.h) && (!region_c || s.pa.c_base) && (!aov || s.aov_di)) return IGX_OK;
     free_slot_buffers(s);
     // shard capacity: a generated chunk puts at most ceil(cap / (64 NSH)) groups
     // of 64 paths in one shard, and a shard's outputs never exceed its inputs
@@ -1953,6 +2001,7 @@ igx_status ensure_slot(igx_device* dev, Slot& s, size_t cap, bool hits, bool reg
     s.pa.c_base = s.pb.c_base = region_c ? (int)recs : 0;
     if ((st = alloc4(&s.sh.s0, recs)) || (st = alloc4(&s.sh.s1, recs)) || (st = alloc4(&s.sh.s2, recs))) return st;
     if ((st = alloc4(&s.L, cap))) return st; // radiance is indexed by path slot, not sharded
+    if (aov && ((st = alloc4(&s.aov_di, cap)) || (st = alloc4(&s.aov_nee, cap)))) return st;
     if (hits) {
         if ((st = alloc4(&s.hb.h, recs))) return st;
         HIPCHK(hipMalloc((void**)&s.hb.prim, recs * sizeof(int)));
@@ -2469,6 +2518,8 @@ extern "C" igx_status igx_destroy(igx_device* dev) {
         for (auto& e : s.ev_pool) (void)hipEventDestroy(e);
     }
     if (dev->fb) (void)hipFree(dev->fb);
+    for (float* a : dev->aov_fb)
+        if (a) (void)hipFree(a);
     if (dev->dstats) (void)hipFree(dev->dstats);
     if (dev->tail_counts) (void)hipFree(dev->tail_counts);
     if (dev->ray_list) (void)hipFree(dev->ray_list);
@@ -3311,6 +3362,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     sv.nee = desc->technique.nee;
     sv.clamp = desc->technique.clamp;
     dev->cam_desc = desc->camera;
+    dev->aov_on = desc->technique.aov_mis != 0;
     dev->sv = sv;
     // stack: TLAS pushes + BLAS pushes (the depth for BVH2) + marker + resume entry + exit sentinel
 #ifndef IGX_STACK_SLACK
@@ -3516,7 +3568,7 @@ igx_status ChunkScheduler::step(igx_device* dev, bool& progress) {
                 return fail(dev, IGX_ERR_HIP, "injected failure (option fail_chunk)");
             }
             igx_status st;
-            if ((st = harvest(dev, S)) != IGX_OK || (st = ensure_slot(dev, S, pl.slot_cap, false, pl.fa.classify == 4)) != IGX_OK) {
+            if ((st = harvest(dev, S)) != IGX_OK || (st = ensure_slot(dev, S, pl.slot_cap, false, pl.fa.classify == 4, dev->aov_on)) != IGX_OK) {
                 restore();
                 return st;
             }
@@ -3524,6 +3576,11 @@ igx_status ChunkScheduler::step(igx_device* dev, bool& progress) {
             r.started = true;
             r.slot = k;
             r.fa = pl.fa;
+            // the slot keeps AOV buffers from an earlier aov_mis scene: only
+            // a scene with the AOVs (and their films) writes them
+            r.fa.aov_di = dev->aov_on && dev->aov_fb[0] ? S.aov_di : nullptr;
+            r.fa.aov_nee = dev->aov_on && dev->aov_fb[1] ? S.aov_nee : nullptr;
+            S.sh.aov_nee = r.fa.aov_nee;
             r.fa.iter = pl.iteration + r.it0;
             r.fa.chunk_iters = std::min(pl.iters_per_chunk, pl.count - r.it0);
             r.chunk_pixels = (int)std::min<long long>(pl.chunk_pixels_max, pl.local_pixels - r.px0);
@@ -3645,11 +3702,17 @@ igx_status ChunkScheduler::step(igx_device* dev, bool& progress) {
         SchedItem& r = items.front();
         if (r.clear) {
             IGX_CC(hipMemsetAsync(dev->fb, 0, dev->fb_count * sizeof(float), tail0));
+            for (float* a : dev->aov_fb)
+                if (a) IGX_CC(hipMemsetAsync(a, 0, dev->fb_count * sizeof(float), tail0));
         } else {
             Slot& S = dev->slots[r.slot];
             IGX_CC(hipStreamWaitEvent(tail0, r.fin_ev, 0));
             begin_timed(S, 3, -1, tail0);
             hipLaunchKernelGGL(k_resolve, dim3((r.chunk_pixels + 63) / 64), dim3(64 * RES_G), 0, tail0, r.fa, S.L, dev->fb, r.plan->width);
+            if (r.fa.aov_di) // the MIS AOVs, resolved like the film
+                for (int k = 0; k < 2; ++k)
+                    hipLaunchKernelGGL(k_resolve, dim3((r.chunk_pixels + 63) / 64), dim3(64 * RES_G), 0, tail0, r.fa,
+                                       k ? S.aov_nee : S.aov_di, dev->aov_fb[k], r.plan->width);
             end_timed(S, tail0);
             IGX_CC(hipGetLastError());
             IGX_CC(hipEventRecord(S.done, tail0));
@@ -3847,13 +3910,23 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
 
     // framebuffer (resize clears, as Device::resize)
     size_t fbc = (size_t)width * height * 3;
-    if (dev->fb_w != width || dev->fb_h != height || !dev->fb) {
+    const bool want_aov = dev->aov_on && !list_mode;
+    if (dev->fb_w != width || dev->fb_h != height || !dev->fb || want_aov != (dev->aov_fb[0] != nullptr)) {
         igx_status dst = drain(dev);
         if (dst != IGX_OK) return dst;
         if (dev->fb) HIPCHK(hipFree(dev->fb));
         dev->fb = nullptr;
+        for (float*& a : dev->aov_fb) {
+            if (a) HIPCHK(hipFree(a));
+            a = nullptr;
+        }
         HIPCHK(hipMalloc((void**)&dev->fb, fbc * sizeof(float)));
         HIPCHK(hipMemsetAsync(dev->fb, 0, fbc * sizeof(float), dev->tail_stream));
+        if (want_aov)
+            for (float*& a : dev->aov_fb) {
+                HIPCHK(hipMalloc((void**)&a, fbc * sizeof(float)));
+                HIPCHK(hipMemsetAsync(a, 0, fbc * sizeof(float), dev->tail_stream));
+            }
         dev->fb_w = width;
         dev->fb_h = height;
         dev->fb_count = fbc;
@@ -3991,7 +4064,10 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
         dev->next_slot ^= 1;
         igx_status st = harvest(dev, S); // waits for the chunk that used this slot two chunks ago (one, with one slot)
         if (st != IGX_OK) return st;
-        if ((st = ensure_slot(dev, S, slot_cap, split, fa.classify == 4)) != IGX_OK) return st;
+        if ((st = ensure_slot(dev, S, slot_cap, split, fa.classify == 4, dev->aov_on && !list_mode)) != IGX_OK) return st;
+        fa.aov_di = dev->aov_on && dev->aov_fb[0] && !list_mode ? S.aov_di : nullptr;
+        fa.aov_nee = dev->aov_on && dev->aov_fb[1] && !list_mode ? S.aov_nee : nullptr;
+        S.sh.aov_nee = fa.aov_nee;
 
         auto begin_timed = [&](int kind, int bounce, hipStream_t strm) {
             if (!dev->timing) return;
@@ -4131,6 +4207,10 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
         }
         begin_timed(3, -1, dev->tail_stream);
         hipLaunchKernelGGL(k_resolve, dim3((chunk_pixels + 63) / 64), dim3(64 * RES_G), 0, dev->tail_stream, fa, S.L, dev->fb, width);
+        if (fa.aov_di)
+            for (int k = 0; k < 2; ++k)
+                hipLaunchKernelGGL(k_resolve, dim3((chunk_pixels + 63) / 64), dim3(64 * RES_G), 0, dev->tail_stream, fa,
+                                   k ? S.aov_nee : S.aov_di, dev->aov_fb[k], width);
         end_timed(dev->tail_stream);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(S.done, dev->tail_stream));
@@ -4169,6 +4249,47 @@ extern "C" igx_status igx_get_framebuffer(igx_device* dev, float* host_rgb, size
     igx_status st = drain(dev);
     if (st != IGX_OK) return st;
     HIPCHK(hipMemcpy(host_rgb, dev->fb, count * sizeof(float), hipMemcpyDeviceToHost));
+    return IGX_OK;
+}
+
+// the path tracer's AOVs (Device::getFramebufferForHost(name), Device.cpp:1330-1363):
+// "Color" (or "" / NULL) is the film; "Direct Weights" and "NEE Weights" exist
+// with the technique's aov_mis (PathTechnique.cpp:23-27); any other name is an
+// unknown AOV (the reference logs it and returns no data)
+static int aov_index(igx_device* dev, const char* name) {
+    const std::string n = name ? name : "";
+    if (n.empty() || n == "Color") return -1;
+    if (dev->aov_on && n == "Direct Weights") return 0;
+    if (dev->aov_on && n == "NEE Weights") return 1;
+    return -2;
+}
+
+extern "C" igx_status igx_get_aov(igx_device* dev, const char* name, float* host_rgb, size_t count, uint64_t* iteration_count) {
+    if (!dev) return IGX_ERR_INVALID_ARGUMENT;
+    const int k = aov_index(dev, name);
+    if (k == -1) return igx_get_framebuffer(dev, host_rgb, count, iteration_count);
+    if (k == -2) return fail(dev, IGX_ERR_INVALID_ARGUMENT, std::string("unknown aov '") + (name ? name : "") + "'");
+    if (iteration_count) *iteration_count = dev->iteration_count;
+    if (!host_rgb) return IGX_OK;
+    if (!dev->aov_fb[k]) {
+        std::memset(host_rgb, 0, count * sizeof(float));
+        return IGX_OK;
+    }
+    if (count != dev->fb_count) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "aov size mismatch: expected " + std::to_string(dev->fb_count));
+    HIPCHK(hipSetDevice(dev->hip_device));
+    igx_status st = drain(dev);
+    if (st != IGX_OK) return st;
+    HIPCHK(hipMemcpy(host_rgb, dev->aov_fb[k], count * sizeof(float), hipMemcpyDeviceToHost));
+    return IGX_OK;
+}
+
+extern "C" igx_status igx_aov_device_ptr(igx_device* dev, const char* name, float** ptr, size_t* count) {
+    if (!dev || !ptr) return IGX_ERR_INVALID_ARGUMENT;
+    const int k = aov_index(dev, name);
+    if (k == -1) return igx_framebuffer_device_ptr(dev, ptr, count);
+    if (k == -2) return fail(dev, IGX_ERR_INVALID_ARGUMENT, std::string("unknown aov '") + (name ? name : "") + "'");
+    *ptr = dev->aov_fb[k];
+    if (count) *count = dev->aov_fb[k] ? dev->fb_count : 0;
     return IGX_OK;
 }
 
@@ -4230,6 +4351,8 @@ extern "C" igx_status igx_clear(igx_device* dev) {
         HIPCHK(hipSetDevice(dev->hip_device));
         // resolves of queued chunks land on the tail stream; clear behind them
         HIPCHK(hipMemsetAsync(dev->fb, 0, dev->fb_count * sizeof(float), dev->tail_stream));
+        for (float* a : dev->aov_fb)
+            if (a) HIPCHK(hipMemsetAsync(a, 0, dev->fb_count * sizeof(float), dev->tail_stream));
     }
     dev->iteration_count = 0;
     return IGX_OK;

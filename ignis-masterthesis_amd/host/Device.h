@@ -251,20 +251,22 @@ public:
     size_t framebufferHeight() const { return mHeight; }
     bool isInteractive() const { return mSettings.IsInteractive; }
 
+    // the film ("" / "Color") or a named AOV of the technique ("Direct Weights",
+    // "NEE Weights" with aov_mis); an unknown name gives {nullptr, 0}, as the
+    // reference's getAOVImageForHost / ForDevice (Device.cpp:1330-1388)
     AOVAccessor getFramebufferForHost(const std::string& name = "") {
-        if (!name.empty() && name != "Color") return AOVAccessor{nullptr, 0}; // only the colour AOV (Device.cpp:1303-1305)
-        mHostFB.resize(mWidth * mHeight * 3);
+        std::vector<float>& buf = mHostFB[name.empty() ? "Color" : name];
+        buf.resize(mWidth * mHeight * 3);
         uint64_t iters = 0;
-        check(igx_get_framebuffer(mDev, mHostFB.data(), mHostFB.size(), &iters));
-        return AOVAccessor{mHostFB.data(), (size_t)iters};
+        if (igx_get_aov(mDev, name.c_str(), buf.data(), buf.size(), &iters) != IGX_OK) return AOVAccessor{nullptr, 0};
+        return AOVAccessor{buf.data(), (size_t)iters};
     }
     AOVAccessor getFramebufferForDevice(const std::string& name = "") {
-        if (!name.empty() && name != "Color") return AOVAccessor{nullptr, 0};
         float* ptr = nullptr;
         size_t n = 0;
         uint64_t iters = 0;
         check(igx_synchronize(mDev));
-        check(igx_framebuffer_device_ptr(mDev, &ptr, &n));
+        if (igx_aov_device_ptr(mDev, name.c_str(), &ptr, &n) != IGX_OK) return AOVAccessor{nullptr, 0};
         check(igx_get_framebuffer(mDev, nullptr, 0, &iters));
         return AOVAccessor{ptr, (size_t)iters};
     }
@@ -329,7 +331,7 @@ private:
     ShadingCopy mLast;
     igx_camera mCamera{};
     size_t mWidth = 0, mHeight = 0;
-    std::vector<float> mHostFB;
+    std::unordered_map<std::string, std::vector<float>> mHostFB; // per AOV name
     Statistics mStats;
 };
 

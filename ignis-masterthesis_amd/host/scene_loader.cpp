@@ -529,7 +529,7 @@ static void build_scene(SceneStore& S, const Value& doc, const std::string& base
     }
 
     // ---- technique (PathTechnique.cpp:8-17) ----
-    igx_technique tech{64, 2, 0.0f, 1, IGX_SELECT_UNIFORM};
+    igx_technique tech{64, 2, 0.0f, 1, IGX_SELECT_UNIFORM, 0};
     if (const Value* t = doc.find("technique")) {
         Props tp{t};
         std::string type = tp.string("type", "path");
@@ -538,7 +538,7 @@ static void build_scene(SceneStore& S, const Value& doc, const std::string& base
         tech.min_depth = tp.integer("min_depth", 2);
         tech.clamp = tp.number("clamp", 0.0f);
         tech.nee = tp.boolean("nee", true) ? 1 : 0;
-        if (tp.boolean("aov_mis", false)) fail("technique.aov_mis (advanced shadow handling) is not supported");
+        tech.aov_mis = tp.boolean("aov_mis", false) ? 1 : 0; // "Direct Weights" / "NEE Weights" (PathTechnique.cpp:16-27)
         // PathTechnique.cpp (light_selector) -> LoaderLight::generateLightSelector (LoaderLight.cpp:423-453):
         // "hierarchy" and "simple" select their sampler, anything else is the uniform selector
         const std::string sel = tp.string("light_selector", "");

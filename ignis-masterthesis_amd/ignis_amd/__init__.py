@@ -273,10 +273,16 @@ class Device:
         """`count` consecutive iterations from params.iteration (igx_render_iterations)."""
         self._check(self._lib.igx_render_iterations(self._h, C.byref(params), int(count)))
 
-    def framebuffer(self, count):
+    def framebuffer(self, count, name=None):
+        """The film, or a named AOV (igx_get_aov: "Color", and with the
+        technique's aov_mis "Direct Weights" / "NEE Weights")."""
         out = np.zeros(count, dtype=np.float32)
         it = C.c_uint64()
-        self._check(self._lib.igx_get_framebuffer(self._h, out.ctypes.data_as(C.POINTER(C.c_float)), count, C.byref(it)))
+        if name is None:
+            self._check(self._lib.igx_get_framebuffer(self._h, out.ctypes.data_as(C.POINTER(C.c_float)), count, C.byref(it)))
+        else:
+            self._check(self._lib.igx_get_aov(self._h, name.encode(), out.ctypes.data_as(C.POINTER(C.c_float)), count,
+                                              C.byref(it)))
         return out, int(it.value)
 
     def framebuffer_device_ptr(self):
@@ -382,8 +388,10 @@ class Runtime:
         self._iteration += 1
         self._iters += 1
 
-    def getFramebufferForHost(self):
-        fb, it = self.device.framebuffer(self._fb_count)
+    def getFramebufferForHost(self, name=""):
+        """Runtime::getFramebufferForHost(name) (Runtime.cpp:417-435): the
+        film ("" / "Color") or a named AOV of the technique."""
+        fb, it = self.device.framebuffer(self._fb_count, name or None)
         self._iters = it
         return fb.reshape(self.FilmHeight, self.FilmWidth, 3)
 

@@ -65,7 +65,7 @@ class Camera(C.Structure):
 
 class Technique(C.Structure):
     _fields_ = [("max_depth", C.c_int32), ("min_depth", C.c_int32), ("clamp", C.c_float), ("nee", C.c_int32),
-                ("light_selector", C.c_int32)]
+                ("light_selector", C.c_int32), ("aov_mis", C.c_int32)]
 
 
 class SceneDesc(C.Structure):
@@ -146,8 +146,8 @@ EXPORTED_SYMBOLS = [
     "igx_scene_load_file", "igx_scene_load_string", "igx_scene_get_desc", "igx_scene_free", "igx_write_exr",
     "igx_scene_from_database", "igx_scene_find_material", "igx_scene_entity_name",
     "igx_create", "igx_destroy", "igx_last_error", "igx_version", "igx_set_option", "igx_upload_scene",
-    "igx_render", "igx_get_framebuffer", "igx_framebuffer_device_ptr", "igx_pack_tiles", "igx_clear",
-    "igx_get_stats", "igx_reset_stats", "igx_trace_hits", "igx_trace_occlusion", "igx_synchronize", "igx_wait_ready",
+    "igx_render", "igx_get_framebuffer", "igx_framebuffer_device_ptr", "igx_get_aov", "igx_aov_device_ptr",
+    "igx_pack_tiles", "igx_clear", "igx_get_stats", "igx_reset_stats", "igx_trace_hits", "igx_trace_occlusion", "igx_synchronize", "igx_wait_ready",
     "igx_render_iterations", "igx_objscene_create", "igx_objscene_free", "igx_objscene_add",
     "igx_objscene_set_property", "igx_scene_from_objects", "igx_set_camera",
 ]
@@ -203,6 +203,8 @@ def lib():
     L.igx_render_iterations.argtypes = [vp, C.POINTER(RenderParams), C.c_int32]
     L.igx_get_framebuffer.argtypes = [vp, C.POINTER(C.c_float), C.c_size_t, C.POINTER(C.c_uint64)]
     L.igx_framebuffer_device_ptr.argtypes = [vp, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
+    L.igx_get_aov.argtypes = [vp, C.c_char_p, C.POINTER(C.c_float), C.c_size_t, C.POINTER(C.c_uint64)]
+    L.igx_aov_device_ptr.argtypes = [vp, C.c_char_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
     L.igx_pack_tiles.argtypes = [vp, C.POINTER(RenderParams), C.c_void_p, C.c_size_t]
     L.igx_clear.argtypes = [vp]
     L.igx_synchronize.argtypes = [vp]
@@ -213,7 +215,8 @@ def lib():
                                  C.POINTER(C.c_float)]
     L.igx_trace_occlusion.argtypes = [vp, C.POINTER(C.c_float), C.c_int32, C.c_uint32, C.POINTER(C.c_int32)]
     for name in ["igx_create", "igx_destroy", "igx_set_option", "igx_upload_scene", "igx_render", "igx_render_iterations",
-                 "igx_get_framebuffer", "igx_framebuffer_device_ptr", "igx_pack_tiles", "igx_clear",
+                 "igx_get_framebuffer", "igx_framebuffer_device_ptr", "igx_get_aov", "igx_aov_device_ptr",
+                 "igx_pack_tiles", "igx_clear",
                  "igx_synchronize", "igx_wait_ready", "igx_get_stats", "igx_reset_stats", "igx_trace_hits", "igx_trace_occlusion"]:
         getattr(L, name).restype = C.c_int
     _lib = L

@@ -166,6 +166,7 @@ typedef struct igx_technique {
     float clamp;           /* <= 0: no clamping */
     int32_t nee;           /* next-event estimation on */
     int32_t light_selector;/* IGX_SELECT_*: "uniform" (default), "simple" (flux CDF), "hierarchy" (light BVH) */
+    int32_t aov_mis;       /* PathTechnique.cpp:16: the "Direct Weights" / "NEE Weights" AOVs (igx_get_aov) */
 } igx_technique;
 
 typedef struct igx_scene_desc {

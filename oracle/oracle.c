@@ -2025,10 +2025,11 @@ static int path_shade(const oracle_scene* s, opath* q, const ohit* h, v3* Lacc, 
 
 /* One path to its end, bounce by bounce (the per-path form of the loop: the
  * checker's default, bit-identical per path to the wavefront form below) */
-static v3 trace_path(const oracle_scene* s, const oracle_params* p, int x, int y, int sample, int list_index, pstats* ps) {
+static v3 trace_path(const oracle_scene* s, const oracle_params* p, int x, int y, int sample, int list_index, pstats* ps,
+                     v3* Ldirect, v3* Lnee) {
     opath q;
     path_begin(s, p, x, y, sample, list_index, &q, ps);
-    v3 Lsum = V(0, 0, 0);
+    v3 Lsum = V(0, 0, 0), Ld = V(0, 0, 0), Ln = V(0, 0, 0);
     for (;;) {
         ohit h;
         trace_scene(s, &q.ray, 0, &h, &ps->tr);
@@ -2037,12 +2038,18 @@ static v3 trace_path(const oracle_scene* s, const oracle_params* p, int x, int y
         int has_shadow;
         int alive = path_shade(s, &q, &h, &Lacc, &has_shadow, &sr, &scol, ps);
         Lsum = vadd(Lsum, Lacc);
+        Ld = vadd(Ld, Lacc); /* aov_di.splat (pathtracer.art:128,158) */
         if (has_shadow) {
             ohit sh;
-            if (!trace_scene(s, &sr, 1, &sh, &ps->tr)) Lsum = vadd(Lsum, scol);
+            if (!trace_scene(s, &sr, 1, &sh, &ps->tr)) {
+                Lsum = vadd(Lsum, scol);
+                Ln = vadd(Ln, scol); /* aov_nee.splat (pathtracer.art:206) */
+            }
         }
         if (!alive) break;
     }
+    *Ldirect = Ld;
+    *Lnee = Ln;
     return Lsum;
 }
 
@@ -2119,6 +2126,7 @@ static void stream_tile(const oracle_scene* s, const oracle_params* p, float* fb
             const int px = q->x, py = q->y;
             const int alive = path_shade(s, q, &S->hit2[i], &Lacc, &has_shadow, &S->sray[ns], &S->scol[ns], ps);
             splat(fb, width, px, py, Lacc, inv);
+            if (p->aov_direct) splat(p->aov_direct, width, px, py, Lacc, inv);
             if (has_shadow) {
                 S->spix[2 * ns] = px;
                 S->spix[2 * ns + 1] = py;
@@ -2129,7 +2137,10 @@ static void stream_tile(const oracle_scene* s, const oracle_params* p, float* fb
         n = alive_n;
         for (int i = 0; i < ns; ++i) {
             ohit sh;
-            if (!trace_scene(s, &S->sray[i], 1, &sh, &ps->tr)) splat(fb, width, S->spix[2 * i], S->spix[2 * i + 1], S->scol[i], inv);
+            if (!trace_scene(s, &S->sray[i], 1, &sh, &ps->tr)) {
+                splat(fb, width, S->spix[2 * i], S->spix[2 * i + 1], S->scol[i], inv);
+                if (p->aov_nee) splat(p->aov_nee, width, S->spix[2 * i], S->spix[2 * i + 1], S->scol[i], inv);
+            }
         }
     }
 }
@@ -2166,17 +2177,31 @@ static void* worker(void* arg) {
         for (int y = ys; y < ys + T && y < j->y1; ++y)
             for (int x = xs; x < xs + T && x < j->x1; ++x) {
                 float r = 0, g = 0, b = 0;
+                v3 ad = V(0, 0, 0), an = V(0, 0, 0); /* the AOVs' sums, in the same order */
                 for (int smp = 0; smp < j->p->spi; ++smp) {
                     if (j->p->probe_sample && smp != j->p->probe_sample - 1) continue; /* per-path probe */
-                    v3 L = trace_path(j->s, j->p, x, y, smp, x, &ps);
+                    v3 Ld, Ln;
+                    v3 L = trace_path(j->s, j->p, x, y, smp, x, &ps, &Ld, &Ln);
                     r += L.x * inv;
                     g += L.y * inv;
                     b += L.z * inv;
+                    ad = V(ad.x + Ld.x * inv, ad.y + Ld.y * inv, ad.z + Ld.z * inv);
+                    an = V(an.x + Ln.x * inv, an.y + Ln.y * inv, an.z + Ln.z * inv);
                 }
                 size_t o = 3 * ((size_t)y * width + x);
                 j->fb[o] += r;
                 j->fb[o + 1] += g;
                 j->fb[o + 2] += b;
+                if (j->p->aov_direct) {
+                    j->p->aov_direct[o] += ad.x;
+                    j->p->aov_direct[o + 1] += ad.y;
+                    j->p->aov_direct[o + 2] += ad.z;
+                }
+                if (j->p->aov_nee) {
+                    j->p->aov_nee[o] += an.x;
+                    j->p->aov_nee[o + 1] += an.y;
+                    j->p->aov_nee[o + 2] += an.z;
+                }
             }
     }
     free(S.q);

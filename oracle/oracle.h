@@ -58,6 +58,11 @@ typedef struct oracle_params {
     /* per-path probes (tests): 0 = every sample; s + 1 = only sample s of
      * each pixel enters the film (scaled by 1 / spi as usual; per-path mode) */
     int32_t probe_sample;
+    /* the path tracer's MIS AOVs (technique aov_mis, PathTechnique.cpp:16-25):
+     * non-null = "Direct Weights" (emission hits and misses, pathtracer.art:128,158)
+     * and "NEE Weights" (unoccluded shadow rays, :206) splat here like the film */
+    float* aov_direct;
+    float* aov_nee;
 } oracle_params;
 
 typedef struct oracle_stats {

@@ -17,7 +17,7 @@ class Params(C.Structure):
                 ("frame", C.c_int32), ("seed", C.c_int32), ("threads", C.c_int32),
                 ("x0", C.c_int32), ("y0", C.c_int32), ("x1", C.c_int32), ("y1", C.c_int32),
                 ("num_rays", C.c_int32), ("rays", C.POINTER(C.c_float)), ("stream", C.c_int32),
-                ("probe_sample", C.c_int32)]
+                ("probe_sample", C.c_int32), ("aov_direct", C.POINTER(C.c_float)), ("aov_nee", C.POINTER(C.c_float))]
 
 
 class OStats(C.Structure):
@@ -71,10 +71,12 @@ class OracleScene:
             raise RuntimeError("oracle_scene_create failed")
 
     def render(self, width, height, spi, iteration=0, frame=0, seed=0, threads=0, window=None, fb=None,
-               rays=None, stream=False, probe_sample=None):
+               rays=None, stream=False, probe_sample=None, aov=None):
         """One iteration added to fb; stream=True runs the reference CPU
         device's per-tile wavefront (cpu_trace) instead of one path at a time;
-        probe_sample=s adds only sample s of each pixel (a per-path probe)."""
+        probe_sample=s adds only sample s of each pixel (a per-path probe);
+        aov = {"Direct Weights": array, "NEE Weights": array} (float32, the
+        film's size) receives the path tracer's MIS AOVs the same way."""
         p = Params()
         p.width, p.height, p.spi = width, height, spi
         p.stream = 1 if stream else 0
@@ -92,6 +94,11 @@ class OracleScene:
             n = rays.shape[0]
         if fb is None:
             fb = np.zeros(n * 3, dtype=np.float32)
+        for key, field in (("Direct Weights", "aov_direct"), ("NEE Weights", "aov_nee")):
+            if aov is not None and key in aov:
+                a = aov[key]
+                assert a.dtype == np.float32 and a.size == n * 3 and a.flags["C_CONTIGUOUS"]
+                setattr(p, field, fptr(a))
         st = OStats()
         rc = lib().oracle_render(self._h, C.byref(p), fptr(fb), C.byref(st))
         if rc != 0:

@@ -504,6 +504,59 @@ def test_face_normal_table_invariance(device, root, name):
     assert imgs[0].sum() > 0
 
 
+AOV_CONFIGS = [{}, {"fuse_generate": 0}, {"concurrent_chunks": 0}, {"tail_threshold": 0}, {"tail_threshold": 1 << 30},
+               {"split": 1}, {"lds_scene_max": 0, "split": 1, "refill": 1, "tail_pairs": 1, "tail_threshold": 0},
+               {"lds_scene_max": 0, "split": 1, "refill": 1, "tail_pairs": 1}]
+
+
+@pytest.mark.parametrize("name,plain", [("primitives_aov.json", "primitives.json"), ("diamond_scene_uniform.json", None)])
+def test_mis_aovs(device, root, name, plain):
+    """The path tracer's MIS AOVs (technique aov_mis, PathTechnique.cpp:16-27;
+    the reference's own AOV scenes): "Direct Weights" collects emission hits
+    and misses (pathtracer.art:128,158), "NEE Weights" the unoccluded shadow
+    rays (:206).  The film is bit-identical to the same scene without the
+    AOVs; the two AOVs sum to the film up to float rounding; every schedule
+    (fused / generate pass / sequential chunks / tail kernels / split /
+    persistent-lane global-table kernels with lane-pair tails) gives the same
+    AOVs bit for bit; and they match the oracle's per-path split (RelSE as the
+    film's parity bound).  An unknown AOV name is an error."""
+    w, h, spi = 160, 120, 4
+    sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", name))
+    assert sc.desc.technique.aov_mis == 1
+    films, aovs = [], []
+    try:
+        for cfg in AOV_CONFIGS:
+            for k, v in cfg.items():
+                device.set_option(k, v)
+            films.append(render_gpu(device, sc, w, h, spi))
+            aovs.append([device.framebuffer(w * h * 3, n)[0] for n in ("Direct Weights", "NEE Weights")])
+            for k in cfg:
+                device.set_option(k, {"fuse_generate": 1, "concurrent_chunks": 1, "tail_threshold": -1, "split": -1,
+                                      "lds_scene_max": 48 * 1024, "refill": -1, "tail_pairs": -1}[k])
+        with pytest.raises(RuntimeError):
+            device.framebuffer(w * h * 3, "Normals")
+    finally:
+        for k, v in (("fuse_generate", 1), ("concurrent_chunks", 1), ("tail_threshold", -1), ("split", -1),
+                     ("lds_scene_max", 48 * 1024), ("refill", -1), ("tail_pairs", -1)):
+            device.set_option(k, v)
+    for f, a in zip(films[1:], aovs[1:]):
+        np.testing.assert_array_equal(films[0], f)
+        np.testing.assert_array_equal(aovs[0][0], a[0])
+        np.testing.assert_array_equal(aovs[0][1], a[1])
+    di, nee = aovs[0]
+    assert di.sum() > 0 and nee.sum() > 0
+    np.testing.assert_allclose(di + nee, films[0], rtol=1e-5, atol=1e-6)
+    if plain:
+        ref = render_gpu(device, ignis_amd.Scene.from_file(os.path.join(root, "scenes", plain)), w, h, spi)
+        np.testing.assert_array_equal(films[0], ref)
+    orc = O.OracleScene(sc)
+    od, on = np.zeros(w * h * 3, np.float32), np.zeros(w * h * 3, np.float32)
+    o, _ = orc.render(w, h, spi, threads=16, aov={"Direct Weights": od, "NEE Weights": on})
+    assert rel_mse(films[0], o) <= 5e-3
+    assert rel_mse(di, od) <= 5e-3
+    assert rel_mse(nee, on) <= 5e-3
+
+
 @pytest.mark.parametrize("name", ["diamond_scene.json", "primitives.json", "s_deep.json"])
 @pytest.mark.parametrize("film", [(112, 80), (640, 400)])
 def test_dynamic_groups_invariance(device, root, name, film):

@@ -152,6 +152,35 @@ def test_oracle_stream_mode_equals_per_path(root, name):
     np.testing.assert_array_equal(b, c)  # tiles are independent: thread count does not matter
 
 
+@pytest.mark.parametrize("name,plain", [("primitives_aov.json", "primitives.json"), ("diamond_scene_uniform.json", None)])
+def test_oracle_mis_aovs(root, name, plain):
+    """The path tracer's MIS AOVs in the oracle (the reference's own AOV
+    scenes, technique aov_mis): "Direct Weights" = emission hits and misses
+    (pathtracer.art:128,158), "NEE Weights" = unoccluded shadow rays (:206).
+    They sum to the film up to float rounding, the per-path and the stream
+    (cpu_trace) forms agree, both are non-zero, and the loader reads the flag
+    (without it the film is unchanged)."""
+    sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", name))
+    assert sc.desc.technique.aov_mis == 1
+    o = O.OracleScene(sc)
+    n = 64 * 48 * 3
+    out = []
+    for stream in (False, True):
+        aov = {"Direct Weights": np.zeros(n, np.float32), "NEE Weights": np.zeros(n, np.float32)}
+        fb, _ = o.render(64, 48, 4, threads=4, stream=stream, aov=aov)
+        out.append((fb, aov["Direct Weights"], aov["NEE Weights"]))
+    for fb, di, nee in out:
+        assert di.sum() > 0 and nee.sum() > 0
+        np.testing.assert_allclose(di + nee, fb, rtol=1e-5, atol=1e-6)
+    for a, b in zip(out[0], out[1]):
+        np.testing.assert_allclose(b, a, rtol=2e-6, atol=1e-7)
+    if plain:
+        p = ignis_amd.Scene.from_file(os.path.join(root, "scenes", plain))
+        assert p.desc.technique.aov_mis == 0
+        fb, _ = O.OracleScene(p).render(64, 48, 4, threads=4)
+        np.testing.assert_array_equal(fb, out[0][0])
+
+
 def test_oracle_furnace_sphere():
     """White diffuse closed sphere in a constant environment: every pixel -> 1 (energy conservation)."""
     scene = {
