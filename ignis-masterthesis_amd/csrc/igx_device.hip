@@ -701,8 +701,11 @@ __device__ __forceinline__ void add_radiance(float4* L, int slot, f3 c) {
     L[slot] = make_float4(l.x + c.x, l.y + c.y, l.z + c.z, 0);
 }
 // an AOV's per-path slot (FrameArgs::aov_di / aov_nee; kernel-argument pointer: a scalar branch)
+// ON: compiled in (the wavefront kernels carry it in their full-shading
+// variant only, which an aov_mis scene selects; the shadow kernels always)
+template <bool ON = true>
 __device__ __forceinline__ void add_aov(float4* A, int slot, f3 c) {
-    if (IGX_AOV && A) add_radiance(A, slot, c);
+    if (ON && IGX_AOV && A) add_radiance(A, slot, c);
 }
 
 // extend_step of the instrumented k_extend (STATS): the trace and shade halves
@@ -750,7 +753,7 @@ __device__ __forceinline__ bool extend_step_instrumented(const FrameArgs& fa, co
         alive = shade_step<variant_full(V), true>(fa, sv, ps, hit_ent, hit_prim, tmax, hu, hv, Lacc, has_l, has_shadow, sr, &st);
         if (has_l) {
             add_radiance(L, ps.slot, Lacc);
-            add_aov(fa.aov_di, ps.slot, Lacc);
+            add_aov<variant_full(V)>(fa.aov_di, ps.slot, Lacc);
         }
     }
     const unsigned long long c_sh = st.cyc[2];
@@ -930,7 +933,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
                 const int i = ((pos >> 6) << 12) | (s << 6) | (pos & 63);
                 ps = camera_path(fa, sv, i);
                 L[i] = make_float4(0, 0, 0, 0);
-                if (IGX_AOV && fa.aov_di) fa.aov_di[i] = fa.aov_nee[i] = make_float4(0, 0, 0, 0);
+                if (variant_full(V0) && IGX_AOV && fa.aov_di) fa.aov_di[i] = fa.aov_nee[i] = make_float4(0, 0, 0, 0);
             } else {
                 ps = load_path(in, path_index(in, s, pos, sc));
             }
@@ -940,7 +943,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
                 alive = extend_step<STATS, V>(fa, sv, ts, ps, Lacc, has_l, has_shadow, sr, st);
                 if (has_l) {
                     add_radiance(L, ps.slot, Lacc);
-                    add_aov(fa.aov_di, ps.slot, Lacc);
+                    add_aov<variant_full(V0)>(fa.aov_di, ps.slot, Lacc);
                 }
             }
         }
@@ -1036,7 +1039,7 @@ __global__ void __launch_bounds__(BLOCK) k_shade(FrameArgs fa, SceneView sv, Pat
                 alive = shade_step<FULL>(fa, sv, ps, __float_as_int(h.w), prim, h.x, h.y, h.z, Lacc, has_l, has_shadow, sr);
                 if (has_l) {
                     add_radiance(L, ps.slot, Lacc);
-                    add_aov(fa.aov_di, ps.slot, Lacc);
+                    add_aov<FULL>(fa.aov_di, ps.slot, Lacc);
                 }
             }
         }
@@ -1087,7 +1090,7 @@ __global__ void __launch_bounds__(BLOCK) k_finish(FrameArgs fa, SceneView gsv, P
             bool alive = extend_step<STATS, V>(fa, sv, ts, ps, Lacc, has_l, has_shadow, sr, st);
             if (has_l) {
                 add_radiance(L, ps.slot, Lacc);
-                add_aov(fa.aov_di, ps.slot, Lacc);
+                add_aov<variant_full(V0)>(fa.aov_di, ps.slot, Lacc);
             }
             if (has_shadow) {
                 ++shadows;
@@ -1096,7 +1099,7 @@ __global__ void __launch_bounds__(BLOCK) k_finish(FrameArgs fa, SceneView gsv, P
                 float u, v;
                 if (!trace_ray<true, STATS, V>(sv, sr.o, sr.d, 0.001f, tm, RAY_SHADOW, ts, e, p, u, v, sst)) {
                     add_radiance(L, ps.slot, sr.color);
-                    add_aov(fa.aov_nee, ps.slot, sr.color);
+                    add_aov<variant_full(V0)>(fa.aov_nee, ps.slot, sr.color);
                 }
             }
             if (!alive) break;
@@ -1210,7 +1213,7 @@ __global__ void __launch_bounds__(BLOCK, FINISH_PAIRS_WAVES) k_finish_pairs(Fram
             const bool occluded = __shfl(sh_trace && t.found, partner) != 0;
             if (path_lane && had_shadow && !occluded) {
                 add_radiance(L, ps.slot, sr.color);
-                add_aov(fa.aov_nee, ps.slot, sr.color);
+                add_aov<variant_full(V0)>(fa.aov_nee, ps.slot, sr.color);
             }
             if (!__ballot(tracing)) break;
             // ---- shade the hits (path lanes) ----
@@ -1221,7 +1224,7 @@ __global__ void __launch_bounds__(BLOCK, FINISH_PAIRS_WAVES) k_finish_pairs(Fram
                 cont = shade_step<variant_full(V)>(fa, sv, ps, hit_ent, hit_prim, htmax, hu, hv, Lacc, has_l, has_shadow, sr);
                 if (has_l) {
                     add_radiance(L, ps.slot, Lacc);
-                    add_aov(fa.aov_di, ps.slot, Lacc);
+                    add_aov<variant_full(V0)>(fa.aov_di, ps.slot, Lacc);
                 }
                 if (has_shadow) ++shadows;
                 if (cont) ++bounces;
@@ -3385,6 +3388,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     for (uint32_t l = 0; l < desc->num_lights; ++l)
         if (desc->lights[l].type == IGX_LIGHT_SPHERE || desc->lights[l].type == IGX_LIGHT_MESH) dev->full_shading = true;
     if (textured) dev->full_shading = true; // textures are looked up by the full shading variant only
+    if (dev->aov_on) dev->full_shading = true; // so are the MIS AOVs (add_aov)
     for (uint32_t e = 0; textured && e < desc->num_entities; ++e) {
         const igx_entity& en = desc->entities[e];
         if (desc->materials[en.material].texture != IGX_TEXTURE_NONE && desc->shapes[en.shape].type == IGX_SHAPE_SPHERE) {
