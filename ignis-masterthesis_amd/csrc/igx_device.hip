@@ -119,6 +119,11 @@ constexpr int WAVES_PER_BLOCK = BLOCK / 64;
 #ifndef SHADOW_TREELET
 #define SHADOW_TREELET 1
 #endif
+// k_finish_pairs (the lane-pair tail of global-table scenes) with a treelet
+// (1, option treelet_kernels bit 8) or global node loads only (0)
+#ifndef FINISH_TREELET
+#define FINISH_TREELET 0
+#endif
 // the if-if shadow kernel of the split schedule with a treelet too (1) or
 // with global node loads only (0)
 #ifndef IGX_KO_SHADOW
@@ -1144,7 +1149,7 @@ template <int V0, bool STATS>
 __global__ void __launch_bounds__(BLOCK, FINISH_PAIRS_WAVES) k_finish_pairs(FrameArgs fa, SceneView gsv, PathBuf in, float4* L, const int* cnt,
                                                         int tail_threshold, unsigned long long* stats,
                                                         unsigned long long* tail_counts) {
-    constexpr int V = V0; // global node loads: the tail kernel stages no treelet
+    constexpr int V = FINISH_TREELET ? kernel_variant(V0, false) : V0; // global node loads unless FINISH_TREELET
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
@@ -2408,6 +2413,8 @@ void configure_treelet(igx_device* dev) {
     if (SHADOW_TREELET && (dev->treelet_kernels & 4) && (SHADOW_IFIF_TREELET || !(refill && use_shadow_ifif(dev)))) dev->tree_shadow = fit([&](size_t t) { return shadow_blocks_per_cu<false>(v, 0, refill, t); });
     // k_finish: none -- the tail kernel overlaps the next chunk's kernels, and
     // LDS it holds keeps their blocks off the CU (soup-1M frame +4 % with one)
+    if (FINISH_TREELET && (dev->treelet_kernels & 8) && use_tail_pairs(dev))
+        dev->tree_fin = fit([&](size_t t) { return finish_blocks_per_cu<false>(v, 0, t, true); });
 }
 
 // Film pixels among the chunk's local pixels (tiles at the film's right and
@@ -2550,7 +2557,7 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
         dev->treelet_opt = value;
         dev->tree_dirty = true;
     }
-    else if (k == "treelet_kernels") dev->treelet_kernels = (int)(value & 7);
+    else if (k == "treelet_kernels") dev->treelet_kernels = (int)(value & 15);
     else if (k == "shadow_classes") dev->shadow_classes_opt = value != 0;
     else if (k == "overlap_shadow") dev->overlap_shadow_opt = value != 0;
     else if (k == "bvh_quantize") {
