@@ -124,6 +124,11 @@ constexpr int WAVES_PER_BLOCK = BLOCK / 64;
 #ifndef FINISH_TREELET
 #define FINISH_TREELET 0
 #endif
+// bounce b >= 2 launches a grid sized to the paths entering bounce b - 1 (1)
+// instead of the chunk's first-bounce grid (0)
+#ifndef IGX_LIVE_GRID
+#define IGX_LIVE_GRID 1
+#endif
 // the if-if shadow kernel of the split schedule with a treelet too (1) or
 // with global node loads only (0)
 #ifndef IGX_KO_SHADOW
@@ -835,7 +840,9 @@ __device__ __forceinline__ int take_group(int* work, int& s, uint64_t& done, int
             if (lane_id() == 0) v = atomicAdd(work + s * CSTRIDE, 1);
             v = __builtin_amdgcn_readfirstlane(v);
             if (v * 64 < n) return v;
-            if (lane_id() == 0) atomicOr(done_mask, 1ull << s);
+            // one atomicOr per shard, not one per wave that finds it exhausted
+            if (lane_id() == 0 && !((__hip_atomic_load(done_mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> s) & 1ull))
+                atomicOr(done_mask, 1ull << s);
             done |= 1ull << s;
         }
         unsigned long long m = 0;
@@ -3659,14 +3666,21 @@ igx_status ChunkScheduler::step(igx_device* dev, bool& progress) {
                 begin_timed(S, 0, b, dev->stream);
                 FrameArgs fb = r.fa;
                 fb.gen_n = r.fuse_gen && b == 0 ? (int)r.n : 0;
-                if (inst) launch_extend<true>(dev, S, r.ext_grid, fb, in, out, kc, r.tail);
-                else launch_extend<false>(dev, S, r.ext_grid, fb, in, out, kc, r.tail);
+                // grids sized to the paths known to remain (r.live: the count
+                // entering bounce b - 1, an upper bound for bounce b's paths and
+                // shadow rays): late bounces launch few waves, not a full chip
+                // of waves that find no group (IGX_LIVE_GRID)
+                const long long bound = IGX_LIVE_GRID && b >= 2 ? r.live : r.n;
+                const int ext_grid = IGX_LIVE_GRID ? grid_for(dev, bound, pl.ext_bpc) : r.ext_grid;
+                const int sh_grid = IGX_LIVE_GRID ? grid_for(dev, bound, pl.sh_bpc) : r.sh_grid;
+                if (inst) launch_extend<true>(dev, S, ext_grid, fb, in, out, kc, r.tail);
+                else launch_extend<false>(dev, S, ext_grid, fb, in, out, kc, r.tail);
                 end_timed(S, dev->stream);
                 begin_timed(S, 1, b, dev->stream);
                 int* const sh_work =
                     (dev->dynamic_opt & (use_refill(dev) ? DYN_REFILL_SHADOW : DYN_SHADOW)) ? row(WORK_ROW0 + 4 * b + 2) : nullptr;
-                if (inst) launch_shadow<true>(dev, S, r.sh_grid, row(2 * b + 1), sh_work, dev->stream);
-                else launch_shadow<false>(dev, S, r.sh_grid, row(2 * b + 1), sh_work, dev->stream);
+                if (inst) launch_shadow<true>(dev, S, sh_grid, row(2 * b + 1), sh_work, dev->stream);
+                else launch_shadow<false>(dev, S, sh_grid, row(2 * b + 1), sh_work, dev->stream);
                 end_timed(S, dev->stream);
                 IGX_CC(hipGetLastError());
                 IGX_CC(hipMemcpyAsync(S.pinned + (size_t)(2 * b + 1) * CROW, row(2 * b + 1), 2 * CROW * sizeof(int),
@@ -4123,11 +4137,7 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
             HIPCHK(hipGetLastError());
         }
         S.n0 = n;
-        const int ext_grid = grid_for(dev, n, ext_bpc);
-        const int tr_grid = grid_for(dev, n, tr_bpc);
-        const int shade_grid = grid_for(dev, n, shade_bpc);
         S.split = split;
-        const int sh_grid = grid_for(dev, n, sh_bpc);
         const int fin_grid = grid_for(dev, std::min<long long>(n, tail) * (pairs ? 2 : 1), fin_bpc);
         // Wavefront bounces on the main stream.  The host learns counts two
         // bounces late (async copies, no per-bounce sync); the device gates
@@ -4145,13 +4155,18 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
         hipEvent_t sh_done = nullptr; // the last shadow launch on the shadow stream
         if (n <= tail) switch_b = 0;
         for (int b = 0; switch_b < 0 && b < max_bounces; ++b) {
+            long long bound = n; // paths known to remain (see the concurrent schedule)
             if (b >= 2) {
                 HIPCHK(hipEventSynchronize(S.bounce_ev[b - 2]));
-                if (row_total(S, 2 * (b - 1)) <= tail) {
+                bound = row_total(S, 2 * (b - 1));
+                if (bound <= tail) {
                     switch_b = b - 1;
                     break;
                 }
             }
+            if (!IGX_LIVE_GRID) bound = n;
+            const int ext_grid = grid_for(dev, bound, ext_bpc), tr_grid = grid_for(dev, bound, tr_bpc);
+            const int shade_grid = grid_for(dev, bound, shade_bpc), sh_grid = grid_for(dev, bound, sh_bpc);
             PathBuf in = (b & 1) ? S.pb : S.pa, out = (b & 1) ? S.pa : S.pb;
             KernelCounters kc{row(2 * b), row(2 * (b + 1)), row(2 * b + 1), dev->dstats, row(WORK_ROW0 + 4 * b)};
             if (split) {
