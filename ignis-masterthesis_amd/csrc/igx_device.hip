@@ -204,13 +204,35 @@ __device__ __forceinline__ void slot_coords(const FrameArgs& fa, int slot, int& 
 }
 
 // local pixel -> global (x, y); false if the slot lies outside the film
+// Pixel order of the local pixel index: eight consecutive pixels (one wave's
+// camera group at spi 8) form a 4 x 2 block instead of a 1 x 8 row run, when
+// the width (tile side) is a multiple of 4 and the height even: the group's
+// camera rays then diverge less in the traversal (IGX_PIXEL_BLOCKS).  Every
+// user of the index (generation, resolve, tile packing) maps it here, and a
+// path's arithmetic depends on its pixel only, so the film is the same.
+#ifndef IGX_PIXEL_BLOCKS
+#define IGX_PIXEL_BLOCKS 1
+#endif
+__device__ __forceinline__ void block_order(int r, int w, int& x, int& y) {
+    const int pair = r / (2 * w), q = r - pair * 2 * w; // row pair, index in it
+    x = (q >> 3) * 4 + (q & 3);
+    y = 2 * pair + ((q >> 2) & 1);
+}
+// BLOCKED false: the row-major order (the packed tile layout of igx_pack_tiles)
+template <bool BLOCKED = true>
 __device__ __forceinline__ bool local_to_global(const FrameArgs& fa, int lp, int& x, int& y) {
     if (fa.num_rays > 0) { x = lp; y = 0; return lp < fa.num_rays; }
-    if (fa.tile_size <= 0) { y = lp / fa.width; x = lp - y * fa.width; return true; }
+    if (fa.tile_size <= 0) {
+        if (BLOCKED && IGX_PIXEL_BLOCKS && (fa.width & 3) == 0 && (fa.height & 1) == 0) block_order(lp, fa.width, x, y);
+        else { y = lp / fa.width; x = lp - y * fa.width; }
+        return true;
+    }
     int T = fa.tile_size;
     int k = lp / (T * T);
     int r = lp - k * T * T;
-    int ty = r / T, tx = r - ty * T;
+    int ty, tx;
+    if (BLOCKED && IGX_PIXEL_BLOCKS && (T & 3) == 0) block_order(r, T, tx, ty);
+    else { ty = r / T; tx = r - ty * T; }
     int t = fa.tile_offset + k * fa.tile_stride;
     int tyy = t / fa.tiles_x, txx = t - tyy * fa.tiles_x;
     x = txx * T + tx;
@@ -1632,7 +1654,7 @@ __global__ void k_pack_tiles(FrameArgs fa, const float* fb, float* dst, int num_
     long long total = (long long)num_tiles * T * T;
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
         int x, y;
-        bool in = local_to_global(fa, (int)i, x, y);
+        bool in = local_to_global<false>(fa, (int)i, x, y); // each packed tile row-major
         for (int c = 0; c < 3; ++c) dst[3 * i + c] = in ? fb[3 * ((size_t)y * fa.width + x) + c] : 0.0f;
     }
 }
@@ -2439,6 +2461,11 @@ long long valid_pixels_in_chunk(const FrameArgs& fa) {
         const long long ty = t / fa.tiles_x, tx = t - ty * fa.tiles_x;
         const long long w = std::max(0ll, std::min(T, fa.width - tx * T)), h = std::max(0ll, std::min(T, fa.height - ty * T));
         auto valid_first = [&](long long m) { // valid pixels among the tile's first m
+            if (IGX_PIXEL_BLOCKS && (T & 3) == 0) { // 4 x 2 blocks along row pairs (block_order)
+                const long long pairs = m / (2 * T), q = m - pairs * 2 * T, nb = q / 8, rem = q - nb * 8;
+                const long long y0 = 2 * pairs, c0 = 4 * nb + std::min(rem, 4ll), c1 = 4 * nb + std::max(0ll, rem - 4);
+                return std::min(y0, h) * w + (y0 < h ? std::min(c0, w) : 0) + (y0 + 1 < h ? std::min(c1, w) : 0);
+            }
             const long long rows = m / T;
             return std::min(rows, h) * w + (rows < h ? std::min(m % T, w) : 0);
         };
