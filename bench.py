@@ -329,6 +329,9 @@ def fused_shadow_roofline(st, inst, si, scene_key):
            "visits_per_ray": {"nodes": round(inst["shadow_node_visits"] / max(1, inst["shadow_rays"]), 2),
                               "triangles": round(inst["shadow_tri_tests"] / max(1, inst["shadow_rays"]), 2)},
            "avg_launch_us": round(t * 1e6, 2), "launches": launches, "ms_per_frame": round(si["ms_shadow"], 3),
+           # the timed frames' launches (each shares the chip with the other chunk's k_extend):
+           # what the rocprof average below is over
+           "avg_launch_us_timed": round(st["ms_shadow"] * 1e3 / max(1, st["launches_shadow"]), 2),
            "classes": classes,
            "note": "the kernel's own launches (concurrent_chunks 0); tables LDS-staged, so the bound is the "
                    "divergent any-hit walk, not HBM (classes: per shadow stream class, instrumented pass)"}
