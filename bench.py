@@ -306,8 +306,8 @@ def fused_shadow_roofline(st, inst, si, scene_key):
     rays = max(1, si["shadow_rays"] - si["tail_shadow_rays"])
     launches = max(1, si["launches_shadow"])
     t = si["ms_shadow"] / 1e3 / launches
-    g, it, vi, cy, oc = (list(inst["shadow_class_" + k]) for k in ("groups", "node_iters", "node_visits", "cycles", "occluded"))
-    occl = sum(oc) / max(1, 64 * sum(g))  # occluded share of the k_shadow rays (instrumented pass)
+    g, it, vi, cy, oc, nr = (list(inst["shadow_class_" + k]) for k in ("groups", "node_iters", "node_visits", "cycles", "occluded", "rays"))
+    occl = sum(oc) / max(1, sum(nr))  # occluded share of the k_shadow rays (instrumented pass; partial groups' padding lanes excluded)
     per_ray = 32 + 48 * (1 - occl)
     per_launch = rays * per_ray / launches
     pmc = load_pmc(1, scene_key, "shadow")
@@ -319,7 +319,7 @@ def fused_shadow_roofline(st, inst, si, scene_key):
         classes[name] = {"groups": g[k], "cycle_share": round(cy[k] / max(1, sum(cy)), 3),
                          "wave_node_iters_per_group": round(it[k] / g[k], 2),
                          "simd_efficiency": round(vi[k] / max(1, 64 * it[k]), 3),
-                         "occluded_share": round(oc[k] / (64.0 * g[k]), 3)}
+                         "rays": nr[k], "occluded_share": round(oc[k] / max(1, nr[k]), 3)}
     out = {"bound": "hbm", "kernel": "k_shadow (any-hit traversal of the fused schedule's shadow rays)",
            "achieved": round(per_launch / t / 1e9, 1) if t > 0 else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(per_launch / t / 1e9 / HBM_PEAK_GBS, 4) if t > 0 else None, "traffic": traffic,
@@ -333,8 +333,9 @@ def fused_shadow_roofline(st, inst, si, scene_key):
            # what the rocprof average below is over
            "avg_launch_us_timed": round(st["ms_shadow"] * 1e3 / max(1, st["launches_shadow"]), 2),
            "classes": classes,
-           "note": "the kernel's own launches (concurrent_chunks 0); tables LDS-staged, so the bound is the "
-                   "divergent any-hit walk, not HBM (classes: per shadow stream class, instrumented pass)"}
+           "limiter": "the divergent any-hit walk below the HBM roof it is priced against (tables LDS-staged; "
+                      "class B's node loop, see classes)",
+           "note": "the kernel's own launches (concurrent_chunks 0); classes: per shadow stream class, instrumented pass"}
     rp = load_rocprof(scene_key, False, "k_shadow<")
     if rp:
         tr = rp["avg_us"] * 1e-6

@@ -51,26 +51,13 @@ __host__ __device__ constexpr bool variant_ifif(int v) { return (v & 16) != 0; }
 // are staged in LDS (the treelet); node steps below that index read LDS.
 // Set by every kernel instantiation that does not stage the whole table.
 constexpr int VARIANT_TREE = 32;
-// Bit 6: speculative while-while (trav_step_core): a lane that reaches a BLAS
-// leaf postpones it and keeps walking inner nodes until every active lane of
-// the wave holds a leaf (Aila & Laine 2009) -- more node fetches in flight per
-// wave on latency-bound scenes.  Set on k_trace_refill launches only (option
-// "speculative").
-constexpr int VARIANT_SPEC = 64;
 // Bit 7: quantised 4-wide nodes (64 B, node_step4q; host Bvh4QNode) instead of
 // the 128-B 4-wide nodes -- half the node bytes per visit on scenes whose
 // tables stay in global memory.  Set by the upload with bit 1 (option
 // "bvh_quantize").
 constexpr int VARIANT_Q4 = 128;
-// Width of the quantised nodes (build knob): 4 (Bvh4QNode, 64 B) or 8
-// (Bvh8QNode, 128 B, node_step8q).
-#ifndef IGX_QWIDTH
-#define IGX_QWIDTH 4
-#endif
-static_assert(IGX_QWIDTH == 4 || IGX_QWIDTH == 8, "IGX_QWIDTH must be 4 or 8");
 __host__ __device__ constexpr bool variant_q4(int v) { return (v & VARIANT_Q4) != 0; }
 constexpr int32_t REF_EMPTY = (int32_t)0x80000002; // absent child of a 4-wide node (host kEmptyRef)
-__host__ __device__ constexpr bool variant_spec(int v) { return (v & VARIANT_SPEC) != 0; }
 __host__ __device__ constexpr bool variant_tree(int v) { return (v & VARIANT_TREE) != 0; }
 __host__ __device__ constexpr int kernel_variant(int v, bool lds) { return lds ? lds_variant(v, true) : (v | VARIANT_TREE); }
 

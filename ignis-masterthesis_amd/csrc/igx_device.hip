@@ -102,45 +102,24 @@ constexpr int NSH = 64;             // shards per stream (one per lane of the co
 constexpr int CSTRIDE = 16;         // ints between two shard counters: one 64-B atomic line each
 constexpr int CROW = NSH * CSTRIDE; // ints per counter row (one row per stream and bounce)
 constexpr int WAVES_PER_BLOCK = BLOCK / 64;
-// k_trace_refill with an LDS treelet (option treelet_kernels bit 2; it loses:
-// the trace kernel's top nodes stay L2 hits anyway).  0 (default) compiles it
-// without one, so its node fetches are global loads instead of the flat loads
-// that serve LDS and global addresses alike: soup-1M 8-iteration frame
-// 315.8 / 313.5 -> 305.6 / 307.2 ms, soup-16M 118.2 -> 117.9 ms
-// (profiles/r03_ab_trace_global.log)
-#ifndef TRACE_TREELET
-#define TRACE_TREELET 0
-#endif
-// k_extend and the shadow kernels on global-table scenes: LDS treelet (1,
-// option treelet_kernels bits 1 and 4) or none and global node loads (0)
+// k_trace_refill stages no treelet: its top nodes stay L2 hits anyway, and
+// without one its node fetches are global loads instead of the flat loads
+// that serve LDS and global addresses alike (soup-1M 8-iteration frame
+// 315.8 / 313.5 -> 305.6 / 307.2 ms, soup-16M 118.2 -> 117.9 ms;
+// profiles/r03_ab_trace_global.log).  k_finish_pairs stages none either
+// (soup-16M k_finish_pairs 6.0 -> 8.5 ms with one, r05_ab_finish_treelet.log).
+// k_extend and the shadow kernels on global-table scenes: LDS treelet (1)
+// or none and global node loads (0)
 #ifndef EXTEND_TREELET
 #define EXTEND_TREELET 1
 #endif
 #ifndef SHADOW_TREELET
 #define SHADOW_TREELET 1
 #endif
-// k_finish_pairs (the lane-pair tail of global-table scenes) with a treelet
-// (1, option treelet_kernels bit 8) or global node loads only (0)
-#ifndef FINISH_TREELET
-#define FINISH_TREELET 0
-#endif
 // bounce b >= 2 launches a grid sized to the paths entering bounce b - 1 (1)
 // instead of the chunk's first-bounce grid (0)
 #ifndef IGX_LIVE_GRID
 #define IGX_LIVE_GRID 1
-#endif
-// the if-if shadow kernel of the split schedule with a treelet too (1) or
-// with global node loads only (0)
-#ifndef IGX_KO_SHADOW
-#define IGX_KO_SHADOW 0
-#endif
-// k_shadow loads the colour and the radiance slot of a shadow ray before its
-// any-hit walk (1) or after it, for unoccluded rays only (0)
-#ifndef IGX_SHADOW_PREFETCH
-#define IGX_SHADOW_PREFETCH 1
-#endif
-#ifndef SHADOW_IFIF_TREELET
-#define SHADOW_IFIF_TREELET 0
 #endif
 [[maybe_unused]] constexpr int GRID_QUANTUM = NSH / WAVES_PER_BLOCK; // grids are multiples of this: every shard gets the same waves
 
@@ -1178,7 +1157,7 @@ template <int V0, bool STATS>
 __global__ void __launch_bounds__(BLOCK, FINISH_PAIRS_WAVES) k_finish_pairs(FrameArgs fa, SceneView gsv, PathBuf in, float4* L, const int* cnt,
                                                         int tail_threshold, unsigned long long* stats,
                                                         unsigned long long* tail_counts) {
-    constexpr int V = FINISH_TREELET ? kernel_variant(V0, false) : V0; // global node loads unless FINISH_TREELET
+    constexpr int V = V0; // global node loads (no treelet)
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
@@ -1306,7 +1285,7 @@ __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, f
     if (row_total(cnt) == 0) return;
     const SceneView sv = LDS ? stage_scene_lds<BLOCK>(gsv, lds_scene) : stage_treelet<BLOCK>(gsv, lds_scene);
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
-    unsigned long long cls_acc[2][5] = {}; // instrumented: per shadow class groups, wave iterations, visits, cycles, occluded
+    unsigned long long cls_acc[2][6] = {}; // instrumented: per shadow class groups, wave iterations, visits, cycles, occluded, rays
     const WaveWork w = wave_work();
     // groups of 64 shadow rays: grid-stride over the wave's own shard, or
     // (work != nullptr) handed out by take_group
@@ -1342,35 +1321,26 @@ __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, f
             float tmax = s1.w;
             int e, p;
             float u, v;
-            // the ray's colour and its radiance slot are loaded before the walk
-            // (IGX_SHADOW_PREFETCH): their latency (the slot is a scattered read)
-            // overlaps the any-hit traversal instead of following it
-            float4 col = make_float4(0, 0, 0, 0), l = make_float4(0, 0, 0, 0);
-            if constexpr (IGX_SHADOW_PREFETCH && !(IGX_KO_SHADOW & 2)) {
-                col = sh.s2[i];
-                l = L[slot];
-            }
-            // IGX_KO_SHADOW (experiment builds only, wrong images): bit 1 skips the
-            // any-hit walk, bit 2 the radiance update -- what each part costs
-            if (!(IGX_KO_SHADOW & 1)) occl = trace_ray<true, STATS, V>(sv, f3of(s0), f3of(s1), 0.001f, tmax, RAY_SHADOW, ts, e, p, u, v, st);
-            if (!(IGX_KO_SHADOW & 2) && !occl) {
-                if constexpr (!IGX_SHADOW_PREFETCH) {
-                    col = sh.s2[i];
-                    l = L[slot];
-                }
+            // the ray's colour and its radiance slot are loaded before the walk:
+            // their latency (the slot is a scattered read) overlaps the any-hit
+            // traversal instead of following it (diamond shadow time 20.6 ->
+            // 20.3 ms per frame, round 5)
+            const float4 col = sh.s2[i], l = L[slot];
+            occl = trace_ray<true, STATS, V>(sv, f3of(s0), f3of(s1), 0.001f, tmax, RAY_SHADOW, ts, e, p, u, v, st);
+            if (!occl) {
                 L[slot] = make_float4(l.x + col.x, l.y + col.y, l.z + col.z, 0); // add_radiance
                 add_aov(sh.aov_nee, slot, f3of(col));
             }
-            if ((IGX_KO_SHADOW & 2) && !occl && s0.x == 1.2345f) L[0].x = s1.x; // keep the loads live
         }
         if constexpr (STATS) {
             __builtin_amdgcn_s_waitcnt(0);
             const unsigned long long c1 = __builtin_amdgcn_s_memtime();
-            uint32_t visits = st.nodes - ln0, witers = st.wnodes - wn0, occ = occl ? 1 : 0;
+            uint32_t visits = st.nodes - ln0, witers = st.wnodes - wn0, occ = occl ? 1 : 0, nr = pos < sc.n ? 1 : 0;
             for (int off = 32; off > 0; off >>= 1) {
                 visits += __shfl_xor(visits, off);
                 witers += __shfl_xor(witers, off);
                 occ += __shfl_xor(occ, off);
+                nr += __shfl_xor(nr, off);
             }
             // accumulated per wave (lane 0), flushed once at the end: no atomics in the timed region
             if (lane_id() == 0) {
@@ -1379,14 +1349,15 @@ __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, f
                 cls_acc[cls][2] += visits;
                 cls_acc[cls][3] += c1 - c0;
                 cls_acc[cls][4] += occ;
+                cls_acc[cls][5] += nr;
             }
         }
     }
     if constexpr (STATS) {
         if (lane_id() == 0)
             for (int c = 0; c < 2; ++c)
-                for (int k = 0; k < 5; ++k)
-                    if (cls_acc[c][k]) atomicAdd(&stats[40 + 2 * k + c], cls_acc[c][k]);
+                for (int k = 0; k < 6; ++k)
+                    if (cls_acc[c][k]) atomicAdd(&stats[k < 5 ? 40 + 2 * k + c : 70 + c], cls_acc[c][k]);
     }
     if (STATS) flush_stats<STATS>(st, stats, 4, false);
 }
@@ -1513,10 +1484,8 @@ template <int V0, bool STATS, bool LDS>
 __global__ void __launch_bounds__(BLOCK, LDS ? REFILL_WAVES_LDS : (variant_q4(V0) ? REFILL_WAVES_Q4 : REFILL_WAVES)) k_trace_refill(FrameArgs fa, SceneView gsv, PathBuf in, HitBuf hits,
                                                                      const int* cnt, int tail_threshold,
                                                                      unsigned long long* stats, int refill_min, int* work) {
-    // LDS-staged nodes: padded stride; global tables: treelet (device_scene.h),
-    // unless the trace kernel stages none (TRACE_TREELET 0): then its node
-    // fetches are global loads, not the flat loads that serve both spaces
-    constexpr int V = LDS ? kernel_variant(V0, true) : (TRACE_TREELET ? kernel_variant(V0, false) : V0);
+    // LDS-staged nodes: padded stride; global tables: global node loads (no treelet)
+    constexpr int V = LDS ? kernel_variant(V0, true) : V0;
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
@@ -1557,7 +1526,7 @@ __global__ void __launch_bounds__(BLOCK, LDS ? REFILL_WAVES_LDS : (variant_ifif(
     // stepping (the split schedule's scenes), where global node loads beat the
     // treelet's flat loads: soup-1M 32-iteration frame 1179.6 / 1188.1 ->
     // 1154.5 / 1153.5 ms (profiles/r03_ab_treelet_global.log)
-    constexpr int V = LDS ? kernel_variant(V0, true) : ((SHADOW_TREELET && (SHADOW_IFIF_TREELET || !variant_ifif(V0))) ? kernel_variant(V0, false) : V0);
+    constexpr int V = LDS ? kernel_variant(V0, true) : ((SHADOW_TREELET && !variant_ifif(V0)) ? kernel_variant(V0, false) : V0);
     __shared__ int stack_mem[LDS_STACK * BLOCK];
     extern __shared__ float4 lds_scene[];
     const TStack ts = make_tstack(stack_mem, LDS_STACK, gsv.spill);
@@ -1736,7 +1705,7 @@ constexpr int WORK_ROW0 = 2 * MAX_BOUNCES + 4;
 // instrumentation counters (igx_get_stats): 0-12 visit counts, 16-19 k_extend
 // phase clocks, 20-39 k_extend by group class, 40-49 k_shadow by class, 50-53
 // closest-hit node visits in the TLAS and by hot-order rank, 54-69 k_extend
-// shading sub-phase clocks by class
+// shading sub-phase clocks by class, 70-71 k_shadow rays by class
 [[maybe_unused]] constexpr int DSTATS = 80;
 constexpr int CTR_ROWS = WORK_ROW0 + 4 * MAX_BOUNCES;
 // BLAS with more triangles build without spatial splits (load time; their
@@ -1797,18 +1766,16 @@ struct igx_device {
     // register-bound occupancy), recomputed when the scene or option changes.
     // Option "treelet": -1 auto, 0 off, n > 0 at most n nodes
     int tail_pairs_opt = -1;  // k_finish_pairs on global-table scenes (-1 auto = on, 0 off, 1 on)
+    // The treelet kernels are k_extend and k_shadow / k_shadow_refill (not the
+    // if-if variant): primitives 8.89 -> 8.37, S-deep 48.2 -> 45.8, soup-1M
+    // 187.9 -> 184.9 ms per frame
     int64_t treelet_opt = -1;
-    // option "treelet_kernels": bit 1 k_extend, 2 k_trace_refill, 4 k_shadow / k_shadow_refill.  Default 5:
-    // primitives 8.89 -> 8.37, S-deep 48.2 -> 45.8, soup-1M 187.9 -> 184.9 ms per frame; the persistent-lane
-    // trace kernel loses with one (soup-1M trace 100.9 -> 102.6 ms), its top nodes stay L2 hits anyway
-    int treelet_kernels = 5;
     bool tree_dirty = true;
-    int tree_ext = 0, tree_trace = 0, tree_shadow = 0, tree_fin = 0;
+    int tree_ext = 0, tree_shadow = 0;
     int64_t tail_opt = -1;   // paths at or below which k_finish takes over (-1 = auto)
     int64_t tail_last_opt = -1; // the same for the last chunk of a render call, whose tail overlaps nothing (-1 = tail_opt)
     bool fuse_generate = true; // bounce 0 of the fused k_extend builds its camera paths (no k_generate pass)
     int split_opt = -1;      // k_trace + k_shade per bounce instead of the fused k_extend (-1: auto = global-table scenes)
-    int trace_waves = 5;     // occupancy target of k_trace (5 waves per SIMD, anything else = compiler's choice)
     int refill_opt = -1;     // persistent-lane trace / shadow, refilled once this many lanes idle (0: off, -1: auto = 16)
     int shadow_ifif_opt = -1; // if-if stepping in k_shadow_refill (-1: auto = split-schedule scenes)
     int64_t lds_scene_max = 48 * 1024; // stage traversal tables in LDS when they fit (0 = never)
@@ -1884,11 +1851,6 @@ struct igx_device {
     int* spill_main2 = nullptr;
     hipStream_t shadow_stream = nullptr; // split schedule: shadow rays of bounce b overlap the trace of bounce b + 1
     int overlap_shadow_opt = 1;           // option "overlap_shadow" (0/1)
-    // option "speculative": k_trace_refill with speculative while-while (VARIANT_SPEC).
-    // Round 3 measured soup-16M 76.4 -> 75.6 ms; with the round-5 kernels it is
-    // slower (soup-16M 61.6 -> 62.7 ms) and it changed 2-3 of 10^6 S-deep pixels
-    // (by <= 3.6e-5) from run to run, so it is off (DESIGN_EXPERIMENTS.md)
-    int spec_opt = 0;
     // streams
     Slot slots[2];
     int next_slot = 0;
@@ -2155,34 +2117,20 @@ void launch_extend(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, cons
     IGX_DISPATCH_VARIANT8(dev->variant, L_EXT);
 #undef L_EXT
 }
-// k_trace variants: an occupancy target (waves per SIMD, option
-// "trace_waves"), unless the traversal tables are staged in LDS (small
-// scenes), where LDS sets occupancy.
-template <bool STATS, int W>
-void launch_trace_w(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const PathBuf& in, const int* cnt, int tail) {
-#define L_TR(S) hipLaunchKernelGGL((k_trace<S, STATS, W, false>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, s.hb, cnt, tail, dev->dstats)
-    IGX_DISPATCH_VARIANT(dev->variant, L_TR);
-#undef L_TR
-}
+// k_trace (the split schedule without persistent lanes): 5 waves per SIMD on
+// global tables; LDS-staged tables set occupancy themselves
 template <bool STATS>
 void launch_trace(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const PathBuf& in, const int* cnt, int tail,
                   int* work) {
-    SceneView tsv = dev->sv;
-    tsv.tree_n = dev->tree_trace;
     if (use_refill(dev)) {
 #define L_TRR(S)                                                                                                        \
     if (dev->lds_scene_bytes)                                                                                            \
         hipLaunchKernelGGL((k_trace_refill<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->stream, fa, \
                            dev->sv, in, s.hb, cnt, tail, dev->dstats, refill_min(dev), work);                            \
     else                                                                                                                 \
-        hipLaunchKernelGGL((k_trace_refill<S, STATS, false>), dim3(grid), dim3(BLOCK), tree_bytes(dev, tsv.tree_n), dev->stream, \
-                           fa, tsv, in, s.hb, cnt, tail, dev->dstats, refill_min(dev), work)
-#define L_TRRS(S)                                                                                                       \
-    hipLaunchKernelGGL((k_trace_refill<S | VARIANT_SPEC, STATS, false>), dim3(grid), dim3(BLOCK), tree_bytes(dev, tsv.tree_n), \
-                       dev->stream, fa, tsv, in, s.hb, cnt, tail, dev->dstats, refill_min(dev), work)
-        if (!dev->lds_scene_bytes && dev->spec_opt) IGX_DISPATCH_VARIANT(dev->variant, L_TRRS);
-        else IGX_DISPATCH_VARIANT(dev->variant, L_TRR);
-#undef L_TRRS
+        hipLaunchKernelGGL((k_trace_refill<S, STATS, false>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, s.hb, \
+                           cnt, tail, dev->dstats, refill_min(dev), work)
+        IGX_DISPATCH_VARIANT(dev->variant, L_TRR);
 #undef L_TRR
         return;
     }
@@ -2192,8 +2140,9 @@ void launch_trace(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const
 #undef L_TRL
         return;
     }
-    if (dev->trace_waves == 5) launch_trace_w<STATS, 5>(dev, s, grid, fa, in, cnt, tail);
-    else launch_trace_w<STATS, 1>(dev, s, grid, fa, in, cnt, tail);
+#define L_TR(S) hipLaunchKernelGGL((k_trace<S, STATS, 5, false>), dim3(grid), dim3(BLOCK), 0, dev->stream, fa, dev->sv, in, s.hb, cnt, tail, dev->dstats)
+    IGX_DISPATCH_VARIANT(dev->variant, L_TR);
+#undef L_TR
 }
 template <bool STATS>
 void launch_shadow(igx_device* dev, Slot& s, int grid, const int* cnt, int* work, hipStream_t strm) {
@@ -2231,7 +2180,7 @@ template <bool STATS>
 void launch_finish(igx_device* dev, Slot& s, int grid, const FrameArgs& fa, const PathBuf& in, const int* cnt, int tail) {
     SceneView tsv = dev->sv;
     tsv.spill = dev->spill_tail; // k_finish runs concurrently with the main stream's kernels
-    tsv.tree_n = dev->tree_fin;
+    tsv.tree_n = 0;              // the tail kernels stage no treelet
     if (dev->lds_scene_bytes) {
 #define L_FINL(S) hipLaunchKernelGGL((k_finish<S, STATS, true>), dim3(grid), dim3(BLOCK), dev->lds_scene_bytes, dev->tail_stream, fa, tsv, in, s.L, cnt, tail, dev->dstats, dev->tail_counts)
         IGX_DISPATCH_VARIANT8(dev->variant, L_FINL);
@@ -2303,11 +2252,11 @@ int finish_blocks_per_cu(int v, size_t lds, size_t tree, bool pairs) {
     IGX_RESIDENT8(k_finish, STATS);
 }
 template <bool STATS>
-int trace_blocks_per_cu(int v, int waves, size_t lds, bool refill, size_t tree) {
+int trace_blocks_per_cu(int v, size_t lds, bool refill) {
+    const size_t tree = 0; // no treelet (IGX_RES1)
     if (refill) IGX_RESIDENT_G(k_trace_refill);
     if (lds) IGX_RESIDENT(k_trace, STATS, 1);
-    if (waves == 5) IGX_RESIDENT(k_trace, STATS, 5);
-    IGX_RESIDENT(k_trace, STATS, 1);
+    IGX_RESIDENT(k_trace, STATS, 5);
 }
 #undef IGX_RESIDENT
 #undef IGX_RESIDENT8
@@ -2336,7 +2285,7 @@ int shade_blocks_per_cu(bool full) { return full ? resident_blocks(k_shade<true>
 #define IGX_TRACE_HELPERS(X, S)                                                                                      \
     X void launch_trace<S>(igx_device*, Slot&, int, const FrameArgs&, const PathBuf&, const int*, int, int*);              \
     X void launch_shadow<S>(igx_device*, Slot&, int, const int*, int*, hipStream_t);                                       \
-    X int trace_blocks_per_cu<S>(int, int, size_t, bool, size_t);                                                    \
+    X int trace_blocks_per_cu<S>(int, size_t, bool);                                                                  \
     X int shadow_blocks_per_cu<S>(int, size_t, bool, size_t);
 #if IGX_PART == 1
 IGX_EXTEND_HELPERS(template, true)
@@ -2419,7 +2368,7 @@ igx_status drain(igx_device* dev) {
 // blocks per CU (set by its register budget) -- the treelet takes LDS that
 // would otherwise stay unused.  Binary search over hipOccupancy answers.
 void configure_treelet(igx_device* dev) {
-    dev->tree_ext = dev->tree_trace = dev->tree_shadow = dev->tree_fin = 0;
+    dev->tree_ext = dev->tree_shadow = 0;
     dev->tree_dirty = false;
     if (!dev->has_scene || dev->lds_scene_bytes || dev->treelet_opt == 0) return;
     int cap = (int)std::min<size_t>(TREELET_FRONT, (size_t)dev->sv.num_nodes);
@@ -2436,14 +2385,13 @@ void configure_treelet(igx_device* dev) {
         }
         return lo;
     };
-    if (EXTEND_TREELET && (dev->treelet_kernels & 1)) dev->tree_ext = fit([&](size_t t) { return extend_blocks_per_cu<false>(v, 0, t); });
-    if (TRACE_TREELET && refill && (dev->treelet_kernels & 2))
-        dev->tree_trace = fit([&](size_t t) { return trace_blocks_per_cu<false>(v, dev->trace_waves, 0, true, t); });
-    if (SHADOW_TREELET && (dev->treelet_kernels & 4) && (SHADOW_IFIF_TREELET || !(refill && use_shadow_ifif(dev)))) dev->tree_shadow = fit([&](size_t t) { return shadow_blocks_per_cu<false>(v, 0, refill, t); });
-    // k_finish: none -- the tail kernel overlaps the next chunk's kernels, and
-    // LDS it holds keeps their blocks off the CU (soup-1M frame +4 % with one)
-    if (FINISH_TREELET && (dev->treelet_kernels & 8) && use_tail_pairs(dev))
-        dev->tree_fin = fit([&](size_t t) { return finish_blocks_per_cu<false>(v, 0, t, true); });
+    if (EXTEND_TREELET) dev->tree_ext = fit([&](size_t t) { return extend_blocks_per_cu<false>(v, 0, t); });
+    // the if-if shadow kernel of the split schedule: global node loads beat a
+    // treelet's flat loads there (profiles/r03_ab_treelet_global.log)
+    if (SHADOW_TREELET && !(refill && use_shadow_ifif(dev))) dev->tree_shadow = fit([&](size_t t) { return shadow_blocks_per_cu<false>(v, 0, refill, t); });
+    // k_trace_refill and the tail kernels: none -- the tail kernel overlaps the
+    // next chunk's kernels, and LDS it holds keeps their blocks off the CU
+    // (soup-1M frame +4 % with one)
 }
 
 // Film pixels among the chunk's local pixels (tiles at the film's right and
@@ -2591,14 +2539,12 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
         dev->treelet_opt = value;
         dev->tree_dirty = true;
     }
-    else if (k == "treelet_kernels") dev->treelet_kernels = (int)(value & 15);
     else if (k == "shadow_classes") dev->shadow_classes_opt = value != 0;
     else if (k == "overlap_shadow") dev->overlap_shadow_opt = value != 0;
     else if (k == "bvh_quantize") {
         if (value < -1 || value > 1) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "bvh_quantize must be -1 (auto), 0 or 1");
         dev->quantize_opt = (int)value;
     }
-    else if (k == "speculative") dev->spec_opt = value != 0;
     else if (k == "tail_pairs") {
         if (value < -1 || value > 1) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "tail_pairs must be -1 (auto), 0 or 1");
         dev->tail_pairs_opt = (int)value;
@@ -2637,7 +2583,6 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
         if (value < -1 || value > 1) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "shadow_ifif must be -1 (auto), 0 or 1");
         dev->shadow_ifif_opt = (int)value;
     }
-    else if (k == "trace_waves") dev->trace_waves = (int)value;
     else if (k == "refill") {
         if (value < -1 || value > 64) return fail(dev, IGX_ERR_INVALID_ARGUMENT, "refill must be -1 (auto) or in [0, 64]");
         dev->refill_opt = (int)value;
@@ -2709,28 +2654,17 @@ extern "C" igx_status igx_synchronize(igx_device* dev) {
 // nodes keep their relative (depth-first) order.  Every inner-node reference
 // (node children, instance BLAS roots, the TLAS root) is renumbered; the
 // traversal result does not depend on node numbering.
-// `format`: 2 (BVH2, 64 B), 4 (4-wide, 128 B), 5 (quantised 4-wide, 64 B) or
-// 8 (quantised 8-wide, 128 B).
+// `format`: 2 (BVH2, 64 B), 4 (4-wide, 128 B) or 5 (quantised 4-wide, 64 B).
 static void order_hot_nodes(std::vector<float4>& nodes, int format, std::vector<float4>& inst, int& tlas_root, size_t front) {
-    const int nf4 = format == 4 || format == 8 ? 8 : 4;
+    const int nf4 = format == 4 ? 8 : 4;
     const size_t nn = nodes.size() / nf4;
     if (nn == 0 || front == 0) return;
-    const int width = format == 2 ? 2 : format == 8 ? 8 : 4;
+    const int width = format == 2 ? 2 : 4;
     auto ref = [&](size_t n, int k) -> int32_t& {
-        return reinterpret_cast<int32_t*>(&nodes[n * nf4])[format == 4 ? 24 + k : format == 8 ? 20 + k : 12 + k];
+        return reinterpret_cast<int32_t*>(&nodes[n * nf4])[format == 4 ? 24 + k : 12 + k];
     };
     auto box = [&](size_t n, int k, float lo[3], float hi[3]) {
         const float* f = reinterpret_cast<const float*>(&nodes[n * nf4]);
-        if (format == 8) { // origin + code * scale (Bvh8QNode)
-            const uint32_t* u = reinterpret_cast<const uint32_t*>(f);
-            const float sc[3] = {f[3], f[4], f[5]};
-            for (int a = 0; a < 3; ++a) {
-                lo[a] = f[a] + (float)((u[6 + 4 * a + k / 4] >> (8 * (k % 4))) & 255u) * sc[a];
-                hi[a] = f[a] + (float)((u[8 + 4 * a + k / 4] >> (8 * (k % 4))) & 255u) * sc[a];
-            }
-            if (ref(n, k) == igx::kEmptyRef) lo[0] = INFINITY;
-            return;
-        }
         if (format == 5) { // origin + code * scale (Bvh4QNode)
             const uint32_t* u = reinterpret_cast<const uint32_t*>(f);
             const float sc[3] = {f[3], f[4], f[5]};
@@ -2755,7 +2689,7 @@ static void order_hot_nodes(std::vector<float4>& nodes, int format, std::vector<
     // children of node n with the node's likelihood pn: f(child ref, child likelihood)
     auto children = [&](size_t n, double pn, auto&& f) {
         float ulo[3] = {INFINITY, INFINITY, INFINITY}, uhi[3] = {-INFINITY, -INFINITY, -INFINITY};
-        double ak[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        double ak[4] = {0, 0, 0, 0};
         for (int k = 0; k < width; ++k) {
             float lo[3], hi[3];
             box(n, k, lo, hi);
@@ -2944,7 +2878,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     for (const auto& b : brs) est_tri += b.prim_order.size();
     const size_t est_bytes = est_tri * 48 + (size_t)desc->num_entities * 64 + (est_tri / 2 + desc->num_entities) * 128;
     const bool quantize = width == 4 && (dev->quantize_opt == 1 || (dev->quantize_opt < 0 && est_bytes > SPLIT_TABLE_BYTES));
-    const int nf4 = quantize ? (IGX_QWIDTH == 8 ? 8 : 4) : node_f4(width);
+    const int nf4 = quantize ? 4 : node_f4(width);
 
     // ---- phase 2: node, triangle and instance tables ----------------------
     std::vector<float4> nodes; // nf4 float4s per node
@@ -2982,19 +2916,6 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
                 nodes.insert(nodes.end(), f, f + 4);
             }
             need = br.depth;
-        } else if (quantize && IGX_QWIDTH == 8) {
-            igx::Bvh8Result b8 = igx::collapse_bvh8(br);
-            for (auto nd : b8.nodes) {
-                for (int k = 0; k < 8; ++k) {
-                    if (nd.ref[k] >= 0) nd.ref[k] += node_off;
-                    else if (nd.ref[k] != igx::kEmptyRef) nd.ref[k] = move_leaf(nd.ref[k]);
-                }
-                const igx::Bvh8QNode qn = igx::quantize_bvh8(nd);
-                float4 f[8];
-                std::memcpy(f, &qn, 128);
-                nodes.insert(nodes.end(), f, f + 8);
-            }
-            need = b8.stack_need;
         } else {
             igx::Bvh4Result b4 = igx::collapse_bvh4(br);
             for (auto nd : b4.nodes) {
@@ -3353,7 +3274,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     }
 
     // hot nodes first: any prefix of the node array is a treelet (stage_treelet)
-    order_hot_nodes(nodes, quantize ? (IGX_QWIDTH == 8 ? 8 : 5) : width, inst, tlas_root, TREELET_FRONT);
+    order_hot_nodes(nodes, quantize ? 5 : width, inst, tlas_root, TREELET_FRONT);
 
     // ---- upload ----------------------------------------------------------
     SceneView sv{};
@@ -3374,7 +3295,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     sv.tlas_root = tlas_root;
     sv.num_nodes = (int)(nodes.size() / nf4);
     sv.node_f4 = nf4;
-    dev->bvh_width = quantize && IGX_QWIDTH == 8 ? 8 : width; // reported; the variant's width bit is set for 4 and 8
+    dev->bvh_width = width;
     dev->quantized = quantize;
     dev->nf4 = nf4;
     sv.num_inst = (int)(inst.size() / 4);
@@ -4040,9 +3961,11 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
     // -> 179 ms, S-deep 4096^2 865 -> 823 ms from 32 M to 128 M paths
     // (tools/sweep_frame.py).  Per path and slot: two path buffers (56 B a
     // record; twice that with the class-C region), shadow ray 48 B, hit
-    // record 20 B (split schedule), radiance 16 B.
+    // record 20 B (split schedule), radiance 16 B, and the two MIS AOV slots
+    // (32 B) of an aov_mis scene.
     if (split && fa.classify == 4) fa.classify = 3; // hit records have no class-C region
-    const long long path_slot_bytes = 2 * 56 * (fa.classify == 4 ? 2 : 1) + 48 + (split ? 20 : 0) + 16;
+    const long long path_slot_bytes =
+        2 * 56 * (fa.classify == 4 ? 2 : 1) + 48 + (split ? 20 : 0) + 16 + (dev->aov_on && !list_mode ? 32 : 0);
     const long long slot_budget =
         dev->slot_budget_mb > 0 ? dev->slot_budget_mb * (1ll << 20) : (long long)((double)dev->mem_total * 0.3);
     long long auto_chunk_paths = 1ll << 24;
@@ -4066,16 +3989,14 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
     const int ext_bpc = inst ? extend_blocks_per_cu<true>(sd, ldsb, tree_bytes(dev, dev->tree_ext))
                              : extend_blocks_per_cu<false>(sd, ldsb, tree_bytes(dev, dev->tree_ext));
     const bool refill = use_refill(dev);
-    const size_t tr_tree = refill ? tree_bytes(dev, dev->tree_trace) : 0;
-    const int tr_bpc = inst ? trace_blocks_per_cu<true>(sd, dev->trace_waves, dev->lds_scene_bytes, refill, tr_tree)
-                            : trace_blocks_per_cu<false>(sd, dev->trace_waves, dev->lds_scene_bytes, refill, tr_tree);
+    const int tr_bpc = inst ? trace_blocks_per_cu<true>(sd, dev->lds_scene_bytes, refill)
+                            : trace_blocks_per_cu<false>(sd, dev->lds_scene_bytes, refill);
     const bool full = variant_full(sd);
     const int shade_bpc = shade_blocks_per_cu(full);
     const int sh_bpc = inst ? shadow_blocks_per_cu<true>(sd, dev->lds_scene_bytes, refill, tree_bytes(dev, dev->tree_shadow))
                             : shadow_blocks_per_cu<false>(sd, dev->lds_scene_bytes, refill, tree_bytes(dev, dev->tree_shadow));
     const bool pairs = use_tail_pairs(dev);
-    const int fin_bpc = inst ? finish_blocks_per_cu<true>(sd, ldsb, tree_bytes(dev, dev->tree_fin), pairs)
-                             : finish_blocks_per_cu<false>(sd, ldsb, tree_bytes(dev, dev->tree_fin), pairs);
+    const int fin_bpc = inst ? finish_blocks_per_cu<true>(sd, ldsb, 0, pairs) : finish_blocks_per_cu<false>(sd, ldsb, 0, pairs);
 
     if (conc) {
         auto plan = std::make_shared<ChunkPlan>();
@@ -4427,6 +4348,7 @@ extern "C" igx_status igx_get_stats(igx_device* dev, igx_stats* out) {
         out->shadow_class_node_visits[k] = h[44 + k];
         out->shadow_class_cycles[k] = h[46 + k];
         out->shadow_class_occluded[k] = h[48 + k];
+        out->shadow_class_rays[k] = h[70 + k];
     }
     for (int k = 0; k < 16; ++k) out->extend_class_shade_cycles[k] = h[54 + k];
     out->tlas_node_visits = h[50];
@@ -4461,14 +4383,15 @@ extern "C" igx_status igx_get_stats(igx_device* dev, igx_stats* out) {
     out->shadow_blocks_per_cu = dev->has_scene ? shadow_blocks_per_cu<false>(dev->variant, dev->lds_scene_bytes, use_refill(dev),
                                                                             tree_bytes(dev, dev->tree_shadow)) : 0;
     out->treelet_nodes[0] = dev->tree_ext;
-    out->treelet_nodes[1] = dev->tree_trace;
+    out->treelet_nodes[1] = 0; // k_trace_refill: no treelet
     out->treelet_nodes[2] = dev->tree_shadow;
-    out->treelet_nodes[3] = dev->tree_fin;
+    out->treelet_nodes[3] = 0; // tail kernels: no treelet
     out->table_bytes = dev->table_bytes;
     out->shading_bytes = dev->shading_bytes;
     out->slot_bytes = 0;
     for (const Slot& s : dev->slots)
-        out->slot_bytes += (uint64_t)s.shard_cap * NSH * (2 * 56 * (s.pa.c_base ? 2 : 1) + 48 + (s.hb.h ? 20 : 0)) + (uint64_t)s.cap * 16;
+        out->slot_bytes += (uint64_t)s.shard_cap * NSH * (2 * 56 * (s.pa.c_base ? 2 : 1) + 48 + (s.hb.h ? 20 : 0)) +
+                           (uint64_t)s.cap * (16 + (s.aov_di ? 32 : 0));
     return IGX_OK;
 }
 

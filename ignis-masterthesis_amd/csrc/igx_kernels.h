@@ -275,7 +275,7 @@ __device__ __forceinline__ TStack make_tstack(int* lds_base, int cap, int* spill
 // same distance the larger (entity, primitive) wins.  The reference keeps the
 // later-visited one (t <= tmax, intersection.art:97), which depends on BVH
 // topology and traversal order; this rule makes the result independent of
-// both (speculative traversal, tile sharding, tail vs wavefront kernel).
+// both (tile sharding, tail vs wavefront kernel, persistent-lane refill).
 __device__ __forceinline__ bool accept_hit(const Trav& t, float th, int ent, int prim) {
     return th >= t.tmin && (th < t.tmax || (th == t.tmax && (ent > t.hit_ent || (ent == t.hit_ent && prim > t.hit_prim))));
 }
@@ -359,13 +359,8 @@ __device__ __forceinline__ int4 as_int4(float4 v) {
 // ms (trace 178.0 / 172.9 -> 160.0 / 163.2, shadow 228.7 / 227.1 -> 213.2 /
 // 213.8), S-soup-16M 1-iteration frame 66.3 / 66.7 -> 63.2 / 62.8 ms
 // (profiles/r04_ab_ordered_slab.log).
-// 4-wide float nodes (IGX_ORDERED_SLAB, default off): the near and far float4
-// of each axis come by load address (offset 0 or 16 B by the sign); the same
-// A/B gave S-deep 79.0 / 78.9 -> 78.6 / 78.3 ms but primitives 30.6 / 30.7 ->
-// 31.8 / 31.7 ms (32 iterations), so the float nodes keep min / max.
-#ifndef IGX_ORDERED_SLAB
-#define IGX_ORDERED_SLAB 0
-#endif
+// (4-wide float nodes keep min / max: the same ordering by load address
+// measured S-deep -1 % but primitives +4 %, round 4.)
 #ifndef IGX_ORDERED_SLAB_Q
 #define IGX_ORDERED_SLAB_Q 1
 #endif
@@ -379,32 +374,6 @@ __device__ __forceinline__ int4 as_int4(float4 v) {
 // 1e6 node extents away).  Only |exit| matters: a box with exit < tmin is
 // rejected either way.
 constexpr float QSLAB_EXIT_WIDEN = 1.0f + 0x1p-20f;
-// 4-wide node (SoA float4 bounds lx hx ly hy lz hz, then refs): the near and
-// far float4 of each axis come by load address (offset 0 or 16 B by the sign),
-// the select costing one address add instead of four min and four max.
-template <int NS, bool TREE>
-__device__ __forceinline__ void load_node4_ordered(const SceneView& sv, const Trav& t, int node, float4 (&f)[7]) {
-    const int sx = __float_as_int(t.idir.x) < 0, sy = __float_as_int(t.idir.y) < 0, sz = __float_as_int(t.idir.z) < 0;
-    const int ix[7] = {sx, 1 - sx, 2 + sy, 3 - sy, 4 + sz, 5 - sz, 6};
-    if constexpr (TREE) {
-        if (node < sv.tree_n) {
-            lds_f4v* np = (lds_f4v*)(sv.tree + NS * node);
-#pragma unroll
-            for (int k = 0; k < 7; ++k) {
-                const f4v v = np[ix[k]];
-                f[k] = make_float4(v.x, v.y, v.z, v.w);
-            }
-            return;
-        }
-    }
-    global_f4v* np = (global_f4v*)(sv.nodes + NS * node);
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-        const f4v v = np[ix[k]];
-        f[k] = make_float4(v.x, v.y, v.z, v.w);
-    }
-}
-
 // Slab test of both children of BVH2 node `node` (intersect_ray_box,
 // intersection.art:170-181, with ray.tmin folded in).  Returns the next node
 // (nearer child first; the other is pushed) or the popped entry.
@@ -467,8 +436,7 @@ __device__ __forceinline__ int node_step4(const SceneView& sv, const Trav& t, in
                                           TraceStats& st) {
     if (STATS) count_node(st, t.in_blas, node);
     float4 f[7];
-    if constexpr (IGX_ORDERED_SLAB) load_node4_ordered<NS, TREE>(sv, t, node, f); // near, far per axis
-    else load_node<7, NS, TREE>(sv, node, f); // see node_step2
+    load_node<7, NS, TREE>(sv, node, f); // see node_step2
     const float4 lx = f[0], hx = f[1], ly = f[2], hy = f[3], lz = f[4], hz = f[5];
     const int4 r = as_int4(f[6]);
     float d[4];
@@ -480,15 +448,9 @@ __device__ __forceinline__ int node_step4(const SceneView& sv, const Trav& t, in
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         float nx, fx, ny, fy, nz, fz;
-        if constexpr (IGX_ORDERED_SLAB) { // LX .. are the near, HX .. the far bounds
-            nx = fmaf(LX[k], t.idir.x, t.iorg.x), fx = fmaf(HX[k], t.idir.x, t.iorg.x);
-            ny = fmaf(LY[k], t.idir.y, t.iorg.y), fy = fmaf(HY[k], t.idir.y, t.iorg.y);
-            nz = fmaf(LZ[k], t.idir.z, t.iorg.z), fz = fmaf(HZ[k], t.idir.z, t.iorg.z);
-        } else {
-            slab4(LX[k], HX[k], t.idir.x, t.iorg.x, nx, fx);
-            slab4(LY[k], HY[k], t.idir.y, t.iorg.y, ny, fy);
-            slab4(LZ[k], HZ[k], t.idir.z, t.iorg.z, nz, fz);
-        }
+        slab4(LX[k], HX[k], t.idir.x, t.iorg.x, nx, fx);
+        slab4(LY[k], HY[k], t.idir.y, t.iorg.y, ny, fy);
+        slab4(LZ[k], HZ[k], t.idir.z, t.iorg.z, nz, fz);
         float en = fmaxf(fmaxf(nx, ny), fmaxf(nz, t.tmin));
         float ex = fminf(fminf(fx, fy), fminf(fz, t.tmax));
         bool h = en <= ex;
@@ -561,64 +523,11 @@ __device__ __forceinline__ int node_step4q(const SceneView& sv, const Trav& t, i
     return ref[0];
 }
 
-// Quantised 8-wide node (128 B, host Bvh8QNode): the decode of node_step4q for
-// eight children (child k's byte is byte k % 4 of word k / 4 of each bound),
-// hit children ordered by entry distance with the 19-exchange sorting network
-// of eight inputs, the nearest returned and the others pushed farthest-first.
-// One visit reads one 128-B line, the line a 64-B quantised 4-wide node costs
-// as well, and covers twice the children.
-__device__ __forceinline__ float qbyte(uint32_t w, int b) { return (float)((w >> (8 * b)) & 255u); }
-template <bool STATS, bool SPILL, bool TREE>
-__device__ __forceinline__ int node_step8q(const SceneView& sv, const Trav& t, int node, const TStack& ts, int& sp,
-                                           TraceStats& st) {
-    if (STATS) count_node(st, t.in_blas, node);
-    float4 f[7];
-    load_node<7, 8, TREE>(sv, node, f); // see node_step2
-    const float4 A = f[0], B = f[1], C = f[2], D = f[3], E = f[4];
-    const int4 r0 = as_int4(f[5]), r1 = as_int4(f[6]);
-    const float SX = A.w * t.idir.x, SY = B.x * t.idir.y, SZ = B.y * t.idir.z;
-    const float OX = fmaf(A.x, t.idir.x, t.iorg.x), OY = fmaf(A.y, t.idir.y, t.iorg.y), OZ = fmaf(A.z, t.idir.z, t.iorg.z);
-    const uint32_t qlx[2] = {__float_as_uint(B.z), __float_as_uint(B.w)}, qhx[2] = {__float_as_uint(C.x), __float_as_uint(C.y)};
-    const uint32_t qly[2] = {__float_as_uint(C.z), __float_as_uint(C.w)}, qhy[2] = {__float_as_uint(D.x), __float_as_uint(D.y)};
-    const uint32_t qlz[2] = {__float_as_uint(D.z), __float_as_uint(D.w)}, qhz[2] = {__float_as_uint(E.x), __float_as_uint(E.y)};
-    float d[8];
-    int ref[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
-    int n = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int w = k >> 2, b = k & 3;
-        const float ax = fmaf(qbyte(qlx[w], b), SX, OX), bx = fmaf(qbyte(qhx[w], b), SX, OX);
-        const float ay = fmaf(qbyte(qly[w], b), SY, OY), by = fmaf(qbyte(qhy[w], b), SY, OY);
-        const float az = fmaf(qbyte(qlz[w], b), SZ, OZ), bz = fmaf(qbyte(qhz[w], b), SZ, OZ);
-        const float en = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), t.tmin));
-        const float ex = fminf(fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz)) * QSLAB_EXIT_WIDEN, t.tmax);
-        const bool h = en <= ex && ref[k] != REF_EMPTY;
-        d[k] = h ? en : INFINITY;
-        n += h ? 1 : 0;
-    }
-    if (n == 0) return tpop<SPILL>(ts, sp);
-    // optimal 8-input network (19 exchanges, depth 6)
-    cswap(d[0], ref[0], d[2], ref[2]); cswap(d[1], ref[1], d[3], ref[3]);
-    cswap(d[4], ref[4], d[6], ref[6]); cswap(d[5], ref[5], d[7], ref[7]);
-    cswap(d[0], ref[0], d[4], ref[4]); cswap(d[1], ref[1], d[5], ref[5]);
-    cswap(d[2], ref[2], d[6], ref[6]); cswap(d[3], ref[3], d[7], ref[7]);
-    cswap(d[0], ref[0], d[1], ref[1]); cswap(d[2], ref[2], d[3], ref[3]);
-    cswap(d[4], ref[4], d[5], ref[5]); cswap(d[6], ref[6], d[7], ref[7]);
-    cswap(d[2], ref[2], d[4], ref[4]); cswap(d[3], ref[3], d[5], ref[5]);
-    cswap(d[1], ref[1], d[4], ref[4]); cswap(d[3], ref[3], d[6], ref[6]);
-    cswap(d[1], ref[1], d[2], ref[2]); cswap(d[3], ref[3], d[4], ref[4]); cswap(d[5], ref[5], d[6], ref[6]);
-#pragma unroll
-    for (int k = 7; k > 0; --k)
-        if (n > k) tpush<SPILL>(ts, sp, ref[k]);
-    return ref[0];
-}
-
 template <bool STATS, int V>
 __device__ __forceinline__ int node_step(const SceneView& sv, const Trav& t, int node, const TStack& ts, int& sp,
                                          TraceStats& st) {
     constexpr int PAD = variant_ldspad(V) ? 1 : 0;
-    if constexpr (variant_q4(V) && IGX_QWIDTH == 8) return node_step8q<STATS, variant_spill(V), variant_tree(V)>(sv, t, node, ts, sp, st);
-    else if constexpr (variant_q4(V)) return node_step4q<STATS, variant_spill(V), variant_tree(V)>(sv, t, node, ts, sp, st);
+    if constexpr (variant_q4(V)) return node_step4q<STATS, variant_spill(V), variant_tree(V)>(sv, t, node, ts, sp, st);
     else if constexpr (variant_width(V) == 4) return node_step4<STATS, variant_spill(V), 8 + PAD, variant_tree(V)>(sv, t, node, ts, sp, st);
     else return node_step2<STATS, variant_spill(V), 4 + PAD, variant_tree(V)>(sv, t, node, ts, sp, st);
 }
@@ -761,28 +670,6 @@ __device__ __forceinline__ bool trav_step_core(const SceneView& sv, Trav& t, con
             t.node = node_step<STATS, V>(sv, t, node, ts, sp, st);
             t.sp = sp;
             return false;
-        }
-    } else if constexpr (variant_spec(V)) {
-        // speculative while-while: the first BLAS leaf a lane meets is
-        // postponed and the lane keeps popping and walking inner nodes until
-        // no active lane is still walking without a postponed leaf; then the
-        // postponed leaf is tested, its pending entry pushed back.  Leaves are
-        // tested in a different order than depth-first; the closest hit does
-        // not depend on the order (accept_hit), an any-hit ray stops at any hit
-        bool post = false;
-        int leaf = 0;
-        while (node >= 0) {
-            node = node_step<STATS, V>(sv, t, node, ts, sp, st);
-            if (!post && t.in_blas && is_leaf_ref(node)) {
-                post = true;
-                leaf = node;
-                node = tpop<SPILL>(ts, sp);
-            }
-            if (__ballot(!post && node >= 0) == 0) break;
-        }
-        if (post) {
-            tpush<SPILL>(ts, sp, node);
-            node = leaf;
         }
     } else {
         while (node >= 0) node = node_step<STATS, V>(sv, t, node, ts, sp, st);
@@ -1073,17 +960,8 @@ __device__ __forceinline__ Surface surface_element(const SceneView& sv, int ent_
         float nn = len(n);
         fn = mulf(n, 1 / nn);
     }
-#ifndef IGX_KO_SURF
-#define IGX_KO_SURF 0
-#endif
-    // IGX_KO_SURF (experiment builds only, wrong images): shading normal = face normal
-    f3 normal;
-    if (IGX_KO_SURF) {
-        normal = fn;
-    } else {
-        f3 ln = lerp2(f3of(sv.nrm[info.z + f.x]), f3of(sv.nrm[info.z + f.y]), f3of(sv.nrm[info.z + f.z]), hu, hv);
-        normal = normalize(xform_dir_rows(n0, n1, n2, ln));
-    }
+    f3 ln = lerp2(f3of(sv.nrm[info.z + f.x]), f3of(sv.nrm[info.z + f.y]), f3of(sv.nrm[info.z + f.z]), hu, hv);
+    f3 normal = normalize(xform_dir_rows(n0, n1, n2, ln));
     s.entering = dot(rd, fn) <= 0;
     s.face_normal = s.entering ? fn : neg(fn);
     s.local = make_frame(s.entering ? normal : neg(normal));

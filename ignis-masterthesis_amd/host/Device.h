@@ -26,15 +26,23 @@
 //     file;
 //   * the framebuffer, statistics, resize and release calls map one to one.
 // tonemap / evaluateGlare / imageinfo / bake (Device.h:66-69) are outside the
-// hot path and are not provided.  Errors from the C-ABI become
-// std::runtime_error, which a Runtime turns into its bool / IG_LOG path
-// (Runtime.cpp:159-162).
+// hot path ("stub or CPU fallback"): tonemap and imageinfo run
+// on the host over getFramebufferForHost (restating entrypoints/tonemap.art and
+// entrypoints/imageinfo.art with core/color.art); evaluateGlare and bake have
+// no igx counterpart (the glare shader needs the camera's solid-angle model,
+// bake a compiled shading-tree shader) and log and return an empty result.
+// Errors from the C-ABI become std::runtime_error, which a Runtime turns into
+// its bool / IG_LOG path (Runtime.cpp:159-162); an unknown AOV name alone gives
+// the reference's empty accessor {nullptr, 0}.
 #pragma once
 
+#include "film_tools.h"
 #include "igx.h"
 #include "scene_database.h"
 
+#include <algorithm>
 #include <array>
+#include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -77,6 +85,60 @@ struct ParameterSet { // RuntimeStructs.h:56-70
     std::unordered_map<std::string, Vector4f> ColorParameters;
     bool empty() const { return IntParameters.empty() && FloatParameters.empty() && VectorParameters.empty() && ColorParameters.empty(); }
 };
+
+// RuntimeStructs.h:6-54 (the reference's utility-shader settings and outputs)
+struct TonemapSettings {
+    const char* AOV;
+    size_t Method;
+    bool UseGamma;
+    float Scale;
+    float ExposureFactor;
+    float ExposureOffset;
+};
+struct GlareSettings {
+    const char* AOV;
+    float Scale;
+    float LuminanceMax;
+    float LuminanceAverage;
+    float LuminanceMultiplier;
+    float VerticalIlluminance;
+};
+struct GlareOutput {
+    float DGP;
+    float VerticalIlluminance;
+    int NumPixels;
+    float AvgLum;
+    float AvgOmega;
+};
+struct ImageInfoSettings {
+    const char* AOV;
+    float Scale;
+    size_t Bins;
+    int* HistogramR;
+    int* HistogramG;
+    int* HistogramB;
+    int* HistogramL;
+    bool AcquireErrorStats;
+    bool AcquireHistogram;
+};
+struct ImageInfoOutput {
+    float Min;
+    float Max;
+    float Average;
+    float SoftMin;
+    float SoftMax;
+    float Median;
+    int InfCount;
+    int NaNCount;
+    int NegCount;
+};
+// shader/ShaderUtils.h: a compiled shader and its local registry; igx has no
+// shader JIT, so a bake request carries nothing it could run
+template <typename T>
+struct ShaderOutput {
+    T Exec = nullptr;
+};
+
 
 // The shader set of a scene igx loaded itself (igx_scene_load_* or, for the
 // reference's in-memory scenes, igx_scene_from_objects): its film, camera,
@@ -253,20 +315,25 @@ public:
 
     // the film ("" / "Color") or a named AOV of the technique ("Direct Weights",
     // "NEE Weights" with aov_mis); an unknown name gives {nullptr, 0}, as the
-    // reference's getAOVImageForHost / ForDevice (Device.cpp:1330-1388)
+    // reference's getAOVImageForHost / ForDevice (Device.cpp:1330-1388).  Every
+    // other failure (a HIP error, a failed asynchronous render) throws: the
+    // name is resolved first (igx_aov_device_ptr needs no GPU work), so only
+    // IGX_ERR_INVALID_ARGUMENT on an unknown name maps to the empty accessor
     AOVAccessor getFramebufferForHost(const std::string& name = "") {
+        if (!knownAOV(name)) return AOVAccessor{nullptr, 0};
         std::vector<float>& buf = mHostFB[name.empty() ? "Color" : name];
         buf.resize(mWidth * mHeight * 3);
         uint64_t iters = 0;
-        if (igx_get_aov(mDev, name.c_str(), buf.data(), buf.size(), &iters) != IGX_OK) return AOVAccessor{nullptr, 0};
+        check(igx_get_aov(mDev, name.c_str(), buf.data(), buf.size(), &iters));
         return AOVAccessor{buf.data(), (size_t)iters};
     }
     AOVAccessor getFramebufferForDevice(const std::string& name = "") {
+        if (!knownAOV(name)) return AOVAccessor{nullptr, 0};
         float* ptr = nullptr;
         size_t n = 0;
         uint64_t iters = 0;
         check(igx_synchronize(mDev));
-        if (igx_aov_device_ptr(mDev, name.c_str(), &ptr, &n) != IGX_OK) return AOVAccessor{nullptr, 0};
+        check(igx_aov_device_ptr(mDev, name.c_str(), &ptr, &n));
         check(igx_get_framebuffer(mDev, nullptr, 0, &iters));
         return AOVAccessor{ptr, (size_t)iters};
     }
@@ -278,11 +345,46 @@ public:
         return &mStats;
     }
 
+    // entrypoints/tonemap.art on the host over the AOV's host copy (film_tools.h)
+    void tonemap(uint32_t* out_pixels, const TonemapSettings& ts) {
+        const AOVAccessor acc = getFramebufferForHost(ts.AOV ? ts.AOV : "");
+        if (!acc.Data || !out_pixels) return;
+        const float inv_iter = acc.IterationCount > 0 ? 1.0f / (float)acc.IterationCount : 0.0f;
+        igx::tonemap_film(acc.Data, mWidth * mHeight, ts.Scale * inv_iter, (int)ts.Method, ts.UseGamma, ts.ExposureFactor,
+                          ts.ExposureOffset, out_pixels);
+    }
+    // The glare shader (Device.cpp:1689-1723) evaluates the daylight glare
+    // probability over the camera's solid-angle model; igx has none: logged, empty
+    GlareOutput evaluateGlare(uint32_t*, const GlareSettings&) {
+        std::fprintf(stderr, "igx: evaluateGlare is not provided by the igx device (outside the traced path)\n");
+        return GlareOutput{0, 0, 0, 0, 0};
+    }
+    // entrypoints/imageinfo.art on the host over the AOV's host copy (film_tools.h)
+    ImageInfoOutput imageinfo(const ImageInfoSettings& is) {
+        const AOVAccessor acc = getFramebufferForHost(is.AOV ? is.AOV : "");
+        if (!acc.Data) return ImageInfoOutput{0, 0, 0, 0, 0, 0, 0, 0, 0};
+        const float inv_iter = acc.IterationCount > 0 ? 1.0f / (float)acc.IterationCount : 0.0f;
+        const igx::FilmInfo f = igx::imageinfo_film(acc.Data, mWidth, mHeight, is.Scale * inv_iter, is.Bins, is.HistogramR, is.HistogramG,
+                                                    is.HistogramB, is.HistogramL, is.AcquireErrorStats, is.AcquireHistogram);
+        return ImageInfoOutput{f.min, f.max, f.avg, f.soft_min, f.soft_max, f.median, f.inf_count, f.nan_count, f.neg_count};
+    }
+    // Device::bake (Device.cpp:1761-1774) runs a shading-tree shader compiled
+    // by the reference's JIT (ShadingTree.cpp:527); igx compiles none: logged,
+    // `output` left untouched
+    void bake(const ShaderOutput<void*>&, const std::vector<std::string>*, float*) {
+        std::fprintf(stderr, "igx: bake is not provided by the igx device (no shading-tree shaders)\n");
+    }
+
     // igx extras: render() only queues work; wait for it (timing, host reads)
     void synchronize() { check(igx_synchronize(mDev)); }
     igx_device* handle() { return mDev; }
 
 private:
+    // "" / "Color", and the MIS AOVs when the uploaded technique has them
+    bool knownAOV(const std::string& name) const {
+        if (name.empty() || name == "Color") return true;
+        return mLast.valid && mLast.technique.aov_mis && (name == "Direct Weights" || name == "NEE Weights");
+    }
     void check(igx_status s) {
         if (s != IGX_OK) throw std::runtime_error(std::string("igx: ") + igx_last_error(mDev));
     }

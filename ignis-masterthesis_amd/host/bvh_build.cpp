@@ -698,14 +698,8 @@ Bvh4Result collapse_bvh4(const BvhBuildResult& in) {
     return res;
 }
 
-Bvh8Result collapse_bvh8(const BvhBuildResult& in) {
-    Bvh8Result res;
-    collapse_wide<8>(in, res.nodes, res.depth, res.stack_need);
-    return res;
-}
-
 // ---------------------------------------------------------------------------
-// Quantised wide nodes (Bvh4QNode, Bvh8QNode; bvh_build.h)
+// Quantised wide nodes (Bvh4QNode; bvh_build.h)
 // ---------------------------------------------------------------------------
 Bvh4QNode quantize_bvh4(const Bvh4Node& n) {
     WideNode<4> w;
@@ -723,16 +717,6 @@ Bvh4QNode quantize_bvh4(const Bvh4Node& n) {
     uint32_t* qlo[3] = {&q.qlo_x, &q.qlo_y, &q.qlo_z};
     uint32_t* qhi[3] = {&q.qhi_x, &q.qhi_y, &q.qhi_z};
     for (int a = 0; a < 3; ++a) quantize_axis<4>(w.lo[a], w.hi[a], valid, q.origin[a], *sc[a], qlo[a], qhi[a]);
-    return q;
-}
-
-Bvh8QNode quantize_bvh8(const Bvh8Node& n) {
-    bool valid[8];
-    valid_children<8>(n, valid);
-    Bvh8QNode q{};
-    for (int k = 0; k < 8; ++k) q.ref[k] = n.ref[k];
-    float* sc[3] = {&q.sx, &q.sy, &q.sz};
-    for (int a = 0; a < 3; ++a) quantize_axis<8>(n.lo[a], n.hi[a], valid, q.origin[a], *sc[a], &q.q[4 * a], &q.q[4 * a + 2]);
     return q;
 }
 

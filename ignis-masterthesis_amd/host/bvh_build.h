@@ -112,40 +112,13 @@ struct Bvh4QNode {
 static_assert(sizeof(Bvh4QNode) == 64, "Bvh4QNode must be 64 bytes");
 Bvh4QNode quantize_bvh4(const Bvh4Node& n);
 
-// N-wide node before quantisation (collapse_bvh8): bounds per axis, child k in
+// N-wide node before quantisation (quantize_bvh4): bounds per axis, child k in
 // column k; absent children as in Bvh4Node (kEmptyRef, +inf bounds).
 template <int N>
 struct WideNode {
     float lo[3][N], hi[3][N];
     int32_t ref[N];
 };
-using Bvh8Node = WideNode<8>;
-struct Bvh8Result {
-    std::vector<Bvh8Node> nodes; // nodes[0] is the root
-    int stack_need = 0;          // as Bvh4Result
-    int depth = 0;               // 8-wide levels
-};
-// Surface-area collapse into 8-wide nodes (collapse_bvh4's rule with eight
-// children per node).
-Bvh8Result collapse_bvh8(const BvhBuildResult& bvh2);
-
-// 8-wide node with quantised child boxes (128 B: one 128-B cache line per
-// visit, the line a 64-B Bvh4QNode costs as well; traversed by node_step8q).
-// Quantisation as Bvh4QNode; child k's byte is byte k % 4 of word k / 4.
-//   float o_x, o_y, o_z, s_x | float s_y, s_z, u32 qlo_x[2] |
-//   u32 qhi_x[2], qlo_y[2] | u32 qhi_y[2], qlo_z[2] | u32 qhi_z[2], pad[2] |
-//   int32 ref[8] | pad[4]
-struct Bvh8QNode {
-    float origin[3];
-    float sx, sy, sz;
-    uint32_t q[12]; // axis a: qlo words q[4a], q[4a+1]; qhi words q[4a+2], q[4a+3]
-    uint32_t pad0[2];
-    int32_t ref[8];
-    int32_t pad1[4];
-};
-static_assert(sizeof(Bvh8QNode) == 128, "Bvh8QNode must be 128 bytes");
-Bvh8QNode quantize_bvh8(const Bvh8Node& n);
-
 // Read the reference's GPU BLAS (one FixTables["trimesh_primbvh"] entry:
 // u32 node_count, tri_count, 0, 0; Node2[]; Tri1[], TriMeshProvider.cpp:307-326)
 // into the device's BVH2 form: same boxes and topology, leaf codes over the

@@ -134,7 +134,8 @@ class Stats(C.Structure):
                 ("shadow_class_groups", C.c_uint64 * 2), ("shadow_class_node_iters", C.c_uint64 * 2),
                 ("shadow_class_node_visits", C.c_uint64 * 2), ("shadow_class_cycles", C.c_uint64 * 2),
                 ("shadow_class_occluded", C.c_uint64 * 2), ("tlas_node_visits", C.c_uint64),
-                ("hot_node_visits", C.c_uint64 * 3), ("extend_class_shade_cycles", C.c_uint64 * 16)]
+                ("hot_node_visits", C.c_uint64 * 3), ("extend_class_shade_cycles", C.c_uint64 * 16),
+                ("shadow_class_rays", C.c_uint64 * 2)]
 
     def as_dict(self):
         return {name: (list(getattr(self, name)) if isinstance(getattr(self, name), C.Array) else getattr(self, name))

@@ -161,7 +161,7 @@ def test_quantised_nodes_match(device, root):
             device.set_option("bvh_quantize", q)
             device.upload(sc)
             st = device.stats()
-            assert st["node_bytes"] == (16 * st["bvh_width"] if q else 128)  # 64-B 4-wide or 128-B 8-wide (IGX_QWIDTH)
+            assert st["node_bytes"] == (64 if q else 128)  # quantised or float 4-wide nodes
             res.append(device.trace_hits(rays, 0x1))
             imgs.append(render_gpu(device, sc, 128, 128, 4))
     finally:
@@ -368,15 +368,13 @@ def test_treelet_invariance(device, root, name):
     """The LDS treelet of the hottest BVH nodes (global-table scenes: k_extend
     and the shadow kernels read nodes below tree_n from LDS) changes where a
     node is read from, never what is traced: images bit for bit equal and
-    ray counts equal with the treelet off, automatic and at 32 nodes, and
-    with the speculative trace kernel on and off."""
+    ray counts equal with the treelet off, automatic and at 32 nodes."""
     sc = ignis_amd.Scene.from_file(os.path.join(root, "scenes", name))
     imgs, counts, staged = [], [], []
     try:
         device.upload(sc)
-        for treelet, spec in [(0, 1), (-1, 1), (32, 1), (-1, 0)]:
+        for treelet in (0, -1, 32):
             device.set_option("treelet", treelet)
-            device.set_option("speculative", spec)
             device.reset_stats()
             imgs.append(render_gpu(device, sc, 112, 80, 4))
             st = device.stats()
@@ -384,7 +382,6 @@ def test_treelet_invariance(device, root, name):
             staged.append(list(st["treelet_nodes"]))
     finally:
         device.set_option("treelet", -1)
-        device.set_option("speculative", 1)
     assert staged[0] == [0, 0, 0, 0] and max(staged[1]) > 0 and max(staged[2]) <= 32, staged
     for im, c in zip(imgs[1:], counts[1:]):
         np.testing.assert_array_equal(imgs[0], im)

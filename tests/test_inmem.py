@@ -124,17 +124,31 @@ def test_object_scene_array_without_data():
         assert L.igx_objscene_set_property(o._h, h, b"width", ptype, None, 1) == -1
 
 
-def _build_native(tmp_path):
-    exe = str(tmp_path / "inmem_kats")
-    subprocess.run(["g++", "-O1", "-std=c++17", "-I", os.path.join(ROOT, "include"), "-I", os.path.join(PKG, "host"),
-                    os.path.join(ROOT, "tests", "native", "inmem_kats.cpp"), "-o", exe, "-L", PKG, "-ligx",
+def _build_native(tmp_path, name="inmem_kats"):
+    exe = str(tmp_path / name)
+    subprocess.run(["g++", "-O1", "-std=c++17", "-Wall", "-I", os.path.join(ROOT, "include"), "-I", os.path.join(PKG, "host"),
+                    os.path.join(ROOT, "tests", "native", name + ".cpp"), "-o", exe, "-L", PKG, "-ligx",
                     f"-Wl,-rpath,{PKG}", "-L/opt/rocm/lib", "-lamdhip64"], check=True)
     return exe
 
 
 def test_facade_program_builds(tmp_path):
-    """The facade program compiles against include/ and host/Device.h (no GPU call)."""
+    """The facade programs compile against include/ and host/Device.h (no GPU call)."""
     assert os.path.exists(_build_native(tmp_path))
+    assert os.path.exists(_build_native(tmp_path, "facade_members"))
+
+
+@pytest.mark.gpu
+def test_facade_defines_every_device_member(tmp_path):
+    """Every member of the reference's IG::Device (Device.h:49-73) through the
+    facade (tests/native/facade_members.cpp): accessors, tonemap / imageinfo on
+    the host against the film, the glare / bake stubs, {nullptr, 0} for an
+    unknown AOV only, exceptions (not a null accessor) after a failed
+    asynchronous render, and a failed capture that throws."""
+    exe = _build_native(tmp_path, "facade_members")
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    print(out.stdout, out.stderr)
+    assert out.returncode == 0 and out.stdout.strip().endswith("ok"), out.stdout + out.stderr
 
 
 @pytest.mark.gpu
