@@ -30,18 +30,12 @@ __host__ __device__ constexpr int variant_width(int v) { return (v & 2) ? 4 : 2;
 __host__ __device__ constexpr bool variant_spill(int v) { return (v & 1) != 0; }
 __host__ __device__ constexpr bool variant_full(int v) { return (v & 4) != 0; }
 __host__ __device__ constexpr int node_f4(int width) { return width == 4 ? 8 : 4; }
-// LDS-staged node tables keep one float4 of padding per node (BVH2 nodes 80 B,
-// 4-wide 144 B apart): lanes that read the same float4 of different nodes then
-// hit different 16-B bank groups (an odd multiple of 16 B cycles through all
-// 16 groups of the 256-B bank period) instead of the two groups a 64/128-B
-// stride maps every node to.  Bit 3 of the variant selects that stride; the
-// kernels set it on their LDS-staged SceneView only.
-#ifndef IGX_LDS_NODE_PAD
-#define IGX_LDS_NODE_PAD 0
-#endif
-__host__ __device__ constexpr bool variant_ldspad(int v) { return (v & 8) != 0; }
-__host__ __device__ constexpr int lds_variant(int v, bool lds) { return (lds && IGX_LDS_NODE_PAD) ? (v | 8) : v; }
-__host__ __device__ constexpr int lds_node_pad() { return IGX_LDS_NODE_PAD ? 1 : 0; }
+// Bit 3: the node tables are staged in LDS (stage_scene_lds; set by the
+// kernels on their LDS-staged SceneView).  The node steps then skip the
+// stack-top peek (IGX_PEEK_POP), whose extra LDS read costs there what it
+// saves where the nodes come from global memory.  (One float4 of padding per
+// LDS node, round 2, measured neutral and was removed.)
+__host__ __device__ constexpr bool variant_lds_nodes(int v) { return (v & 8) != 0; }
 // Bit 4: if-if stepping (trav_step advances one inner node or one leaf per
 // call) -- set only on k_shadow_refill launches for scenes on the split
 // schedule (igx_device.hip, use_shadow_ifif).
@@ -59,7 +53,7 @@ constexpr int VARIANT_Q4 = 128;
 __host__ __device__ constexpr bool variant_q4(int v) { return (v & VARIANT_Q4) != 0; }
 constexpr int32_t REF_EMPTY = (int32_t)0x80000002; // absent child of a 4-wide node (host kEmptyRef)
 __host__ __device__ constexpr bool variant_tree(int v) { return (v & VARIANT_TREE) != 0; }
-__host__ __device__ constexpr int kernel_variant(int v, bool lds) { return lds ? lds_variant(v, true) : (v | VARIANT_TREE); }
+__host__ __device__ constexpr int kernel_variant(int v, bool lds) { return lds ? (v | 8) : (v | VARIANT_TREE); }
 
 // Instance record (one per TLAS leaf slot): 64 B
 //   row0..row2: to_local 3x4 (row-major, xyz = linear row, w = translation)

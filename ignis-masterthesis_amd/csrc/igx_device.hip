@@ -90,6 +90,7 @@ static_assert(MAX_CHUNK_PATHS <= (1ll << SLOT_BITS), "path slots must fit the sl
 #define EXTEND_WAVES_LDS 4
 #endif
 
+
 // ---------------------------------------------------------------------------
 // Streams (SoA of 16-byte records)
 // ---------------------------------------------------------------------------
@@ -115,6 +116,11 @@ constexpr int WAVES_PER_BLOCK = BLOCK / 64;
 #endif
 #ifndef SHADOW_TREELET
 #define SHADOW_TREELET 1
+#endif
+// k_extend's dynamic groups: the append's atomic round trip also takes the
+// wave's next group (1, wave_append_paths) or take_group issues its own (0)
+#ifndef IGX_CLAIM_NEXT
+#define IGX_CLAIM_NEXT 1
 #endif
 // bounce b >= 2 launches a grid sized to the paths entering bounce b - 1 (1)
 // instead of the chunk's first-bounce grid (0)
@@ -295,8 +301,13 @@ __device__ __forceinline__ int path_index(const PathBuf& b, int s, int pos, cons
 // instruction; positions inside the wave by ballot prefix.  `dst` is the
 // record offset from the start of the shard (c_base added for class C).
 // Needs every lane of the wave active.
+// `claim` (k_extend's dynamic groups): lane 3 also takes the wave's next group
+// of its shard from that shard's work counter in the same round trip
+// (`claimed`, wave-uniform; -1 without `claim`), so the next group's path
+// loads follow the stores without a second returning atomic in between.
 __device__ __forceinline__ void wave_append_paths(bool alive, int cls, bool shadow, bool sh_b, int* cp, int* cs,
-                                                  int shard_cap, int c_base, int sh_cap, int& dst, int& sdst) {
+                                                  int shard_cap, int c_base, int sh_cap, int& dst, int& sdst,
+                                                  int* claim = nullptr, int* claimed = nullptr) {
     const int lane = lane_id();
     const uint64_t ma = __ballot(alive && cls == 0), mb = __ballot(alive && cls == 1), mc = __ballot(alive && cls == 2);
     const uint64_t sa = __ballot(shadow && !sh_b), sb = __ballot(shadow && sh_b);
@@ -305,7 +316,10 @@ __device__ __forceinline__ void wave_append_paths(bool alive, int cls, bool shad
                                     : lane == 1 ? ((unsigned long long)__popcll(sa) | ((unsigned long long)__popcll(sb) << 32))
                                                 : (unsigned long long)__popcll(mc);
     unsigned long long r = 0;
+    int nx = 0;
     if (lane < 3 && want != 0) r = atomicAdd(reinterpret_cast<unsigned long long*>(lane == 0 ? cp : lane == 1 ? cs : cp + 2), want);
+    if (claim && lane == 3) nx = atomicAdd(claim, 1);
+    if (claim) *claimed = __builtin_amdgcn_readfirstlane(__shfl(nx, 3));
     const int lo = (int)(uint32_t)r, hi = (int)(uint32_t)(r >> 32);
     const int a0 = __shfl(lo, 0), b0 = __shfl(hi, 0), s0 = __shfl(lo, 1), t0 = __shfl(hi, 1), c0 = __shfl(lo, 2);
     dst = cls == 1   ? shard_cap - 1 - (b0 + __popcll(mb & below))
@@ -832,14 +846,20 @@ __device__ __forceinline__ void flush_stats(const TraceStats& st, unsigned long 
 // in shard s (s and n updated), or -1 once every shard is exhausted.  Waves
 // that drew short paths take more groups, so a launch no longer waits on the
 // wave with the slowest fixed share.
+// `claimed` >= 0: the wave already took group `claimed` of shard s (k_extend's
+// append, wave_append_paths): no atomic for it.
 template <class CountOf>
-__device__ __forceinline__ int take_group(int* work, int& s, uint64_t& done, int n, CountOf count_of) {
+__device__ __forceinline__ int take_group(int* work, int& s, uint64_t& done, int n, CountOf count_of, int claimed = -1) {
     unsigned long long* const done_mask = reinterpret_cast<unsigned long long*>(work + CROW);
     for (;;) {
         if (!((done >> s) & 1ull)) {
-            int v = 0;
-            if (lane_id() == 0) v = atomicAdd(work + s * CSTRIDE, 1);
-            v = __builtin_amdgcn_readfirstlane(v);
+            int v = claimed;
+            claimed = -1;
+            if (v < 0) {
+                v = 0;
+                if (lane_id() == 0) v = atomicAdd(work + s * CSTRIDE, 1);
+                v = __builtin_amdgcn_readfirstlane(v);
+            }
             if (v * 64 < n) return v;
             // one atomicOr per shard, not one per wave that finds it exhausted
             if (lane_id() == 0 && !((__hip_atomic_load(done_mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> s) & 1ull))
@@ -919,13 +939,14 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
     ShardCount sc = count_of(s);
     uint64_t done = 0; // shards this wave knows to be exhausted (dynamic)
     int p0 = w.k * 64;
+    int claimed = -1; // next group of shard s, taken by the previous group's append (IGX_CLAIM_NEXT)
     unsigned long long t_last = STATS ? __builtin_amdgcn_s_memtime() : 0; // phase clocks (instrumented builds)
     for (;;) {
         if (fa.dynamic) {
             const int g = take_group(kc.work, s, done, sc.n, [&](int sh_) {
                 sc = count_of(sh_);
                 return sc.n;
-            });
+            }, claimed);
             if (g < 0) break;
             p0 = g * 64;
         } else if (p0 >= sc.n) {
@@ -967,9 +988,13 @@ __global__ void __launch_bounds__(BLOCK, LDS ? EXTEND_WAVES_LDS : (variant_full(
             alive = extend_step_instrumented<V>(fa, sv, ts, L, ps, q < ns && ps.depth > 0, bucket, has_shadow, sr, st, t_last);
         }
         int dst, sdst;
+        // dynamic groups: the append's round trip also takes the next group of
+        // shard s, unless s is known exhausted
+        int* const claim = (IGX_CLAIM_NEXT && fa.dynamic && !((done >> s) & 1ull)) ? kc.work + s * CSTRIDE : nullptr;
         wave_append_paths(alive, path_class(fa.classify, sv, ps), has_shadow,
                           has_shadow && shadow_class_b(fa.shadow_classes, sv, sr.o, sr.d, sr.tmax), c_out, c_sh, out.shard_cap,
-                          out.c_base, sh.shard_cap, dst, sdst);
+                          out.c_base, sh.shard_cap, dst, sdst, claim, &claimed);
+        if (!claim) claimed = -1;
         if (alive) store_path(out, s * out.shard_cap + dst, ps);
         if (has_shadow) {
             const int e = s * sh.shard_cap + sdst;
@@ -1275,6 +1300,25 @@ __global__ void __launch_bounds__(BLOCK, FINISH_PAIRS_WAVES) k_finish_pairs(Fram
 // shadow: any-hit traversal; on miss add the NEE contribution
 // (gpu_traverse_secondary, mapping_gpu.art:70-112; on_shadow_miss, pathtracer.art:202-209)
 // ---------------------------------------------------------------------------
+// One shadow ray's any-hit walk; unoccluded, its colour goes to the radiance
+// slot (l: the slot's value, loaded before the walk so that the scattered
+// read's latency overlaps the walk: diamond shadow time 20.6 -> 20.3 ms per
+// frame, round 5).  Returns whether the ray is occluded.
+template <bool STATS, int V>
+__device__ __forceinline__ bool shadow_walk(const SceneView& sv, const TStack& ts, float4 s0, float4 s1, float4 col, float4 l,
+                                            float4* L, float4* aov_nee, TraceStats& st) {
+    float tmax = s1.w;
+    int e, p;
+    float u, v;
+    const bool occl = trace_ray<true, STATS, V>(sv, f3of(s0), f3of(s1), 0.001f, tmax, RAY_SHADOW, ts, e, p, u, v, st);
+    if (!occl) {
+        const int slot = __float_as_int(s0.w);
+        L[slot] = make_float4(l.x + col.x, l.y + col.y, l.z + col.z, 0); // add_radiance
+        add_aov(aov_nee, slot, f3of(col));
+    }
+    return occl;
+}
+
 template <int V0, bool STATS, bool LDS>
 __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, float4* L, const int* cnt,
                                                   unsigned long long* stats, int* work) {
@@ -1287,55 +1331,26 @@ __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, f
     TraceStats st{0, 0, 0, 0, 0, 0, 0};
     unsigned long long cls_acc[2][6] = {}; // instrumented: per shadow class groups, wave iterations, visits, cycles, occluded, rays
     const WaveWork w = wave_work();
+    const int lane = lane_id();
     // groups of 64 shadow rays: grid-stride over the wave's own shard, or
     // (work != nullptr) handed out by take_group
     int s = w.s;
     ShardCount sc = shard_count(cnt, s); // two shadow classes (wave_append_paths)
-    uint64_t done = 0;
-    for (int p0 = w.k * 64;; p0 += w.K * 64) {
-        if (work) {
-            p0 = take_group(work, s, done, sc.n, [&](int sh_) {
-                sc = shard_count(cnt, sh_);
-                return sc.n;
-            });
-            if (p0 < 0) break;
-            p0 *= 64;
-        } else if (p0 >= sc.n) {
-            break;
-        }
-        const int pos = p0 + lane_id();
-        // instrumented: the class of the group (wave-uniform), its wave cycles and visits
-        const int cls = p0 < sc.a ? 0 : 1;
-        unsigned long long c0 = 0;
-        uint32_t wn0 = 0, ln0 = 0;
+    // instrumented: the class of the group (wave-uniform), its wave cycles and visits
+    unsigned long long c0 = 0;
+    uint32_t wn0 = 0, ln0 = 0;
+    auto stats_begin = [&]() {
         if constexpr (STATS) {
             c0 = __builtin_amdgcn_s_memtime();
             wn0 = st.wnodes;
             ln0 = st.nodes;
         }
-        bool occl = false;
-        if (pos < sc.n) {
-            const int i = stream_index(s, pos, sc.a, sh.shard_cap);
-            const float4 s0 = sh.s0[i], s1 = sh.s1[i];
-            const int slot = __float_as_int(s0.w);
-            float tmax = s1.w;
-            int e, p;
-            float u, v;
-            // the ray's colour and its radiance slot are loaded before the walk:
-            // their latency (the slot is a scattered read) overlaps the any-hit
-            // traversal instead of following it (diamond shadow time 20.6 ->
-            // 20.3 ms per frame, round 5)
-            const float4 col = sh.s2[i], l = L[slot];
-            occl = trace_ray<true, STATS, V>(sv, f3of(s0), f3of(s1), 0.001f, tmax, RAY_SHADOW, ts, e, p, u, v, st);
-            if (!occl) {
-                L[slot] = make_float4(l.x + col.x, l.y + col.y, l.z + col.z, 0); // add_radiance
-                add_aov(sh.aov_nee, slot, f3of(col));
-            }
-        }
+    };
+    auto stats_end = [&](int p0, bool act, bool occl) {
         if constexpr (STATS) {
             __builtin_amdgcn_s_waitcnt(0);
             const unsigned long long c1 = __builtin_amdgcn_s_memtime();
-            uint32_t visits = st.nodes - ln0, witers = st.wnodes - wn0, occ = occl ? 1 : 0, nr = pos < sc.n ? 1 : 0;
+            uint32_t visits = st.nodes - ln0, witers = st.wnodes - wn0, occ = occl ? 1 : 0, nr = act ? 1 : 0;
             for (int off = 32; off > 0; off >>= 1) {
                 visits += __shfl_xor(visits, off);
                 witers += __shfl_xor(witers, off);
@@ -1343,7 +1358,8 @@ __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, f
                 nr += __shfl_xor(nr, off);
             }
             // accumulated per wave (lane 0), flushed once at the end: no atomics in the timed region
-            if (lane_id() == 0) {
+            const int cls = p0 < sc.a ? 0 : 1;
+            if (lane == 0) {
                 cls_acc[cls][0] += 1;
                 cls_acc[cls][1] += witers;
                 cls_acc[cls][2] += visits;
@@ -1352,9 +1368,32 @@ __global__ void __launch_bounds__(BLOCK) k_shadow(SceneView gsv, ShadowBuf sh, f
                 cls_acc[cls][5] += nr;
             }
         }
+    };
+    {
+        uint64_t done = 0;
+        for (int p0 = w.k * 64;; p0 += w.K * 64) {
+            if (work) {
+                p0 = take_group(work, s, done, sc.n, [&](int sh_) {
+                    sc = shard_count(cnt, sh_);
+                    return sc.n;
+                });
+                if (p0 < 0) break;
+                p0 *= 64;
+            } else if (p0 >= sc.n) {
+                break;
+            }
+            const int pos = p0 + lane;
+            stats_begin();
+            bool occl = false;
+            if (pos < sc.n) {
+                const int i = stream_index(s, pos, sc.a, sh.shard_cap);
+                occl = shadow_walk<STATS, V>(sv, ts, sh.s0[i], sh.s1[i], sh.s2[i], L[__float_as_int(sh.s0[i].w)], L, sh.aov_nee, st);
+            }
+            stats_end(p0, pos < sc.n, occl);
+        }
     }
     if constexpr (STATS) {
-        if (lane_id() == 0)
+        if (lane == 0)
             for (int c = 0; c < 2; ++c)
                 for (int k = 0; k < 6; ++k)
                     if (cls_acc[c][k]) atomicAdd(&stats[k < 5 ? 40 + 2 * k + c : 70 + c], cls_acc[c][k]);
@@ -2589,7 +2628,7 @@ extern "C" igx_status igx_set_option(igx_device* dev, const char* key, int64_t v
     }
     else if (k == "lds_scene_max") {
         dev->lds_scene_max = value;
-        size_t b = ((size_t)dev->sv.num_nodes * (dev->sv.node_f4 + lds_node_pad()) + (size_t)dev->sv.num_inst * 4 +
+        size_t b = ((size_t)dev->sv.num_nodes * dev->sv.node_f4 + (size_t)dev->sv.num_inst * 4 +
                     (size_t)dev->sv.num_tris * 3) * 16; // LDS layout (stage_scene_lds)
         dev->lds_scene_bytes = dev->has_scene && (int64_t)b <= value ? b : 0;
     }
@@ -3303,7 +3342,7 @@ extern "C" igx_status igx_upload_scene(igx_device* dev, const igx_scene_desc* de
     sv.num_tris = (int)(tris.size() / 3);
     {
         size_t b = ((size_t)sv.num_nodes * nf4 + (size_t)sv.num_inst * 4 + (size_t)sv.num_tris * 3) * 16;
-        const size_t bl = b + (size_t)sv.num_nodes * lds_node_pad() * 16; // LDS layout (stage_scene_lds)
+        const size_t bl = b; // LDS layout (stage_scene_lds): the same tables back to back
         dev->lds_scene_bytes = (int64_t)bl <= dev->lds_scene_max ? bl : 0;
         dev->table_bytes = b;
         dev->shading_bytes = ent.size() * sizeof(ent[0]) + vtx.size() * sizeof(vtx[0]) + nrm.size() * sizeof(nrm[0]) +

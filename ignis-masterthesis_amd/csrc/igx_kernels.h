@@ -75,7 +75,7 @@ __device__ __forceinline__ const float4* stage_enc_boxes(const SceneView& sv) {
 
 template <int BLOCK_>
 __device__ __forceinline__ SceneView stage_scene_lds(const SceneView& sv, float4* lds) {
-    const int nf = sv.node_f4, sh = nf == 8 ? 3 : 2, ns = nf + lds_node_pad(); // node stride in LDS (float4)
+    const int nf = sv.node_f4, sh = nf == 8 ? 3 : 2, ns = nf; // node stride in LDS (float4)
     const int n4 = sv.num_nodes * ns, i4 = sv.num_inst * 4, t3 = sv.num_tris * 3;
     for (int k = threadIdx.x; k < sv.num_nodes * nf; k += BLOCK_) lds[(k >> sh) * ns + (k & (nf - 1))] = sv.nodes[k];
     for (int k = threadIdx.x; k < i4; k += BLOCK_) lds[n4 + k] = sv.inst[k];
@@ -238,6 +238,38 @@ __device__ __forceinline__ int tpop(const TStack& s, int& sp) {
         return (!SPILL || sp < s.cap) ? s.lds[sp * TSTACK_STRIDE] : s.spill[(sp - s.cap) * s.sstride];
     }
 }
+// The entry a pop would return (entry sp - 1; sp >= 1 inside a walk, entry 0
+// holds the exit sentinel), read at the start of a node step or leaf together
+// with the node's own loads: a step that ends in a pop then takes the entry
+// from a register instead of waiting on a second, dependent LDS read
+// (IGX_PEEK_POP; 0: the pop reads the entry when it happens).
+#ifndef IGX_PEEK_POP
+#define IGX_PEEK_POP 1
+#endif
+template <bool SPILL>
+__device__ __forceinline__ int tpeek(const TStack& s, int sp) {
+    const int e = sp > 0 ? sp - 1 : 0;
+    if constexpr (SPILL) {
+        if (e >= s.cap) return ((global_int*)s.spill)[(e - s.cap) * s.sstride];
+    }
+    return ((lds_int*)s.lds)[e * TSTACK_STRIDE];
+}
+// the pop of a step that peeked (top = tpeek(ts, sp) at its start)
+template <bool SPILL, bool PEEK>
+__device__ __forceinline__ int tpop_peeked(const TStack& s, int& sp, int top) {
+    if constexpr (PEEK) {
+        --sp;
+        return top;
+    } else {
+        return tpop<SPILL>(s, sp);
+    }
+}
+template <bool SPILL, bool PEEK>
+__device__ __forceinline__ int tpeek_opt(const TStack& s, int sp) {
+    if constexpr (PEEK) return tpeek<SPILL>(s, sp);
+    else return 0;
+}
+
 // Push the farther hit children of a 4-wide node: r1 .. r(n-1) of the
 // children sorted nearest first (n hit children, r(n-1) the deepest entry,
 // r1 on top).  When all of them fit the LDS column with a slot to spare, the
@@ -377,7 +409,7 @@ constexpr float QSLAB_EXIT_WIDEN = 1.0f + 0x1p-20f;
 // Slab test of both children of BVH2 node `node` (intersect_ray_box,
 // intersection.art:170-181, with ray.tmin folded in).  Returns the next node
 // (nearer child first; the other is pushed) or the popped entry.
-template <bool STATS, bool SPILL, int NS, bool TREE>
+template <bool STATS, bool SPILL, int NS, bool TREE, bool PEEK>
 __device__ __forceinline__ int node_step2(const SceneView& sv, const Trav& t, int node, const TStack& ts, int& sp,
                                          TraceStats& st) {
     if (STATS) count_node(st, t.in_blas, node);
@@ -385,6 +417,7 @@ __device__ __forceinline__ int node_step2(const SceneView& sv, const Trav& t, in
     // memory (load_node: a branch per address space)
     float4 f[4];
     load_node<4, NS, TREE>(sv, node, f);
+    const int top = tpeek_opt<SPILL, PEEK>(ts, sp);
     const float4 a = f[0], b = f[1], c = f[2];
     const int4 r = as_int4(f[3]);
     // child 0 box: lo (a.x, a.z, b.x) hi (a.y, a.w, b.y)
@@ -409,7 +442,7 @@ __device__ __forceinline__ int node_step2(const SceneView& sv, const Trav& t, in
     }
     if (h0) return r.x;
     if (h1) return r.y;
-    return tpop<SPILL>(ts, sp);
+    return tpop_peeked<SPILL, PEEK>(ts, sp, top);
 }
 
 // Slab test of the four children of a 4-wide node (SoA bounds: one float4 per
@@ -431,12 +464,13 @@ __device__ __forceinline__ void cswap(float& da, int& ra, float& db, int& rb) {
     da = td;
     ra = tr;
 }
-template <bool STATS, bool SPILL, int NS, bool TREE>
+template <bool STATS, bool SPILL, int NS, bool TREE, bool PEEK>
 __device__ __forceinline__ int node_step4(const SceneView& sv, const Trav& t, int node, const TStack& ts, int& sp,
                                           TraceStats& st) {
     if (STATS) count_node(st, t.in_blas, node);
     float4 f[7];
     load_node<7, NS, TREE>(sv, node, f); // see node_step2
+    const int top = tpeek_opt<SPILL, PEEK>(ts, sp);
     const float4 lx = f[0], hx = f[1], ly = f[2], hy = f[3], lz = f[4], hz = f[5];
     const int4 r = as_int4(f[6]);
     float d[4];
@@ -457,7 +491,7 @@ __device__ __forceinline__ int node_step4(const SceneView& sv, const Trav& t, in
         d[k] = h ? en : INFINITY;
         n += h ? 1 : 0;
     }
-    if (n == 0) return tpop<SPILL>(ts, sp);
+    if (n == 0) return tpop_peeked<SPILL, PEEK>(ts, sp, top);
     cswap(d[0], ref[0], d[1], ref[1]);
     cswap(d[2], ref[2], d[3], ref[3]);
     cswap(d[0], ref[0], d[2], ref[2]);
@@ -473,12 +507,13 @@ __device__ __forceinline__ int node_step4(const SceneView& sv, const Trav& t, in
 // least half a quantum of slack (quantize_bvh4) and the exit distance is
 // widened by QSLAB_EXIT_WIDEN, so every ray the exact box accepts is accepted
 // here.  Absent children (kEmptyRef) are masked by ref.
-template <bool STATS, bool SPILL, bool TREE>
+template <bool STATS, bool SPILL, bool TREE, bool PEEK>
 __device__ __forceinline__ int node_step4q(const SceneView& sv, const Trav& t, int node, const TStack& ts, int& sp,
                                            TraceStats& st) {
     if (STATS) count_node(st, t.in_blas, node);
     float4 f[4];
     load_node<4, 4, TREE>(sv, node, f); // see node_step2
+    const int top = tpeek_opt<SPILL, PEEK>(ts, sp);
     const float4 A = f[0], B = f[1], C = f[2];
     const int4 r = as_int4(f[3]);
     const float SX = A.w * t.idir.x, SY = B.x * t.idir.y, SZ = B.y * t.idir.z;
@@ -513,7 +548,7 @@ __device__ __forceinline__ int node_step4q(const SceneView& sv, const Trav& t, i
         d[k] = h ? en : INFINITY;
         n += h ? 1 : 0;
     }
-    if (n == 0) return tpop<SPILL>(ts, sp);
+    if (n == 0) return tpop_peeked<SPILL, PEEK>(ts, sp, top);
     cswap(d[0], ref[0], d[1], ref[1]);
     cswap(d[2], ref[2], d[3], ref[3]);
     cswap(d[0], ref[0], d[2], ref[2]);
@@ -523,13 +558,20 @@ __device__ __forceinline__ int node_step4q(const SceneView& sv, const Trav& t, i
     return ref[0];
 }
 
+// stack-top peek (tpeek) in the node steps and leaves of kernels whose nodes
+// come from global memory (the peek's LDS read overlaps the node fetch);
+// with LDS-staged nodes it is one more LDS read per step for no latency saved.
+// Round 6: soup-16M frame 55.4 -> 54.5 ms, S-deep 146.6 -> 145.9 ms, diamond
+// (LDS-staged) 90.2 -> 90.9 ms with it, so it is off there.
+template <int V>
+constexpr bool variant_peek() { return IGX_PEEK_POP && !variant_lds_nodes(V); }
 template <bool STATS, int V>
 __device__ __forceinline__ int node_step(const SceneView& sv, const Trav& t, int node, const TStack& ts, int& sp,
                                          TraceStats& st) {
-    constexpr int PAD = variant_ldspad(V) ? 1 : 0;
-    if constexpr (variant_q4(V)) return node_step4q<STATS, variant_spill(V), variant_tree(V)>(sv, t, node, ts, sp, st);
-    else if constexpr (variant_width(V) == 4) return node_step4<STATS, variant_spill(V), 8 + PAD, variant_tree(V)>(sv, t, node, ts, sp, st);
-    else return node_step2<STATS, variant_spill(V), 4 + PAD, variant_tree(V)>(sv, t, node, ts, sp, st);
+    constexpr bool PK = variant_peek<V>();
+    if constexpr (variant_q4(V)) return node_step4q<STATS, variant_spill(V), variant_tree(V), PK>(sv, t, node, ts, sp, st);
+    else if constexpr (variant_width(V) == 4) return node_step4<STATS, variant_spill(V), 8, variant_tree(V), PK>(sv, t, node, ts, sp, st);
+    else return node_step2<STATS, variant_spill(V), 4, variant_tree(V), PK>(sv, t, node, ts, sp, st);
 }
 
 // Back from a BLAS: restore the world ray (recomputed: cheaper than keeping
@@ -680,9 +722,13 @@ __device__ __forceinline__ bool trav_step_core(const SceneView& sv, Trav& t, con
         return true;
     }
     if (STATS && first_active_lane()) st.wleaves++;
+    // every leaf and marker ends in a pop (or an instance's BLAS entry): its
+    // entry is read with the leaf's first loads (tpeek)
+    constexpr bool PK = variant_peek<V>();
+    const int top = tpeek_opt<SPILL, PK>(ts, sp);
     if (node == REF_MARKER) {
         leave_blas(t);
-        t.node = tpop<SPILL>(ts, sp);
+        t.node = tpop_peeked<SPILL, PK>(ts, sp, top);
         t.sp = sp;
         return false;
     }
@@ -706,7 +752,7 @@ __device__ __forceinline__ bool trav_step_core(const SceneView& sv, Trav& t, con
             tpush<SPILL>(ts, sp, REF_MARKER);
             t.node = root;
         } else {
-            t.node = tpop<SPILL>(ts, sp);
+            t.node = tpop_peeked<SPILL, PK>(ts, sp, top);
         }
     } else {
 #pragma unroll 1
@@ -718,7 +764,7 @@ __device__ __forceinline__ bool trav_step_core(const SceneView& sv, Trav& t, con
                 return true;
             }
         }
-        t.node = tpop<SPILL>(ts, sp);
+        t.node = tpop_peeked<SPILL, PK>(ts, sp, top);
     }
     t.sp = sp;
     return false;

@@ -83,3 +83,18 @@ gpu_trace() {
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/trace_$tag -o run --output-format csv -- \
     python3 "$@" > gpurun_out/trace_$tag.log 2>&1
 }
+
+# round-6 SQ / L2 / LDS counter passes: gpu_sq TAG ITERATIONS SCENE [OPTIONS_JSON] [SIZE]
+gpu_sq() {
+  bash tools/gpu_pmc_sq.sh "$@" && python3 tools/pmc_sq_summary.py gpurun_out/sq_$1 gpurun_out/sq_$1.json
+}
+
+# rank frames of the N-GPU shares on one GPU (tools/rank_pipeline.py, two
+# handles alternating as bench.py does at N > 1): gpu_ranks TAG SCENE ITERATIONS SIZE "N..." [stream_slots]
+gpu_ranks() {
+  local tag=$1 sc=$2 it=$3 sz=$4 ns=$5 slots=${6:-1}
+  for n in $ns; do
+    echo "== $tag n$n" | tee -a gpurun_out/ranks_$tag.log
+    IGX_PIPE_READY=1 timeout -k 10 300 python3 tools/rank_pipeline.py scenes/$sc $n 6 $slots $it $sz 2>&1 | tee -a gpurun_out/ranks_$tag.log || return 1
+  done
+}

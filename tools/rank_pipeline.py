@@ -16,7 +16,7 @@ n = int(sys.argv[2])
 K = int(sys.argv[3]) if len(sys.argv) > 3 else 6
 W, H = scene.film_size
 ITERS = int(sys.argv[5]) if len(sys.argv) > 5 else 32
-if len(sys.argv) > 6:
+if len(sys.argv) > 6 and int(sys.argv[6]) > 0:
     W = H = int(sys.argv[6])
 devs = [ignis_amd.Device(0), ignis_amd.Device(0)]
 slots = int(sys.argv[4]) if len(sys.argv) > 4 else 2
