@@ -3573,7 +3573,7 @@ igx_status ChunkScheduler::step(igx_device* dev, bool& progress) {
                 return fail(dev, IGX_ERR_HIP, "injected failure (option fail_chunk)");
             }
             igx_status st;
-            if ((st = harvest(dev, S)) != IGX_OK || (st = ensure_slot(dev, S, pl.slot_cap, false, pl.fa.classify == 4, dev->aov_on)) != IGX_OK) {
+            if ((st = harvest(dev, S)) != IGX_OK || (st = ensure_slot(dev, S, pl.slot_cap, false, pl.fa.classify >= 4, dev->aov_on)) != IGX_OK) {
                 restore();
                 return st;
             }
@@ -4002,9 +4002,9 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
     // record; twice that with the class-C region), shadow ray 48 B, hit
     // record 20 B (split schedule), radiance 16 B, and the two MIS AOV slots
     // (32 B) of an aov_mis scene.
-    if (split && fa.classify == 4) fa.classify = 3; // hit records have no class-C region
+    if (split && fa.classify >= 4) fa.classify = 3; // hit records have no class-C region
     const long long path_slot_bytes =
-        2 * 56 * (fa.classify == 4 ? 2 : 1) + 48 + (split ? 20 : 0) + 16 + (dev->aov_on && !list_mode ? 32 : 0);
+        2 * 56 * (fa.classify >= 4 ? 2 : 1) + 48 + (split ? 20 : 0) + 16 + (dev->aov_on && !list_mode ? 32 : 0);
     const long long slot_budget =
         dev->slot_budget_mb > 0 ? dev->slot_budget_mb * (1ll << 20) : (long long)((double)dev->mem_total * 0.3);
     long long auto_chunk_paths = 1ll << 24;
@@ -4076,7 +4076,7 @@ static igx_status render_impl(igx_device* dev, const igx_render_params* p, int c
         dev->next_slot ^= 1;
         igx_status st = harvest(dev, S); // waits for the chunk that used this slot two chunks ago (one, with one slot)
         if (st != IGX_OK) return st;
-        if ((st = ensure_slot(dev, S, slot_cap, split, fa.classify == 4, dev->aov_on && !list_mode)) != IGX_OK) return st;
+        if ((st = ensure_slot(dev, S, slot_cap, split, fa.classify >= 4, dev->aov_on && !list_mode)) != IGX_OK) return st;
         fa.aov_di = dev->aov_on && dev->aov_fb[0] && !list_mode ? S.aov_di : nullptr;
         fa.aov_nee = dev->aov_on && dev->aov_fb[1] && !list_mode ? S.aov_nee : nullptr;
         S.sh.aov_nee = fa.aov_nee;
