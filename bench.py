@@ -168,6 +168,30 @@ def load_rocprof(scene_key, split, kernel=None):
     return None
 
 
+SQ_PROFILES = {"diamond_scene": "r06_sq_diamond.json", "s_deep": "r06_sq_sdeep.json", "s_soup_16m": "r06_sq_soup16.json"}
+
+
+def sq_limiter(scene_key, kernel):
+    """Where the kernel's wave cycles go, from the committed round-6 SQ/TCC
+    counter summary of the same workload (tools/gpu_pmc_sq.sh ->
+    tools/pmc_sq_summary.py): SQ_WAIT_ANY (waiting on a memory or LDS counter),
+    SQ_WAIT_INST_ANY (waiting to issue) and SQ_ACTIVE_INST_ANY (issuing) over
+    SQ_WAVE_CYCLES, VALU lane use SQ_THREAD_CYCLES_VALU / (64 SQ_ACTIVE_INST_VALU)
+    and the L2 hit rate TCC_HIT / (TCC_HIT + TCC_MISS)."""
+    name = SQ_PROFILES.get(scene_key)
+    path = os.path.join(ROOT, "profiles", name) if name else None
+    if not path or not os.path.exists(path):
+        return "no SQ counter profile committed for this workload"
+    with open(path) as f:
+        ks = json.load(f)["kernels"]
+    for k, v in ks.items():
+        if k.split("<")[0] == kernel:
+            return (f"wave cycles {v['wait_any']:.0%} waiting on memory/LDS, {v['wait_inst_any']:.0%} waiting to issue, "
+                    f"{v['active_inst_any']:.0%} issuing; VALU lane use {v['lane_util']:.0%}; L2 hit {v['l2_hit']:.0%} "
+                    f"(profiles/{name})")
+    return f"{kernel} not in profiles/{name}"
+
+
 def roofline(dev, st, render_one, n_gpus, scene_key):
     """Roofline object of the dominant kernel: algorithmic HBM bytes (visit
     counts from an instrumented, untimed pass) over its HIP-event launch time,
@@ -226,10 +250,9 @@ def roofline(dev, st, render_one, n_gpus, scene_key):
         out["rocprof"] = dict(rp, frac=round(alg_bytes / launches / t / 1e9 / HBM_PEAK_GBS, 4),
                               frac_traffic=round(traffic / t / 1e9 / HBM_PEAK_GBS, 4) if traffic else None)
     out["_inst"] = inst  # visit counts for shadow_roofline (dropped before the line is printed)
-    out["limiter"] = (f"not HBM: tables on chip, node loop at {simd:.0%} SIMD efficiency (divergent per-lane "
-                      "traversal; VALU-issue bound, profiles/r01_pmc_diamond.md)" if resident else
-                      f"dependent node-fetch latency: {simd:.0%} SIMD efficiency, L2 hit rate ~44% "
-                      "(profiles/pmc_trace_s_soup_16m.json)")
+    sq = sq_limiter(scene_key, "k_trace_refill" if split else "k_extend")
+    out["limiter"] = (f"not HBM: tables on chip, divergent per-lane traversal, node loop at {simd:.0%} SIMD efficiency; {sq}"
+                      if resident else f"dependent node-fetch latency: node loop at {simd:.0%} SIMD efficiency; {sq}")
     return out
 
 
@@ -285,6 +308,7 @@ def shadow_roofline(st, inst, si, scene_key):
                               "instances": round(inst["shadow_leaf_visits"] / ns, 2),
                               "triangles": round(inst["shadow_tri_tests"] / ns, 2)},
            "avg_launch_us": round(t * 1e6, 2), "launches": launches,
+           "limiter": "dependent node-fetch latency of the any-hit walk; " + sq_limiter(scene_key, "k_shadow_refill"),
            "note": "the kernel's own launches (overlap_shadow 0); 48 B per ray counted as if every shadow ray were unoccluded"}
     rp = load_rocprof(scene_key, True, "k_shadow_refill<")
     if rp:
@@ -334,7 +358,7 @@ def fused_shadow_roofline(st, inst, si, scene_key):
            "avg_launch_us_timed": round(st["ms_shadow"] * 1e3 / max(1, st["launches_shadow"]), 2),
            "classes": classes,
            "limiter": "the divergent any-hit walk below the HBM roof it is priced against (tables LDS-staged; "
-                      "class B's node loop, see classes)",
+                      "class B's node loop, see classes); " + sq_limiter(scene_key, "k_shadow"),
            "note": "the kernel's own launches (concurrent_chunks 0); classes: per shadow stream class, instrumented pass"}
     rp = load_rocprof(scene_key, False, "k_shadow<")
     if rp:
