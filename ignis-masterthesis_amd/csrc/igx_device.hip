@@ -1178,6 +1178,17 @@ __global__ void __launch_bounds__(BLOCK) k_finish(FrameArgs fa, SceneView gsv, P
 #ifndef FINISH_PAIRS_WAVES
 #define FINISH_PAIRS_WAVES 3
 #endif
+// Pairs step independently (round 6): a wave keeps stepping its busy lanes
+// until TAIL_READY pairs have finished both walks (or none is busy), then
+// processes those pairs alone (shadow verdict, shading, hand-over, next
+// walks), so a pair no longer waits each bounce for the slowest walk of the
+// wave.  Soup-1M 2-iteration frame 72.4-72.8 -> 71.8 ms (tail 4.1 -> 3.6-3.7
+// ms), soup-16M and S-deep within noise, identical images (4 / 8 / 16 ready
+// pairs alike; profiles/r06_ab_tail_pairs_desync.log).  The soup-16M tail
+// stays ~5.5 ms: its first 8 bounces (98 K paths) take 3.2 ms of it
+// (profiles/r06_tail_vs_max_depth_soup16.log), each a chain of dependent
+// node fetches at 3 waves per SIMD.
+constexpr int TAIL_READY = 8;
 template <int V0, bool STATS>
 __global__ void __launch_bounds__(BLOCK, FINISH_PAIRS_WAVES) k_finish_pairs(FrameArgs fa, SceneView gsv, PathBuf in, float4* L, const int* cnt,
                                                         int tail_threshold, unsigned long long* stats,
@@ -1197,6 +1208,7 @@ __global__ void __launch_bounds__(BLOCK, FINISH_PAIRS_WAVES) k_finish_pairs(Fram
     const int ns = sc.n;
     const int lane = lane_id(), partner = lane ^ 1;
     const bool path_lane = (lane & 1) == 0;
+    constexpr uint64_t EVEN = 0x5555555555555555ull;
     for (int pos0 = w.k * 32; pos0 < ns; pos0 += w.K * 32) { // 32 paths per wave and pass
         const int pos = pos0 + (lane >> 1);
         PathState ps;
@@ -1208,58 +1220,62 @@ __global__ void __launch_bounds__(BLOCK, FINISH_PAIRS_WAVES) k_finish_pairs(Fram
         ShadowRec sr;
         f3 so = mk(0, 0, 0), sd = mk(0, 0, 1);
         float stmax = 0;
-        int hit_ent = -1, hit_prim = -1;
-        float hu = 0, hv = 0, htmax = 0;
+        Trav t;
+        bool busy = false, enclosed = false;
+        bool fresh = false; // this lane's walk has run since its pair was last processed
+        TraceStats& tst = path_lane ? st : sst;
+        bool start = true;  // the pair is at a bounce boundary: start its walks
         for (;;) {
-            // ---- both walks of the pair ----
-            Trav t;
-            bool busy = false, enclosed = false;
-            TraceStats& tst = path_lane ? st : sst;
-            if (tracing) {
-                float tmin, tmax;
-                uint32_t rflags;
-                ray_extent(fa, sv, ps.depth, ps.slot, tmin, tmax, rflags);
-                enclosed = ps.inside >= 0 && trav_init_enclosed<STATS>(sv, t, ps.inside, ps.o, ps.d, tmin, tmax, rflags, ts, tst);
-                if (!enclosed) trav_init(sv, t, ps.o, ps.d, tmin, tmax, rflags, ts);
-                busy = true;
-            } else if (sh_trace) {
-                trav_init(sv, t, so, sd, 0.001f, stmax, RAY_SHADOW, ts);
-                busy = true;
-            }
-            for (;;) {
-                while (__ballot(busy)) {
-                    if (busy && trav_step_core<2, STATS, V>(sv, t, ts, tst, !path_lane)) busy = false;
+            // ---- start the walks of the pairs at a bounce boundary ----
+            if (start) {
+                if (tracing) {
+                    float tmin, tmax;
+                    uint32_t rflags;
+                    ray_extent(fa, sv, ps.depth, ps.slot, tmin, tmax, rflags);
+                    enclosed = ps.inside >= 0 && trav_init_enclosed<STATS>(sv, t, ps.inside, ps.o, ps.d, tmin, tmax, rflags, ts, tst);
+                    if (!enclosed) trav_init(sv, t, ps.o, ps.d, tmin, tmax, rflags, ts);
+                    busy = fresh = true;
+                } else if (sh_trace) {
+                    trav_init(sv, t, so, sd, 0.001f, stmax, RAY_SHADOW, ts);
+                    busy = fresh = true;
                 }
-                // an enclosed walk that found nothing: the full traversal from the TLAS root
-                if (!(tracing && enclosed && !t.found)) break;
-                float tmin, tmax;
-                uint32_t rflags;
-                ray_extent(fa, sv, ps.depth, ps.slot, tmin, tmax, rflags);
-                trav_init(sv, t, ps.o, ps.d, tmin, tmax, rflags, ts);
-                enclosed = false;
-                busy = true;
+                start = false;
             }
-            if (tracing) {
-                htmax = t.tmax;
-                hit_ent = t.hit_ent;
-                hit_prim = t.hit_prim;
-                hu = t.hu;
-                hv = t.hv;
-                if (STATS && hit_ent >= 0) st.hits++;
+            // ---- step the busy lanes until TAIL_READY pairs (or all) have finished
+            // both walks: a pair does not wait for the slowest walk of the wave ----
+            uint64_t ready;
+            for (;;) {
+                const uint64_t bm = __ballot(busy), fm = __ballot(fresh);
+                ready = ((fm | (fm >> 1)) & EVEN) & ~((bm | (bm >> 1)) & EVEN);
+                if (bm == 0 || __popcll(ready) >= TAIL_READY) break;
+                if (busy && trav_step_core<2, STATS, V>(sv, t, ts, tst, !path_lane)) {
+                    busy = false;
+                    if (tracing && enclosed && !t.found) {
+                        // an enclosed walk that found nothing: the full traversal from the TLAS root
+                        float tmin, tmax;
+                        uint32_t rflags;
+                        ray_extent(fa, sv, ps.depth, ps.slot, tmin, tmax, rflags);
+                        trav_init(sv, t, ps.o, ps.d, tmin, tmax, rflags, ts);
+                        enclosed = false;
+                        busy = true;
+                    }
+                }
             }
-            // ---- the shadow ray's verdict back to its path lane ----
+            if (ready == 0) break; // no walk running and none to process: every pair is done
+            if (!((ready >> (lane & ~1)) & 1)) continue;
+            // ---- a ready pair: its shadow verdict, then the shading of its hit ----
+            fresh = false;
             const bool occluded = __shfl(sh_trace && t.found, partner) != 0;
             if (path_lane && had_shadow && !occluded) {
                 add_radiance(L, ps.slot, sr.color);
                 add_aov<variant_full(V0)>(fa.aov_nee, ps.slot, sr.color);
             }
-            if (!__ballot(tracing)) break;
-            // ---- shade the hits (path lanes) ----
             bool cont = false, has_shadow = false;
             if (tracing) {
+                if (STATS && t.hit_ent >= 0) st.hits++;
                 f3 Lacc;
                 bool has_l;
-                cont = shade_step<variant_full(V)>(fa, sv, ps, hit_ent, hit_prim, htmax, hu, hv, Lacc, has_l, has_shadow, sr);
+                cont = shade_step<variant_full(V)>(fa, sv, ps, t.hit_ent, t.hit_prim, t.tmax, t.hu, t.hv, Lacc, has_l, has_shadow, sr);
                 if (has_l) {
                     add_radiance(L, ps.slot, Lacc);
                     add_aov<variant_full(V0)>(fa.aov_di, ps.slot, Lacc);
@@ -1280,6 +1296,7 @@ __global__ void __launch_bounds__(BLOCK, FINISH_PAIRS_WAVES) k_finish_pairs(Fram
                 sd = mk(dx, dy, dz);
                 stmax = tm;
             }
+            start = true;
         }
     }
     for (int off = 32; off > 0; off >>= 1) {
