@@ -53,3 +53,32 @@ def test_world_size_mismatch_is_refused():
                        capture_output=True, text=True, timeout=120)
     assert r.returncode != 0
     assert "WORLD_SIZE=2 but --gpus 4" in r.stderr
+
+
+def _bench_module():
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_under_test", os.path.join(root, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_limiters_come_from_committed_counter_profiles():
+    """Every `limiter` string of the bench line is derived from a committed
+    round-6 SQ/TCC summary of the same workload (bench.py sq_limiter), and the
+    fractions it prints recompute from that file."""
+    b = _bench_module()
+    for scene, kernel in [("diamond_scene", "k_extend"), ("diamond_scene", "k_shadow"), ("s_deep", "k_extend"),
+                          ("s_soup_16m", "k_trace_refill"), ("s_soup_16m", "k_shadow_refill")]:
+        text = b.sq_limiter(scene, kernel)
+        name = b.SQ_PROFILES[scene]
+        assert f"profiles/{name}" in text, text
+        with open(os.path.join(os.path.dirname(b.__file__), "profiles", name)) as f:
+            ks = json.load(f)["kernels"]
+        v = next(v for k, v in ks.items() if k.split("<")[0] == kernel)
+        c = v["counters"]
+        assert abs(v["wait_any"] - c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"]) < 1e-3
+        assert abs(v["l2_hit"] - c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])) < 1e-3
+        assert f"{v['wait_any']:.0%} waiting" in text
+    assert "no SQ counter profile" in b.sq_limiter("primitives", "k_extend")
